@@ -1,0 +1,75 @@
+/*
+ * vacv_oracle.h -- CPU restatement of the vacv (b1xian/arm-neon-opencv) pixel
+ * operators.  TEST INFRASTRUCTURE ONLY: nothing in the product path may link,
+ * load or call this.  Only tests/, __graft_entry__.smoke() and bench.py's
+ * cpu_baseline leg use it, and only as the checker / CPU baseline.
+ *
+ * Every function restates one reference routine (file:line under
+ * /root/reference/src) and is pinned against golden vectors produced by the
+ * reference's own sources (oracle/_ref, built by oracle/Makefile) -- see
+ * tests/golden/make_golden.py and tests/test_oracle.py.
+ *
+ * Conventions: single image, host memory, dense rows.  "cc" = channels that
+ * are interleaved in one row (HWC: c; a CHW plane: 1).  u8 pixels are
+ * unsigned (ARM `char` semantics; the reference's x86 build is the odd one).
+ */
+#ifndef VACV_ORACLE_H
+#define VACV_ORACLE_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* resize mode for u8 bilinear */
+enum { ORACLE_LINEAR_NAIVE = 0, ORACLE_LINEAR_NEON = 1, ORACLE_LINEAR_OPENCV = 2 };
+
+/* --- geometry / tables ------------------------------------------------- */
+int  oracle_sat_short(float x);
+void oracle_linear_table(int n_in, int n_out, int mode, int32_t* ofs, int16_t* w0, int16_t* w1);
+void oracle_linear_table_f32(int n_in, int n_out, int32_t* ofs, float* w0, float* w1);
+void oracle_cubic_table(int n_in, int n_out, int32_t* ofs, float* coef /* 4*n_out */);
+void oracle_invert_affine(const float m[6], float inv[6]);
+void oracle_rotation_matrix(float scale, float rot_deg, const double aux[4], float m[6]);
+
+/* --- samplers ---------------------------------------------------------- */
+void oracle_resize_linear_u8(const uint8_t* src, int w_in, int h_in, int cc,
+                             uint8_t* dst, int w_out, int h_out, int mode);
+void oracle_resize_linear_f32(const float* src, int w_in, int h_in, int cc,
+                              float* dst, int w_out, int h_out);
+void oracle_resize_cubic_f32(const float* src, int w_in, int h_in, int cc,
+                             float* dst, int w_out, int h_out);
+void oracle_warp_affine_u8(const uint8_t* src, int w_in, int h_in, int cc,
+                           uint8_t* dst, int w_out, int h_out, const float inv[6]);
+void oracle_warp_affine_f32(const float* src, int w_in, int h_in, int cc,
+                            float* dst, int w_out, int h_out, const float inv[6]);
+
+/* --- colour ------------------------------------------------------------ */
+void oracle_yuv420sp_to_bgr(const uint8_t* src, uint8_t* dst, int w, int h, int v_first, int rgb_out);
+void oracle_bgr2nv21(const uint8_t* bgr, uint8_t* dst, int w, int h);
+
+/* --- layout / dtype / crop -------------------------------------------- */
+void oracle_hwc_to_chw(const void* src, void* dst, int w, int h, int c, int esize);
+void oracle_chw_to_hwc(const void* src, void* dst, int w, int h, int c, int esize);
+void oracle_u8_to_f32(const uint8_t* src, float* dst, int64_t count);
+void oracle_f32_to_u8(const float* src, uint8_t* dst, int64_t count);
+void oracle_crop(const void* src, int w, int h, int row_elems_per_px, int planes, int esize,
+                 void* dst, int left, int top, int cw, int chh);
+
+/* --- normalize / statistics ------------------------------------------- */
+void oracle_normalize_f32(const float* src, float* dst, int64_t pixels, int cc,
+                          const float* mean, const float* stddev);
+void oracle_mean_stddev_ref_f32(const float* src, int64_t pixels, int cc, float* mean, float* stddev);
+void oracle_channel_sums_f64(const float* src, int64_t pixels, int cc, double* sums /* 2*cc */);
+void oracle_channel_sums_u8(const uint8_t* src, int64_t pixels, int cc, double* sums /* 2*cc */);
+void oracle_stats_from_sums(const double* sums, double count, int cc, float* mean, float* stddev);
+
+/* --- harness helper (image_util.h:16-32) ------------------------------ */
+float  oracle_cosine_f32acc_u8(const uint8_t* a, const uint8_t* b, int64_t len);
+double oracle_cosine_f64_f32(const float* a, const float* b, int64_t len);
+
+#ifdef __cplusplus
+}
+#endif
+#endif
