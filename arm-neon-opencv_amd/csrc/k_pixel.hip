@@ -1,0 +1,500 @@
+// k_pixel.hip -- streaming per-pixel operators: crop (row copy), HWC<->CHW,
+// u8<->fp32, NV21/NV12 -> BGR (+normalize), normalize, per-channel sums.
+// All HBM-bound; every kernel moves 16 bytes per lane per access where the
+// alignment allows and falls back to narrower accesses only at row tails.
+#pragma clang fp contract(off)
+
+#include "vacv_device.hpp"
+
+namespace vacv {
+namespace {
+
+__device__ __forceinline__ int64_t gtid() { return (int64_t)blockIdx.x * blockDim.x + threadIdx.x; }
+__device__ __forceinline__ int64_t gstride() { return (int64_t)gridDim.x * blockDim.x; }
+
+int grid_for(int64_t work_items, int cap = 256 * 16) {
+    int64_t g = (work_items + kBlock - 1) / kBlock;
+    if (g < 1) g = 1;
+    if (g > cap) g = cap;
+    return (int)g;
+}
+
+// --------------------------------------------------------------------------
+// crop / clone: copy `row_bytes` from every (image, plane, row) of src to dst.
+// crop.cpp:44-125 restated as one strided 2-D copy per plane.
+__global__ void __launch_bounds__(kBlock) row_copy_kernel(CopyLaunch L) {
+    const int64_t rows_per_img = (int64_t)L.src.planes * L.src.h;
+    const int64_t rows = rows_per_img * L.n;
+    const int row_in_block = threadIdx.x / 64;  // 4 waves, one row each per step
+    const int lane = threadIdx.x & 63;
+    for (int64_t r = (int64_t)blockIdx.x * 4 + row_in_block; r < rows; r += (int64_t)gridDim.x * 4) {
+        const int64_t img = r / rows_per_img;
+        const int64_t rr = r - img * rows_per_img;
+        const int64_t plane = rr / L.src.h, y = rr - plane * L.src.h;
+        const unsigned char* s = L.src.base + img * L.src.img_pitch + plane * L.src.plane_pitch + y * L.src.row_pitch;
+        unsigned char* d = const_cast<unsigned char*>(L.dst.base) + img * L.dst.img_pitch +
+                           plane * L.dst.plane_pitch + y * L.dst.row_pitch;
+        const uintptr_t mis = (reinterpret_cast<uintptr_t>(s) | reinterpret_cast<uintptr_t>(d));
+        if ((mis & 15) == 0) {
+            const int64_t n16 = L.row_bytes >> 4;
+            for (int64_t i = lane; i < n16; i += 64)
+                reinterpret_cast<uint4*>(d)[i] = reinterpret_cast<const uint4*>(s)[i];
+            for (int64_t i = (n16 << 4) + lane; i < L.row_bytes; i += 64) d[i] = s[i];
+        } else if ((mis & 3) == 0) {
+            const int64_t n4 = L.row_bytes >> 2;
+            for (int64_t i = lane; i < n4; i += 64)
+                reinterpret_cast<uint32_t*>(d)[i] = reinterpret_cast<const uint32_t*>(s)[i];
+            for (int64_t i = (n4 << 2) + lane; i < L.row_bytes; i += 64) d[i] = s[i];
+        } else {
+            for (int64_t i = lane; i < L.row_bytes; i += 64) d[i] = s[i];
+        }
+    }
+}
+
+// --------------------------------------------------------------------------
+// HWC <-> CHW (tensor.cpp:160-182).  Generic: one element per step.
+template <typename T>
+__global__ void __launch_bounds__(kBlock) layout_kernel(LayoutLaunch L) {
+    const int64_t hw = (int64_t)L.w * L.h;
+    const int64_t per_img = hw * L.c;
+    const int64_t total = per_img * L.n;
+    for (int64_t e = gtid(); e < total; e += gstride()) {
+        const int64_t img = e / per_img;
+        const int64_t r = e - img * per_img;
+        // e indexes the DESTINATION densely -> writes are coalesced
+        int64_t si;
+        if (L.to_chw) {
+            const int64_t k = r / hw, i = r - k * hw;
+            si = i * L.c + k;
+        } else {
+            const int64_t i = r / L.c, k = r - i * L.c;
+            si = k * hw + i;
+        }
+        reinterpret_cast<T*>(L.dst + img * L.dst_img)[r] = reinterpret_cast<const T*>(L.src + img * L.src_img)[si];
+    }
+}
+
+// u8, c == 3, HWC -> CHW: 4 pixels per step, dword loads and stores.
+__global__ void __launch_bounds__(kBlock) hwc3_to_chw_u8_kernel(LayoutLaunch L) {
+    const int64_t hw = (int64_t)L.w * L.h;
+    const int64_t groups = hw / 4;
+    const int64_t total = groups * L.n;
+    for (int64_t gi = gtid(); gi < total; gi += gstride()) {
+        const int64_t img = gi / groups, g = gi - img * groups;
+        const uint32_t* s = reinterpret_cast<const uint32_t*>(L.src + img * L.src_img) + g * 3;
+        const uint32_t a = s[0], b = s[1], c = s[2];  // b0 g0 r0 b1 | g1 r1 b2 g2 | r2 b3 g3 r3
+        uint32_t ch0 = (a & 0xFFu) | (((a >> 24) & 0xFFu) << 8) | (((b >> 16) & 0xFFu) << 16) | (((c >> 8) & 0xFFu) << 24);
+        uint32_t ch1 = ((a >> 8) & 0xFFu) | ((b & 0xFFu) << 8) | (((b >> 24) & 0xFFu) << 16) | (((c >> 16) & 0xFFu) << 24);
+        uint32_t ch2 = ((a >> 16) & 0xFFu) | (((b >> 8) & 0xFFu) << 8) | ((c & 0xFFu) << 16) | (((c >> 24) & 0xFFu) << 24);
+        uint32_t* d = reinterpret_cast<uint32_t*>(L.dst + img * L.dst_img);
+        d[g] = ch0;
+        d[groups + g] = ch1;
+        d[2 * groups + g] = ch2;
+    }
+}
+
+// u8, c == 3, CHW -> HWC: 4 pixels per step.
+__global__ void __launch_bounds__(kBlock) chw_to_hwc3_u8_kernel(LayoutLaunch L) {
+    const int64_t hw = (int64_t)L.w * L.h;
+    const int64_t groups = hw / 4;
+    const int64_t total = groups * L.n;
+    for (int64_t gi = gtid(); gi < total; gi += gstride()) {
+        const int64_t img = gi / groups, g = gi - img * groups;
+        const uint32_t* s = reinterpret_cast<const uint32_t*>(L.src + img * L.src_img);
+        const uint32_t x = s[g], y = s[groups + g], z = s[2 * groups + g];
+        const uint32_t a = (x & 0xFFu) | ((y & 0xFFu) << 8) | ((z & 0xFFu) << 16) | (((x >> 8) & 0xFFu) << 24);
+        const uint32_t b = ((y >> 8) & 0xFFu) | (((z >> 8) & 0xFFu) << 8) | (((x >> 16) & 0xFFu) << 16) | (((y >> 16) & 0xFFu) << 24);
+        const uint32_t c = ((z >> 16) & 0xFFu) | (((x >> 24) & 0xFFu) << 8) | (((y >> 24) & 0xFFu) << 16) | (((z >> 24) & 0xFFu) << 24);
+        uint32_t* d = reinterpret_cast<uint32_t*>(L.dst + img * L.dst_img) + g * 3;
+        d[0] = a;
+        d[1] = b;
+        d[2] = c;
+    }
+}
+
+// --------------------------------------------------------------------------
+// u8 <-> f32 over a dense buffer (tensor.cpp:459-502).
+__global__ void __launch_bounds__(kBlock) u8_to_f32_kernel(DtypeLaunch L) {
+    const int64_t n16 = L.count >> 4;
+    for (int64_t i = gtid(); i < n16; i += gstride()) {
+        const uint4 v = reinterpret_cast<const uint4*>(L.src)[i];
+        float4* d = reinterpret_cast<float4*>(L.dst) + i * 4;
+        const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+            d[j] = make_float4((float)(w[j] & 0xFF), (float)((w[j] >> 8) & 0xFF), (float)((w[j] >> 16) & 0xFF),
+                               (float)(w[j] >> 24));
+    }
+    for (int64_t i = (n16 << 4) + gtid(); i < L.count; i += gstride())
+        reinterpret_cast<float*>(L.dst)[i] = (float)L.src[i];
+}
+
+__global__ void __launch_bounds__(kBlock) f32_to_u8_kernel(DtypeLaunch L) {
+    const int64_t n16 = L.count >> 4;
+    for (int64_t i = gtid(); i < n16; i += gstride()) {
+        const float4* s = reinterpret_cast<const float4*>(L.src) + i * 4;
+        uint32_t w[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const float4 f = s[j];
+            w[j] = (uint32_t)f32_to_u8_neon(f.x) | ((uint32_t)f32_to_u8_neon(f.y) << 8) |
+                   ((uint32_t)f32_to_u8_neon(f.z) << 16) | ((uint32_t)f32_to_u8_neon(f.w) << 24);
+        }
+        reinterpret_cast<uint4*>(L.dst)[i] = make_uint4(w[0], w[1], w[2], w[3]);
+    }
+    for (int64_t i = (n16 << 4) + gtid(); i < L.count; i += gstride())
+        L.dst[i] = f32_to_u8_neon(reinterpret_cast<const float*>(L.src)[i]);
+}
+
+// --------------------------------------------------------------------------
+// YUV420sp -> BGR (cvt_color.cpp:39-135).  One thread = a 4x2 pixel block:
+// two 4-byte Y loads and one 4-byte chroma load (two VU pairs), 2 rows x
+// 4 pixels x 3 channels out.
+template <int OUT>
+__global__ void __launch_bounds__(kBlock) color_kernel(ColorLaunch L) {
+    using TOut = typename std::conditional<(OUT == kOutSame), uint8_t, float>::type;
+    constexpr bool kLut = (OUT == kOutNorm);
+    __shared__ float lut[kLut ? 3 * 256 : 1];
+
+    const int img = blockIdx.z;
+    if (kLut) {
+        for (int i = threadIdx.y * blockDim.x + threadIdx.x; i < 3 * 256; i += kBlock) {
+            float m, s;
+            norm_params(L.norm, img, i >> 8, m, s);
+            lut[i] = normalize_value((float)(i & 255), m, s);
+        }
+        __syncthreads();
+    }
+    const int x0 = (blockIdx.x * blockDim.x + threadIdx.x) * 4;
+    const int yy = blockIdx.y * blockDim.y + threadIdx.y;  // row pair
+    if (x0 >= L.w || 2 * yy >= L.h) return;
+
+    const unsigned char* yb = L.src + (int64_t)img * L.src_img;
+    const unsigned char* y0p = yb + (int64_t)(2 * yy) * L.src_row + x0;
+    const unsigned char* y1p = y0p + L.src_row;
+    const unsigned char* uvp = yb + (int64_t)L.h * L.src_row + (int64_t)yy * L.src_row + x0;
+    const int valid = min(4, L.w - x0);
+
+    uint8_t ys[2][4], uv[4];
+    if (valid == 4 && ((reinterpret_cast<uintptr_t>(y0p) | reinterpret_cast<uintptr_t>(y1p) |
+                        reinterpret_cast<uintptr_t>(uvp)) & 3) == 0) {
+        const uint32_t a = *reinterpret_cast<const uint32_t*>(y0p);
+        const uint32_t b = *reinterpret_cast<const uint32_t*>(y1p);
+        const uint32_t c = *reinterpret_cast<const uint32_t*>(uvp);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            ys[0][j] = (a >> (8 * j)) & 0xFF;
+            ys[1][j] = (b >> (8 * j)) & 0xFF;
+            uv[j] = (c >> (8 * j)) & 0xFF;
+        }
+    } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int jj = j < valid ? j : 0;
+            ys[0][j] = y0p[jj];
+            ys[1][j] = y1p[jj];
+            uv[j] = uvp[jj];
+        }
+    }
+
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+        TOut out[12];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int pair = (j >> 1) * 2;
+            const int v = L.v_first ? uv[pair] : uv[pair + 1];
+            const int u = L.v_first ? uv[pair + 1] : uv[pair];
+            const Chroma ch = chroma_terms(u, v);
+            const int Y = ys[r][j];
+            const int R = clamp_u8(Y + ch.ra), G = clamp_u8(Y - ch.ga), B = clamp_u8(Y + ch.ba);
+            const int c0 = L.rgb ? R : B, c2 = L.rgb ? B : R;
+            if (OUT == kOutSame) {
+                out[3 * j + 0] = (TOut)c0; out[3 * j + 1] = (TOut)G; out[3 * j + 2] = (TOut)c2;
+            } else if (OUT == kOutF32) {
+                out[3 * j + 0] = (TOut)(float)c0; out[3 * j + 1] = (TOut)(float)G; out[3 * j + 2] = (TOut)(float)c2;
+            } else {
+                out[3 * j + 0] = lut[c0]; out[3 * j + 1] = lut[256 + G]; out[3 * j + 2] = lut[512 + c2];
+            }
+        }
+        unsigned char* dp = L.dst + (int64_t)img * L.dst_img + (int64_t)(2 * yy + r) * L.dst_row +
+                            (int64_t)x0 * 3 * sizeof(TOut);
+        constexpr int kBytes = 12 * (int)sizeof(TOut);
+        if (valid == 4 && (kBytes % 16 == 0) && ((reinterpret_cast<uintptr_t>(dp) & 15) == 0)) {
+#pragma unroll
+            for (int b = 0; b < kBytes / 16; ++b) reinterpret_cast<uint4*>(dp)[b] = reinterpret_cast<const uint4*>(out)[b];
+        } else if (valid == 4 && ((reinterpret_cast<uintptr_t>(dp) & 3) == 0)) {
+#pragma unroll
+            for (int b = 0; b < kBytes / 4; ++b) reinterpret_cast<uint32_t*>(dp)[b] = reinterpret_cast<const uint32_t*>(out)[b];
+        } else {
+            TOut* o = reinterpret_cast<TOut*>(dp);
+#pragma unroll
+            for (int e = 0; e < 12; ++e)
+                if (e < 3 * valid) o[e] = out[e];
+        }
+    }
+}
+
+// --------------------------------------------------------------------------
+// normalize (normalize_naive.cpp:74-90) over rows of (w * cc) elements.
+// One thread = 4 consecutive elements of a row.
+template <typename TIn>
+__global__ void __launch_bounds__(kBlock) normalize_kernel(NormLaunch L) {
+    const int64_t row_elems = (int64_t)L.src.w * L.src.cc;
+    const int64_t chunks = (row_elems + 3) / 4;
+    const int64_t rows_per_plane = L.src.h;
+    const int64_t total = chunks * rows_per_plane * L.src.planes * L.n;
+    for (int64_t i = gtid(); i < total; i += gstride()) {
+        int64_t r = i / chunks;
+        const int64_t cidx = i - r * chunks;
+        const int64_t y = r % rows_per_plane;
+        r /= rows_per_plane;
+        const int64_t plane = r % L.src.planes;
+        const int64_t img = r / L.src.planes;
+        const TIn* s = reinterpret_cast<const TIn*>(L.src.base + img * L.src.img_pitch + plane * L.src.plane_pitch +
+                                                    y * L.src.row_pitch);
+        float* d = reinterpret_cast<float*>(const_cast<unsigned char*>(L.dst.base) + img * L.dst.img_pitch +
+                                            plane * L.dst.plane_pitch + y * L.dst.row_pitch);
+        const int64_t e0 = cidx * 4;
+        float o[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int64_t e = e0 + j < row_elems ? e0 + j : row_elems - 1;
+            const int ch = (L.src.cc == 1) ? (int)plane : (int)(e % L.src.cc);
+            float m, sd;
+            norm_params(L.norm, (int)img, ch, m, sd);
+            o[j] = normalize_value((float)s[e], m, sd);
+        }
+        if (e0 + 4 <= row_elems && ((reinterpret_cast<uintptr_t>(d + e0) & 15) == 0)) {
+            *reinterpret_cast<float4*>(d + e0) = make_float4(o[0], o[1], o[2], o[3]);
+        } else {
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                if (e0 + j < row_elems) d[e0 + j] = o[j];
+        }
+    }
+}
+
+// --------------------------------------------------------------------------
+// Per-channel (Sum x, Sum x^2).  Each workgroup reduces a contiguous range of
+// one plane (dense) in chunks of 16*CC elements, so element j of a chunk is
+// always channel j % CC; partials are written per block and summed in a
+// fixed order by stats_reduce_kernel (deterministic).
+template <int CC, typename TIn>
+__global__ void __launch_bounds__(kBlock) channel_sums_kernel(SumsLaunch L) {
+    constexpr int kChunk = 16 * CC;
+    const int pidx = blockIdx.y;  // image * planes + plane
+    const int img = pidx / L.src.planes;
+    const int plane = pidx - img * L.src.planes;
+    const TIn* base = reinterpret_cast<const TIn*>(L.src.base + (int64_t)img * L.src.img_pitch +
+                                                   (int64_t)plane * L.src.plane_pitch);
+    const int64_t elems = (int64_t)L.src.w * L.src.h * CC;
+    const int64_t nchunks = L.scalar_only ? 0 : elems / kChunk;
+    const int64_t per_block = (nchunks + gridDim.x - 1) / gridDim.x;
+    const int64_t c_begin = blockIdx.x * per_block;
+    const int64_t c_end = min(nchunks, c_begin + per_block);
+
+    double s1[CC], s2[CC];
+#pragma unroll
+    for (int k = 0; k < CC; ++k) { s1[k] = 0.0; s2[k] = 0.0; }
+
+    if (sizeof(TIn) == 1) {
+        uint32_t a1[CC], a2[CC];
+#pragma unroll
+        for (int k = 0; k < CC; ++k) { a1[k] = 0; a2[k] = 0; }
+        int steps = 0;
+        for (int64_t c = c_begin + threadIdx.x; c < c_end; c += kBlock) {
+            const uint4* p = reinterpret_cast<const uint4*>(base + c * kChunk);
+#pragma unroll
+            for (int q = 0; q < CC; ++q) {
+                const uint4 v = p[q];
+                const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+                for (int j = 0; j < 16; ++j) {
+                    const uint32_t b = (w[j >> 2] >> (8 * (j & 3))) & 0xFFu;
+                    const int k = (q * 16 + j) % CC;
+                    a1[k] += b;
+                    a2[k] += b * b;
+                }
+            }
+            // a2 grows by <= 16*65025 per step: flush well before 2^32
+            if (++steps == 2048) {
+#pragma unroll
+                for (int k = 0; k < CC; ++k) { s1[k] += a1[k]; s2[k] += a2[k]; a1[k] = 0; a2[k] = 0; }
+                steps = 0;
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < CC; ++k) { s1[k] += a1[k]; s2[k] += a2[k]; }
+    } else {
+        for (int64_t c = c_begin + threadIdx.x; c < c_end; c += kBlock) {
+            const float4* p = reinterpret_cast<const float4*>(base + c * kChunk);
+#pragma unroll
+            for (int q = 0; q < 4 * CC; ++q) {
+                const float4 v = p[q];
+                const float f[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const int k = (q * 4 + j) % CC;
+                    const double d = f[j];
+                    s1[k] += d;
+                    s2[k] += d * d;
+                }
+            }
+        }
+    }
+    // tail elements (all of them on a misaligned plane), split over blocks
+    {
+        const int64_t t0 = nchunks * kChunk, tn = elems - t0;
+        const int64_t tper = (tn + gridDim.x - 1) / gridDim.x;
+        const int64_t tb = t0 + blockIdx.x * tper, te = min(elems, tb + tper);
+        for (int64_t e = tb + threadIdx.x; e < te; e += kBlock) {
+            const double d = (double)base[e];
+            const int k = (int)(e % CC);
+#pragma unroll
+            for (int kk = 0; kk < CC; ++kk)
+                if (kk == k) { s1[kk] += d; s2[kk] += d * d; }
+        }
+    }
+
+    __shared__ double red[kBlock / 64][2 * CC];
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+#pragma unroll
+    for (int k = 0; k < CC; ++k) {
+        const double t1 = wave_sum(s1[k]);
+        const double t2 = wave_sum(s2[k]);
+        if (lane == 0) { red[wave][2 * k] = t1; red[wave][2 * k + 1] = t2; }
+    }
+    __syncthreads();
+    if (threadIdx.x < 2 * CC) {
+        double acc = 0.0;
+#pragma unroll
+        for (int wv = 0; wv < kBlock / 64; ++wv) acc += red[wv][threadIdx.x];
+        // partials[img][plane][block][CC][2]
+        const int64_t o = (((int64_t)pidx * gridDim.x) + blockIdx.x) * (2 * CC) + threadIdx.x;
+        L.partials[o] = acc;
+    }
+}
+
+// sums[g][c][2] from partials, fixed order: image-major, then plane, block.
+__global__ void stats_reduce_kernel(SumsLaunch L, int cc) {
+    const int c = L.c;
+    const int groups = L.per_image ? L.n : 1;
+    const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= groups * c * 2) return;
+    const int g = idx / (2 * c);
+    const int r = idx - g * 2 * c;
+    const int ch = r >> 1, mom = r & 1;
+    const int plane = (cc == 1) ? ch : 0;  // NCHW: channel = plane
+    const int k = (cc == 1) ? 0 : ch;
+    const int img_lo = L.per_image ? g : 0, img_hi = L.per_image ? g + 1 : L.n;
+    double acc = 0.0;
+    for (int img = img_lo; img < img_hi; ++img) {
+        const int64_t pidx = (int64_t)img * L.src.planes + plane;
+        for (int b = 0; b < L.blocks_per_image; ++b)
+            acc += L.partials[((pidx * L.blocks_per_image) + b) * (2 * cc) + 2 * k + mom];
+    }
+    L.sums[idx] = acc;
+}
+
+__global__ void stats_kernel(const double* sums, int groups, int c, double count, float* mean, float* stddev) {
+    const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= groups * c) return;
+    const double m = sums[2 * idx] / count;
+    double var = sums[2 * idx + 1] / count - m * m;
+    if (var < 0) var = 0;
+    mean[idx] = (float)m;
+    stddev[idx] = (float)sqrt(var);
+}
+
+template <int CC, typename TIn>
+hipError_t launch_sums_cc(const SumsLaunch& L, hipStream_t s) {
+    dim3 grid(L.blocks_per_image, L.n * L.src.planes);
+    hipLaunchKernelGGL((channel_sums_kernel<CC, TIn>), grid, dim3(kBlock), 0, s, L);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    const int groups = L.per_image ? L.n : 1;
+    const int work = groups * L.c * 2;
+    hipLaunchKernelGGL(stats_reduce_kernel, dim3((work + 255) / 256), dim3(256), 0, s, L, CC);
+    return hipGetLastError();
+}
+
+template <typename TIn>
+hipError_t launch_sums_t(const SumsLaunch& L, hipStream_t s) {
+    switch (L.src.cc) {
+        case 1: return launch_sums_cc<1, TIn>(L, s);
+        case 2: return launch_sums_cc<2, TIn>(L, s);
+        case 3: return launch_sums_cc<3, TIn>(L, s);
+        case 4: return launch_sums_cc<4, TIn>(L, s);
+        default: return hipErrorInvalidValue;
+    }
+}
+
+}  // namespace
+
+hipError_t launch_row_copy(const CopyLaunch& L, hipStream_t s) {
+    const int64_t rows = (int64_t)L.src.planes * L.src.h * L.n;
+    int g = (int)std::min<int64_t>((rows + 3) / 4, 256 * 32);
+    hipLaunchKernelGGL(row_copy_kernel, dim3(g < 1 ? 1 : g), dim3(kBlock), 0, s, L);
+    return hipGetLastError();
+}
+
+hipError_t launch_layout(const LayoutLaunch& L, hipStream_t s) {
+    const int64_t hw = (int64_t)L.w * L.h;
+    const bool aligned = ((reinterpret_cast<uintptr_t>(L.src) | reinterpret_cast<uintptr_t>(L.dst)) & 3) == 0 &&
+                         (L.src_img & 3) == 0 && (L.dst_img & 3) == 0;
+    if (L.esize == 1 && L.c == 3 && hw % 4 == 0 && aligned) {
+        const int g = grid_for(hw / 4 * L.n);
+        if (L.to_chw) hipLaunchKernelGGL(hwc3_to_chw_u8_kernel, dim3(g), dim3(kBlock), 0, s, L);
+        else hipLaunchKernelGGL(chw_to_hwc3_u8_kernel, dim3(g), dim3(kBlock), 0, s, L);
+        return hipGetLastError();
+    }
+    const int g = grid_for(hw * L.c * L.n);
+    switch (L.esize) {
+        case 1: hipLaunchKernelGGL(layout_kernel<uint8_t>, dim3(g), dim3(kBlock), 0, s, L); break;
+        case 2: hipLaunchKernelGGL(layout_kernel<uint16_t>, dim3(g), dim3(kBlock), 0, s, L); break;
+        case 4: hipLaunchKernelGGL(layout_kernel<uint32_t>, dim3(g), dim3(kBlock), 0, s, L); break;
+        case 8: hipLaunchKernelGGL(layout_kernel<uint64_t>, dim3(g), dim3(kBlock), 0, s, L); break;
+        default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_dtype(const DtypeLaunch& L, hipStream_t s) {
+    const int g = grid_for(L.count / 16 + 1);
+    if (L.to_f32) hipLaunchKernelGGL(u8_to_f32_kernel, dim3(g), dim3(kBlock), 0, s, L);
+    else hipLaunchKernelGGL(f32_to_u8_kernel, dim3(g), dim3(kBlock), 0, s, L);
+    return hipGetLastError();
+}
+
+hipError_t launch_color(const ColorLaunch& L, hipStream_t s) {
+    dim3 block(64, 4);
+    dim3 grid((L.w / 4 + 64) / 64, (L.h / 2 + 3) / 4, L.n);
+    if (L.out == kOutSame) hipLaunchKernelGGL(color_kernel<kOutSame>, grid, block, 0, s, L);
+    else if (L.out == kOutF32) hipLaunchKernelGGL(color_kernel<kOutF32>, grid, block, 0, s, L);
+    else hipLaunchKernelGGL(color_kernel<kOutNorm>, grid, block, 0, s, L);
+    return hipGetLastError();
+}
+
+hipError_t launch_normalize(const NormLaunch& L, hipStream_t s) {
+    const int64_t row_elems = (int64_t)L.src.w * L.src.cc;
+    const int64_t total = (row_elems + 3) / 4 * L.src.h * L.src.planes * L.n;
+    const int g = grid_for(total);
+    if (L.src_u8) hipLaunchKernelGGL(normalize_kernel<uint8_t>, dim3(g), dim3(kBlock), 0, s, L);
+    else hipLaunchKernelGGL(normalize_kernel<float>, dim3(g), dim3(kBlock), 0, s, L);
+    return hipGetLastError();
+}
+
+hipError_t launch_channel_sums(const SumsLaunch& L, hipStream_t s) {
+    if (L.src_u8) return launch_sums_t<uint8_t>(L, s);
+    return launch_sums_t<float>(L, s);
+}
+
+hipError_t launch_stats(const double* sums, int groups, int c, double count, float* mean, float* stddev,
+                        hipStream_t s) {
+    const int work = groups * c;
+    hipLaunchKernelGGL(stats_kernel, dim3((work + 255) / 256), dim3(256), 0, s, sums, groups, c, count, mean, stddev);
+    return hipGetLastError();
+}
+
+}  // namespace vacv

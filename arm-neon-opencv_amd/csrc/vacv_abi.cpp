@@ -1,0 +1,760 @@
+// vacv_abi.cpp -- the extern "C" entry points of include/vacv_hip.h.
+//
+// Host side of every operator: validate the descriptors (the reference
+// silently does nothing or recurses forever on unsupported input, SURVEY.md
+// App. C; here that is a status code), derive the geometry, plan the tiles,
+// and queue kernels on the caller's stream.  No call synchronises the device
+// and no C++ exception escapes.
+#pragma clang fp contract(off)
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdint>
+#include <cstring>
+#include <map>
+#include <mutex>
+#include <utility>
+
+#include "vacv_internal.hpp"
+#include "vacv_semantics.hpp"
+
+namespace vacv {
+namespace {
+
+int esize_of(int dtype) {
+    switch (dtype) {
+        case VACV_FP32: return 4;
+        case VACV_FP16: return 2;
+        case VACV_INT8: return 1;
+        case VACV_FP64: return 8;
+        default: return 0;
+    }
+}
+
+// A validated descriptor with every pitch filled in.
+struct Img {
+    unsigned char* data;
+    int n, w, h, c, dtype, layout, es;
+    int64_t row, plane, batch;
+};
+
+int load(const vacv_image* d, Img& m) {
+    if (!d || !d->data) return VACV_ERR_INVALID_ARG;
+    if (d->n < 1 || d->w < 1 || d->h < 1 || d->c < 1) return VACV_ERR_INVALID_ARG;
+    m.es = esize_of(d->dtype);
+    if (!m.es) return VACV_ERR_UNSUPPORTED;
+    if (d->layout != VACV_NHWC && d->layout != VACV_NCHW) return VACV_ERR_UNSUPPORTED;
+    m.data = static_cast<unsigned char*>(d->data);
+    m.n = d->n; m.w = d->w; m.h = d->h; m.c = d->c;
+    m.dtype = d->dtype; m.layout = d->layout;
+    const int64_t min_row = (int64_t)m.w * (m.layout == VACV_NHWC ? m.c : 1) * m.es;
+    m.row = d->row_pitch ? d->row_pitch : min_row;
+    if (m.row < min_row) return VACV_ERR_INVALID_ARG;
+    if (m.layout == VACV_NCHW) {
+        const int64_t min_plane = m.row * (m.h - 1) + min_row;
+        m.plane = d->plane_pitch ? d->plane_pitch : m.row * m.h;
+        if (m.plane < min_plane) return VACV_ERR_INVALID_ARG;
+        const int64_t min_batch = m.plane * (m.c - 1) + min_plane;
+        m.batch = d->batch_pitch ? d->batch_pitch : m.plane * m.c;
+        if (m.n > 1 && m.batch < min_batch) return VACV_ERR_INVALID_ARG;
+    } else {
+        m.plane = 0;
+        const int64_t min_batch = m.row * (m.h - 1) + min_row;
+        m.batch = d->batch_pitch ? d->batch_pitch : m.row * m.h;
+        if (m.n > 1 && m.batch < min_batch) return VACV_ERR_INVALID_ARG;
+    }
+    return VACV_OK;
+}
+
+bool dense(const Img& m) {
+    const int64_t row = (int64_t)m.w * (m.layout == VACV_NHWC ? m.c : 1) * m.es;
+    if (m.row != row) return false;
+    if (m.layout == VACV_NCHW && m.plane != row * m.h) return false;
+    const int64_t img = row * m.h * (m.layout == VACV_NCHW ? m.c : 1);
+    return m.n == 1 || m.batch == img;
+}
+
+PlaneGeom geom(const Img& m) {
+    PlaneGeom g;
+    g.base = m.data;
+    g.img_pitch = m.batch;
+    g.row_pitch = m.row;
+    g.w = m.w;
+    g.h = m.h;
+    g.esize = m.es;
+    if (m.layout == VACV_NHWC) {
+        g.planes = 1;
+        g.cc = m.c;
+        g.plane_pitch = 0;
+    } else {
+        g.planes = m.c;
+        g.cc = 1;
+        g.plane_pitch = m.plane;
+    }
+    g.plane_bytes = m.row * (m.h - 1) + (int64_t)m.w * g.cc * m.es;
+    return g;
+}
+
+int hip_status(hipError_t e) { return e == hipSuccess ? VACV_OK : VACV_ERR_HIP; }
+
+bool same_shape(const Img& a, const Img& b) {
+    return a.n == b.n && a.w == b.w && a.h == b.h && a.c == b.c && a.layout == b.layout;
+}
+
+// ---- per-(device, stream) workspace for the statistics paths ---------------
+struct Workspace {
+    void* buf = nullptr;
+    size_t cap = 0;
+};
+std::mutex g_ws_mu;
+std::map<std::pair<int, void*>, Workspace> g_ws;
+
+int workspace(hipStream_t s, size_t bytes, void** out) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return VACV_ERR_HIP;
+    std::lock_guard<std::mutex> lk(g_ws_mu);
+    Workspace& w = g_ws[{dev, (void*)s}];
+    if (w.cap < bytes) {
+        if (w.buf) {
+            // the previous buffer may still be read by queued work
+            if (hipStreamSynchronize(s) != hipSuccess) return VACV_ERR_HIP;
+            (void)hipFree(w.buf);
+            w.buf = nullptr;
+            w.cap = 0;
+        }
+        size_t cap = std::max<size_t>(bytes, 1 << 20);
+        if (hipMalloc(&w.buf, cap) != hipSuccess) return VACV_ERR_NO_MEMORY;
+        w.cap = cap;
+    }
+    *out = w.buf;
+    return VACV_OK;
+}
+
+size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
+
+// ---- statistics -------------------------------------------------------------
+// Sum / Sum^2 per channel of `m` into `sums` ([groups][c][2] doubles, device).
+int channel_sums_into(const Img& m, double* sums, int per_image, double* partials, int blocks, hipStream_t s) {
+    SumsLaunch L{};
+    L.src = geom(m);
+    L.n = m.n;
+    L.c = m.c;
+    L.src_u8 = m.dtype == VACV_INT8;
+    L.blocks_per_image = blocks;
+    L.partials = partials;
+    L.sums = sums;
+    L.per_image = per_image;
+    L.scalar_only = 0;
+    for (int i = 0; i < m.n && !L.scalar_only; ++i)
+        for (int p = 0; p < L.src.planes; ++p) {
+            uintptr_t a = reinterpret_cast<uintptr_t>(m.data + (int64_t)i * m.batch + (int64_t)p * L.src.plane_pitch);
+            if (a & 15) { L.scalar_only = 1; break; }
+        }
+    return hip_status(launch_channel_sums(L, s));
+}
+
+int sums_blocks(const Img& m) {
+    const int64_t elems = (int64_t)m.w * m.h * (m.layout == VACV_NHWC ? m.c : 1);
+    const int64_t planes = (int64_t)m.n * (m.layout == VACV_NHWC ? 1 : m.c);
+    // ~1-4K workgroups over the whole batch, >= 4K elements each
+    int64_t b = std::max<int64_t>(1, 2048 / std::max<int64_t>(planes, 1));
+    b = std::min<int64_t>(b, std::max<int64_t>(1, elems / 4096));
+    return (int)std::min<int64_t>(b, 1024);
+}
+
+// Per-image mean/std of `m` into workspace arrays; returns device pointers.
+int per_image_stats(const Img& m, hipStream_t s, float** mean, float** stdv) {
+    if (m.layout == VACV_NHWC && m.c > 4) return VACV_ERR_UNSUPPORTED;
+    if (!dense(m)) return VACV_ERR_UNSUPPORTED;
+    const int blocks = sums_blocks(m);
+    const int planes = m.layout == VACV_NHWC ? 1 : m.c;
+    const int cc = m.layout == VACV_NHWC ? m.c : 1;
+    const size_t part_b = align_up((size_t)m.n * planes * blocks * 2 * cc * sizeof(double), 256);
+    const size_t sums_b = align_up((size_t)m.n * m.c * 2 * sizeof(double), 256);
+    const size_t stat_b = align_up((size_t)m.n * m.c * sizeof(float), 256);
+    void* ws = nullptr;
+    int st = workspace(s, part_b + sums_b + 2 * stat_b, &ws);
+    if (st) return st;
+    char* p = static_cast<char*>(ws);
+    double* partials = reinterpret_cast<double*>(p);
+    double* sums = reinterpret_cast<double*>(p + part_b);
+    *mean = reinterpret_cast<float*>(p + part_b + sums_b);
+    *stdv = reinterpret_cast<float*>(p + part_b + sums_b + stat_b);
+    st = channel_sums_into(m, sums, 1, partials, blocks, s);
+    if (st) return st;
+    return hip_status(launch_stats(sums, m.n, m.c, (double)m.w * m.h, *mean, *stdv, s));
+}
+
+int norm_spec(const Img& shape, const float* mean, const float* stdv, NormSpec& ns) {
+    std::memset(&ns, 0, sizeof(ns));
+    ns.c_total = shape.c;
+    if (!mean && !stdv) return VACV_OK;  // caller fills mode 2
+    if (!mean || !stdv) return VACV_ERR_INVALID_ARG;
+    if (shape.c > kMaxC) return VACV_ERR_UNSUPPORTED;
+    ns.mode = 1;
+    for (int k = 0; k < shape.c; ++k) {
+        ns.mean[k] = mean[k];
+        ns.stdv[k] = stdv[k];
+    }
+    return VACV_OK;
+}
+
+// In-place normalize of an fp32 image with per-image device statistics.
+int normalize_with(const Img& src, const Img& dst, const NormSpec& ns, hipStream_t s) {
+    NormLaunch L{};
+    L.src = geom(src);
+    L.dst = geom(dst);
+    L.n = src.n;
+    L.src_u8 = src.dtype == VACV_INT8;
+    L.norm = ns;
+    return hip_status(launch_normalize(L, s));
+}
+
+// ---- resize planning ---------------------------------------------------------
+template <typename F>
+int max_over_tiles(int n_out, int tile, F&& f) {
+    int best = 0;
+    for (int t0 = 0; t0 < n_out; t0 += tile) best = std::max(best, f(t0, std::min(tile, n_out - t0)));
+    return best;
+}
+
+int origin(const ResizeLaunch& L, int d, bool vertical) {
+    const int n_in = vertical ? L.src.h : L.src.w;
+    if (L.kind == kLinearFixed) {
+        const int n_out = vertical ? L.dst.h : L.dst.w;
+        return fixed_tap(d, n_in, n_out, vertical ? L.scale_yf : L.scale_xf, vertical ? L.scale_yd : L.scale_xd,
+                         L.mode).i;
+    }
+    if (L.kind == kLinearFloat) return float_tap(d, n_in, vertical ? L.scale_yf : L.scale_xf).i;
+    return cubic_tap(d, n_in, vertical ? L.scale_yd : L.scale_xd).i - 1;
+}
+
+int nonzero_taps(const ResizeLaunch& L, int y0, int ny) {
+    int cnt = 0;
+    for (int t = 0; t < ny; ++t) {
+        const int d = y0 + t;
+        if (L.kind == kLinearFixed) {
+            FixedTap q = fixed_tap(d, L.src.h, L.dst.h, L.scale_yf, L.scale_yd, L.mode);
+            cnt += (q.w0 != 0) + (q.w1 != 0);
+        } else if (L.kind == kLinearFloat) {
+            FloatTap q = float_tap(d, L.src.h, L.scale_yf);
+            cnt += (q.w0 != 0.f) + (q.w1 != 0.f);
+        } else {
+            CubicTap q = cubic_tap(d, L.src.h, L.scale_yd);
+            for (int j = 0; j < 4; ++j) cnt += q.c[j] != 0.f;
+        }
+    }
+    return cnt;
+}
+
+constexpr int kLdsBudget = 48 * 1024;
+
+int plan_resize(ResizeLaunch& L) {
+    const int taps = L.kind == kCubic ? 4 : 2;
+    const int bp = L.src.cc * L.src.esize;
+    const int w_out = L.dst.w, h_out = L.dst.h;
+    const double sx = (double)L.src.w / w_out, sy = (double)L.src.h / h_out;
+    L.sparse = sy >= taps ? 1 : 0;
+
+    // tile width: whole output rows when the staged source row is small
+    int tile_w;
+    if ((int64_t)(L.src.w + taps) * bp <= 12288) {
+        tile_w = w_out;
+    } else {
+        int px = (int)(8192.0 / (sx * bp));
+        px = std::max(64, px / 64 * 64);
+        tile_w = std::min(px, w_out);
+    }
+    for (;;) {
+        const int groups = (tile_w + 3) / 4;
+        int tile_h = std::max(1, std::min((1024 + groups - 1) / groups, L.sparse ? 64 / taps : 32));
+        tile_h = std::min(tile_h, h_out);
+        for (;;) {
+            const int span = max_over_tiles(w_out, tile_w, [&](int x0, int nx) {
+                return (origin(L, x0 + nx - 1, false) + taps - 1 - origin(L, x0, false) + 1) * bp;
+            });
+            const int slot_stride = (span + 30) / 16 * 16;
+            const int slots = L.sparse ? max_over_tiles(h_out, tile_h, [&](int y0, int ny) { return nonzero_taps(L, y0, ny); })
+                                       : max_over_tiles(h_out, tile_h, [&](int y0, int ny) {
+                                             return origin(L, y0 + ny - 1, true) + taps - 1 - origin(L, y0, true) + 1;
+                                         });
+            const int xw_bytes = L.kind == kLinearFixed ? tile_w * 4 : tile_w * taps * 4;
+            const bool lut = L.kind == kLinearFixed && L.out == kOutNorm;
+            const int lds = (int)(align_up(tile_w * 4, 16) + align_up(xw_bytes, 16) + 80 * 4 +
+                                  2 * align_up(std::max(slots, 1) * 4, 16) + (lut ? 256 * L.src.cc * 4 : 0) +
+                                  (size_t)std::max(slots, 1) * slot_stride);
+            if (lds <= kLdsBudget || (tile_h == 1 && tile_w <= 64)) {
+                if (lds > 160 * 1024) return VACV_ERR_UNSUPPORTED;
+                L.tile_w = tile_w;
+                L.tile_h = tile_h;
+                L.tiles_x = (w_out + tile_w - 1) / tile_w;
+                L.tiles_y = (h_out + tile_h - 1) / tile_h;
+                L.max_slots = std::max(slots, 1);
+                L.slot_stride = slot_stride;
+                L.lds_bytes = lds;
+                return VACV_OK;
+            }
+            if (tile_h == 1) break;
+            tile_h = std::max(1, tile_h * 3 / 4);
+        }
+        tile_w = std::max(64, (tile_w / 2) / 64 * 64);
+    }
+}
+
+int resize_impl(const vacv_image* src_d, const vacv_image* dst_d, int interpolation, int mode, int out_kind,
+                const NormSpec* ns, hipStream_t s) {
+    Img src, dst;
+    int st = load(src_d, src);
+    if (st) return st;
+    if ((st = load(dst_d, dst))) return st;
+    if (src.n != dst.n || src.c != dst.c || src.layout != dst.layout) return VACV_ERR_INVALID_ARG;
+    if (src.layout == VACV_NHWC && src.c > 4) return VACV_ERR_UNSUPPORTED;
+    if (mode < VACV_LINEAR_REFERENCE || mode > VACV_LINEAR_OPENCV) return VACV_ERR_INVALID_ARG;
+
+    ResizeLaunch L{};
+    L.src = geom(src);
+    L.dst = geom(dst);
+    L.n = src.n;
+    L.mode = mode;
+    L.out = out_kind;
+    if (ns) L.norm = *ns;
+    if (interpolation == VACV_INTER_LINEAR) {
+        if (src.w < 2 || src.h < 2) return VACV_ERR_INVALID_ARG;  // resize_naive.cpp:28-31 needs 2 taps
+        if (src.dtype == VACV_INT8) {
+            L.kind = kLinearFixed;
+            const int want = out_kind == kOutSame ? VACV_INT8 : VACV_FP32;
+            if (dst.dtype != want) return VACV_ERR_INVALID_ARG;
+        } else if (src.dtype == VACV_FP32) {
+            L.kind = kLinearFloat;
+            if (dst.dtype != VACV_FP32) return VACV_ERR_INVALID_ARG;
+            if (out_kind == kOutF32) L.out = kOutSame;
+        } else {
+            return VACV_ERR_UNSUPPORTED;
+        }
+    } else if (interpolation == VACV_INTER_CUBIC) {
+        if (src.w < 4 || src.h < 4) return VACV_ERR_INVALID_ARG;  // resize_naive.cpp:154-181 folds need 4
+        if (src.dtype != VACV_INT8 && src.dtype != VACV_FP32) return VACV_ERR_UNSUPPORTED;
+        if (dst.dtype != VACV_FP32) return VACV_ERR_UNSUPPORTED;  // u8 cubic = fused widen to fp32
+        L.kind = kCubic;
+        if (L.out == kOutSame && src.dtype == VACV_INT8) L.out = kOutF32;
+        if (L.out == kOutF32 && src.dtype == VACV_FP32) L.out = kOutSame;
+    } else {
+        return VACV_ERR_UNSUPPORTED;  // resize.cpp:46-49 recurses forever for other modes
+    }
+    L.scale_xf = (float)src.w / (float)dst.w;
+    L.scale_yf = (float)src.h / (float)dst.h;
+    L.scale_xd = (double)src.w / (double)dst.w;
+    L.scale_yd = (double)src.h / (double)dst.h;
+    if ((st = plan_resize(L))) return st;
+    return hip_status(launch_resize(L, s));
+}
+
+int copy_rows(const Img& src, const Img& dst, int64_t src_off, int rows_h, int64_t row_bytes, hipStream_t s) {
+    CopyLaunch L{};
+    L.src = geom(src);
+    L.dst = geom(dst);
+    L.src.base += src_off;
+    L.src.h = rows_h;
+    L.n = src.n;
+    L.row_bytes = row_bytes;
+    return hip_status(launch_row_copy(L, s));
+}
+
+int dtype_convert(const Img& src, const Img& dst, hipStream_t s) {
+    if (!dense(src) || !dense(dst)) return VACV_ERR_UNSUPPORTED;
+    DtypeLaunch L{};
+    L.src = src.data;
+    L.dst = dst.data;
+    L.count = (int64_t)src.n * src.w * src.h * src.c;
+    L.to_f32 = src.dtype == VACV_INT8;
+    return hip_status(launch_dtype(L, s));
+}
+
+int border_values(const Img& src, const double* bv, float out[4]) {
+    for (int k = 0; k < 4; ++k) {
+        const double v = bv ? bv[k] : 0.0;
+        if (src.dtype == VACV_INT8) {
+            double r = std::nearbyint(v);
+            out[k] = (float)std::min(255.0, std::max(0.0, r));
+        } else {
+            out[k] = (float)v;
+        }
+    }
+    return VACV_OK;
+}
+
+int warp_impl(const vacv_image* src_d, const vacv_image* dst_d, const float m[6], int flags, int border_mode,
+              const double bv[4], int out_kind, const NormSpec* ns, hipStream_t s) {
+    Img src, dst;
+    int st = load(src_d, src);
+    if (st) return st;
+    if ((st = load(dst_d, dst))) return st;
+    if (!m) return VACV_ERR_INVALID_ARG;
+    if (src.n != dst.n || src.c != dst.c || src.layout != dst.layout) return VACV_ERR_INVALID_ARG;
+    if (src.dtype != VACV_INT8 && src.dtype != VACV_FP32) return VACV_ERR_UNSUPPORTED;
+    // warp_affine.cpp:114-118: anything else recurses into the OpenCV stub
+    if (flags != VACV_INTER_LINEAR || border_mode != VACV_BORDER_CONSTANT) return VACV_ERR_UNSUPPORTED;
+    if (src.layout == VACV_NHWC && src.c > 4) return VACV_ERR_UNSUPPORTED;
+    if (src.w < 2 || src.h < 2) return VACV_ERR_INVALID_ARG;
+    WarpLaunch L{};
+    L.src = geom(src);
+    L.dst = geom(dst);
+    L.n = src.n;
+    L.out = out_kind;
+    if (src.dtype == VACV_FP32 && out_kind == kOutF32) L.out = kOutSame;
+    const int want = (L.out == kOutSame) ? src.dtype : VACV_FP32;
+    if (dst.dtype != want) return VACV_ERR_INVALID_ARG;
+    vacv_invert_affine(m, L.inv);
+    border_values(src, bv, L.border);
+    if (ns) L.norm = *ns;
+    return hip_status(launch_warp(L, s));
+}
+
+int color_impl(const vacv_image* src_d, const vacv_image* dst_d, int code, int out_kind, const NormSpec* ns,
+               hipStream_t s) {
+    Img src, dst;
+    int st = load(src_d, src);
+    if (st) return st;
+    if ((st = load(dst_d, dst))) return st;
+    int v_first, rgb;
+    switch (code) {
+        case VACV_COLOR_YUV2BGR_NV21: v_first = 1; rgb = 0; break;
+        case VACV_COLOR_YUV2RGB_NV21: v_first = 1; rgb = 1; break;
+        case VACV_COLOR_YUV2BGR_NV12: v_first = 0; rgb = 0; break;
+        case VACV_COLOR_YUV2RGB_NV12: v_first = 0; rgb = 1; break;
+        default: return VACV_ERR_UNSUPPORTED;
+    }
+    if (src.dtype != VACV_INT8 || src.c != 1) return VACV_ERR_INVALID_ARG;
+    const int h = src.h / 3 * 2;  // cvt_color.cpp:152
+    if (src.w % 2 || h % 2 || h < 2 || src.h != h / 2 * 3) return VACV_ERR_INVALID_ARG;
+    if (dst.w != src.w || dst.h != h || dst.c != 3 || dst.layout != VACV_NHWC || dst.n != src.n)
+        return VACV_ERR_INVALID_ARG;
+    const int want = out_kind == kOutSame ? VACV_INT8 : VACV_FP32;
+    if (dst.dtype != want) return VACV_ERR_INVALID_ARG;
+    ColorLaunch L{};
+    L.src = src.data;
+    L.src_img = src.batch;
+    L.src_row = src.row;
+    L.dst = dst.data;
+    L.dst_img = dst.batch;
+    L.dst_row = dst.row;
+    L.n = src.n;
+    L.w = src.w;
+    L.h = h;
+    L.v_first = v_first;
+    L.rgb = rgb;
+    L.out = out_kind;
+    if (ns) L.norm = *ns;
+    return hip_status(launch_color(L, s));
+}
+
+// Shape of the fp32 output viewed as its own image (for the auto-stats passes).
+int fused_normalize(const vacv_image* dst_d, const float* mean, const float* stddev, hipStream_t s,
+                    int (*pass)(const void*, int, const NormSpec*, hipStream_t), const void* ctx) {
+    Img dst;
+    int st = load(dst_d, dst);
+    if (st) return st;
+    if (dst.dtype != VACV_FP32) return VACV_ERR_INVALID_ARG;
+    NormSpec ns;
+    if ((st = norm_spec(dst, mean, stddev, ns))) return st;
+    if (ns.mode == 1) return pass(ctx, kOutNorm, &ns, s);
+    // auto statistics: raw fp32 result, per-image stats of it, normalize in place
+    if ((st = pass(ctx, kOutF32, nullptr, s))) return st;
+    float *dm = nullptr, *ds = nullptr;
+    if ((st = per_image_stats(dst, s, &dm, &ds))) return st;
+    ns.mode = 2;
+    ns.dev_mean = dm;
+    ns.dev_std = ds;
+    return normalize_with(dst, dst, ns, s);
+}
+
+struct ResizeCtx {
+    const vacv_image* src;
+    const vacv_image* dst;
+    int interpolation, mode;
+};
+int resize_pass(const void* c, int out, const NormSpec* ns, hipStream_t s) {
+    const ResizeCtx* r = static_cast<const ResizeCtx*>(c);
+    return resize_impl(r->src, r->dst, r->interpolation, r->mode, out, ns, s);
+}
+
+struct WarpCtx {
+    const vacv_image* src;
+    const vacv_image* dst;
+    const float* m;
+    int flags, border;
+    const double* bv;
+};
+int warp_pass(const void* c, int out, const NormSpec* ns, hipStream_t s) {
+    const WarpCtx* w = static_cast<const WarpCtx*>(c);
+    return warp_impl(w->src, w->dst, w->m, w->flags, w->border, w->bv, out, ns, s);
+}
+
+struct ColorCtx {
+    const vacv_image* src;
+    const vacv_image* dst;
+    int code;
+};
+int color_pass(const void* c, int out, const NormSpec* ns, hipStream_t s) {
+    const ColorCtx* k = static_cast<const ColorCtx*>(c);
+    return color_impl(k->src, k->dst, k->code, out, ns, s);
+}
+
+}  // namespace
+}  // namespace vacv
+
+using namespace vacv;
+
+extern "C" {
+
+int vacv_abi_version(void) { return VACV_ABI_VERSION; }
+
+const char* vacv_status_string(int status) {
+    switch (status) {
+        case VACV_OK: return "ok";
+        case VACV_ERR_INVALID_ARG: return "invalid argument";
+        case VACV_ERR_UNSUPPORTED: return "unsupported";
+        case VACV_ERR_HIP: return "HIP runtime error";
+        case VACV_ERR_NO_MEMORY: return "out of device memory";
+        default: return "unknown status";
+    }
+}
+
+int64_t vacv_image_bytes(const vacv_image* d) {
+    Img m;
+    if (load(d, m)) return -1;
+    return m.layout == VACV_NCHW ? m.plane * (m.c - 1) + m.row * (m.h - 1) + (int64_t)m.w * m.es
+                                 : m.row * (m.h - 1) + (int64_t)m.w * m.c * m.es;
+}
+
+int vacv_crop(const vacv_image* src_d, const vacv_image* dst_d, int left, int top, void* stream) {
+    Img src, dst;
+    int st = load(src_d, src);
+    if (st) return st;
+    if ((st = load(dst_d, dst))) return st;
+    if (src.n != dst.n || src.c != dst.c || src.layout != dst.layout || src.dtype != dst.dtype)
+        return VACV_ERR_INVALID_ARG;
+    if (left < 0 || top < 0 || left + dst.w > src.w || top + dst.h > src.h) return VACV_ERR_INVALID_ARG;
+    const int cc = src.layout == VACV_NHWC ? src.c : 1;
+    const int64_t off = (int64_t)top * src.row + (int64_t)left * cc * src.es;
+    return copy_rows(src, dst, off, dst.h, (int64_t)dst.w * cc * src.es, (hipStream_t)stream);
+}
+
+int vacv_change_layout(const vacv_image* src_d, const vacv_image* dst_d, void* stream) {
+    Img src, dst;
+    int st = load(src_d, src);
+    if (st) return st;
+    if ((st = load(dst_d, dst))) return st;
+    if (src.n != dst.n || src.w != dst.w || src.h != dst.h || src.c != dst.c || src.dtype != dst.dtype)
+        return VACV_ERR_INVALID_ARG;
+    hipStream_t s = (hipStream_t)stream;
+    if (src.layout == dst.layout || src.c == 1) {
+        // clone() (tensor.cpp:398-400); a 1-channel image is the same bytes in both layouts
+        if (src.layout != dst.layout) {
+            if (!dense(src) || !dense(dst)) return VACV_ERR_UNSUPPORTED;
+            Img a = src, b = dst;
+            a.layout = b.layout = VACV_NHWC;
+            return copy_rows(a, b, 0, a.h, (int64_t)a.w * a.es, s);
+        }
+        const int cc = src.layout == VACV_NHWC ? src.c : 1;
+        return copy_rows(src, dst, 0, src.h, (int64_t)src.w * cc * src.es, s);
+    }
+    if (!dense(src) || !dense(dst)) return VACV_ERR_UNSUPPORTED;
+    LayoutLaunch L{};
+    L.src = src.data;
+    L.dst = dst.data;
+    L.n = src.n;
+    L.w = src.w;
+    L.h = src.h;
+    L.c = src.c;
+    L.esize = src.es;
+    L.to_chw = dst.layout == VACV_NCHW;
+    L.src_img = src.batch;
+    L.dst_img = dst.batch;
+    return hip_status(launch_layout(L, s));
+}
+
+int vacv_change_dtype(const vacv_image* src_d, const vacv_image* dst_d, void* stream) {
+    Img src, dst;
+    int st = load(src_d, src);
+    if (st) return st;
+    if ((st = load(dst_d, dst))) return st;
+    if (!same_shape(src, dst)) return VACV_ERR_INVALID_ARG;
+    hipStream_t s = (hipStream_t)stream;
+    if (src.dtype == dst.dtype) {
+        const int cc = src.layout == VACV_NHWC ? src.c : 1;
+        return copy_rows(src, dst, 0, src.h, (int64_t)src.w * cc * src.es, s);
+    }
+    const bool ok = (src.dtype == VACV_INT8 && dst.dtype == VACV_FP32) ||
+                    (src.dtype == VACV_FP32 && dst.dtype == VACV_INT8);
+    if (!ok) return VACV_ERR_UNSUPPORTED;  // tensor.cpp:494-499 returns garbage
+    return dtype_convert(src, dst, s);
+}
+
+int vacv_resize(const vacv_image* src_d, const vacv_image* dst_d, int interpolation, int mode, void* stream) {
+    Img src, dst;
+    int st = load(src_d, src);
+    if (st) return st;
+    if ((st = load(dst_d, dst))) return st;
+    hipStream_t s = (hipStream_t)stream;
+    if (src.w == dst.w && src.h == dst.h && (interpolation == VACV_INTER_LINEAR || interpolation == VACV_INTER_CUBIC) &&
+        same_shape(src, dst)) {
+        // resize.cpp:58-61 short-circuits equal sizes with a copy (the
+        // reference copies w*h*c BYTES, a quarter of an fp32 image; this
+        // copies the whole image)
+        if (src.dtype == dst.dtype) {
+            const int cc = src.layout == VACV_NHWC ? src.c : 1;
+            return copy_rows(src, dst, 0, src.h, (int64_t)src.w * cc * src.es, s);
+        }
+        if (src.dtype == VACV_INT8 && dst.dtype == VACV_FP32 && interpolation == VACV_INTER_CUBIC)
+            return dtype_convert(src, dst, s);
+    }
+    return resize_impl(src_d, dst_d, interpolation, mode, kOutSame, nullptr, s);
+}
+
+int vacv_rotation_matrix(float scale, float rot_deg, const double aux[4], float m[6]) {
+    if (!m) return VACV_ERR_INVALID_ARG;
+    const double a[4] = {aux ? aux[0] : 0.0, aux ? aux[1] : 0.0, aux ? aux[2] : 0.0, aux ? aux[3] : 0.0};
+    // warp_affine.cpp:76-94 with point (0,0): angle in float radians,
+    // alpha/beta = scale * cosf/sinf (float products widened to double)
+    const float angle = (float)((double)rot_deg * (M_PI / 180));
+    const double alpha = (double)(scale * cosf(angle));
+    const double beta = (double)(scale * sinf(angle));
+    m[0] = (float)alpha;
+    m[1] = (float)beta;
+    m[3] = (float)-beta;
+    m[4] = (float)alpha;
+    // warp_affine.cpp:105-106 (aux translation fix, double arithmetic)
+    m[2] = (float)(a[2] - (double)m[0] * a[0] - (double)m[1] * a[1]);
+    m[5] = (float)(a[3] - (double)m[3] * a[0] - (double)m[4] * a[1]);
+    return VACV_OK;
+}
+
+int vacv_invert_affine(const float m[6], float inv[6]) {
+    if (!m || !inv) return VACV_ERR_INVALID_ARG;
+    // warp_affine.cpp:121-133: float products, double D, stored as float
+    float a[6];
+    std::memcpy(a, m, sizeof(a));
+    double D = (double)(a[0] * a[4] - a[1] * a[3]);
+    D = D != 0 ? 1. / D : 0;
+    const double A11 = (double)a[4] * D;
+    const double A22 = (double)a[0] * D;
+    a[0] = (float)A11;
+    a[1] = (float)((double)a[1] * -D);
+    a[3] = (float)((double)a[3] * -D);
+    a[4] = (float)A22;
+    const float b1 = -a[0] * a[2] - a[1] * a[5];
+    const float b2 = -a[3] * a[2] - a[4] * a[5];
+    a[2] = b1;
+    a[5] = b2;
+    std::memcpy(inv, a, sizeof(a));
+    return VACV_OK;
+}
+
+int vacv_warp_affine(const vacv_image* src, const vacv_image* dst, const float m[6], int flags, int border_mode,
+                     const double border_value[4], void* stream) {
+    return warp_impl(src, dst, m, flags, border_mode, border_value, kOutSame, nullptr, (hipStream_t)stream);
+}
+
+int vacv_cvt_color(const vacv_image* src, const vacv_image* dst, int code, void* stream) {
+    return color_impl(src, dst, code, kOutSame, nullptr, (hipStream_t)stream);
+}
+
+int vacv_normalize(const vacv_image* src_d, const vacv_image* dst_d, const float* mean, const float* stddev,
+                   void* stream) {
+    Img src, dst;
+    int st = load(src_d, src);
+    if (st) return st;
+    if ((st = load(dst_d, dst))) return st;
+    if (!same_shape(src, dst) || dst.dtype != VACV_FP32) return VACV_ERR_INVALID_ARG;
+    if (src.dtype != VACV_INT8 && src.dtype != VACV_FP32) return VACV_ERR_UNSUPPORTED;
+    hipStream_t s = (hipStream_t)stream;
+    NormSpec ns;
+    if ((st = norm_spec(src, mean, stddev, ns))) return st;
+    if (ns.mode == 0) {
+        float *dm = nullptr, *ds = nullptr;
+        if ((st = per_image_stats(src, s, &dm, &ds))) return st;
+        ns.mode = 2;
+        ns.dev_mean = dm;
+        ns.dev_std = ds;
+    }
+    return normalize_with(src, dst, ns, s);
+}
+
+int vacv_channel_sums(const vacv_image* src_d, double* sums, int per_image, void* stream) {
+    Img src;
+    int st = load(src_d, src);
+    if (st) return st;
+    if (!sums) return VACV_ERR_INVALID_ARG;
+    if (src.dtype != VACV_INT8 && src.dtype != VACV_FP32) return VACV_ERR_UNSUPPORTED;
+    if (src.layout == VACV_NHWC && src.c > 4) return VACV_ERR_UNSUPPORTED;
+    if (!dense(src)) return VACV_ERR_UNSUPPORTED;
+    hipStream_t s = (hipStream_t)stream;
+    const int blocks = sums_blocks(src);
+    const int planes = src.layout == VACV_NHWC ? 1 : src.c;
+    const int cc = src.layout == VACV_NHWC ? src.c : 1;
+    void* ws = nullptr;
+    if ((st = workspace(s, (size_t)src.n * planes * blocks * 2 * cc * sizeof(double), &ws))) return st;
+    return channel_sums_into(src, sums, per_image ? 1 : 0, static_cast<double*>(ws), blocks, s);
+}
+
+int vacv_stats_from_sums(const double* sums, int groups, int c, double count, float* mean, float* stddev,
+                         void* stream) {
+    if (!sums || !mean || !stddev || groups < 1 || c < 1 || !(count > 0)) return VACV_ERR_INVALID_ARG;
+    return hip_status(launch_stats(sums, groups, c, count, mean, stddev, (hipStream_t)stream));
+}
+
+int vacv_mean_stddev(const vacv_image* src_d, float* mean, float* stddev, void* stream) {
+    Img src;
+    int st = load(src_d, src);
+    if (st) return st;
+    if (!mean || !stddev) return VACV_ERR_INVALID_ARG;
+    if (src.dtype != VACV_INT8 && src.dtype != VACV_FP32) return VACV_ERR_UNSUPPORTED;
+    hipStream_t s = (hipStream_t)stream;
+    float *dm = nullptr, *ds = nullptr;
+    if ((st = per_image_stats(src, s, &dm, &ds))) return st;
+    const size_t b = (size_t)src.n * src.c * sizeof(float);
+    if (hipMemcpyAsync(mean, dm, b, hipMemcpyDeviceToDevice, s) != hipSuccess) return VACV_ERR_HIP;
+    if (hipMemcpyAsync(stddev, ds, b, hipMemcpyDeviceToDevice, s) != hipSuccess) return VACV_ERR_HIP;
+    return VACV_OK;
+}
+
+int vacv_resize_normalize(const vacv_image* src, const vacv_image* dst, int interpolation, int mode,
+                          const float* mean, const float* stddev, void* stream) {
+    ResizeCtx c{src, dst, interpolation, mode};
+    return fused_normalize(dst, mean, stddev, (hipStream_t)stream, resize_pass, &c);
+}
+
+int vacv_warp_affine_normalize(const vacv_image* src, const vacv_image* dst, const float m[6], int flags,
+                               int border_mode, const double border_value[4], const float* mean, const float* stddev,
+                               void* stream) {
+    WarpCtx c{src, dst, m, flags, border_mode, border_value};
+    return fused_normalize(dst, mean, stddev, (hipStream_t)stream, warp_pass, &c);
+}
+
+int vacv_cvt_color_normalize(const vacv_image* src, const vacv_image* dst, int code, const float* mean,
+                             const float* stddev, void* stream) {
+    ColorCtx c{src, dst, code};
+    return fused_normalize(dst, mean, stddev, (hipStream_t)stream, color_pass, &c);
+}
+
+int vacv_stream_synchronize(void* stream) {
+    return hipStreamSynchronize((hipStream_t)stream) == hipSuccess ? VACV_OK : VACV_ERR_HIP;
+}
+
+int vacv_release_workspace(void) {
+    std::lock_guard<std::mutex> lk(g_ws_mu);
+    int st = VACV_OK;
+    for (auto& kv : g_ws) {
+        if (kv.second.buf) {
+            if (hipStreamSynchronize((hipStream_t)kv.first.second) != hipSuccess) st = VACV_ERR_HIP;
+            if (hipFree(kv.second.buf) != hipSuccess) st = VACV_ERR_HIP;
+        }
+    }
+    g_ws.clear();
+    return st;
+}
+
+}  // extern "C"

@@ -1,0 +1,56 @@
+// vacv_device.hpp -- small gfx950 device helpers shared by the kernels.
+#pragma once
+#pragma clang fp contract(off)
+
+#include <hip/hip_runtime.h>
+#include <cstdint>
+
+#include "vacv_internal.hpp"
+#include "vacv_semantics.hpp"
+
+namespace vacv {
+
+// A raw buffer resource over [base16, base16 + bytes): loads past the end
+// return zeros instead of faulting, so a 16-byte staging load may overhang
+// the last row of a batch.  base16 is the 16-byte aligned-down plane base;
+// `delta` is what has to be added to offsets relative to the true base.
+struct Rsrc {
+    __amdgpu_buffer_rsrc_t r;
+    uint32_t delta;
+};
+
+__device__ __forceinline__ Rsrc make_rsrc(const unsigned char* base, int64_t bytes) {
+    uintptr_t p = reinterpret_cast<uintptr_t>(base);
+    uintptr_t a = p & ~uintptr_t(15);
+    Rsrc s;
+    s.delta = static_cast<uint32_t>(p - a);
+    int64_t n = bytes + s.delta;
+    if (n > 0x7FFFFFF0LL) n = 0x7FFFFFF0LL;
+    s.r = __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(a), (short)0, (int)n, 0x00020000);
+    return s;
+}
+
+__device__ __forceinline__ uint4 load16(const Rsrc& s, uint32_t off_from_base16) {
+    auto v = __builtin_amdgcn_raw_buffer_load_b128(s.r, (int)off_from_base16, 0, 0);
+    return *reinterpret_cast<uint4*>(&v);
+}
+
+// Per-workgroup mean/stddev for channel ch of image img.
+__device__ __forceinline__ void norm_params(const NormSpec& ns, int img, int ch, float& m, float& s) {
+    if (ns.mode == 2) {
+        m = ns.dev_mean[(int64_t)img * ns.c_total + ch];
+        s = ns.dev_std[(int64_t)img * ns.c_total + ch];
+    } else {
+        m = ns.mean[ch];
+        s = ns.stdv[ch];
+    }
+}
+
+template <typename T>
+__device__ __forceinline__ T wave_sum(T v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+}  // namespace vacv

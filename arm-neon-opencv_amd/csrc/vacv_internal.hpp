@@ -1,0 +1,143 @@
+// vacv_internal.hpp -- kernel parameter blocks and launcher declarations
+// shared between the C-ABI layer (vacv_abi.cpp) and the kernels (*.hip).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <cstdint>
+
+#include "../../include/vacv_hip.h"
+
+namespace vacv {
+
+constexpr int kBlock = 256;         // threads per workgroup (4 waves)
+constexpr int kMaxC = VACV_MAX_CHANNELS;
+
+// How a batch is walked: a "plane" is what one sampler pass sees -- a whole
+// NHWC image (cc = c interleaved channels) or one NCHW channel plane (cc = 1).
+struct PlaneGeom {
+    const unsigned char* base;   // image 0, plane 0, pixel (0,0)
+    int64_t img_pitch;           // bytes between images
+    int64_t plane_pitch;         // bytes between planes of one image (NCHW)
+    int64_t row_pitch;           // bytes between rows
+    int planes;                  // planes per image (NCHW: c, NHWC: 1)
+    int w, h;
+    int cc;                      // interleaved channels per pixel
+    int esize;                   // bytes per element
+    int64_t plane_bytes;         // readable bytes from one plane's base
+};
+
+// Normalisation applied by a fused epilogue.
+struct NormSpec {
+    int mode;                    // 0 none, 1 host constants, 2 per-image device arrays
+    int c_total;                 // channels of the image (NCHW plane p -> channel p % c_total)
+    const float* dev_mean;       // [n][c_total] (mode 2)
+    const float* dev_std;
+    float mean[kMaxC];
+    float stdv[kMaxC];
+};
+
+enum SampleKind : int {
+    kLinearFixed = 0,   // u8 bilinear (modes REFERENCE / NEON / OPENCV)
+    kLinearFloat = 1,   // fp32 bilinear
+    kCubic = 2,         // fp32 (or u8 widened) Keys cubic
+};
+
+enum OutKind : int {
+    kOutSame = 0,       // u8 -> u8 or f32 -> f32
+    kOutF32 = 1,        // widened to f32, no normalisation
+    kOutNorm = 2,       // f32, normalised
+};
+
+struct ResizeLaunch {
+    PlaneGeom src;
+    PlaneGeom dst;
+    int n;
+    int kind;                    // SampleKind
+    int mode;                    // VACV_LINEAR_* for kLinearFixed
+    int out;                     // OutKind
+    float scale_xf, scale_yf;    // (float)w_in / w_out (naive)
+    double scale_xd, scale_yd;   // (double)w_in / w_out (NEON, cubic)
+    int tile_w, tile_h, tiles_x, tiles_y;
+    int sparse;                  // 1: one LDS slot per (row, tap); 0: dense row window
+    int max_slots;               // LDS row slots per workgroup
+    int slot_stride;             // bytes per slot
+    int lds_bytes;               // dynamic LDS per workgroup
+    NormSpec norm;
+};
+
+hipError_t launch_resize(const ResizeLaunch& L, hipStream_t s);
+
+struct WarpLaunch {
+    PlaneGeom src;
+    PlaneGeom dst;
+    int n;
+    float inv[6];
+    float border[4];
+    int out;                     // OutKind
+    NormSpec norm;
+};
+hipError_t launch_warp(const WarpLaunch& L, hipStream_t s);
+
+struct CopyLaunch {                // crop / clone: row copies
+    PlaneGeom src;                 // base already offset to the crop origin
+    PlaneGeom dst;
+    int n;
+    int64_t row_bytes;
+};
+hipError_t launch_row_copy(const CopyLaunch& L, hipStream_t s);
+
+struct LayoutLaunch {
+    const unsigned char* src;
+    unsigned char* dst;
+    int n, w, h, c, esize;
+    int to_chw;                    // 1: NHWC -> NCHW, 0: NCHW -> NHWC
+    int64_t src_img, dst_img;      // dense per-image bytes
+};
+hipError_t launch_layout(const LayoutLaunch& L, hipStream_t s);
+
+struct DtypeLaunch {
+    const unsigned char* src;
+    unsigned char* dst;
+    int64_t count;                 // elements (dense)
+    int to_f32;                    // 1: u8 -> f32, 0: f32 -> u8
+};
+hipError_t launch_dtype(const DtypeLaunch& L, hipStream_t s);
+
+struct ColorLaunch {
+    const unsigned char* src;      // Y plane of image 0
+    int64_t src_img, src_row;      // bytes
+    unsigned char* dst;
+    int64_t dst_img, dst_row;
+    int n, w, h;                   // BGR size
+    int v_first;                   // NV21
+    int rgb;                       // swap output order
+    int out;                       // kOutSame (u8) / kOutF32 / kOutNorm
+    NormSpec norm;
+};
+hipError_t launch_color(const ColorLaunch& L, hipStream_t s);
+
+struct NormLaunch {                // elementwise normalize
+    PlaneGeom src;
+    PlaneGeom dst;
+    int n;
+    int src_u8;
+    NormSpec norm;
+};
+hipError_t launch_normalize(const NormLaunch& L, hipStream_t s);
+
+struct SumsLaunch {
+    PlaneGeom src;                 // whole images (NHWC: cc = c; NCHW: planes = c, cc = 1)
+    int n;
+    int c;
+    int src_u8;
+    int blocks_per_image;
+    double* partials;              // [n][blocks][c][2]
+    double* sums;                  // [groups][c][2]
+    int per_image;
+    int scalar_only;               // plane base not 16-byte aligned
+};
+hipError_t launch_channel_sums(const SumsLaunch& L, hipStream_t s);
+hipError_t launch_stats(const double* sums, int groups, int c, double count,
+                        float* mean, float* stddev, hipStream_t s);
+
+}  // namespace vacv

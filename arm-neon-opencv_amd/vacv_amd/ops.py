@@ -1,0 +1,300 @@
+"""Batched vacv operators on device tensors, through the C ABI.
+
+The names and argument meanings follow the reference's ``va_cv::`` API
+(/root/reference/src/cv/cv.h:85-209); every call goes straight to a HIP
+kernel in lib/libvacv_hip.so.  PyTorch is only the allocator and the stream
+provider here: tensors must live on a HIP device, and nothing is computed on
+the CPU.
+
+Image tensors
+  NHWC: (n, h, w, c), (h, w, c) or (h, w)          -- the reference's default
+  NCHW: (n, c, h, w) or (c, h, w)                   -- pass layout=NCHW
+Rows may be pitched (e.g. a slice of a larger image) as long as each row's
+pixels are contiguous; the descriptor carries the byte pitches.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Optional, Sequence, Tuple
+
+import numpy as np
+import torch
+
+from . import _lib as L
+from ._lib import (BORDER_CONSTANT, FP16, FP32, FP64, INT8, INTER_CUBIC, INTER_LINEAR, LINEAR_REFERENCE, NCHW,
+                   NHWC, VacvImage, check)
+
+_DTYPES = {torch.uint8: INT8, torch.float32: FP32, torch.float16: FP16, torch.float64: FP64}
+_TORCH = {v: k for k, v in _DTYPES.items()}
+
+
+def _stream(stream=None) -> int:
+    if stream is None:
+        stream = torch.cuda.current_stream()
+    return int(stream.cuda_stream) if hasattr(stream, "cuda_stream") else int(stream)
+
+
+def _as4d(t: torch.Tensor, layout: int) -> torch.Tensor:
+    if t.dim() == 4:
+        return t
+    if t.dim() == 3:
+        return t.unsqueeze(0)
+    if t.dim() == 2:
+        return t.unsqueeze(0).unsqueeze(-1 if layout == NHWC else 1)
+    raise ValueError(f"expected a 2-4 dimensional image tensor, got shape {tuple(t.shape)}")
+
+
+def describe(t: torch.Tensor, layout: int = NHWC) -> VacvImage:
+    """vacv_image descriptor of a device tensor (no copy)."""
+    if not t.is_cuda:
+        raise ValueError("vacv operators take device tensors (the C++ API stages host images)")
+    if t.dtype not in _DTYPES:
+        raise TypeError(f"unsupported dtype {t.dtype}")
+    t4 = _as4d(t, layout)
+    es = t4.element_size()
+    st = t4.stride()
+    if layout == NHWC:
+        n, h, w, c = t4.shape
+        if st[3] != 1 or (st[2] != c and w > 1):
+            raise ValueError("NHWC rows must be contiguous (pixel stride == c)")
+        row, plane, batch = st[1] * es, 0, st[0] * es
+    else:
+        n, c, h, w = t4.shape
+        if st[3] != 1:
+            raise ValueError("NCHW rows must be contiguous")
+        row, plane, batch = st[2] * es, st[1] * es, st[0] * es
+    return VacvImage(t4.data_ptr(), n, w, h, c, _DTYPES[t.dtype], layout, row, plane, batch)
+
+
+def _empty_like_shape(src4: torch.Tensor, layout: int, w: int, h: int, dtype, squeeze: bool, src_dim: int,
+                      c: Optional[int] = None):
+    n = src4.shape[0]
+    c = c if c is not None else (src4.shape[3] if layout == NHWC else src4.shape[1])
+    shape = (n, h, w, c) if layout == NHWC else (n, c, h, w)
+    out = torch.empty(shape, dtype=dtype, device=src4.device)
+    return out
+
+
+def _shape_back(out4: torch.Tensor, src: torch.Tensor, layout: int) -> torch.Tensor:
+    if src.dim() == 4:
+        return out4
+    if src.dim() == 3:
+        return out4[0]
+    return out4[0, ..., 0] if layout == NHWC else out4[0, 0]
+
+
+def _fptr(a) -> Tuple[object, ctypes.POINTER(ctypes.c_float)]:
+    arr = np.ascontiguousarray(np.asarray(a, dtype=np.float32).reshape(-1))
+    return arr, arr.ctypes.data_as(ctypes.POINTER(ctypes.c_float))
+
+
+def _dptr(a) -> Tuple[object, ctypes.POINTER(ctypes.c_double)]:
+    arr = np.ascontiguousarray(np.asarray(a, dtype=np.float64).reshape(-1))
+    return arr, arr.ctypes.data_as(ctypes.POINTER(ctypes.c_double))
+
+
+def _meanstd(mean, std, c):
+    if mean is None and std is None:
+        return (None, None), (None, None)
+    if mean is None or std is None:
+        raise ValueError("give both mean and stddev, or neither (per-image statistics)")
+    m, s = _fptr(mean), _fptr(std)
+    if m[0].size != c or s[0].size != c:
+        raise ValueError(f"mean/stddev need {c} values")
+    return m, s
+
+
+# ---------------------------------------------------------------------------
+# geometry / dtype
+
+def crop(src: torch.Tensor, rect: Sequence[float], layout: int = NHWC, out=None, stream=None) -> torch.Tensor:
+    """va_cv::crop (cv.h:209): rect = (left, top, right, bottom), truncated
+    to int exactly as crop_naive does (crop.cpp:128-131)."""
+    left, top = int(rect[0]), int(rect[1])
+    cw, ch = int(np.float32(rect[2]) - np.float32(rect[0])), int(np.float32(rect[3]) - np.float32(rect[1]))
+    s4 = _as4d(src, layout)
+    if out is None:
+        out = _empty_like_shape(s4, layout, cw, ch, src.dtype, True, src.dim())
+    o4 = _as4d(out, layout)
+    check("vacv_crop", L.load().vacv_crop(ctypes.byref(describe(s4, layout)), ctypes.byref(describe(o4, layout)),
+                                          left, top, _stream(stream)))
+    return _shape_back(o4, src, layout)
+
+
+def change_layout(src: torch.Tensor, to_layout: int, layout: int = NHWC, stream=None) -> torch.Tensor:
+    """Tensor::change_layout (tensor.cpp:393-457)."""
+    s4 = _as4d(src, layout)
+    if layout == NHWC:
+        n, h, w, c = s4.shape
+    else:
+        n, c, h, w = s4.shape
+    out = torch.empty((n, h, w, c) if to_layout == NHWC else (n, c, h, w), dtype=src.dtype, device=src.device)
+    check("vacv_change_layout", L.load().vacv_change_layout(ctypes.byref(describe(s4, layout)),
+                                                            ctypes.byref(describe(out, to_layout)), _stream(stream)))
+    return out
+
+
+def change_dtype(src: torch.Tensor, dtype: torch.dtype, layout: int = NHWC, stream=None) -> torch.Tensor:
+    """Tensor::change_dtype (tensor.cpp:459-502): u8<->fp32."""
+    s4 = _as4d(src, layout)
+    out = torch.empty(s4.shape, dtype=dtype, device=src.device)
+    check("vacv_change_dtype", L.load().vacv_change_dtype(ctypes.byref(describe(s4, layout)),
+                                                          ctypes.byref(describe(out, layout)), _stream(stream)))
+    return _shape_back(out, src, layout)
+
+
+def resize(src: torch.Tensor, w: int, h: int, interpolation: int = INTER_LINEAR, mode: int = LINEAR_REFERENCE,
+           layout: int = NHWC, out=None, stream=None) -> torch.Tensor:
+    """va_cv::resize (cv.h:85-87).  INTER_CUBIC on u8 input returns fp32."""
+    s4 = _as4d(src, layout)
+    dt = torch.float32 if (interpolation == INTER_CUBIC) else src.dtype
+    if out is None:
+        out = _empty_like_shape(s4, layout, w, h, dt, True, src.dim())
+    check("vacv_resize", L.load().vacv_resize(ctypes.byref(describe(s4, layout)), ctypes.byref(describe(out, layout)),
+                                              interpolation, mode, _stream(stream)))
+    return _shape_back(out, src, layout)
+
+
+def resize_normalize(src: torch.Tensor, w: int, h: int, mean=None, std=None, interpolation: int = INTER_LINEAR,
+                     mode: int = LINEAR_REFERENCE, layout: int = NHWC, out=None, stream=None) -> torch.Tensor:
+    """va_cv::resize_normalize (cv.h:154-158): resize, fp32, normalize."""
+    s4 = _as4d(src, layout)
+    c = s4.shape[3] if layout == NHWC else s4.shape[1]
+    if out is None:
+        out = _empty_like_shape(s4, layout, w, h, torch.float32, True, src.dim())
+    (ma, mp), (sa, sp) = _meanstd(mean, std, c)
+    check("vacv_resize_normalize",
+          L.load().vacv_resize_normalize(ctypes.byref(describe(s4, layout)), ctypes.byref(describe(out, layout)),
+                                         interpolation, mode, mp, sp, _stream(stream)))
+    return _shape_back(out, src, layout)
+
+
+def rotation_matrix(scale: float, rot: float, aux: Sequence[float] = (0, 0, 0, 0)) -> np.ndarray:
+    """get_rotation_matrix_2D + aux fix (warp_affine.cpp:76-109), host."""
+    m = np.zeros(6, np.float32)
+    a, ap = _dptr(aux)
+    check("vacv_rotation_matrix", L.load().vacv_rotation_matrix(scale, rot, ap,
+                                                                m.ctypes.data_as(ctypes.POINTER(ctypes.c_float))))
+    return m
+
+
+def invert_affine(m) -> np.ndarray:
+    mm, mp = _fptr(m)
+    inv = np.zeros(6, np.float32)
+    check("vacv_invert_affine", L.load().vacv_invert_affine(mp, inv.ctypes.data_as(ctypes.POINTER(ctypes.c_float))))
+    return inv
+
+
+def warp_affine(src: torch.Tensor, m, w: int, h: int, flags: int = INTER_LINEAR, border_mode: int = BORDER_CONSTANT,
+                border_value=(0, 0, 0, 0), layout: int = NHWC, out=None, stream=None) -> torch.Tensor:
+    """va_cv::warp_affine (cv.h:118-122); m is the forward 2x3 map."""
+    s4 = _as4d(src, layout)
+    if out is None:
+        out = _empty_like_shape(s4, layout, w, h, src.dtype, True, src.dim())
+    mm, mp = _fptr(m)
+    bv, bp = _dptr(border_value)
+    check("vacv_warp_affine", L.load().vacv_warp_affine(ctypes.byref(describe(s4, layout)),
+                                                        ctypes.byref(describe(out, layout)), mp, flags, border_mode,
+                                                        bp, _stream(stream)))
+    return _shape_back(out, src, layout)
+
+
+def warp_affine_rot(src: torch.Tensor, scale: float, rot: float, w: int, h: int, aux=(0, 0, 0, 0), **kw):
+    """va_cv::warp_affine(src, dst, scale, rot, dsize, aux, ...) (cv.h:136-141)."""
+    return warp_affine(src, rotation_matrix(scale, rot, aux), w, h, **kw)
+
+
+def warp_affine_normalize(src: torch.Tensor, m, w: int, h: int, mean=None, std=None, flags: int = INTER_LINEAR,
+                          border_mode: int = BORDER_CONSTANT, border_value=(0, 0, 0, 0), layout: int = NHWC,
+                          out=None, stream=None) -> torch.Tensor:
+    """va_cv::warp_affine_normalize (cv.h:172-201)."""
+    s4 = _as4d(src, layout)
+    c = s4.shape[3] if layout == NHWC else s4.shape[1]
+    if out is None:
+        out = _empty_like_shape(s4, layout, w, h, torch.float32, True, src.dim())
+    mm, mp = _fptr(m)
+    bv, bp = _dptr(border_value)
+    (ma, meanp), (sa, stdp) = _meanstd(mean, std, c)
+    check("vacv_warp_affine_normalize",
+          L.load().vacv_warp_affine_normalize(ctypes.byref(describe(s4, layout)), ctypes.byref(describe(out, layout)),
+                                              mp, flags, border_mode, bp, meanp, stdp, _stream(stream)))
+    return _shape_back(out, src, layout)
+
+
+# ---------------------------------------------------------------------------
+# colour
+
+def _yuv_desc(yuv: torch.Tensor) -> VacvImage:
+    y4 = yuv if yuv.dim() == 3 else yuv.unsqueeze(0)
+    return describe(y4.unsqueeze(-1), NHWC)
+
+
+def cvt_color(yuv: torch.Tensor, code: int = L.COLOR_YUV2BGR_NV21, stream=None) -> torch.Tensor:
+    """va_cv::cvt_color (cv.h:95): (n, h*3/2, w) u8 -> (n, h, w, 3) u8."""
+    y4 = yuv if yuv.dim() == 3 else yuv.unsqueeze(0)
+    n, hh, w = y4.shape
+    out = torch.empty((n, hh // 3 * 2, w, 3), dtype=torch.uint8, device=yuv.device)
+    check("vacv_cvt_color", L.load().vacv_cvt_color(ctypes.byref(_yuv_desc(y4)), ctypes.byref(describe(out, NHWC)),
+                                                    code, _stream(stream)))
+    return out if yuv.dim() == 3 else out[0]
+
+
+def cvt_color_normalize(yuv: torch.Tensor, code: int = L.COLOR_YUV2BGR_NV21, mean=None, std=None, out=None,
+                        stream=None) -> torch.Tensor:
+    y4 = yuv if yuv.dim() == 3 else yuv.unsqueeze(0)
+    n, hh, w = y4.shape
+    if out is None:
+        out = torch.empty((n, hh // 3 * 2, w, 3), dtype=torch.float32, device=yuv.device)
+    (ma, mp), (sa, sp) = _meanstd(mean, std, 3)
+    check("vacv_cvt_color_normalize",
+          L.load().vacv_cvt_color_normalize(ctypes.byref(_yuv_desc(y4)), ctypes.byref(describe(out, NHWC)), code, mp,
+                                            sp, _stream(stream)))
+    return out if yuv.dim() == 3 else out[0]
+
+
+# ---------------------------------------------------------------------------
+# normalize / statistics
+
+def normalize(src: torch.Tensor, mean=None, std=None, layout: int = NHWC, out=None, stream=None) -> torch.Tensor:
+    """va_cv::normalize (cv.h:104-106)."""
+    s4 = _as4d(src, layout)
+    c = s4.shape[3] if layout == NHWC else s4.shape[1]
+    if out is None:
+        out = torch.empty(s4.shape, dtype=torch.float32, device=src.device)
+    (ma, mp), (sa, sp) = _meanstd(mean, std, c)
+    check("vacv_normalize", L.load().vacv_normalize(ctypes.byref(describe(s4, layout)), ctypes.byref(describe(out, layout)),
+                                                    mp, sp, _stream(stream)))
+    return _shape_back(out, src, layout)
+
+
+def channel_sums(src: torch.Tensor, per_image: bool = True, layout: int = NHWC, stream=None) -> torch.Tensor:
+    """(groups, c, 2) fp64 device tensor of (Sum x, Sum x^2)."""
+    s4 = _as4d(src, layout)
+    n = s4.shape[0]
+    c = s4.shape[3] if layout == NHWC else s4.shape[1]
+    out = torch.empty((n if per_image else 1, c, 2), dtype=torch.float64, device=src.device)
+    check("vacv_channel_sums", L.load().vacv_channel_sums(ctypes.byref(describe(s4, layout)), out.data_ptr(),
+                                                          int(per_image), _stream(stream)))
+    return out
+
+
+def stats_from_sums(sums: torch.Tensor, count: float, stream=None) -> Tuple[torch.Tensor, torch.Tensor]:
+    sums = sums.contiguous()
+    groups, c = sums.shape[0], sums.shape[1]
+    mean = torch.empty((groups, c), dtype=torch.float32, device=sums.device)
+    std = torch.empty((groups, c), dtype=torch.float32, device=sums.device)
+    check("vacv_stats_from_sums", L.load().vacv_stats_from_sums(sums.data_ptr(), groups, c, float(count),
+                                                                mean.data_ptr(), std.data_ptr(), _stream(stream)))
+    return mean, std
+
+
+def mean_stddev(src: torch.Tensor, layout: int = NHWC, stream=None) -> Tuple[torch.Tensor, torch.Tensor]:
+    """Per-image (n, c) population mean / stddev (normalize_naive.cpp:7-72)."""
+    s4 = _as4d(src, layout)
+    n = s4.shape[0]
+    c = s4.shape[3] if layout == NHWC else s4.shape[1]
+    mean = torch.empty((n, c), dtype=torch.float32, device=src.device)
+    std = torch.empty((n, c), dtype=torch.float32, device=src.device)
+    check("vacv_mean_stddev", L.load().vacv_mean_stddev(ctypes.byref(describe(s4, layout)), mean.data_ptr(),
+                                                        std.data_ptr(), _stream(stream)))
+    return mean, std

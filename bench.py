@@ -1,0 +1,194 @@
+#!/usr/bin/env python3
+"""vacv MI355X benchmark -- the driver's contract (one JSON line on rank 0).
+
+Workload (BASELINE.json north_star target, configs[1] geometry): fused
+resize_normalize, 1920x1080x3 u8 NHWC -> 640x360x3 fp32, INTER_LINEAR with
+the reference's arithmetic, mean (103.94,116.78,123.68) / std
+(57.375,57.12,58.395), a batch of --batch images per GPU resident in HBM.
+One step = one vacv_resize_normalize call over the whole per-GPU batch (one
+kernel launch).  Metric = input-frame Mpixels/s over all GPUs ("at 1080p").
+
+Multi-GPU: torchrun one process per GPU; images are independent, so each rank
+owns its own batch (weak scaling) and there is no data-path collective.
+Timing: barrier + synchronize around exactly --steps steps, max over ranks.
+
+Also reported: the roofline of the kernel (algorithmic bytes per launch /
+average launch time from HIP events on the launch stream, vs 8 TB/s) and the
+reference's own CPU path (oracle/_ref, compiled from the reference sources;
+the C restatement when that is absent) timed on a bounded sample on rank 0.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+REPO = Path(__file__).resolve().parent
+sys.path.insert(0, str(REPO / "arm-neon-opencv_amd"))
+
+W_IN, H_IN, C = 1920, 1080, 3
+W_OUT, H_OUT = 640, 360
+MEAN = [103.94, 116.78, 123.68]
+STD = [57.375, 57.12, 58.395]
+PROFILES = REPO / "profiles"
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--batch", type=int, default=256, help="images per GPU")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget of the CPU baseline sample")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    return ap.parse_args()
+
+
+def ensure_built():
+    import vacv_amd
+    if not vacv_amd._lib.HIP_LIB.exists():
+        vacv_amd._lib.build()
+    vacv_amd._lib.load()
+
+
+def cpu_baseline(budget_s: float):
+    """The reference's own naive path on the host (bounded sample, 1 thread)."""
+    import numpy as np
+    sys.path.insert(0, str(REPO / "oracle"))
+    from oracle import Oracle, Reference, synthetic_image
+    mean = np.array(MEAN, np.float32)
+    std = np.array(STD, np.float32)
+    imgs = [synthetic_image(1000 + k, H_IN, W_IN, C) for k in range(4)]
+    if Reference.available():
+        R, kind = Reference(), "reference"
+
+        def one(img):
+            r = R.resize_linear(img, W_OUT, H_OUT)           # resize_naive.cpp:10-68
+            return R.normalize(r.astype(np.float32), mean, std)  # tensor.cpp:477-481 + normalize_naive.cpp:74-80
+    else:
+        O, kind = Oracle(), "port"
+
+        def one(img):
+            return O.normalize(O.u8_to_f32(O.resize_linear(img, W_OUT, H_OUT)), mean, std)
+    one(imgs[0])  # warm
+    n = 0
+    t0 = time.perf_counter()
+    while True:
+        one(imgs[n % len(imgs)])
+        n += 1
+        el = time.perf_counter() - t0
+        if (el >= budget_s and n >= 3) or n >= 100000:
+            break
+    return {"value": round(n * W_IN * H_IN / el / 1e6, 3), "unit": "Mpixels/s", "cores": 1, "kind": kind,
+            "sample": f"{n} synthetic 1920x1080x3 u8 frames, resize_naive 640x360 + u8->fp32 + normalize, "
+                      f"1 thread, {el:.1f} s"}
+
+
+def pmc_traffic():
+    """Corrected HBM bytes per launch from the committed rocprofv3 PMC passes
+    (profiles/pmc_resize_normalize.json, written by tools/pmc_summary.py)."""
+    p = PROFILES / "pmc_resize_normalize.json"
+    if not p.exists():
+        return None
+    try:
+        return json.loads(p.read_text()).get("hbm_bytes_per_launch")
+    except Exception:
+        return None
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local if world > 1 else 0)
+    torch.cuda.set_device(dev)
+
+    ensure_built()
+    from vacv_amd import ops
+    from vacv_amd.roofline import HBM_PEAK_GBS, resize_bytes
+
+    B = args.batch
+    g = torch.Generator(device=dev)
+    g.manual_seed(1234 + rank)
+    src = torch.randint(0, 256, (B, H_IN, W_IN, C), dtype=torch.uint8, device=dev, generator=g)
+    dst = torch.empty((B, H_OUT, W_OUT, C), dtype=torch.float32, device=dev)
+    stream = torch.cuda.current_stream(dev)
+
+    def step():
+        ops.resize_normalize(src, W_OUT, H_OUT, MEAN, STD, out=dst, stream=stream)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+
+    # per-launch HIP events on the launch stream (kernel duration)
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        ev[i][0].record(stream)
+        step()
+        ev[i][1].record(stream)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    kern_ms = sum(a.elapsed_time(b) for a, b in ev) / args.steps
+
+    t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed, kern_ms = float(t[0]), float(t[1])
+    ms_per_step = elapsed * 1e3 / args.steps
+
+    n_img = B * world
+    value = n_img * W_IN * H_IN / (ms_per_step / 1e3) / 1e6
+    b_alg = resize_bytes(W_IN, H_IN, C, W_OUT, H_OUT, 1, 4) * B  # per launch (one GPU's batch)
+    achieved = b_alg / (kern_ms / 1e3) / 1e9
+    traffic = pmc_traffic()
+
+    out = None
+    if rank == 0:
+        cpu = None if args.no_cpu_baseline else cpu_baseline(args.cpu_seconds)
+        out = {
+            "metric": "Mpixels/sec per op (resize/warp/normalize) at 1080p; achieved HBM GB/s vs peak",
+            "value": round(value, 2),
+            "unit": "Mpixels/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u8",
+            "data": "synthetic (torch.randint u8 frames resident in HBM)",
+            "config": {"workload": "resize_normalize INTER_LINEAR 1920x1080x3 u8 NHWC -> 640x360x3 fp32 "
+                                   "(reference arithmetic) + per-channel normalize",
+                       "global_batch": n_img, "batch_per_gpu": B, "parallelism": f"dp{world}",
+                       "frame": "1920x1080x3", "output": "640x360x3 fp32"},
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                         "kernel_ms": round(kern_ms, 4), "alg_bytes_per_launch": b_alg},
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

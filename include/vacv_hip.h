@@ -1,0 +1,197 @@
+/*
+ * vacv_hip.h -- C ABI of the MI355X-native vacv pixel operators.
+ *
+ * This is the drop-in boundary for the reference's operator API
+ * (/root/reference/src/cv/cv.h:85-209, vision::Tensor in
+ * src/common/tensor.h:27-84).  The C++ surface in
+ * arm-neon-opencv_amd/src/{common,cv,util} keeps the reference's names and
+ * signatures and is a thin wrapper over these entry points; any FFI
+ * (ctypes, cgo, JNI, N-API) binds this header directly.
+ *
+ * Conventions
+ *  - Every image pointer is DEVICE-accessible memory (hipMalloc, or mapped
+ *    hipHostMalloc).  Nothing here copies host<->device; the C++ wrapper
+ *    stages host tensors.
+ *  - Batched: an image descriptor covers `n` images, `batch_pitch` bytes
+ *    apart.  One call = one launch sequence on `stream` (a hipStream_t, or
+ *    NULL for the default stream).  Calls are asynchronous and never
+ *    synchronise the device; host-side arrays passed in (mean, stddev, M,
+ *    border values) are consumed before the call returns.
+ *  - Return value: VACV_OK (0) or a negative vacv_status.  No C++ exception
+ *    crosses this boundary.
+ *  - dtype / layout codes are the reference's vision::DType / DLayout values
+ *    (tensor.h:12-24); interpolation, border and colour codes are the
+ *    reference's va_cv enums (cv.h:27-74).
+ */
+#ifndef VACV_HIP_H
+#define VACV_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define VACV_ABI_VERSION 1
+#define VACV_MAX_CHANNELS 16
+
+typedef enum vacv_status {
+    VACV_OK = 0,
+    VACV_ERR_INVALID_ARG = -1,  /* bad pointer / size / pitch / rect */
+    VACV_ERR_UNSUPPORTED = -2,  /* dtype, layout, mode or code not implemented */
+    VACV_ERR_HIP = -3,          /* a HIP runtime call failed */
+    VACV_ERR_NO_MEMORY = -4     /* device workspace allocation failed */
+} vacv_status;
+
+/* vision::DType (tensor.h:12-18) */
+enum { VACV_FP32 = 0, VACV_FP16 = 1, VACV_INT8 = 2 /* unsigned bytes */, VACV_FP64 = 3 };
+/* vision::DLayout (tensor.h:21-24) */
+enum { VACV_NCHW = 0, VACV_NHWC = 1 };
+/* va_cv::VInterMode (cv.h:27-35) */
+enum { VACV_INTER_NEAREST = 0, VACV_INTER_LINEAR = 1, VACV_INTER_CUBIC = 2 };
+/* va_cv::VBorderMode (cv.h:38-48) */
+enum { VACV_BORDER_CONSTANT = 0, VACV_BORDER_REPLICATE = 1 };
+/* va_cv::InputImageFormat (cv.h:62-74) */
+enum {
+    VACV_COLOR_YUV2RGB_NV12 = 90, VACV_COLOR_YUV2BGR_NV12 = 91,
+    VACV_COLOR_YUV2RGB_NV21 = 92, VACV_COLOR_YUV2BGR_NV21 = 93
+};
+/* Arithmetic of the u8 bilinear sampler.
+ *  REFERENCE: the path the reference's public API actually dispatches to,
+ *             ResizeNaive::resize_naive_inter_linear_u8 (resize_naive.cpp:10-68).
+ *  NEON:      ResizeNeon (resize_neon.cpp:12-188), two-pass fixed point.
+ *  OPENCV:    NEON arithmetic with round-half-even coefficients (OpenCV 2.4's
+ *             saturate_cast<short>); SURVEY.md App. B. */
+enum { VACV_LINEAR_REFERENCE = 0, VACV_LINEAR_NEON = 1, VACV_LINEAR_OPENCV = 2 };
+
+/* A batch of images.  Pitches are in BYTES; 0 selects the dense value.
+ *   NHWC: pixel (x,y) channel k of image i at
+ *         data + i*batch_pitch + y*row_pitch + (x*c + k)*esize
+ *   NCHW: data + i*batch_pitch + k*plane_pitch + y*row_pitch + x*esize
+ * For the NV21/NV12 input of vacv_cvt_color the descriptor is the
+ * reference's (w, h*3/2, c=1) single-plane tensor (cvt_color.cpp:151-152). */
+typedef struct vacv_image {
+    void* data;
+    int32_t n;
+    int32_t w;
+    int32_t h;
+    int32_t c;
+    int32_t dtype;
+    int32_t layout;
+    int64_t row_pitch;
+    int64_t plane_pitch;
+    int64_t batch_pitch;
+} vacv_image;
+
+int vacv_abi_version(void);
+const char* vacv_status_string(int status);
+/* bytes of one image's valid data under the dense-pitch rules above */
+int64_t vacv_image_bytes(const vacv_image* img);
+
+/* ---- geometry / dtype ------------------------------------------------- */
+
+/* Crop::crop (crop.cpp:22-142, cv.h:209).  The rect is already truncated to
+ * int as crop_naive does (crop.cpp:128-131); dst->w/h are the crop size and
+ * dst->layout/dtype must equal src's.  Rect must lie inside src. */
+int vacv_crop(const vacv_image* src, const vacv_image* dst, int left, int top, void* stream);
+
+/* Tensor::change_layout (tensor.cpp:393-457): NHWC <-> NCHW of 1,2,4 or 8
+ * byte elements.  Same layout or c == 1 is a plain copy (clone()). */
+int vacv_change_layout(const vacv_image* src, const vacv_image* dst, void* stream);
+
+/* Tensor::change_dtype (tensor.cpp:459-502): INT8 -> FP32 exact; FP32 ->
+ * INT8 with the NEON f32_2_u8_neon semantics (truncate; NaN/negative -> 0;
+ * low 8 bits kept).  Same dtype is a copy; other pairs VACV_ERR_UNSUPPORTED
+ * (the reference silently returns an uninitialised tensor). */
+int vacv_change_dtype(const vacv_image* src, const vacv_image* dst, void* stream);
+
+/* Resize::resize (resize.cpp:19-100, cv.h:85-87).  Only dst->w/h select the
+ * output size (fx/fy are ignored, as in the reference).
+ *  INTER_LINEAR: INT8->INT8 (mode = VACV_LINEAR_*), FP32->FP32.
+ *  INTER_CUBIC:  FP32->FP32 and INT8->FP32 (the u8->fp32 conversion the
+ *                reference requires before cubic, fused).
+ * NHWC channels 1..4; NCHW any c (per plane, as resize.cpp:72-88). */
+int vacv_resize(const vacv_image* src, const vacv_image* dst, int interpolation, int mode, void* stream);
+
+/* WarpAffine::warp_affine (warp_affine.cpp:16-36, :111-169, cv.h:118-122).
+ * m = the FORWARD 2x3 map, row-major; it is inverted on the host with the
+ * reference's arithmetic and is NOT modified (the reference inverts the
+ * caller's M in place).  INTER_LINEAR + BORDER_CONSTANT only; pixels whose
+ * taps fall outside are written with border_value (the reference leaves
+ * them untouched).  border_value may be NULL (zeros). */
+int vacv_warp_affine(const vacv_image* src, const vacv_image* dst, const float m[6],
+                     int flags, int border_mode, const double border_value[4], void* stream);
+
+/* get_rotation_matrix_2D(VPoint(0,0), rot, scale) + the aux translation fix
+ * of the (scale, rot) overload (warp_affine.cpp:76-109).  Host only. */
+int vacv_rotation_matrix(float scale, float rot_deg, const double aux[4], float m_out[6]);
+/* The in-place inverse of warp_affine.cpp:121-133, out of place.  Host only. */
+int vacv_invert_affine(const float m[6], float inv_out[6]);
+
+/* ---- colour ----------------------------------------------------------- */
+
+/* CvtColor::cvt_color (cvt_color.cpp:20-157, cv.h:95): YUV420sp -> 3ch u8
+ * NHWC.  src = (w, h*3/2, 1) INT8; dst = (w, h, 3) INT8 NHWC.  Codes:
+ * COLOR_YUV2BGR_NV21 (bit-exact with nv_to_bgr_naive), COLOR_YUV2BGR_NV12
+ * (correct UV order; the reference decodes it as NV21), and the two RGB
+ * variants.  w and h must be even. */
+int vacv_cvt_color(const vacv_image* src, const vacv_image* dst, int code, void* stream);
+
+/* ---- normalize / statistics ------------------------------------------- */
+
+/* Normalize::normalize (normalize.cpp:84-121, cv.h:104-106):
+ *   dst = (float)(((float)x - mean[k]) / ((double)stddev[k] + 1e-6))
+ * src INT8 or FP32, dst FP32, same layout.  mean/stddev are HOST arrays of
+ * c floats; both NULL = per-image statistics first (exact, see
+ * vacv_mean_stddev).  Exactly one NULL is VACV_ERR_INVALID_ARG. */
+int vacv_normalize(const vacv_image* src, const vacv_image* dst,
+                   const float* mean, const float* stddev, void* stream);
+
+/* Per-channel sums for mean_stddev: sums[g*2c + 2k] = Sum x,
+ * sums[g*2c + 2k + 1] = Sum x^2 over channel k, g = image (per_image=1) or
+ * the whole batch (per_image=0, one group).  DEVICE output, fp64; exact for
+ * INT8 input (integer sums), deterministic order for FP32.  These are the
+ * partials the multi-GPU path all-reduces over RCCL. */
+int vacv_channel_sums(const vacv_image* src, double* sums, int per_image, void* stream);
+
+/* mean = S1/count, stddev = sqrt(max(S2/count - mean^2, 0)) per group and
+ * channel, on the device: sums[groups][c][2] -> mean/stddev[groups][c]. */
+int vacv_stats_from_sums(const double* sums, int groups, int c, double count,
+                         float* mean, float* stddev, void* stream);
+
+/* NormalizeNaive::mean_stddev_naive_* (normalize_naive.cpp:7-72): per-image
+ * population mean/stddev, DEVICE outputs [n][c].  Computed exactly (the
+ * reference accumulates sequentially in fp32; DESIGN.md quantifies it). */
+int vacv_mean_stddev(const vacv_image* src, float* mean, float* stddev, void* stream);
+
+/* ---- fused pipelines -------------------------------------------------- */
+
+/* ResizeNormalize::resize_normalize (resize_normalize.cpp:15-107, cv.h:154):
+ * resize, convert to fp32, normalize -- one pass, dst FP32.  Identical to
+ * vacv_resize followed by vacv_normalize (u8 resize results are normalized
+ * exactly as the reference normalizes a converted u8 tensor).  NULL mean and
+ * stddev: per-image statistics of the resized image. */
+int vacv_resize_normalize(const vacv_image* src, const vacv_image* dst, int interpolation, int mode,
+                          const float* mean, const float* stddev, void* stream);
+
+/* WarpAffineNormalize::warp_affine_normalize (warp_affine_normalize.cpp,
+ * cv.h:172-201): warp then normalize, dst FP32. */
+int vacv_warp_affine_normalize(const vacv_image* src, const vacv_image* dst, const float m[6],
+                               int flags, int border_mode, const double border_value[4],
+                               const float* mean, const float* stddev, void* stream);
+
+/* cvt_color then normalize (the cfg3 pipeline), dst (w,h,3) FP32 NHWC. */
+int vacv_cvt_color_normalize(const vacv_image* src, const vacv_image* dst, int code,
+                             const float* mean, const float* stddev, void* stream);
+
+/* ---- runtime ---------------------------------------------------------- */
+
+/* Block until all work this library queued on `stream` has finished. */
+int vacv_stream_synchronize(void* stream);
+/* Release the per-device workspace the statistics paths cache. */
+int vacv_release_workspace(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* VACV_HIP_H */

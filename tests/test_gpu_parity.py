@@ -1,0 +1,353 @@
+"""GPU parity: every operator through the C ABI against the oracle.
+
+Bar (DESIGN.md "Parity"): integer / byte / index outputs are bit-exact;
+fp32 outputs are value-exact (the kernels perform the reference's IEEE
+operations in the reference's order; the only permitted difference is the
+sign of an exact zero where a zero-weight tap row is skipped instead of
+multiplied by 0).  Statistics are compared with the tolerances written next
+to each assert.
+"""
+from __future__ import annotations
+
+import hashlib
+
+import numpy as np
+import pytest
+
+from conftest import load_bgr
+from oracle import synthetic_image
+
+pytestmark = pytest.mark.gpu
+
+MEAN = np.array([103.94, 116.78, 123.68], np.float32)
+STD = np.array([57.375, 57.12, 58.395], np.float32)
+
+
+def sha(a):
+    return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
+
+
+@pytest.fixture(scope="module")
+def ops(hip_device):
+    from vacv_amd import ops
+    return ops
+
+
+@pytest.fixture(scope="module")
+def dev(hip_device):
+    return hip_device
+
+
+def to_dev(a, dev):
+    import torch
+    return torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+
+
+def host(t):
+    import torch
+    torch.cuda.synchronize()
+    return t.cpu().numpy()
+
+
+def assert_same(got, want, what=""):
+    assert got.shape == want.shape, (what, got.shape, want.shape)
+    assert got.dtype == want.dtype, (what, got.dtype, want.dtype)
+    if got.dtype.kind == "f":
+        bad = ~((got == want) | (np.isnan(got) & np.isnan(want)))
+        assert not bad.any(), f"{what}: {bad.sum()} of {bad.size} differ, max |d| {np.nanmax(np.abs(got - want))}"
+    else:
+        bad = got != want
+        assert not bad.any(), f"{what}: {bad.sum()} of {bad.size} differ"
+
+
+def batch(images):
+    return np.stack(images)
+
+
+# ---------------------------------------------------------------------------
+# resize
+
+SIZES = [((23, 37), 1), ((48, 64), 3), ((61, 97), 3), ((5, 7), 3), ((16, 16), 4), ((144, 176), 3), ((2, 2), 1)]
+OUTS = [(20, 11), (33, 29), (111, 40), (7, 5), (2, 2), (160, 90), (1, 1), (300, 7)]
+
+
+@pytest.mark.parametrize("mode", [0, 1, 2])
+def test_resize_linear_u8_hwc(ops, dev, oracle, mode):
+    for i, ((h, w), c) in enumerate(SIZES):
+        imgs = [synthetic_image(100 * i + k, h, w, c) for k in range(3)]
+        src = to_dev(batch(imgs) if c > 1 else batch(imgs)[..., None], dev)
+        for wo, ho in OUTS:
+            out = host(ops.resize(src, wo, ho, mode=mode))
+            for k in range(3):
+                want = oracle.resize_linear(imgs[k], wo, ho, mode=mode)
+                got = out[k] if c > 1 else out[k, ..., 0]
+                assert_same(got, want, f"u8 mode{mode} {h}x{w}x{c}->{ho}x{wo}")
+
+
+def test_resize_linear_chw_and_fp32(ops, dev, oracle):
+    from vacv_amd import NCHW
+    rng = np.random.default_rng(7)
+    for i, ((h, w), c) in enumerate(SIZES):
+        img = synthetic_image(7 + i, h, w, c)
+        img = img if c > 1 else img[..., None]
+        chw = np.ascontiguousarray(img.transpose(2, 0, 1))
+        f = (img.astype(np.float32) + rng.standard_normal(img.shape).astype(np.float32)).astype(np.float32)
+        for wo, ho in OUTS:
+            out = host(ops.resize(to_dev(chw[None], dev), wo, ho, layout=NCHW))[0]
+            for k in range(c):
+                assert_same(out[k], oracle.resize_linear(chw[k], wo, ho), f"chw {h}x{w} k{k}")
+            outf = host(ops.resize(to_dev(f[None], dev), wo, ho))[0]
+            wantf = oracle.resize_linear(f if c > 1 else f[..., 0], wo, ho)
+            assert_same(outf if c > 1 else outf[..., 0], wantf, f"f32 {h}x{w}x{c}->{ho}x{wo}")
+
+
+def test_resize_cubic(ops, dev, oracle):
+    from vacv_amd import INTER_CUBIC, NCHW
+    rng = np.random.default_rng(11)
+    for i, ((h, w), c) in enumerate(SIZES):
+        if h < 4 or w < 4:
+            continue
+        img = synthetic_image(50 + i, h, w, c)
+        img = img if c > 1 else img[..., None]
+        f = (img.astype(np.float32) * np.float32(0.5) + rng.standard_normal(img.shape).astype(np.float32) * 4).astype(np.float32)
+        for wo, ho in OUTS + [(224, 224)]:
+            got = host(ops.resize(to_dev(f[None], dev), wo, ho, interpolation=INTER_CUBIC))[0]
+            want = oracle.resize_cubic(f if c > 1 else f[..., 0], wo, ho)
+            assert_same(got if c > 1 else got[..., 0], want, f"cubic f32 {h}x{w}x{c}->{ho}x{wo}")
+            # u8 input: the u8 -> fp32 conversion the reference needs first, fused
+            got8 = host(ops.resize(to_dev(img[None], dev), wo, ho, interpolation=INTER_CUBIC))[0]
+            want8 = oracle.resize_cubic(oracle.u8_to_f32(img if c > 1 else img[..., 0]), wo, ho)
+            assert_same(got8 if c > 1 else got8[..., 0], want8, f"cubic u8 {h}x{w}x{c}->{ho}x{wo}")
+        chw = np.ascontiguousarray(f.transpose(2, 0, 1))
+        got = host(ops.resize(to_dev(chw[None], dev), 31, 17, interpolation=INTER_CUBIC, layout=NCHW))[0]
+        for k in range(c):
+            assert_same(got[k], oracle.resize_cubic(chw[k], 31, 17), "cubic chw")
+
+
+def test_resize_full_size_batch(ops, dev, oracle):
+    """BASELINE cfg2 at full size: 1920x1080 -> 640x360 / 1280x720, batch of 3,
+    plus a pitched source (a sub-window of a wider buffer)."""
+    imgs = [synthetic_image(2 + k, 1080, 1920, 3) for k in range(3)]
+    src = to_dev(batch(imgs), dev)
+    for wo, ho in [(640, 360), (1280, 720), (224, 224), (2560, 1440)]:
+        out = host(ops.resize(src, wo, ho))
+        for k in range(3):
+            assert_same(out[k], oracle.resize_linear(imgs[k], wo, ho), f"1080p->{wo}x{ho}")
+    wide = to_dev(synthetic_image(99, 200, 300, 3), dev)
+    view = wide[10:150, 20:220]  # pitched rows
+    got = host(ops.resize(view, 77, 55))
+    want = oracle.resize_linear(np.ascontiguousarray(synthetic_image(99, 200, 300, 3)[10:150, 20:220]), 77, 55)
+    assert_same(got, want, "pitched")
+
+
+def test_resize_normalize(ops, dev, oracle):
+    from vacv_amd import INTER_CUBIC
+    imgs = [synthetic_image(40 + k, 1080, 1920, 3) for k in range(2)]
+    src = to_dev(batch(imgs), dev)
+    out = host(ops.resize_normalize(src, 640, 360, MEAN, STD))
+    for k in range(2):
+        want = oracle.normalize(oracle.u8_to_f32(oracle.resize_linear(imgs[k], 640, 360)), MEAN, STD)
+        assert_same(out[k], want, "resize_normalize u8")
+    # fp32 input, cubic, odd sizes
+    f = oracle.u8_to_f32(synthetic_image(5, 61, 97, 3))
+    got = host(ops.resize_normalize(to_dev(f[None], dev), 45, 33, MEAN, STD, interpolation=INTER_CUBIC))[0]
+    assert_same(got, oracle.normalize(oracle.resize_cubic(f, 45, 33), MEAN, STD), "cubic normalize")
+    got = host(ops.resize_normalize(to_dev(f[None], dev), 45, 33, MEAN, STD))[0]
+    assert_same(got, oracle.normalize(oracle.resize_linear(f, 45, 33), MEAN, STD), "f32 linear normalize")
+    # auto statistics: exact per-image stats of the resized image
+    out = host(ops.resize_normalize(src, 640, 360))
+    for k in range(2):
+        r = oracle.resize_linear(imgs[k], 640, 360)
+        m, s = oracle.mean_stddev_exact(r)
+        assert_same(out[k], oracle.normalize(oracle.u8_to_f32(r), m, s), "resize_normalize auto")
+
+
+# ---------------------------------------------------------------------------
+# warp affine
+
+def test_warp_affine(ops, dev, oracle):
+    from vacv_amd import NCHW
+    mats = [np.array([0.5, 0.1, 3.0, -0.2, 0.7, 5.0], np.float32),
+            oracle.rotation_matrix(0.9, 15.0, [32, 24, 32, 24]),
+            oracle.rotation_matrix(1.3, -40.0, [10, 10, 20, 8]),
+            np.array([1.25, 0.0, -2.0, 0.0, 1.25, -2.0], np.float32),
+            np.array([1, 0, 0, 0, 1, 0], np.float32),
+            np.array([0, 0, 0, 0, 0, 0], np.float32)]
+    rng = np.random.default_rng(3)
+    for i, ((h, w), c) in enumerate(SIZES[:5]):
+        img = synthetic_image(70 + i, h, w, c)
+        img = img if c > 1 else img[..., None]
+        f = (img.astype(np.float32) + rng.standard_normal(img.shape).astype(np.float32)).astype(np.float32)
+        for m in mats:
+            for wo, ho in [(64, 48), (33, 17), (5, 3)]:
+                got = host(ops.warp_affine(to_dev(img[None], dev), m, wo, ho))[0]
+                want = oracle.warp_affine(img if c > 1 else img[..., 0], m, wo, ho)
+                assert_same(got if c > 1 else got[..., 0], want, f"warp u8 {h}x{w}x{c}")
+                gotf = host(ops.warp_affine(to_dev(f[None], dev), m, wo, ho))[0]
+                wantf = oracle.warp_affine(f if c > 1 else f[..., 0], m, wo, ho)
+                assert_same(gotf if c > 1 else gotf[..., 0], wantf, f"warp f32 {h}x{w}x{c}")
+        chw = np.ascontiguousarray(img.transpose(2, 0, 1))
+        got = host(ops.warp_affine(to_dev(chw[None], dev), mats[1], 40, 30, layout=NCHW))[0]
+        for k in range(c):
+            assert_same(got[k], oracle.warp_affine(chw[k], mats[1], 40, 30), "warp chw")
+
+
+def test_warp_affine_config_and_harness(ops, dev, oracle, golden):
+    meta, _ = golden
+    d = meta["digests"]
+    b720 = load_bgr("1280x720.jpg")
+    if sha(b720) != d["input_1280x720"]["sha256"]:
+        pytest.skip("PIL decodes differently here")
+    rot = ops.rotation_matrix(0.9, 15.0, (640, 360, 640, 360))
+    assert rot.tolist() == d["cfg4_rotation_matrix"]["m"]
+    imgs = np.stack([b720, synthetic_image(4, 720, 1280, 3)])
+    out = host(ops.warp_affine(to_dev(imgs, dev), rot, 1280, 720))
+    assert sha(out[0]) == d["cfg4_warp_1280x720_rot15_u8"]["sha256"]
+    assert_same(out[1], oracle.warp_affine(imgs[1], rot, 1280, 720), "cfg4 synthetic")
+    M = np.array([0.849158, 0.012257, -474.827, -0.01225, 0.849158, -379.18], np.float32)
+    assert sha(host(ops.warp_affine(to_dev(b720, dev), M, 240, 240))) == d["harness_warp_hwc_u8_240"]["sha256"]
+    rot2 = ops.rotation_matrix(1.073914, -3.314525, (738.518372, 537.672852, 204.766998, 73.329681))
+    g = load_bgr("1280x720_grey.jpg")
+    assert sha(host(ops.warp_affine(to_dev(g, dev), rot2, 140, 210))) == d["harness_rotation_u8_140x210"]["sha256"]
+    # normalize fused
+    got = host(ops.warp_affine_normalize(to_dev(imgs, dev), rot, 1280, 720, MEAN, STD))
+    want = oracle.normalize(oracle.u8_to_f32(oracle.warp_affine(imgs[1], rot, 1280, 720)), MEAN, STD)
+    assert_same(got[1], want, "warp_affine_normalize")
+
+
+# ---------------------------------------------------------------------------
+# colour
+
+@pytest.mark.parametrize("v_first,rgb", [(True, False), (False, False), (True, True), (False, True)])
+def test_cvt_color(ops, dev, oracle, v_first, rgb):
+    import vacv_amd as V
+    code = {(True, False): V.COLOR_YUV2BGR_NV21, (False, False): V.COLOR_YUV2BGR_NV12,
+            (True, True): V.COLOR_YUV2RGB_NV21, (False, True): V.COLOR_YUV2RGB_NV12}[(v_first, rgb)]
+    rng = np.random.default_rng(17)
+    for h, w in [(2, 2), (16, 24), (36, 50), (144, 176), (1080, 1920), (6, 10)]:
+        yuv = np.stack([rng.integers(0, 256, (h * 3 // 2, w), dtype=np.uint8) for _ in range(2)])
+        out = host(ops.cvt_color(to_dev(yuv, dev), code))
+        for k in range(2):
+            assert_same(out[k], oracle.yuv420sp_to_bgr(yuv[k], v_first=v_first, rgb=rgb), f"cvt {h}x{w}")
+        outn = host(ops.cvt_color_normalize(to_dev(yuv, dev), code, MEAN, STD))
+        for k in range(2):
+            want = oracle.normalize(oracle.u8_to_f32(oracle.yuv420sp_to_bgr(yuv[k], v_first=v_first, rgb=rgb)), MEAN, STD)
+            assert_same(outn[k], want, "cvt normalize")
+
+
+def test_cvt_color_pipeline_digests(ops, dev, oracle, golden):
+    meta, _ = golden
+    d = meta["digests"]
+    b = load_bgr("1920x1080.jpeg")
+    if sha(b) != d["input_1920x1080"]["sha256"]:
+        pytest.skip("PIL decodes differently here")
+    nv = oracle.bgr2nv21(b)
+    assert sha(nv) == d["cfg3_nv21_1080p"]["sha256"]
+    bgr = host(ops.cvt_color(to_dev(nv, dev)))
+    assert sha(bgr) == d["cfg3_nv21_to_bgr_1080p"]["sha256"]
+    out = host(ops.cvt_color_normalize(to_dev(nv, dev), mean=MEAN, std=STD))
+    assert sha(out) == d["cfg3_nv21_bgr_normalize_1080p"]["sha256"]
+
+
+# ---------------------------------------------------------------------------
+# normalize / stats
+
+def test_normalize_and_stats(ops, dev, oracle):
+    from vacv_amd import NCHW
+    rng = np.random.default_rng(23)
+    for (h, w), c in [((144, 176), 3), ((20, 30), 1), ((33, 17), 4), ((1080, 1920), 3)]:
+        img = synthetic_image(h + w, h, w, c)
+        img = img if c > 1 else img[..., None]
+        f = (img.astype(np.float32) * np.float32(0.9) + rng.standard_normal(img.shape).astype(np.float32)).astype(np.float32)
+        mean = np.arange(c, dtype=np.float32) * 7 + 50
+        std = np.arange(c, dtype=np.float32) * 3 + 40
+        got = host(ops.normalize(to_dev(f[None], dev), mean, std))[0]
+        assert_same(got, oracle.normalize(f, mean, std), "normalize f32")
+        got = host(ops.normalize(to_dev(img[None], dev), mean, std))[0]
+        assert_same(got, oracle.normalize(oracle.u8_to_f32(img), mean, std), "normalize u8")
+        # exact statistics: u8 sums are integers (bit-exact)
+        sums = host(ops.channel_sums(to_dev(img[None], dev)))[0].reshape(-1)
+        assert np.array_equal(sums, oracle.channel_sums(img)), "u8 channel sums exact"
+        m, s = ops.mean_stddev(to_dev(img[None], dev))
+        me, se = oracle.mean_stddev_exact(img)
+        assert_same(host(m)[0], me, "mean exact")
+        assert_same(host(s)[0], se, "std exact")
+        # fp32: fp64 sums in a different order -> tolerance vs exact double
+        mf, sf = ops.mean_stddev(to_dev(f[None], dev))
+        ref = f.reshape(-1, c).astype(np.float64)
+        assert np.allclose(host(mf)[0], ref.mean(0), rtol=0, atol=1e-3)          # |dmean| <= 1e-3
+        assert np.allclose(host(sf)[0], ref.std(0), rtol=1e-4, atol=0)           # |dstd|/std <= 1e-4
+        # reference fp32 sequential stats (normalize_naive.cpp:7-72) vs ours
+        rm, rs = oracle.mean_stddev_ref(f)
+        assert np.allclose(host(mf)[0], rm, rtol=0, atol=0.5)
+        assert np.allclose(host(sf)[0], rs, rtol=1e-2)
+        # auto normalize = normalize with our exact stats
+        got = host(ops.normalize(to_dev(img[None], dev)))[0]
+        assert_same(got, oracle.normalize(oracle.u8_to_f32(img), me, se), "normalize auto")
+        chw = np.ascontiguousarray(f.transpose(2, 0, 1))
+        got = host(ops.normalize(to_dev(chw[None], dev), mean, std, layout=NCHW))[0]
+        for k in range(c):
+            assert_same(got[k], oracle.normalize(chw[k], mean[k:k + 1], std[k:k + 1]), "normalize chw")
+        mc, sc = ops.mean_stddev(to_dev(chw[None], dev), layout=NCHW)
+        assert np.allclose(host(mc)[0], ref.mean(0), atol=1e-3)
+
+
+def test_batch_global_stats(ops, dev, oracle):
+    imgs = np.stack([synthetic_image(300 + k, 224, 224, 3) for k in range(5)])
+    sums = host(ops.channel_sums(to_dev(imgs, dev), per_image=False))[0].reshape(-1)
+    assert np.array_equal(sums, oracle.channel_sums(imgs.reshape(-1, 224, 3)))
+
+
+# ---------------------------------------------------------------------------
+# crop / layout / dtype
+
+def test_crop_layout_dtype(ops, dev, oracle):
+    import torch
+    from vacv_amd import NCHW, NHWC
+    for (h, w), c in [((360, 640), 3), ((37, 53), 1), ((21, 33), 4), ((144, 176), 3)]:
+        img = synthetic_image(h * w, h, w, c)
+        img = img if c > 1 else img[..., None]
+        src = to_dev(np.stack([img, img[::-1].copy()]), dev)
+        for rect in [(0, 0, w // 2, h // 2), (10.7, 20.2, w - 1.5, h - 3.9), (3, 1, 8, 6)]:
+            got = host(ops.crop(src, rect))
+            l, t = int(rect[0]), int(rect[1])
+            cw, chh = int(np.float32(rect[2]) - np.float32(rect[0])), int(np.float32(rect[3]) - np.float32(rect[1]))
+            assert_same(got[0], oracle.crop(img, l, t, cw, chh), f"crop {rect}")
+        chw = host(ops.change_layout(src, NCHW))
+        assert_same(chw[0], oracle.hwc_to_chw(img), "hwc->chw")
+        back = host(ops.change_layout(to_dev(chw, dev), NHWC, layout=NCHW))
+        assert_same(back[0], img, "chw->hwc")
+        got = host(ops.crop(to_dev(chw, dev), (2, 3, 9, 11), layout=NCHW))
+        assert_same(got[0], oracle.crop(chw[0], 2, 3, 7, 8, chw=True), "crop chw")
+        f = host(ops.change_dtype(src, torch.float32))
+        assert_same(f[0], oracle.u8_to_f32(img), "u8->f32")
+        ff = (np.random.default_rng(1).standard_normal(img.shape) * 200 + 100).astype(np.float32)
+        u = host(ops.change_dtype(to_dev(ff[None], dev), torch.uint8))
+        assert_same(u[0], oracle.f32_to_u8(ff), "f32->u8")
+    # fp32 / fp16 layout change
+    x = np.random.default_rng(2).standard_normal((2, 17, 19, 3)).astype(np.float32)
+    assert_same(host(ops.change_layout(to_dev(x, dev), NCHW)), x.transpose(0, 3, 1, 2), "f32 layout")
+    x16 = x.astype(np.float16)
+    assert_same(host(ops.change_layout(to_dev(x16, dev), NCHW)), x16.transpose(0, 3, 1, 2), "f16 layout")
+
+
+def test_error_statuses(ops, dev):
+    import torch
+    import vacv_amd as V
+    x = torch.zeros((1, 8, 8, 3), dtype=torch.uint8, device=dev)
+    with pytest.raises(V.VacvError) as e:
+        ops.crop(x, (4, 4, 12, 12))           # rect outside the image
+    assert e.value.status == V._lib.ERR_INVALID_ARG
+    with pytest.raises(V.VacvError) as e:
+        ops.resize(x, 4, 4, interpolation=V.INTER_NEAREST)
+    assert e.value.status == V._lib.ERR_UNSUPPORTED
+    with pytest.raises(V.VacvError) as e:
+        ops.warp_affine(x, np.eye(2, 3, dtype=np.float32), 8, 8, border_mode=V.BORDER_REPLICATE)
+    assert e.value.status == V._lib.ERR_UNSUPPORTED
+    with pytest.raises(V.VacvError):
+        ops.resize(x, 4, 4, interpolation=V.INTER_CUBIC, out=torch.zeros((1, 4, 4, 3), dtype=torch.uint8, device=dev))
+    with pytest.raises(ValueError):
+        ops.normalize(x.float(), mean=[1, 2, 3])
+    odd = torch.zeros((1, 9, 5), dtype=torch.uint8, device=dev)
+    with pytest.raises(V.VacvError):
+        ops.cvt_color(odd)
