@@ -5,18 +5,21 @@
 // (resize_naive.cpp:10-128), ResizeNeon (resize_neon.cpp:12-188), the cubic
 // pair (resize_naive.cpp:130-569), and the fused ResizeNormalize semantics
 // (resize_normalize.cpp:33-107 = resize, convertTo fp32, per-channel
-// (x-mean)/(std+1e-6)).
+// (x-mean)/(std+1e-6)).  The tap tables come from the host planner
+// (resize_plan.cpp), computed with the same arithmetic.
 //
-// One workgroup = one output tile (tile_w x tile_h pixels) of one plane.
-//   1. tap tables for the tile's columns go to LDS (the arithmetic is the
-//      reference's; see vacv_semantics.hpp), one entry per output column;
-//   2. every source row with a non-zero vertical weight is staged into LDS
-//      once, as the column span the tile needs, by 16-byte buffer loads
-//      (coalesced, bounds-safe past the end of the batch);
-//   3. each work item produces 4 consecutive output pixels x CC channels from
-//      LDS and writes them with 16-byte (fp32) / 4-byte (u8) stores.
-// Rows whose vertical weight is zero are never read from HBM: at an exact
-// 3x downscale only every third source row moves (B_alg).
+// Structure (HBM-bound gather; no MFMA):
+//   * a workgroup owns a strip: one plane, one tile column, a run of
+//     consecutive row tiles ("tasks");
+//   * per task the source rows with a non-zero vertical weight are staged
+//     into LDS as the column span the tile needs, by 16-byte buffer loads
+//     (bounds-safe past the end of the batch).  Task i+1's loads are issued
+//     into registers before task i is computed, so HBM latency hides under
+//     the compute of the previous tile (register-staged software pipeline);
+//   * every lane produces 4 consecutive output ELEMENTS, so each wave store
+//     is 64 contiguous 16-byte (fp32) or 4-byte (u8) chunks.
+// Rows whose vertical weight is zero are never read: at an exact 3x
+// downscale only every third source row moves (B_alg).
 #pragma clang fp contract(off)
 
 #include "vacv_device.hpp"
@@ -24,68 +27,23 @@
 namespace vacv {
 namespace {
 
-constexpr int kPx = 4;  // output pixels per work item
+constexpr int kElems = 4;      // output elements per work item
+constexpr int kMaxChunks = 8;  // 16-byte prefetch registers per thread (planner bound)
 
-struct TileCtx {
-    int x0, nx, y0, ny;
-    int col_first;      // first staged source column
-    int span_bytes;     // staged bytes per row
-    int cpr;            // 16-byte chunks per staged row
-    int lo;             // dense mode: first staged row
-    int nslots;
-};
-
-template <int KIND>
-__device__ __forceinline__ int tap_origin(const ResizeLaunch& L, int d, bool vertical) {
-    const int n_in = vertical ? L.src.h : L.src.w;
-    if (KIND == kLinearFixed) {
-        const int n_out = vertical ? L.dst.h : L.dst.w;
-        return fixed_tap(d, n_in, n_out, vertical ? L.scale_yf : L.scale_xf,
-                         vertical ? L.scale_yd : L.scale_xd, L.mode).i;
-    } else if (KIND == kLinearFloat) {
-        return float_tap(d, n_in, vertical ? L.scale_yf : L.scale_xf).i;
-    } else {
-        return cubic_tap(d, n_in, vertical ? L.scale_yd : L.scale_xd).i - 1;
+// 16 bytes at byte offset o (from the 16-aligned base) with a clean tail: a
+// raw-buffer load that straddles num_records returns all zeros, so the
+// chunk that crosses the end of a plane is assembled byte by byte.
+__device__ __forceinline__ uint4 load16_safe(const Rsrc& rs, uint32_t o, uint32_t limit) {
+    if (o + 16u <= limit) return load16(rs, o);
+    uint32_t w[4] = {0, 0, 0, 0};
+#pragma unroll
+    for (int b = 0; b < 16; ++b) {
+        if (o + b < limit) {
+            const uint32_t v = __builtin_amdgcn_raw_buffer_load_b8(rs.r, (int)(o + b), 0, 0);
+            w[b >> 2] |= (v & 0xFFu) << (8 * (b & 3));
+        }
     }
-}
-
-// Vertical taps of output row d: origin row, TAPS weights (as float for the
-// float kinds, as int for the fixed kind).
-template <int KIND>
-struct VTaps {
-    int row0;
-    int wi[2];
-    float wf[4];
-};
-
-template <int KIND>
-__device__ __forceinline__ VTaps<KIND> vtaps(const ResizeLaunch& L, int d) {
-    VTaps<KIND> v;
-    if (KIND == kLinearFixed) {
-        FixedTap t = fixed_tap(d, L.src.h, L.dst.h, L.scale_yf, L.scale_yd, L.mode);
-        v.row0 = t.i;
-        v.wi[0] = t.w0;
-        v.wi[1] = t.w1;
-    } else if (KIND == kLinearFloat) {
-        FloatTap t = float_tap(d, L.src.h, L.scale_yf);
-        v.row0 = t.i;
-        v.wf[0] = t.w0;
-        v.wf[1] = t.w1;
-    } else {
-        CubicTap t = cubic_tap(d, L.src.h, L.scale_yd);
-        v.row0 = t.i - 1;
-        v.wf[0] = t.c[0]; v.wf[1] = t.c[1]; v.wf[2] = t.c[2]; v.wf[3] = t.c[3];
-    }
-    return v;
-}
-
-// j may be a run-time value: select with constant indices so VTaps stays in
-// registers (a dynamic index would spill the arrays to scratch).
-template <int KIND>
-__device__ __forceinline__ bool vweight_nonzero(const VTaps<KIND>& v, int j) {
-    if (KIND == kLinearFixed) return (j == 0 ? v.wi[0] : v.wi[1]) != 0;
-    const float w = j == 0 ? v.wf[0] : (j == 1 ? v.wf[1] : (j == 2 ? v.wf[2] : v.wf[3]));
-    return w != 0.f;
+    return make_uint4(w[0], w[1], w[2], w[3]);
 }
 
 template <int KIND, int CC, typename TIn, int OUT>
@@ -94,235 +52,199 @@ resize_kernel(ResizeLaunch L) {
     constexpr int TAPS = (KIND == kCubic) ? 4 : 2;
     constexpr int ES = sizeof(TIn);
     constexpr bool kLut = (KIND == kLinearFixed) && (OUT == kOutNorm);
+    constexpr int XW = (KIND == kLinearFixed) ? 4 : (KIND == kLinearFloat ? 8 : 16);
     using TOut = typename std::conditional<(OUT == kOutSame), TIn, float>::type;
 
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
-
     const int tid = threadIdx.x;
-    const int tile = blockIdx.x;
-    const int pidx = blockIdx.y;                  // image * planes + plane
+
+    // ---- which strip ---------------------------------------------------------
+    const int strip = blockIdx.x % L.strips;
+    const int col = blockIdx.x / L.strips;
+    const int tx = col % L.tiles_x;
+    const int pidx = col / L.tiles_x;                 // image * planes + plane
     const int img = pidx / L.src.planes;
     const int plane = pidx - img * L.src.planes;
+    const int task0 = strip * L.tasks_per_strip;
+    const int task1 = min(L.tiles_y, task0 + L.tasks_per_strip);
+    if (task0 >= task1) return;
 
-    TileCtx T;
-    {
-        const int tx = tile % L.tiles_x, ty = tile / L.tiles_x;
-        T.x0 = tx * L.tile_w;
-        T.nx = min(L.tile_w, L.dst.w - T.x0);
-        T.y0 = ty * L.tile_h;
-        T.ny = min(L.tile_h, L.dst.h - T.y0);
-        T.col_first = tap_origin<KIND>(L, T.x0, false);
-        const int col_last = tap_origin<KIND>(L, T.x0 + T.nx - 1, false) + TAPS - 1;
-        T.span_bytes = (col_last - T.col_first + 1) * CC * ES;
-        T.cpr = (T.span_bytes + 15 + 15) >> 4;
-        if (L.sparse) {
-            T.lo = 0;
-            T.nslots = TAPS * T.ny;
-        } else {
-            T.lo = tap_origin<KIND>(L, T.y0, true);
-            T.nslots = tap_origin<KIND>(L, T.y0 + T.ny - 1, true) + TAPS - 1 - T.lo + 1;
-        }
-    }
+    const int x0 = tx * L.tile_w;
+    const int nx = min(L.tile_w, L.dst.w - x0);
+    const int cpr = L.plan.cpr[tx];
 
-    // ---- LDS carve-up ----------------------------------------------------
-    // xoff[tile_w] int | xw[tile_w][TAPS] (short pairs or floats) |
-    // cand_slot[64] int | slot_row[max_slots] int | slot_head[max_slots] int |
-    // lut[256*CC] float | rows[max_slots][slot_stride]
-    int* xoff = reinterpret_cast<int*>(lds);
+    // ---- LDS carve-up: xoff | xw | cand[64] | head[max_slots] | lut | rows ------
+    int* xoff_l = reinterpret_cast<int*>(lds);
     unsigned char* p = lds + ((L.tile_w * 4 + 15) & ~15);
-    unsigned char* xw = p;
-    const int xw_bytes = (KIND == kLinearFixed) ? L.tile_w * 4 : L.tile_w * TAPS * 4;
-    p += (xw_bytes + 15) & ~15;
-    int* cand_slot = reinterpret_cast<int*>(p);   // [64] + slot count at [64]
-    p += 80 * 4;
-    int* slot_row = reinterpret_cast<int*>(p);
-    p += ((L.max_slots * 4) + 15) & ~15;
-    int* slot_head = reinterpret_cast<int*>(p);
-    p += ((L.max_slots * 4) + 15) & ~15;
-    float* lut = reinterpret_cast<float*>(p);
-    if (kLut) p += 256 * CC * 4;
-    unsigned char* rows = p;
+    unsigned char* xw_l = p;
+    p += (L.tile_w * XW + 15) & ~15;
+    int* cand_l = reinterpret_cast<int*>(p);
+    p += 64 * 4;
+    int* head_l = reinterpret_cast<int*>(p);
+    p += (L.max_slots * 4 + 15) & ~15;
+    float* lut_l = reinterpret_cast<float*>(p);
+    if (kLut) p += L.norm.c_total * 256 * 4;
+    unsigned char* rows_l = p;
 
     const unsigned char* src_plane = L.src.base + (int64_t)img * L.src.img_pitch + (int64_t)plane * L.src.plane_pitch;
     const Rsrc rs = make_rsrc(src_plane, L.src.plane_bytes);
+    const uint32_t limit = (uint32_t)L.src.plane_bytes + rs.delta;
+    const uint32_t span_off = (uint32_t)(L.plan.col_first[tx] * CC * ES) + rs.delta;
+    const int64_t rp = L.src.row_pitch;
 
-    // ---- 1. column taps ----------------------------------------------------
-    for (int i = tid; i < T.nx; i += kBlock) {
-        const int d = T.x0 + i;
-        if (KIND == kLinearFixed) {
-            FixedTap t = fixed_tap(d, L.src.w, L.dst.w, L.scale_xf, L.scale_xd, L.mode);
-            xoff[i] = (t.i - T.col_first) * CC * ES;
-            reinterpret_cast<short2*>(xw)[i] = make_short2((short)t.w0, (short)t.w1);
-        } else if (KIND == kLinearFloat) {
-            FloatTap t = float_tap(d, L.src.w, L.scale_xf);
-            xoff[i] = (t.i - T.col_first) * CC * ES;
-            reinterpret_cast<float2*>(xw)[i] = make_float2(t.w0, t.w1);
-        } else {
-            CubicTap t = cubic_tap(d, L.src.w, L.scale_xd);
-            xoff[i] = (t.i - 1 - T.col_first) * CC * ES;
-            reinterpret_cast<float4*>(xw)[i] = make_float4(t.c[0], t.c[1], t.c[2], t.c[3]);
-        }
-    }
-    // ---- 2a. which source row lives in which slot --------------------------
-    // sparse: only (output row, tap) pairs with a non-zero vertical weight get
-    // a slot, compacted by one wave (tile_h * TAPS <= 64); dense: the window
-    // [lo, lo + nslots) of consecutive source rows.
-    const uint32_t span_off = (uint32_t)(T.col_first * CC * ES) + rs.delta;
-    if (L.sparse) {
-        if (tid < 64) {
-            const int t = tid / TAPS, j = tid - t * TAPS;
-            int row = -1;
-            if (t < T.ny) {
-                VTaps<KIND> v = vtaps<KIND>(L, T.y0 + t);
-                if (vweight_nonzero<KIND>(v, j)) row = v.row0 + j;
-            }
-            const uint64_t m = __ballot(row >= 0);
-            const int slot = __popcll(m & ((1ull << tid) - 1ull));
-            cand_slot[tid] = row >= 0 ? slot : -1;
-            if (tid == 0) cand_slot[64] = __popcll(m);
-            if (row >= 0) {
-                slot_row[slot] = row;
-                slot_head[slot] = (int)(((uint32_t)((int64_t)row * L.src.row_pitch) + span_off) & 15u);
+    // ---- prefetch a task's rows into registers ------------------------------
+    uint4 R[kMaxChunks];
+    auto prefetch = [&](int task) {
+        const int ns = L.plan.task_nslots[task];
+        const int total = ns * cpr;
+        const int* trow = L.plan.task_rows + (int64_t)task * L.max_slots;
+#pragma unroll
+        for (int m = 0; m < kMaxChunks; ++m) {
+            const int k = tid + m * kBlock;
+            if (k < total) {
+                const int s = k / cpr, c = k - s * cpr;
+                const uint32_t off = (uint32_t)((int64_t)trow[s] * rp) + span_off;
+                R[m] = load16_safe(rs, (off & ~15u) + 16u * c, limit);
             }
         }
-    } else {
-        for (int s = tid; s < T.nslots; s += kBlock) {
-            const int row = T.lo + s;
-            slot_row[s] = row;
-            slot_head[s] = (int)(((uint32_t)((int64_t)row * L.src.row_pitch) + span_off) & 15u);
-        }
+    };
+    prefetch(task0);
+
+    // ---- per-strip tables (overlap the first task's loads) ------------------
+    for (int i = tid; i < nx; i += kBlock) {
+        const int e = tx * L.tile_w + i;
+        xoff_l[i] = L.plan.xoff[e];
+        if (XW == 4) reinterpret_cast<uint32_t*>(xw_l)[i] = reinterpret_cast<const uint32_t*>(L.plan.xw)[e];
+        else if (XW == 8) reinterpret_cast<uint2*>(xw_l)[i] = reinterpret_cast<const uint2*>(L.plan.xw)[e];
+        else reinterpret_cast<uint4*>(xw_l)[i] = reinterpret_cast<const uint4*>(L.plan.xw)[e];
     }
     if (kLut) {
-        const int ch_base = (CC == 1) ? plane : 0;
-        for (int i = tid; i < 256 * CC; i += kBlock) {
-            const int k = i >> 8, v = i & 255;
-            float m, sd;
-            norm_params(L.norm, img, ch_base + k, m, sd);
-            lut[i] = normalize_value((float)v, m, sd);
-        }
-    }
-    __syncthreads();
-    if (L.sparse) T.nslots = cand_slot[64];
-
-    // ---- 2b. stage rows: 16-byte loads, all issued before the LDS writes ----
-    {
-        const int total = T.nslots * T.cpr;
-        constexpr int kBatch = 4;
-        for (int base = tid; base < total; base += kBlock * kBatch) {
-            uint4 v[kBatch];
-            int dsto[kBatch];
-#pragma unroll
-            for (int b = 0; b < kBatch; ++b) {
-                const int k = base + b * kBlock;
-                dsto[b] = -1;
-                if (k < total) {
-                    const int s = k / T.cpr, c = k - s * T.cpr;
-                    const int row = slot_row[s];
-                    if (row >= 0) {
-                        const uint32_t off = (uint32_t)((int64_t)row * L.src.row_pitch) + span_off;
-                        v[b] = load16(rs, (off & ~15u) + 16u * c);
-                        dsto[b] = s * L.slot_stride + 16 * c;
-                    }
-                }
+        for (int i = tid; i < L.norm.c_total * 256; i += kBlock) {
+            if (L.plan.lut) {
+                lut_l[i] = L.plan.lut[i];
+            } else {
+                float m, sd;
+                norm_params(L.norm, img, i >> 8, m, sd);
+                lut_l[i] = normalize_value((float)(i & 255), m, sd);
             }
-#pragma unroll
-            for (int b = 0; b < kBatch; ++b)
-                if (dsto[b] >= 0) *reinterpret_cast<uint4*>(rows + dsto[b]) = v[b];
         }
     }
-    __syncthreads();
-
-    // ---- 3. compute ---------------------------------------------------------
-    unsigned char* dst_plane = const_cast<unsigned char*>(L.dst.base) + (int64_t)img * L.dst.img_pitch +
-                               (int64_t)plane * L.dst.plane_pitch;
-    const int groups = (T.nx + kPx - 1) / kPx;
-    const int items = groups * T.ny;
-
     float nmean[CC], nstd[CC];
     if (OUT == kOutNorm && !kLut) {
 #pragma unroll
-        for (int k = 0; k < CC; ++k) norm_params(L.norm, img, (CC == 1 ? plane : k), nmean[k], nstd[k]);
+        for (int k = 0; k < CC; ++k) norm_params(L.norm, img, (CC == 1 ? plane % L.norm.c_total : k), nmean[k], nstd[k]);
     }
+    const int lut_base = (CC == 1) ? (plane % max(L.norm.c_total, 1)) * 256 : 0;
 
-    for (int it = tid; it < items; it += kBlock) {
-        const int t = it / groups;
-        const int g = it - t * groups;
-        const VTaps<KIND> v = vtaps<KIND>(L, T.y0 + t);
-        // LDS base of each vertical tap's row (or -1 when its weight is 0)
-        int rb[TAPS];
+    unsigned char* dst_plane = const_cast<unsigned char*>(L.dst.base) + (int64_t)img * L.dst.img_pitch +
+                               (int64_t)plane * L.dst.plane_pitch;
+    const int row_elems = nx * CC;
+    const int ipr = (row_elems + kElems - 1) / kElems;  // items per output row
+
+    for (int task = task0; task < task1; ++task) {
+        if (task != task0) __syncthreads();  // everyone is done reading the previous tile
+        // ---- registers -> LDS ------------------------------------------------
+        {
+            const int ns = L.plan.task_nslots[task];
+            const int total = ns * cpr;
 #pragma unroll
-        for (int j = 0; j < TAPS; ++j) {
-            const int s = L.sparse ? cand_slot[t * TAPS + j] : v.row0 + j - T.lo;
-            rb[j] = (s >= 0 && vweight_nonzero<KIND>(v, j)) ? s * L.slot_stride + slot_head[s] : -1;
+            for (int m = 0; m < kMaxChunks; ++m) {
+                const int k = tid + m * kBlock;
+                if (k < total) {
+                    const int s = k / cpr, c = k - s * cpr;
+                    *reinterpret_cast<uint4*>(rows_l + s * L.slot_stride + 16 * c) = R[m];
+                }
+            }
+            const int nc = L.tile_h * TAPS;
+            if (tid < nc) cand_l[tid] = L.plan.task_cand[(int64_t)task * nc + tid];
+            if (tid < ns) {
+                const int row = L.plan.task_rows[(int64_t)task * L.max_slots + tid];
+                head_l[tid] = (int)(((uint32_t)((int64_t)row * rp) + span_off) & 15u);
+            }
         }
+        __syncthreads();
+        if (task + 1 < task1) prefetch(task + 1);  // in flight during this tile's compute
 
-        TOut out[kPx * CC];
+        // ---- compute this tile ------------------------------------------------
+        const int y0 = task * L.tile_h;
+        const int ny = min(L.tile_h, L.dst.h - y0);
+        const int items = ny * ipr;
+        for (int it = tid; it < items; it += kBlock) {
+            const int t = it / ipr;
+            const int j = it - t * ipr;
+            const int dy = y0 + t;
+            int rb[TAPS];
 #pragma unroll
-        for (int q = 0; q < kPx; ++q) {
-            const int i = g * kPx + q;
-            const int ii = i < T.nx ? i : T.nx - 1;  // clamp; the store masks it
-            const int xo = xoff[ii];
+            for (int q = 0; q < TAPS; ++q) {
+                const int s = cand_l[t * TAPS + q];
+                rb[q] = s >= 0 ? s * L.slot_stride + head_l[s] : -1;
+            }
+            int wyi[2] = {0, 0};
+            float wyf[4] = {0.f, 0.f, 0.f, 0.f};
             if (KIND == kLinearFixed) {
-                const short2 w = reinterpret_cast<const short2*>(xw)[ii];
-                const int a0 = w.x, a1 = w.y;
+                const int2 w = reinterpret_cast<const int2*>(L.plan.yw)[dy];
+                wyi[0] = w.x; wyi[1] = w.y;
+            } else if (KIND == kLinearFloat) {
+                const float2 w = reinterpret_cast<const float2*>(L.plan.yw)[dy];
+                wyf[0] = w.x; wyf[1] = w.y;
+            } else {
+                const float4 w = reinterpret_cast<const float4*>(L.plan.yw)[dy];
+                wyf[0] = w.x; wyf[1] = w.y; wyf[2] = w.z; wyf[3] = w.w;
+            }
+
+            TOut out[kElems];
 #pragma unroll
-                for (int k = 0; k < CC; ++k) {
+            for (int q = 0; q < kElems; ++q) {
+                int e = j * kElems + q;
+                e = e < row_elems ? e : row_elems - 1;  // clamp; the store masks it
+                const int px = e / CC;
+                const int k = e - px * CC;
+                const int xo = xoff_l[px] + k * ES;
+                if (KIND == kLinearFixed) {
+                    const uint32_t wx = reinterpret_cast<const uint32_t*>(xw_l)[px];
+                    const int a0 = (int)(short)(wx & 0xFFFFu), a1 = (int)(short)(wx >> 16);
                     int t0l = 0, t0r = 0, t1l = 0, t1r = 0;
-                    if (rb[0] >= 0) {
-                        t0l = rows[rb[0] + xo + k];
-                        t0r = rows[rb[0] + xo + CC + k];
-                    }
-                    if (rb[1] >= 0) {
-                        t1l = rows[rb[1] + xo + k];
-                        t1r = rows[rb[1] + xo + CC + k];
-                    }
+                    if (rb[0] >= 0) { t0l = rows_l[rb[0] + xo]; t0r = rows_l[rb[0] + xo + CC]; }
+                    if (rb[1] >= 0) { t1l = rows_l[rb[1] + xo]; t1r = rows_l[rb[1] + xo + CC]; }
                     int val;
                     if (L.mode == VACV_LINEAR_REFERENCE) {
-                        // resize_naive.cpp:61-64
-                        val = (t0l * a0 * v.wi[0] + t1l * a0 * v.wi[1] + t0r * a1 * v.wi[0] + t1r * a1 * v.wi[1]) >> 22;
-                        val &= 0xFF;
+                        // resize_naive.cpp:61-64 (truncating >> 22, stored as a byte)
+                        val = ((t0l * a0 * wyi[0] + t1l * a0 * wyi[1] + t0r * a1 * wyi[0] + t1r * a1 * wyi[1]) >> 22) & 0xFF;
                     } else {
-                        // resize_neon.cpp:103,122-123 then :150-167
+                        // resize_neon.cpp:103,122-123 (int16 rows) then :150-167
                         const int h0 = (int)(short)((t0l * a0 + t0r * a1) >> 4);
                         const int h1 = (int)(short)((t1l * a0 + t1r * a1) >> 4);
-                        val = (((h0 * v.wi[0]) >> 16) + ((h1 * v.wi[1]) >> 16) + 2) >> 2;
-                        val = clamp_u8(val);
+                        val = clamp_u8((((h0 * wyi[0]) >> 16) + ((h1 * wyi[1]) >> 16) + 2) >> 2);
                     }
-                    if (OUT == kOutSame) out[q * CC + k] = (TOut)val;
-                    else if (OUT == kOutF32) out[q * CC + k] = (TOut)(float)val;
-                    else out[q * CC + k] = (TOut)lut[k * 256 + val];
-                }
-            } else if (KIND == kLinearFloat) {
-                const float2 w = reinterpret_cast<const float2*>(xw)[ii];
-#pragma unroll
-                for (int k = 0; k < CC; ++k) {
+                    if (OUT == kOutSame) out[q] = (TOut)val;
+                    else if (OUT == kOutF32) out[q] = (TOut)(float)val;
+                    else out[q] = (TOut)lut_l[lut_base + (CC == 1 ? 0 : k * 256) + val];
+                } else if (KIND == kLinearFloat) {
+                    const float2 wx = reinterpret_cast<const float2*>(xw_l)[px];
                     float t0l = 0.f, t0r = 0.f, t1l = 0.f, t1r = 0.f;
                     if (rb[0] >= 0) {
-                        t0l = *reinterpret_cast<const float*>(rows + rb[0] + xo + 4 * k);
-                        t0r = *reinterpret_cast<const float*>(rows + rb[0] + xo + 4 * (CC + k));
+                        t0l = *reinterpret_cast<const float*>(rows_l + rb[0] + xo);
+                        t0r = *reinterpret_cast<const float*>(rows_l + rb[0] + xo + 4 * CC);
                     }
                     if (rb[1] >= 0) {
-                        t1l = *reinterpret_cast<const float*>(rows + rb[1] + xo + 4 * k);
-                        t1r = *reinterpret_cast<const float*>(rows + rb[1] + xo + 4 * (CC + k));
+                        t1l = *reinterpret_cast<const float*>(rows_l + rb[1] + xo);
+                        t1r = *reinterpret_cast<const float*>(rows_l + rb[1] + xo + 4 * CC);
                     }
                     // resize_naive.cpp:121-124, summed left to right
-                    float val = t0l * w.x * v.wf[0];
-                    val += t1l * w.x * v.wf[1];
-                    val += t0r * w.y * v.wf[0];
-                    val += t1r * w.y * v.wf[1];
+                    float val = t0l * wx.x * wyf[0];
+                    val += t1l * wx.x * wyf[1];
+                    val += t0r * wx.y * wyf[0];
+                    val += t1r * wx.y * wyf[1];
                     if (OUT == kOutNorm) val = normalize_value(val, nmean[k], nstd[k]);
-                    out[q * CC + k] = (TOut)val;
-                }
-            } else {
-                const float4 a = reinterpret_cast<const float4*>(xw)[ii];
-#pragma unroll
-                for (int k = 0; k < CC; ++k) {
+                    out[q] = (TOut)val;
+                } else {
+                    const float4 a = reinterpret_cast<const float4*>(xw_l)[px];
                     float h[4];
 #pragma unroll
-                    for (int j = 0; j < 4; ++j) {
-                        h[j] = 0.f;
-                        if (rb[j] >= 0) {
-                            const unsigned char* sp = rows + rb[j] + xo + ES * k;
+                    for (int r = 0; r < 4; ++r) {
+                        h[r] = 0.f;
+                        if (rb[r] >= 0) {
+                            const unsigned char* sp = rows_l + rb[r] + xo;
                             float s0, s1, s2, s3;
                             if (ES == 1) {
                                 s0 = (float)sp[0]; s1 = (float)sp[CC]; s2 = (float)sp[2 * CC]; s3 = (float)sp[3 * CC];
@@ -333,43 +255,48 @@ resize_kernel(ResizeLaunch L) {
                                 s3 = *reinterpret_cast<const float*>(sp + 12 * CC);
                             }
                             // resize_naive.cpp:325-328
-                            h[j] = s0 * a.x + s1 * a.y + s2 * a.z + s3 * a.w;
+                            h[r] = s0 * a.x + s1 * a.y + s2 * a.z + s3 * a.w;
                         }
                     }
                     // resize_naive.cpp:349-351
-                    float val = h[0] * v.wf[0] + h[1] * v.wf[1] + h[2] * v.wf[2] + h[3] * v.wf[3];
+                    float val = h[0] * wyf[0] + h[1] * wyf[1] + h[2] * wyf[2] + h[3] * wyf[3];
                     if (OUT == kOutNorm) val = normalize_value(val, nmean[k], nstd[k]);
-                    out[q * CC + k] = (TOut)val;
+                    out[q] = (TOut)val;
                 }
             }
-        }
 
-        // ---- store ---------------------------------------------------------
-        const int x = T.x0 + g * kPx;
-        unsigned char* dp = dst_plane + (int64_t)(T.y0 + t) * L.dst.row_pitch + (int64_t)x * CC * sizeof(TOut);
-        const int valid = min(kPx, T.nx - g * kPx);
-        constexpr int kBytes = kPx * CC * (int)sizeof(TOut);
-        if (valid == kPx && (kBytes % 16 == 0) && ((reinterpret_cast<uintptr_t>(dp) & 15) == 0)) {
+            // ---- store 4 consecutive elements --------------------------------
+            unsigned char* dp = dst_plane + (int64_t)dy * L.dst.row_pitch +
+                                ((int64_t)x0 * CC + (int64_t)j * kElems) * (int64_t)sizeof(TOut);
+            const int valid = min(kElems, row_elems - j * kElems);
+            if (sizeof(TOut) == 4) {
+                if (valid == kElems && (reinterpret_cast<uintptr_t>(dp) & 15) == 0) {
+                    *reinterpret_cast<uint4*>(dp) = *reinterpret_cast<const uint4*>(out);
+                } else {
 #pragma unroll
-            for (int b = 0; b < kBytes / 16; ++b)
-                reinterpret_cast<uint4*>(dp)[b] = reinterpret_cast<const uint4*>(out)[b];
-        } else if (valid == kPx && (kBytes % 4 == 0) && ((reinterpret_cast<uintptr_t>(dp) & 3) == 0)) {
+                    for (int q = 0; q < kElems; ++q)
+                        if (q < valid) reinterpret_cast<TOut*>(dp)[q] = out[q];
+                }
+            } else {
+                if (valid == kElems && (reinterpret_cast<uintptr_t>(dp) & 3) == 0) {
+                    const uint32_t v = (uint32_t)(uint8_t)out[0] | ((uint32_t)(uint8_t)out[1] << 8) |
+                                       ((uint32_t)(uint8_t)out[2] << 16) | ((uint32_t)(uint8_t)out[3] << 24);
+                    *reinterpret_cast<uint32_t*>(dp) = v;
+                } else {
 #pragma unroll
-            for (int b = 0; b < kBytes / 4; ++b)
-                reinterpret_cast<uint32_t*>(dp)[b] = reinterpret_cast<const uint32_t*>(out)[b];
-        } else {
-            TOut* o = reinterpret_cast<TOut*>(dp);
-#pragma unroll
-            for (int e = 0; e < kPx * CC; ++e)
-                if (e < valid * CC) o[e] = out[e];
+                    for (int q = 0; q < kElems; ++q)
+                        if (q < valid) reinterpret_cast<TOut*>(dp)[q] = out[q];
+                }
+            }
         }
     }
 }
 
 template <int KIND, int CC, typename TIn, int OUT>
 hipError_t launch_one(const ResizeLaunch& L, hipStream_t s) {
-    dim3 grid(L.tiles_x * L.tiles_y, L.n * L.src.planes);
-    hipLaunchKernelGGL((resize_kernel<KIND, CC, TIn, OUT>), grid, dim3(kBlock), L.lds_bytes, s, L);
+    const int64_t blocks = (int64_t)L.n * L.src.planes * L.tiles_x * L.strips;
+    if (blocks > 0x7FFFFFFF) return hipErrorInvalidValue;
+    hipLaunchKernelGGL((resize_kernel<KIND, CC, TIn, OUT>), dim3((unsigned)blocks), dim3(kBlock), L.lds_bytes, s, L);
     return hipGetLastError();
 }
 

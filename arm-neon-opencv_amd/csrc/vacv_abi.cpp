@@ -212,97 +212,6 @@ int normalize_with(const Img& src, const Img& dst, const NormSpec& ns, hipStream
     return hip_status(launch_normalize(L, s));
 }
 
-// ---- resize planning ---------------------------------------------------------
-template <typename F>
-int max_over_tiles(int n_out, int tile, F&& f) {
-    int best = 0;
-    for (int t0 = 0; t0 < n_out; t0 += tile) best = std::max(best, f(t0, std::min(tile, n_out - t0)));
-    return best;
-}
-
-int origin(const ResizeLaunch& L, int d, bool vertical) {
-    const int n_in = vertical ? L.src.h : L.src.w;
-    if (L.kind == kLinearFixed) {
-        const int n_out = vertical ? L.dst.h : L.dst.w;
-        return fixed_tap(d, n_in, n_out, vertical ? L.scale_yf : L.scale_xf, vertical ? L.scale_yd : L.scale_xd,
-                         L.mode).i;
-    }
-    if (L.kind == kLinearFloat) return float_tap(d, n_in, vertical ? L.scale_yf : L.scale_xf).i;
-    return cubic_tap(d, n_in, vertical ? L.scale_yd : L.scale_xd).i - 1;
-}
-
-int nonzero_taps(const ResizeLaunch& L, int y0, int ny) {
-    int cnt = 0;
-    for (int t = 0; t < ny; ++t) {
-        const int d = y0 + t;
-        if (L.kind == kLinearFixed) {
-            FixedTap q = fixed_tap(d, L.src.h, L.dst.h, L.scale_yf, L.scale_yd, L.mode);
-            cnt += (q.w0 != 0) + (q.w1 != 0);
-        } else if (L.kind == kLinearFloat) {
-            FloatTap q = float_tap(d, L.src.h, L.scale_yf);
-            cnt += (q.w0 != 0.f) + (q.w1 != 0.f);
-        } else {
-            CubicTap q = cubic_tap(d, L.src.h, L.scale_yd);
-            for (int j = 0; j < 4; ++j) cnt += q.c[j] != 0.f;
-        }
-    }
-    return cnt;
-}
-
-constexpr int kLdsBudget = 48 * 1024;
-
-int plan_resize(ResizeLaunch& L) {
-    const int taps = L.kind == kCubic ? 4 : 2;
-    const int bp = L.src.cc * L.src.esize;
-    const int w_out = L.dst.w, h_out = L.dst.h;
-    const double sx = (double)L.src.w / w_out, sy = (double)L.src.h / h_out;
-    L.sparse = sy >= taps ? 1 : 0;
-
-    // tile width: whole output rows when the staged source row is small
-    int tile_w;
-    if ((int64_t)(L.src.w + taps) * bp <= 12288) {
-        tile_w = w_out;
-    } else {
-        int px = (int)(8192.0 / (sx * bp));
-        px = std::max(64, px / 64 * 64);
-        tile_w = std::min(px, w_out);
-    }
-    for (;;) {
-        const int groups = (tile_w + 3) / 4;
-        int tile_h = std::max(1, std::min((1024 + groups - 1) / groups, L.sparse ? 64 / taps : 32));
-        tile_h = std::min(tile_h, h_out);
-        for (;;) {
-            const int span = max_over_tiles(w_out, tile_w, [&](int x0, int nx) {
-                return (origin(L, x0 + nx - 1, false) + taps - 1 - origin(L, x0, false) + 1) * bp;
-            });
-            const int slot_stride = (span + 30) / 16 * 16;
-            const int slots = L.sparse ? max_over_tiles(h_out, tile_h, [&](int y0, int ny) { return nonzero_taps(L, y0, ny); })
-                                       : max_over_tiles(h_out, tile_h, [&](int y0, int ny) {
-                                             return origin(L, y0 + ny - 1, true) + taps - 1 - origin(L, y0, true) + 1;
-                                         });
-            const int xw_bytes = L.kind == kLinearFixed ? tile_w * 4 : tile_w * taps * 4;
-            const bool lut = L.kind == kLinearFixed && L.out == kOutNorm;
-            const int lds = (int)(align_up(tile_w * 4, 16) + align_up(xw_bytes, 16) + 80 * 4 +
-                                  2 * align_up(std::max(slots, 1) * 4, 16) + (lut ? 256 * L.src.cc * 4 : 0) +
-                                  (size_t)std::max(slots, 1) * slot_stride);
-            if (lds <= kLdsBudget || (tile_h == 1 && tile_w <= 64)) {
-                if (lds > 160 * 1024) return VACV_ERR_UNSUPPORTED;
-                L.tile_w = tile_w;
-                L.tile_h = tile_h;
-                L.tiles_x = (w_out + tile_w - 1) / tile_w;
-                L.tiles_y = (h_out + tile_h - 1) / tile_h;
-                L.max_slots = std::max(slots, 1);
-                L.slot_stride = slot_stride;
-                L.lds_bytes = lds;
-                return VACV_OK;
-            }
-            if (tile_h == 1) break;
-            tile_h = std::max(1, tile_h * 3 / 4);
-        }
-        tile_w = std::max(64, (tile_w / 2) / 64 * 64);
-    }
-}
-
 int resize_impl(const vacv_image* src_d, const vacv_image* dst_d, int interpolation, int mode, int out_kind,
                 const NormSpec* ns, hipStream_t s) {
     Img src, dst;
@@ -347,7 +256,7 @@ int resize_impl(const vacv_image* src_d, const vacv_image* dst_d, int interpolat
     L.scale_yf = (float)src.h / (float)dst.h;
     L.scale_xd = (double)src.w / (double)dst.w;
     L.scale_yd = (double)src.h / (double)dst.h;
-    if ((st = plan_resize(L))) return st;
+    if ((st = plan_resize(L, s))) return st;
     return hip_status(launch_resize(L, s));
 }
 
@@ -754,7 +663,8 @@ int vacv_release_workspace(void) {
         }
     }
     g_ws.clear();
-    return st;
+    const int pst = release_plans();
+    return st ? st : pst;
 }
 
 }  // extern "C"

@@ -48,6 +48,23 @@ enum OutKind : int {
     kOutNorm = 2,       // f32, normalised
 };
 
+// Exact tap tables of one resize geometry, built on the host with the
+// reference's arithmetic (vacv_semantics.hpp) and cached on the device (the
+// counterpart of the reference's xofs/ialpha/yofs/ibeta tables,
+// resize_neon.cpp:20-78).  All arrays live in one device allocation.
+struct ResizePlanDev {
+    const int* xoff;             // [tiles_x][tile_w] byte offset of the first tap in the staged span
+    const void* xw;              // [tiles_x][tile_w] short2 (fixed) | float2 | float4 (cubic)
+    const int* col_first;        // [tiles_x] first staged source column
+    const int* cpr;              // [tiles_x] 16-byte chunks per staged row
+    const int* yrow;             // [h_out] first vertical tap row
+    const void* yw;              // [h_out] int2 (fixed) | float2 | float4
+    const int* task_nslots;      // [tiles_y]
+    const int* task_rows;        // [tiles_y][max_slots] source row of each LDS slot
+    const int* task_cand;        // [tiles_y][tile_h*TAPS] slot of (row t, tap j) or -1 (zero weight)
+    const float* lut;            // [c_total][256] normalised u8 values (host-constant mean/std) or null
+};
+
 struct ResizeLaunch {
     PlaneGeom src;
     PlaneGeom dst;
@@ -58,12 +75,19 @@ struct ResizeLaunch {
     float scale_xf, scale_yf;    // (float)w_in / w_out (naive)
     double scale_xd, scale_yd;   // (double)w_in / w_out (NEON, cubic)
     int tile_w, tile_h, tiles_x, tiles_y;
-    int sparse;                  // 1: one LDS slot per (row, tap); 0: dense row window
+    int sparse;                  // 1: slots hold only non-zero-weight rows; 0: dense row window
     int max_slots;               // LDS row slots per workgroup
     int slot_stride;             // bytes per slot
     int lds_bytes;               // dynamic LDS per workgroup
+    int strips;                  // workgroups per (plane, tile column)
+    int tasks_per_strip;         // row tiles per workgroup (software-pipelined)
+    ResizePlanDev plan;
     NormSpec norm;
 };
+
+// Fills tiles, strips and the cached device plan of L (host).
+int plan_resize(ResizeLaunch& L, hipStream_t s);
+int release_plans();
 
 hipError_t launch_resize(const ResizeLaunch& L, hipStream_t s);
 

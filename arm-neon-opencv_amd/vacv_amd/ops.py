@@ -53,16 +53,18 @@ def describe(t: torch.Tensor, layout: int = NHWC) -> VacvImage:
     t4 = _as4d(t, layout)
     es = t4.element_size()
     st = t4.stride()
+    # strides of size-1 dimensions are meaningless (numpy/torch may report 0):
+    # pass 0 there and let the C side use the dense pitch
     if layout == NHWC:
         n, h, w, c = t4.shape
-        if st[3] != 1 or (st[2] != c and w > 1):
+        if (c > 1 and st[3] != 1) or (w > 1 and st[2] != c):
             raise ValueError("NHWC rows must be contiguous (pixel stride == c)")
-        row, plane, batch = st[1] * es, 0, st[0] * es
+        row, plane, batch = (st[1] * es if h > 1 else 0), 0, (st[0] * es if n > 1 else 0)
     else:
         n, c, h, w = t4.shape
-        if st[3] != 1:
+        if w > 1 and st[3] != 1:
             raise ValueError("NCHW rows must be contiguous")
-        row, plane, batch = st[2] * es, st[1] * es, st[0] * es
+        row, plane, batch = (st[2] * es if h > 1 else 0), (st[1] * es if c > 1 else 0), (st[0] * es if n > 1 else 0)
     return VacvImage(t4.data_ptr(), n, w, h, c, _DTYPES[t.dtype], layout, row, plane, batch)
 
 

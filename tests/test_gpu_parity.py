@@ -312,7 +312,8 @@ def test_crop_layout_dtype(ops, dev, oracle):
             got = host(ops.crop(src, rect))
             l, t = int(rect[0]), int(rect[1])
             cw, chh = int(np.float32(rect[2]) - np.float32(rect[0])), int(np.float32(rect[3]) - np.float32(rect[1]))
-            assert_same(got[0], oracle.crop(img, l, t, cw, chh), f"crop {rect}")
+            want = oracle.crop(img if c > 1 else img[..., 0], l, t, cw, chh)
+            assert_same(got[0] if c > 1 else got[0, ..., 0], want, f"crop {rect}")
         chw = host(ops.change_layout(src, NCHW))
         assert_same(chw[0], oracle.hwc_to_chw(img), "hwc->chw")
         back = host(ops.change_layout(to_dev(chw, dev), NHWC, layout=NCHW))
