@@ -73,13 +73,13 @@ resize_kernel(ResizeLaunch L) {
     const int nx = min(L.tile_w, L.dst.w - x0);
     const int cpr = L.plan.cpr[tx];
 
-    // ---- LDS carve-up: xoff | xw | cand[64] | head[max_slots] | lut | rows ------
+    // ---- LDS carve-up: xoff | xw | rowinfo[32][8] | head[max_slots] | lut | rows ------
     int* xoff_l = reinterpret_cast<int*>(lds);
     unsigned char* p = lds + ((L.tile_w * 4 + 15) & ~15);
     unsigned char* xw_l = p;
     p += (L.tile_w * XW + 15) & ~15;
-    int* cand_l = reinterpret_cast<int*>(p);
-    p += 64 * 4;
+    int* rowinfo_l = reinterpret_cast<int*>(p);   // [tile_h][8]
+    p += 32 * 8 * 4;
     int* head_l = reinterpret_cast<int*>(p);
     p += (L.max_slots * 4 + 15) & ~15;
     float* lut_l = reinterpret_cast<float*>(p);
@@ -93,19 +93,34 @@ resize_kernel(ResizeLaunch L) {
     const int64_t rp = L.src.row_pitch;
 
     // ---- prefetch a task's rows into registers ------------------------------
+    // (slot, chunk) of this thread's m-th chunk is fixed per strip
+    int ch_s[kMaxChunks], ch_c[kMaxChunks];
+#pragma unroll
+    for (int m = 0; m < kMaxChunks; ++m) {
+        const int k = tid + m * kBlock;
+        ch_s[m] = k / cpr;
+        ch_c[m] = k - ch_s[m] * cpr;
+    }
     uint4 R[kMaxChunks];
     auto prefetch = [&](int task) {
         const int ns = L.plan.task_nslots[task];
-        const int total = ns * cpr;
         const int* trow = L.plan.task_rows + (int64_t)task * L.max_slots;
+        uint32_t off[kMaxChunks];
+#pragma unroll
+        for (int m = 0; m < kMaxChunks; ++m)
+            off[m] = ch_s[m] < ns ? (((uint32_t)((int64_t)trow[ch_s[m]] * rp) + span_off) & ~15u) + 16u * ch_c[m] : 0u;
+        bool tail = false;
 #pragma unroll
         for (int m = 0; m < kMaxChunks; ++m) {
-            const int k = tid + m * kBlock;
-            if (k < total) {
-                const int s = k / cpr, c = k - s * cpr;
-                const uint32_t off = (uint32_t)((int64_t)trow[s] * rp) + span_off;
-                R[m] = load16_safe(rs, (off & ~15u) + 16u * c, limit);
+            if (ch_s[m] < ns) {
+                if (off[m] + 16u <= limit) R[m] = load16(rs, off[m]);
+                else tail = true;
             }
+        }
+        if (tail) {  // only the chunk that crosses the end of the plane
+#pragma unroll
+            for (int m = 0; m < kMaxChunks; ++m)
+                if (ch_s[m] < ns && off[m] + 16u > limit) R[m] = load16_safe(rs, off[m], limit);
         }
     };
     prefetch(task0);
@@ -143,54 +158,56 @@ resize_kernel(ResizeLaunch L) {
 
     for (int task = task0; task < task1; ++task) {
         if (task != task0) __syncthreads();  // everyone is done reading the previous tile
-        // ---- registers -> LDS ------------------------------------------------
+        // ---- registers -> LDS, per-row tap info ----------------------------
         {
             const int ns = L.plan.task_nslots[task];
-            const int total = ns * cpr;
 #pragma unroll
-            for (int m = 0; m < kMaxChunks; ++m) {
-                const int k = tid + m * kBlock;
-                if (k < total) {
-                    const int s = k / cpr, c = k - s * cpr;
-                    *reinterpret_cast<uint4*>(rows_l + s * L.slot_stride + 16 * c) = R[m];
-                }
-            }
-            const int nc = L.tile_h * TAPS;
-            if (tid < nc) cand_l[tid] = L.plan.task_cand[(int64_t)task * nc + tid];
+            for (int m = 0; m < kMaxChunks; ++m)
+                if (ch_s[m] < ns) *reinterpret_cast<uint4*>(rows_l + ch_s[m] * L.slot_stride + 16 * ch_c[m]) = R[m];
             if (tid < ns) {
                 const int row = L.plan.task_rows[(int64_t)task * L.max_slots + tid];
                 head_l[tid] = (int)(((uint32_t)((int64_t)row * rp) + span_off) & 15u);
             }
         }
         __syncthreads();
+        // rowinfo[t] = LDS byte offset of each vertical tap's row (-1: weight 0)
+        // followed by the TAPS weights
+        const int y0 = task * L.tile_h;
+        const int ny = min(L.tile_h, L.dst.h - y0);
+        if (tid < ny) {
+            const int nc = L.tile_h * TAPS;
+            int* ri = rowinfo_l + tid * 8;
+#pragma unroll
+            for (int q = 0; q < TAPS; ++q) {
+                const int sl = L.plan.task_cand[(int64_t)task * nc + tid * TAPS + q];
+                ri[q] = sl >= 0 ? sl * L.slot_stride + head_l[sl] : -1;
+            }
+            if (KIND == kLinearFixed) {
+                const int2 w = reinterpret_cast<const int2*>(L.plan.yw)[y0 + tid];
+                ri[4] = w.x; ri[5] = w.y;
+            } else if (KIND == kLinearFloat) {
+                const float2 w = reinterpret_cast<const float2*>(L.plan.yw)[y0 + tid];
+                ri[4] = __float_as_int(w.x); ri[5] = __float_as_int(w.y);
+            } else {
+                const float4 w = reinterpret_cast<const float4*>(L.plan.yw)[y0 + tid];
+                ri[4] = __float_as_int(w.x); ri[5] = __float_as_int(w.y);
+                ri[6] = __float_as_int(w.z); ri[7] = __float_as_int(w.w);
+            }
+        }
+        __syncthreads();
         if (task + 1 < task1) prefetch(task + 1);  // in flight during this tile's compute
 
         // ---- compute this tile ------------------------------------------------
-        const int y0 = task * L.tile_h;
-        const int ny = min(L.tile_h, L.dst.h - y0);
         const int items = ny * ipr;
+        int t = tid / ipr;
+        int j = tid - t * ipr;
         for (int it = tid; it < items; it += kBlock) {
-            const int t = it / ipr;
-            const int j = it - t * ipr;
             const int dy = y0 + t;
-            int rb[TAPS];
-#pragma unroll
-            for (int q = 0; q < TAPS; ++q) {
-                const int s = cand_l[t * TAPS + q];
-                rb[q] = s >= 0 ? s * L.slot_stride + head_l[s] : -1;
-            }
-            int wyi[2] = {0, 0};
-            float wyf[4] = {0.f, 0.f, 0.f, 0.f};
-            if (KIND == kLinearFixed) {
-                const int2 w = reinterpret_cast<const int2*>(L.plan.yw)[dy];
-                wyi[0] = w.x; wyi[1] = w.y;
-            } else if (KIND == kLinearFloat) {
-                const float2 w = reinterpret_cast<const float2*>(L.plan.yw)[dy];
-                wyf[0] = w.x; wyf[1] = w.y;
-            } else {
-                const float4 w = reinterpret_cast<const float4*>(L.plan.yw)[dy];
-                wyf[0] = w.x; wyf[1] = w.y; wyf[2] = w.z; wyf[3] = w.w;
-            }
+            const int4 ra = *reinterpret_cast<const int4*>(rowinfo_l + t * 8);
+            const int4 rw = *reinterpret_cast<const int4*>(rowinfo_l + t * 8 + 4);
+            int rb[4] = {ra.x, ra.y, ra.z, ra.w};
+            const int wyi[2] = {rw.x, rw.y};
+            const float wyf[4] = {__int_as_float(rw.x), __int_as_float(rw.y), __int_as_float(rw.z), __int_as_float(rw.w)};
 
             TOut out[kElems];
 #pragma unroll
@@ -288,6 +305,8 @@ resize_kernel(ResizeLaunch L) {
                         if (q < valid) reinterpret_cast<TOut*>(dp)[q] = out[q];
                 }
             }
+            j += kBlock;
+            while (j >= ipr) { j -= ipr; ++t; }
         }
     }
 }

@@ -113,7 +113,7 @@ bool evaluate(const ResizeLaunch& L, const std::vector<Taps>& xt, const std::vec
     g.max_slots = slots;
     const int xw = L.kind == kLinearFixed ? 4 : (L.kind == kLinearFloat ? 8 : 16);
     const bool lut = L.kind == kLinearFixed && L.out == kOutNorm;
-    g.lds = (int)(a16(tile_w * 4) + a16((size_t)tile_w * xw) + 64 * 4 + a16(slots * 4) +
+    g.lds = (int)(a16(tile_w * 4) + a16((size_t)tile_w * xw) + 32 * 8 * 4 + a16(slots * 4) +
                   (lut ? (size_t)L.norm.c_total * 256 * 4 : 0) + (size_t)slots * g.slot_stride);
     if (tile_h * taps > 64) return false;
     if ((int64_t)slots * g.max_cpr > (int64_t)kMaxChunksPerThread * kBlock) return false;

@@ -309,6 +309,8 @@ def test_crop_layout_dtype(ops, dev, oracle):
         img = img if c > 1 else img[..., None]
         src = to_dev(np.stack([img, img[::-1].copy()]), dev)
         for rect in [(0, 0, w // 2, h // 2), (10.7, 20.2, w - 1.5, h - 3.9), (3, 1, 8, 6)]:
+            if int(np.float32(rect[2]) - np.float32(rect[0])) < 1 or int(np.float32(rect[3]) - np.float32(rect[1])) < 1:
+                continue
             got = host(ops.crop(src, rect))
             l, t = int(rect[0]), int(rect[1])
             cw, chh = int(np.float32(rect[2]) - np.float32(rect[0])), int(np.float32(rect[3]) - np.float32(rect[1]))

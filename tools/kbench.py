@@ -1,0 +1,90 @@
+#!/usr/bin/env python3
+"""Kernel micro-bench for profiling (rocprofv3 wraps this; no CPU work).
+
+  python tools/kbench.py --op resize_normalize --iters 20
+Prints one JSON line per op: average launch time from HIP events and the
+algorithmic GB/s (vacv_amd.roofline)."""
+import argparse
+import json
+import sys
+from pathlib import Path
+
+REPO = Path(__file__).resolve().parent.parent
+sys.path.insert(0, str(REPO / "arm-neon-opencv_amd"))
+
+MEAN = [103.94, 116.78, 123.68]
+STD = [57.375, 57.12, 58.395]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--op", default="resize_normalize")
+    ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--batch", type=int, default=0)
+    a = ap.parse_args()
+    import torch
+    import vacv_amd
+    from vacv_amd import ops
+    from vacv_amd.roofline import resize_bytes
+    dev = torch.device("cuda:0")
+    g = torch.Generator(device=dev)
+    g.manual_seed(1)
+
+    def frames(n, h, w, c=3):
+        return torch.randint(0, 256, (n, h, w, c), dtype=torch.uint8, device=dev, generator=g)
+
+    cases = {}
+    if a.op in ("resize_normalize", "all"):
+        n = a.batch or 256
+        src = frames(n, 1080, 1920)
+        out = torch.empty((n, 360, 640, 3), dtype=torch.float32, device=dev)
+        cases["resize_normalize_1080p_640x360"] = (lambda: ops.resize_normalize(src, 640, 360, MEAN, STD, out=out),
+                                                   n * resize_bytes(1920, 1080, 3, 640, 360, 1, 4), n * 1920 * 1080)
+    if a.op in ("resize", "all"):
+        n = a.batch or 256
+        src = frames(n, 1080, 1920)
+        o1 = torch.empty((n, 360, 640, 3), dtype=torch.uint8, device=dev)
+        o2 = torch.empty((n, 720, 1280, 3), dtype=torch.uint8, device=dev)
+        cases["resize_1080p_640x360_u8"] = (lambda: ops.resize(src, 640, 360, out=o1),
+                                            n * resize_bytes(1920, 1080, 3, 640, 360, 1, 1), n * 1920 * 1080)
+        cases["resize_1080p_1280x720_u8"] = (lambda: ops.resize(src, 1280, 720, out=o2),
+                                             n * resize_bytes(1920, 1080, 3, 1280, 720, 1, 1), n * 1920 * 1080)
+    if a.op in ("warp", "all"):
+        n = a.batch or 128
+        src = frames(n, 720, 1280)
+        o = torch.empty_like(src)
+        m = ops.rotation_matrix(0.9, 15.0, (640, 360, 640, 360))
+        cases["warp_720p_rot15_u8"] = (lambda: ops.warp_affine(src, m, 1280, 720, out=o), n * 2 * 1280 * 720 * 3,
+                                       n * 1280 * 720)
+    if a.op in ("cvt", "all"):
+        n = a.batch or 256
+        yuv = torch.randint(0, 256, (n, 1620, 1920), dtype=torch.uint8, device=dev, generator=g)
+        o = torch.empty((n, 1080, 1920, 3), dtype=torch.float32, device=dev)
+        cases["nv21_bgr_normalize_1080p"] = (lambda: ops.cvt_color_normalize(yuv, mean=MEAN, std=STD, out=o),
+                                             n * (1920 * 1620 + 1920 * 1080 * 12), n * 1920 * 1080)
+    if a.op in ("cubic", "all"):
+        n = a.batch or 128
+        src = frames(n, 1440, 2560)
+        o = torch.empty((n, 224, 224, 3), dtype=torch.float32, device=dev)
+        cases["cubic_1440p_224_u8_f32"] = (lambda: ops.resize(src, 224, 224, interpolation=vacv_amd.INTER_CUBIC, out=o),
+                                           n * resize_bytes(2560, 1440, 3, 224, 224, 1, 4, cubic=True), n * 2560 * 1440)
+    for name, (fn, nbytes, px) in cases.items():
+        for _ in range(3):
+            fn()
+        torch.cuda.synchronize()
+        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(a.iters)]
+        s = torch.cuda.current_stream()
+        for e0, e1 in ev:
+            e0.record(s)
+            fn()
+            e1.record(s)
+        torch.cuda.synchronize()
+        ms = sorted(e0.elapsed_time(e1) for e0, e1 in ev)
+        med = ms[len(ms) // 2]
+        print(json.dumps({"case": name, "ms_median": round(med, 4), "ms_min": round(ms[0], 4),
+                          "alg_GBps": round(nbytes / med / 1e6, 1), "frac_8TBps": round(nbytes / med / 1e6 / 8000, 4),
+                          "Mpx_s": round(px / med / 1e3, 1)}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
