@@ -112,9 +112,8 @@ bool evaluate(const ResizeLaunch& L, const std::vector<Taps>& xt, const std::vec
     }
     g.max_slots = slots;
     const int xw = L.kind == kLinearFixed ? 4 : (L.kind == kLinearFloat ? 8 : 16);
-    const bool lut = L.kind == kLinearFixed && L.out == kOutNorm;
     g.lds = (int)(a16(tile_w * 4) + a16((size_t)tile_w * xw) + 32 * 8 * 4 + a16(slots * 4) +
-                  (lut ? (size_t)L.norm.c_total * 256 * 4 : 0) + (size_t)slots * g.slot_stride);
+                  (size_t)slots * g.slot_stride);
     if (tile_h * taps > 64) return false;
     if ((int64_t)slots * g.max_cpr > (int64_t)kMaxChunksPerThread * kBlock) return false;
     return g.lds <= kLdsBudget;
@@ -145,7 +144,7 @@ void put(std::string& k, const T& v) {
 
 int plan_resize(ResizeLaunch& L, hipStream_t stream) {
     const int taps = L.kind == kCubic ? 4 : 2;
-    const bool lut = L.kind == kLinearFixed && L.out == kOutNorm && L.norm.mode == 1;
+    const bool lut = false;  // kernels normalise arithmetically (NormSpec.inv / mul_ok)
 
     std::string key;
     int device = 0;
@@ -154,8 +153,7 @@ int plan_resize(ResizeLaunch& L, hipStream_t stream) {
     put(key, L.kind); put(key, L.mode); put(key, L.out);
     put(key, L.src.w); put(key, L.src.h); put(key, L.src.cc); put(key, L.src.esize);
     put(key, L.dst.w); put(key, L.dst.h); put(key, L.norm.c_total);
-    put(key, L.norm.mode == 1);
-    if (lut) { put(key, L.norm.mean); put(key, L.norm.stdv); }
+
     const int force_h = env_int("VACV_RESIZE_TILE_H", 0);
     const int force_w = env_int("VACV_RESIZE_TILE_W", 0);
     put(key, force_h); put(key, force_w);

@@ -194,9 +194,17 @@ int norm_spec(const Img& shape, const float* mean, const float* stdv, NormSpec& 
     if (!mean || !stdv) return VACV_ERR_INVALID_ARG;
     if (shape.c > kMaxC) return VACV_ERR_UNSUPPORTED;
     ns.mode = 1;
+    ns.mul_ok = 0;
     for (int k = 0; k < shape.c; ++k) {
         ns.mean[k] = mean[k];
         ns.stdv[k] = stdv[k];
+        ns.inv[k] = 1.0 / ((double)stdv[k] + 1e-6);
+        bool ok = true;
+        for (int v = 0; v < 256 && ok; ++v) {
+            const float d = (float)v - mean[k];
+            ok = (float)((double)d * ns.inv[k]) == normalize_value((float)v, mean[k], stdv[k]);
+        }
+        if (ok) ns.mul_ok |= 1u << k;
     }
     return VACV_OK;
 }

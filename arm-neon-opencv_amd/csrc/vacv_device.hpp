@@ -46,6 +46,32 @@ __device__ __forceinline__ void norm_params(const NormSpec& ns, int img, int ch,
     }
 }
 
+// Normalisation constants of one channel, resolved once per workgroup.
+struct ChanNorm {
+    float mean, stdv;
+    double inv;
+    bool mul;  // host-verified multiply is exact for u8-valued inputs
+};
+
+__device__ __forceinline__ ChanNorm chan_norm(const NormSpec& ns, int img, int ch) {
+    ChanNorm c;
+    norm_params(ns, img, ch, c.mean, c.stdv);
+    c.mul = ns.mode == 1 && ((ns.mul_ok >> ch) & 1u);
+    c.inv = c.mul ? ns.inv[ch] : 0.0;
+    return c;
+}
+
+// normalize_naive.cpp:74-90 for a value known to be an integer in [0,255]
+__device__ __forceinline__ float normalize_u8v(const ChanNorm& c, int v) {
+    const float d = (float)v - c.mean;
+    if (c.mul) return (float)((double)d * c.inv);
+    return (float)((double)d / ((double)c.stdv + 1e-6));
+}
+
+__device__ __forceinline__ float normalize_f(const ChanNorm& c, float x) {
+    return normalize_value(x, c.mean, c.stdv);
+}
+
 template <typename T>
 __device__ __forceinline__ T wave_sum(T v) {
 #pragma unroll

@@ -34,6 +34,14 @@ struct NormSpec {
     const float* dev_std;
     float mean[kMaxC];
     float stdv[kMaxC];
+    // mode 1: inv[k] = 1 / ((double)stdv[k] + 1e-6).  Bit k of mul_ok is set
+    // when the host verified, for all 256 u8 values v, that
+    //   (float)((double)((float)v - mean[k]) * inv[k])
+    // equals the reference's (float)((double)((float)v - mean[k]) /
+    // ((double)stdv[k] + 1e-6)); kernels then use the multiply for
+    // u8-valued inputs (an fp64 divide is ~10x the issue cost).
+    double inv[kMaxC];
+    uint32_t mul_ok;
 };
 
 enum SampleKind : int {

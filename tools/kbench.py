@@ -38,35 +38,35 @@ def main():
         n = a.batch or 256
         src = frames(n, 1080, 1920)
         out = torch.empty((n, 360, 640, 3), dtype=torch.float32, device=dev)
-        cases["resize_normalize_1080p_640x360"] = (lambda: ops.resize_normalize(src, 640, 360, MEAN, STD, out=out),
+        cases["resize_normalize_1080p_640x360"] = (lambda src=src, out=out: ops.resize_normalize(src, 640, 360, MEAN, STD, out=out),
                                                    n * resize_bytes(1920, 1080, 3, 640, 360, 1, 4), n * 1920 * 1080)
     if a.op in ("resize", "all"):
         n = a.batch or 256
         src = frames(n, 1080, 1920)
         o1 = torch.empty((n, 360, 640, 3), dtype=torch.uint8, device=dev)
         o2 = torch.empty((n, 720, 1280, 3), dtype=torch.uint8, device=dev)
-        cases["resize_1080p_640x360_u8"] = (lambda: ops.resize(src, 640, 360, out=o1),
+        cases["resize_1080p_640x360_u8"] = (lambda src=src, o1=o1: ops.resize(src, 640, 360, out=o1),
                                             n * resize_bytes(1920, 1080, 3, 640, 360, 1, 1), n * 1920 * 1080)
-        cases["resize_1080p_1280x720_u8"] = (lambda: ops.resize(src, 1280, 720, out=o2),
+        cases["resize_1080p_1280x720_u8"] = (lambda src=src, o2=o2: ops.resize(src, 1280, 720, out=o2),
                                              n * resize_bytes(1920, 1080, 3, 1280, 720, 1, 1), n * 1920 * 1080)
     if a.op in ("warp", "all"):
         n = a.batch or 128
         src = frames(n, 720, 1280)
         o = torch.empty_like(src)
         m = ops.rotation_matrix(0.9, 15.0, (640, 360, 640, 360))
-        cases["warp_720p_rot15_u8"] = (lambda: ops.warp_affine(src, m, 1280, 720, out=o), n * 2 * 1280 * 720 * 3,
+        cases["warp_720p_rot15_u8"] = (lambda src=src, m=m, o=o: ops.warp_affine(src, m, 1280, 720, out=o), n * 2 * 1280 * 720 * 3,
                                        n * 1280 * 720)
     if a.op in ("cvt", "all"):
         n = a.batch or 256
         yuv = torch.randint(0, 256, (n, 1620, 1920), dtype=torch.uint8, device=dev, generator=g)
         o = torch.empty((n, 1080, 1920, 3), dtype=torch.float32, device=dev)
-        cases["nv21_bgr_normalize_1080p"] = (lambda: ops.cvt_color_normalize(yuv, mean=MEAN, std=STD, out=o),
+        cases["nv21_bgr_normalize_1080p"] = (lambda yuv=yuv, o=o: ops.cvt_color_normalize(yuv, mean=MEAN, std=STD, out=o),
                                              n * (1920 * 1620 + 1920 * 1080 * 12), n * 1920 * 1080)
     if a.op in ("cubic", "all"):
         n = a.batch or 128
         src = frames(n, 1440, 2560)
         o = torch.empty((n, 224, 224, 3), dtype=torch.float32, device=dev)
-        cases["cubic_1440p_224_u8_f32"] = (lambda: ops.resize(src, 224, 224, interpolation=vacv_amd.INTER_CUBIC, out=o),
+        cases["cubic_1440p_224_u8_f32"] = (lambda src=src, o=o: ops.resize(src, 224, 224, interpolation=vacv_amd.INTER_CUBIC, out=o),
                                            n * resize_bytes(2560, 1440, 3, 224, 224, 1, 4, cubic=True), n * 2560 * 1440)
     for name, (fn, nbytes, px) in cases.items():
         for _ in range(3):
