@@ -68,6 +68,17 @@ def main():
         o = torch.empty((n, 224, 224, 3), dtype=torch.float32, device=dev)
         cases["cubic_1440p_224_u8_f32"] = (lambda src=src, o=o: ops.resize(src, 224, 224, interpolation=vacv_amd.INTER_CUBIC, out=o),
                                            n * resize_bytes(2560, 1440, 3, 224, 224, 1, 4, cubic=True), n * 2560 * 1440)
+    if a.op in ("dtype", "all", "calib"):
+        n = a.batch or 64
+        src = frames(n, 1080, 1920)
+        o = torch.empty((n, 1080, 1920, 3), dtype=torch.float32, device=dev)
+        cases["u8_to_f32_1080p"] = (lambda src=src, o=o: ops.change_dtype(src, torch.float32, out=o) if False else
+                                    ops.change_dtype(src, torch.float32), n * 1920 * 1080 * 15, n * 1920 * 1080)
+    if a.op in ("layout", "all"):
+        n = a.batch or 256
+        src = frames(n, 360, 640)
+        cases["hwc_to_chw_640x360_u8"] = (lambda src=src: ops.change_layout(src, vacv_amd.NCHW),
+                                          n * 640 * 360 * 6, n * 640 * 360)
     for name, (fn, nbytes, px) in cases.items():
         for _ in range(3):
             fn()

@@ -1,0 +1,39 @@
+#!/usr/bin/env python3
+"""Summarise rocprofv3 --pmc CSV passes per kernel (mean per dispatch).
+
+  python tools/pmc_summary.py gpurun_out/pmc_dir [kernel-substring ...]
+FETCH_SIZE / WRITE_SIZE are reported raw (KB, as rocprofv3 gives them) and
+as bytes with the gfx950 correction of MI355X_MICROARCH.md §HBM (FETCH_SIZE
+counts half of a 16-B/lane streaming read: x2)."""
+import collections
+import csv
+import glob
+import json
+import sys
+
+
+def main():
+    d = sys.argv[1]
+    keys = sys.argv[2:] or [""]
+    rows = collections.defaultdict(lambda: collections.defaultdict(list))
+    for f in sorted(glob.glob(f"{d}/**/*counter_collection.csv", recursive=True)):
+        for r in csv.DictReader(open(f)):
+            name = r["Kernel_Name"]
+            k = next((k for k in keys if k in name), None)
+            if k is None:
+                continue
+            short = name.split("(")[0][-90:]
+            rows[short][r["Counter_Name"]].append(float(r["Counter_Value"]))
+    out = {}
+    for kname, cnt in rows.items():
+        m = {c: sum(v) / len(v) for c, v in cnt.items()}
+        if "FETCH_SIZE" in m:
+            m["fetch_bytes_corrected"] = m["FETCH_SIZE"] * 1024 * 2
+        if "WRITE_SIZE" in m:
+            m["write_bytes"] = m["WRITE_SIZE"] * 1024
+        out[kname] = m
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main()
