@@ -25,6 +25,9 @@
 // downscale only every third source row moves (B_alg).
 #pragma clang fp contract(off)
 
+#include <map>
+#include <mutex>
+
 #include "vacv_device.hpp"
 
 namespace vacv {
@@ -57,35 +60,121 @@ __device__ __forceinline__ float as_f(T v) {
     return (float)v;
 }
 
-// One output pixel: CC channel values.  TW = weight type of the kind.
+// Vertical taps of one output row, as staged in rowinfo: LDS offsets of the
+// tap rows and the weights (int bits for fixed point, float bits otherwise).
+struct RowTaps {
+    int rb[4];
+    int w[4];
+};
+
+__device__ __forceinline__ RowTaps row_taps(const int* ri) {
+    const int4 a = *reinterpret_cast<const int4*>(ri);
+    const int4 b = *reinterpret_cast<const int4*>(ri + 4);
+    return RowTaps{{a.x, a.y, a.z, a.w}, {b.x, b.y, b.z, b.w}};
+}
+
+// Channel k of one output pixel, from the staged rows.  TWO: the second
+// vertical tap may be non-zero (a zero-weight tap adds exactly 0 and is not
+// read).  XW = the column-tap record of the kind.
 template <int KIND, int CC, typename TIn, int MODE>
-struct Pixel;
+struct Sampler;
 
 // u8 bilinear, 11-bit fixed point
 template <int CC, int MODE>
-struct Pixel<kLinearFixed, CC, uint8_t, MODE> {
-    __device__ __forceinline__ static void eval(const unsigned char* rows, int xo, uint32_t xw, int rbA, int rbB,
-                                                int wA, int wB, bool two, int out[CC]) {
+struct Sampler<kLinearFixed, CC, uint8_t, MODE> {
+    using XW = uint32_t;  // short2 {a0, a1}
+    static constexpr int ES = 1;
+    template <bool TWO>
+    __device__ __forceinline__ static int at(const unsigned char* rows, int off, XW xw, const RowTaps& r) {
         const int a0 = (int)(short)(xw & 0xFFFFu), a1 = (int)(short)(xw >> 16);
-        const unsigned char* pa = rows + rbA + xo;
-        const unsigned char* pb = rows + rbB + xo;
-#pragma unroll
-        for (int k = 0; k < CC; ++k) {
-            const int tl = pa[k], tr = pa[CC + k];
-            int bl = 0, br = 0;
-            if (two) { bl = pb[k]; br = pb[CC + k]; }
-            if (MODE == VACV_LINEAR_REFERENCE) {
-                // resize_naive.cpp:61-64: (Sum S*wx*wy) >> 22, stored as a byte
-                out[k] = ((tl * a0 * wA + bl * a0 * wB + tr * a1 * wA + br * a1 * wB) >> 22) & 0xFF;
-            } else {
-                // resize_neon.cpp:103,122-123 (int16 rows), :150-167 (vertical)
-                const int h0 = (int)(short)((tl * a0 + tr * a1) >> 4);
-                const int h1 = (int)(short)((bl * a0 + br * a1) >> 4);
-                out[k] = clamp_u8((((h0 * wA) >> 16) + ((h1 * wB) >> 16) + 2) >> 2);
-            }
+        const unsigned char* pa = rows + r.rb[0] + off;
+        const unsigned char* pb = rows + r.rb[1] + off;
+        const int tl = pa[0], tr = pa[CC];
+        int bl = 0, br = 0;
+        if (TWO) { bl = pb[0]; br = pb[CC]; }
+        const int wA = r.w[0], wB = r.w[1];
+        if (MODE == VACV_LINEAR_REFERENCE) {
+            // resize_naive.cpp:61-64: (Sum S*wx*wy) >> 22, stored as a byte.
+            // With one vertical tap (wB == 0) the sum factors exactly in int32.
+            if (TWO) return ((tl * a0 * wA + bl * a0 * wB + tr * a1 * wA + br * a1 * wB) >> 22) & 0xFF;
+            return (((tl * a0 + tr * a1) * wA) >> 22) & 0xFF;
         }
+        // resize_neon.cpp:103,122-123 (int16 rows), :150-167 (vertical)
+        const int h0 = (int)(short)((tl * a0 + tr * a1) >> 4);
+        const int h1 = (int)(short)((bl * a0 + br * a1) >> 4);
+        return clamp_u8((((h0 * wA) >> 16) + ((h1 * wB) >> 16) + 2) >> 2);
     }
 };
+
+// fp32 bilinear
+template <int CC, int MODE>
+struct Sampler<kLinearFloat, CC, float, MODE> {
+    using XW = float2;
+    static constexpr int ES = 4;
+    template <bool TWO>
+    __device__ __forceinline__ static float at(const unsigned char* rows, int off, XW wx, const RowTaps& r) {
+        const unsigned char* pa = rows + r.rb[0] + off;
+        const unsigned char* pb = rows + r.rb[1] + off;
+        const float wy0 = __int_as_float(r.w[0]), wy1 = __int_as_float(r.w[1]);
+        const float tl = lds_ld<float>(pa), tr = lds_ld<float>(pa + 4 * CC);
+        float bl = 0.f, br = 0.f;
+        if (TWO) { bl = lds_ld<float>(pb); br = lds_ld<float>(pb + 4 * CC); }
+        // resize_naive.cpp:121-124, summed left to right
+        float val = tl * wx.x * wy0;
+        val += bl * wx.x * wy1;
+        val += tr * wx.y * wy0;
+        val += br * wx.y * wy1;
+        return val;
+    }
+};
+
+// Keys cubic (A = -0.75), u8 or fp32 source
+template <int CC, typename TIn, int MODE>
+struct Sampler<kCubic, CC, TIn, MODE> {
+    using XW = float4;
+    static constexpr int ES = sizeof(TIn);
+    template <bool TWO>
+    __device__ __forceinline__ static float at(const unsigned char* rows, int off, XW a, const RowTaps& r) {
+        float h[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            // zero-weight taps read a valid staged row (slot 0); the reference
+            // multiplies them by 0 as well
+            const unsigned char* sp = rows + r.rb[q] + off;
+            const float s0 = as_f(lds_ld<TIn>(sp)), s1 = as_f(lds_ld<TIn>(sp + ES * CC));
+            const float s2 = as_f(lds_ld<TIn>(sp + 2 * ES * CC)), s3 = as_f(lds_ld<TIn>(sp + 3 * ES * CC));
+            // resize_naive.cpp:325-328
+            h[q] = s0 * a.x + s1 * a.y + s2 * a.z + s3 * a.w;
+        }
+        // resize_naive.cpp:349-351
+        return h[0] * __int_as_float(r.w[0]) + h[1] * __int_as_float(r.w[1]) + h[2] * __int_as_float(r.w[2]) +
+               h[3] * __int_as_float(r.w[3]);
+    }
+};
+
+// v[i] for a small runtime i, without a scratch-indexed array
+template <int N, typename T>
+__device__ __forceinline__ T pick(const T (&v)[N], int i) {
+    T r = v[0];
+#pragma unroll
+    for (int q = 1; q < N; ++q)
+        if (i == q) r = v[q];
+    return r;
+}
+
+template <int N>
+__device__ __forceinline__ ChanNorm pick(const ChanNorm (&v)[N], int i) {
+    ChanNorm r = v[0];
+#pragma unroll
+    for (int q = 1; q < N; ++q) {
+        const bool s = i == q;
+        r.mean = s ? v[q].mean : r.mean;
+        r.stdv = s ? v[q].stdv : r.stdv;
+        r.inv = s ? v[q].inv : r.inv;
+        r.mul = s ? v[q].mul : r.mul;
+    }
+    return r;
+}
 
 }  // namespace
 
@@ -96,9 +185,8 @@ resize_kernel(ResizeLaunch L) {
     constexpr int ES = sizeof(TIn);
     constexpr int XW = (KIND == kLinearFixed) ? 4 : (KIND == kLinearFloat ? 8 : 16);
     using TOut = typename std::conditional<(OUT == kOutSame), TIn, float>::type;
-    // pixels per lane per segment: keep each lane's store >= 4 bytes
-    constexpr int PX = (CC * (int)sizeof(TOut) < 4) ? 4 : ((CC * (int)sizeof(TOut) < 8) ? 2 : 1);
-    constexpr int SEG = 64 * PX;
+    constexpr int PX = 4;  // byte output: consecutive pixels per lane
+    using Smp = Sampler<KIND, CC, TIn, MODE>;
 
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     const int tid = threadIdx.x;
@@ -139,25 +227,30 @@ resize_kernel(ResizeLaunch L) {
 
     // ---- prefetch a task's rows into registers ------------------------------
     // (slot, chunk) of this thread's m-th chunk is fixed per strip
-    int ch_s[kMaxChunks], ch_c[kMaxChunks];
-#pragma unroll
-    for (int m = 0; m < kMaxChunks; ++m) {
+    // (recomputed where used rather than held in registers across the compute)
+    const uint32_t cpr_magic = (uint32_t)(((1ull << 32) + cpr - 1) / cpr);  // k / cpr for k < kMaxChunks*kBlock
+    auto chunk_slot = [&](int m, int& sl, int& c) {
         const int k = tid + m * kBlock;
-        ch_s[m] = k / cpr;
-        ch_c[m] = k - ch_s[m] * cpr;
-    }
+        sl = cpr == 1 ? k : (int)__umulhi((uint32_t)k, cpr_magic);
+        c = k - sl * cpr;
+    };
     uint4 R[kMaxChunks];
     auto prefetch = [&](int task) {
         const int ns = L.plan.task_nslots[task];
         const int* trow = L.plan.task_rows + (int64_t)task * L.max_slots;
         uint32_t off[kMaxChunks];
+        bool live[kMaxChunks];
 #pragma unroll
-        for (int m = 0; m < kMaxChunks; ++m)
-            off[m] = ch_s[m] < ns ? (((uint32_t)((int64_t)trow[ch_s[m]] * rp) + span_off) & ~15u) + 16u * ch_c[m] : 0u;
+        for (int m = 0; m < kMaxChunks; ++m) {
+            int sl, c;
+            chunk_slot(m, sl, c);
+            live[m] = sl < ns;
+            off[m] = live[m] ? (((uint32_t)((int64_t)trow[sl] * rp) + span_off) & ~15u) + 16u * c : 0u;
+        }
         bool tail = false;
 #pragma unroll
         for (int m = 0; m < kMaxChunks; ++m) {
-            if (ch_s[m] < ns) {
+            if (live[m]) {
                 if (off[m] + 16u <= limit) R[m] = load16(rs, off[m]);
                 else tail = true;
             }
@@ -165,7 +258,7 @@ resize_kernel(ResizeLaunch L) {
         if (tail) {  // only the chunk that crosses the end of the plane
 #pragma unroll
             for (int m = 0; m < kMaxChunks; ++m)
-                if (ch_s[m] < ns && off[m] + 16u > limit) R[m] = load16_safe(rs, off[m], limit);
+                if (live[m] && off[m] + 16u > limit) R[m] = load16_safe(rs, off[m], limit);
         }
     };
     prefetch(task0);
@@ -178,15 +271,35 @@ resize_kernel(ResizeLaunch L) {
         else if (XW == 8) reinterpret_cast<uint2*>(xw_l)[i] = reinterpret_cast<const uint2*>(L.plan.xw)[e];
         else reinterpret_cast<uint4*>(xw_l)[i] = reinterpret_cast<const uint4*>(L.plan.xw)[e];
     }
-    ChanNorm cn[CC];
+    ChanNorm cn[CC] = {};
     if (OUT == kOutNorm) {
 #pragma unroll
         for (int k = 0; k < CC; ++k) cn[k] = chan_norm(L.norm, img, CC == 1 ? plane % L.norm.c_total : k);
     }
+    // u8 normalisation as one multiply per element when the host verified it
+    // exact for every channel (NormSpec.mul_ok): branch-free inner loop
+    bool all_mul = OUT == kOutNorm;
+#pragma unroll
+    for (int k = 0; k < CC; ++k) all_mul = all_mul && cn[k].mul;
 
     unsigned char* dst_plane = const_cast<unsigned char*>(L.dst.base) + (int64_t)img * L.dst.img_pitch +
                                (int64_t)plane * L.dst.plane_pitch;
-    const int segs_per_row = (nx + SEG - 1) / SEG;
+    const int gpr = (nx + PX - 1) / PX;  // pixel groups per output row
+
+    // fp32-output chunk state (see the compute section)
+    constexpr int E = 4;
+    constexpr int MAXM = kResizeMaxChunksPerLane;
+    const int rl = nx * CC;  // elements per tile row
+    const Rsrc rd = make_rsrc(dst_plane, L.dst.plane_bytes);
+    int c_e0[MAXM];
+    // per element: LDS byte offset of its first tap | pixel << 16, its column
+    // weights (cubic: re-read from LDS, 16 B each), and its channel's
+    // normalisation (x - mean) op a, op = * (verified inverse) or / (divisor)
+    constexpr bool kHoldXW = sizeof(typename Smp::XW) <= 8;
+    int c_off[MAXM][E];
+    typename Smp::XW c_xw[MAXM][kHoldXW ? E : 1];
+    float c_mean[MAXM][E];
+    double c_a[MAXM][E];
 
     for (int task = task0; task < task1; ++task) {
         if (task != task0) __syncthreads();  // everyone is done reading the previous tile
@@ -194,7 +307,11 @@ resize_kernel(ResizeLaunch L) {
         const int ns = L.plan.task_nslots[task];
 #pragma unroll
         for (int m = 0; m < kMaxChunks; ++m)
-            if (ch_s[m] < ns) *reinterpret_cast<uint4*>(rows_l + ch_s[m] * L.slot_stride + 16 * ch_c[m]) = R[m];
+        {
+            int sl, c;
+            chunk_slot(m, sl, c);
+            if (sl < ns) *reinterpret_cast<uint4*>(rows_l + sl * L.slot_stride + 16 * c) = R[m];
+        }
         if (tid < ns) {
             const int row = L.plan.task_rows[(int64_t)task * L.max_slots + tid];
             head_l[tid] = (int)(((uint32_t)((int64_t)row * rp) + span_off) & 15u);
@@ -229,107 +346,126 @@ resize_kernel(ResizeLaunch L) {
         __syncthreads();
         if (task + 1 < task1) prefetch(task + 1);  // in flight during this tile's compute
 
-        // ---- compute: one wave = one segment of one row at a time ----------
-        const int nseg = ny * segs_per_row;
-        for (int sg = wave; sg < nseg; sg += kBlock / 64) {
-            const int t = sg / segs_per_row;               // wave-uniform
-            const int sidx = sg - t * segs_per_row;
-            const int* ri = rowinfo_l + t * 8;
-            int rb[4];
+        // ---- compute -----------------------------------------------------------
+        const bool two = (L.plan.task_flags[task] & 2) != 0;  // uniform: some row uses tap 1
+        auto run = [&](auto two_tag, auto mul_tag) {
+            constexpr bool TWO = decltype(two_tag)::value;
+            constexpr bool MUL = decltype(mul_tag)::value;  // every channel normalises by the verified multiply
+            if constexpr (sizeof(TOut) == 1) {
+                // byte output: a lane takes PX consecutive pixels of a row
+                // (PX*CC bytes, dword stores)
+                const int ngroups = ny * gpr;
+                for (int g = tid; g < ngroups; g += kBlock) {
+                    const int t = g / gpr;
+                    const int pbase = (g - t * gpr) * PX;  // tile-relative first pixel
+                    const RowTaps rt = row_taps(rowinfo_l + t * 8);
+                    unsigned char* drow = dst_plane + (int64_t)(y0 + t) * L.dst.row_pitch;
+                    TOut out[PX * CC];
 #pragma unroll
-            for (int q = 0; q < TAPS; ++q) rb[q] = __builtin_amdgcn_readfirstlane(ri[q]);
-            const int w4 = __builtin_amdgcn_readfirstlane(ri[4]);
-            const int w5 = __builtin_amdgcn_readfirstlane(ri[5]);
-            const int w6 = __builtin_amdgcn_readfirstlane(ri[6]);
-            const int w7 = __builtin_amdgcn_readfirstlane(ri[7]);
-            const int dy = y0 + t;
-            unsigned char* drow = dst_plane + (int64_t)dy * L.dst.row_pitch;
-            const int pbase = sidx * SEG + lane * PX;     // first pixel of this lane (tile-relative)
-
-            TOut out[PX * CC];
+                    for (int q = 0; q < PX; ++q) {
+                        const int pxl = min(pbase + q, nx - 1);  // clamp; the store masks it
+                        const typename Smp::XW xw = reinterpret_cast<const typename Smp::XW*>(xw_l)[pxl];
 #pragma unroll
-            for (int q = 0; q < PX; ++q) {
-                const int pxl = min(pbase + q, nx - 1);       // clamp; the store masks it
-                const int xo = xoff_l[pxl];
-                if (KIND == kLinearFixed) {
-                    const uint32_t wx = reinterpret_cast<const uint32_t*>(xw_l)[pxl];
-                    int v[CC];
-                    const bool two = (w6 & 2) != 0;            // wave-uniform
-                    Pixel<kLinearFixed, CC, uint8_t, MODE>::eval(rows_l, xo, wx, rb[0], rb[1], w4, w5, two, v);
-#pragma unroll
-                    for (int k = 0; k < CC; ++k) {
-                        if (OUT == kOutSame) out[q * CC + k] = (TOut)v[k];
-                        else if (OUT == kOutF32) out[q * CC + k] = (TOut)(float)v[k];
-                        else out[q * CC + k] = (TOut)normalize_u8v(cn[k], v[k]);
+                        for (int k = 0; k < CC; ++k)
+                            out[q * CC + k] = (TOut)Smp::template at<TWO>(rows_l, xoff_l[pxl] + Smp::ES * k, xw, rt);
                     }
-                } else if (KIND == kLinearFloat) {
-                    const float2 wx = reinterpret_cast<const float2*>(xw_l)[pxl];
-                    const float wy0 = __int_as_float(w4), wy1 = __int_as_float(w5);
-                    const bool two = (w6 & 2) != 0;
-                    const unsigned char* pa = rows_l + rb[0] + xo;
-                    const unsigned char* pb = rows_l + rb[1] + xo;
+                    const int valid = min(PX, nx - pbase);
+                    unsigned char* dp = drow + (int64_t)(x0 + pbase) * CC;
+                    constexpr int kBytes = PX * CC;
+                    if (valid == PX && kBytes % 4 == 0 && (reinterpret_cast<uintptr_t>(dp) & 3) == 0) {
 #pragma unroll
-                    for (int k = 0; k < CC; ++k) {
-                        const float tl = lds_ld<float>(pa + 4 * k), tr = lds_ld<float>(pa + 4 * (CC + k));
-                        float bl = 0.f, br = 0.f;
-                        if (two) { bl = lds_ld<float>(pb + 4 * k); br = lds_ld<float>(pb + 4 * (CC + k)); }
-                        // resize_naive.cpp:121-124, summed left to right
-                        float val = tl * wx.x * wy0;
-                        val += bl * wx.x * wy1;
-                        val += tr * wx.y * wy0;
-                        val += br * wx.y * wy1;
-                        if (OUT == kOutNorm) val = normalize_f(cn[k], val);
-                        out[q * CC + k] = (TOut)val;
-                    }
-                } else {
-                    const float4 a = reinterpret_cast<const float4*>(xw_l)[pxl];
-                    const float wy[4] = {__int_as_float(w4), __int_as_float(w5), __int_as_float(w6), __int_as_float(w7)};
+                        for (int b = 0; b < kBytes / 4; ++b)
+                            reinterpret_cast<uint32_t*>(dp)[b] = reinterpret_cast<const uint32_t*>(out)[b];
+                    } else {
 #pragma unroll
-                    for (int k = 0; k < CC; ++k) {
-                        float h[4];
-#pragma unroll
-                        for (int r = 0; r < 4; ++r) {
-                            h[r] = 0.f;
-                            if (wy[r] != 0.f) {  // wave-uniform
-                                const unsigned char* sp = rows_l + rb[r] + xo + ES * k;
-                                const float s0 = as_f(lds_ld<TIn>(sp)), s1 = as_f(lds_ld<TIn>(sp + ES * CC));
-                                const float s2 = as_f(lds_ld<TIn>(sp + 2 * ES * CC)), s3 = as_f(lds_ld<TIn>(sp + 3 * ES * CC));
-                                // resize_naive.cpp:325-328
-                                h[r] = s0 * a.x + s1 * a.y + s2 * a.z + s3 * a.w;
-                            }
-                        }
-                        // resize_naive.cpp:349-351
-                        float val = h[0] * wy[0] + h[1] * wy[1] + h[2] * wy[2] + h[3] * wy[3];
-                        if (OUT == kOutNorm) val = normalize_f(cn[k], val);
-                        out[q * CC + k] = (TOut)val;
+                        for (int e = 0; e < kBytes; ++e)
+                            if (e < valid * CC) dp[e] = out[e];
                     }
                 }
             }
-
-            // ---- store PX*CC contiguous outputs -------------------------------
-            const int valid = min(PX, nx - pbase);
-            if (valid > 0) {
-                unsigned char* dp = drow + ((int64_t)(x0 + pbase) * CC) * (int64_t)sizeof(TOut);
-                constexpr int kBytes = PX * CC * (int)sizeof(TOut);
-                const uintptr_t a = reinterpret_cast<uintptr_t>(dp);
-                if (valid == PX && kBytes % 16 == 0 && (a & 15) == 0) {
+        };
+        if constexpr (sizeof(TOut) == 1) {
+            if (two) run(std::true_type{}, std::false_type{});
+            else run(std::false_type{}, std::false_type{});
+        } else {
+            // fp32 output: lane-stationary chunks.  Lane tid owns 4-element
+            // output chunks j = tid + m*kBlock of every row of the tile (the
+            // planner keeps a row within MAXM*kBlock chunks), so its column
+            // taps, channel constants and store offsets are computed once per
+            // strip; the vertical taps of a row are wave-uniform scalars.  One
+            // wave store instruction writes 1 KiB of contiguous output.
+            if (task == task0) {
 #pragma unroll
-                    for (int b = 0; b < kBytes / 16; ++b) reinterpret_cast<uint4*>(dp)[b] = reinterpret_cast<const uint4*>(out)[b];
-                } else if (valid == PX && kBytes == 12 && (a & 3) == 0) {
-                    const uint32_t* o32 = reinterpret_cast<const uint32_t*>(out);
-                    reinterpret_cast<uint32_t*>(dp)[0] = o32[0];
-                    reinterpret_cast<uint32_t*>(dp)[1] = o32[1];
-                    reinterpret_cast<uint32_t*>(dp)[2] = o32[2];
-                } else if (valid == PX && kBytes % 8 == 0 && (a & 7) == 0) {
+                for (int m = 0; m < MAXM; ++m) {
+                    const int e0 = (tid + m * kBlock) * E;
+                    const int p0 = e0 / CC;
+                    const int k0 = e0 - p0 * CC;
+                    c_e0[m] = e0;
 #pragma unroll
-                    for (int b = 0; b < kBytes / 8; ++b) reinterpret_cast<uint2*>(dp)[b] = reinterpret_cast<const uint2*>(out)[b];
-                } else if (valid == PX && kBytes % 4 == 0 && (a & 3) == 0) {
+                    for (int i = 0; i < E; ++i) {
+                        const int kk = k0 + i;
+                        const int dp = kk / CC;
+                        const int k = kk - dp * CC;
+                        const int px = min(p0 + dp, nx - 1);  // clamp; the store masks it
+                        c_off[m][i] = (xoff_l[px] + Smp::ES * k) | (px << 16);
+                        if constexpr (kHoldXW) c_xw[m][i] = reinterpret_cast<const typename Smp::XW*>(xw_l)[px];
+                        const ChanNorm c = pick(cn, k);
+                        c_mean[m][i] = c.mean;
+                        c_a[m][i] = (KIND == kLinearFixed && all_mul) ? c.inv : (double)c.stdv + 1e-6;  // normalize_naive.cpp:84-87
+                    }
+                }
+            }
+            for (int t = 0; t < ny; ++t) {
+                RowTaps rt;
 #pragma unroll
-                    for (int b = 0; b < kBytes / 4; ++b) reinterpret_cast<uint32_t*>(dp)[b] = reinterpret_cast<const uint32_t*>(out)[b];
+                for (int q = 0; q < 4; ++q) {
+                    rt.rb[q] = __builtin_amdgcn_readfirstlane(rowinfo_l[t * 8 + q]);
+                    rt.w[q] = __builtin_amdgcn_readfirstlane(rowinfo_l[t * 8 + 4 + q]);
+                }
+                const int64_t orow = (int64_t)(y0 + t) * L.dst.row_pitch + (int64_t)x0 * CC * 4;
+                auto row_pass = [&](auto two_tag, auto mul_tag) {
+                    constexpr bool TWO = decltype(two_tag)::value;
+                    constexpr bool MUL = decltype(mul_tag)::value;
+#pragma unroll
+                    for (int m = 0; m < MAXM; ++m) {
+                        if (c_e0[m] >= rl) break;
+                        float out[E];
+#pragma unroll
+                        for (int i = 0; i < E; ++i) {
+                            typename Smp::XW xw;
+                            if constexpr (kHoldXW) xw = c_xw[m][i];
+                            else xw = reinterpret_cast<const typename Smp::XW*>(xw_l)[c_off[m][i] >> 16];
+                            const auto v = Smp::template at<TWO>(rows_l, c_off[m][i] & 0xFFFF, xw, rt);
+                            if constexpr (OUT == kOutNorm) {
+                                // normalize_naive.cpp:74-90: float subtract, fp64 divide
+                                const double d = (double)((float)v - c_mean[m][i]);
+                                if constexpr (MUL) out[i] = (float)(d * c_a[m][i]);
+                                else out[i] = (float)(d / c_a[m][i]);
+                            } else {
+                                out[i] = (float)v;
+                            }
+                        }
+                        const int64_t ob = orow + (int64_t)c_e0[m] * 4;
+                        const int valid = min(E, rl - c_e0[m]);
+                        const uint32_t boff = (uint32_t)ob + rd.delta;
+                        if (valid == E && (boff & 15u) == 0) {
+                            store16(rd, boff, make_uint4(__float_as_uint(out[0]), __float_as_uint(out[1]),
+                                                         __float_as_uint(out[2]), __float_as_uint(out[3])));
+                        } else {
+                            float* dp = reinterpret_cast<float*>(dst_plane + ob);
+#pragma unroll
+                            for (int i = 0; i < E; ++i)
+                                if (i < valid) dp[i] = out[i];
+                        }
+                    }
+                };
+                const bool row_two = KIND == kCubic || (rt.w[2] & 2) != 0;  // linear: w[2] = tap mask
+                if (KIND == kLinearFixed && OUT == kOutNorm && all_mul) {
+                    if (row_two) row_pass(std::true_type{}, std::true_type{});
+                    else row_pass(std::false_type{}, std::true_type{});
                 } else {
-#pragma unroll
-                    for (int e = 0; e < PX * CC; ++e)
-                        if (e < valid * CC) reinterpret_cast<TOut*>(dp)[e] = out[e];
+                    if (row_two) row_pass(std::true_type{}, std::false_type{});
+                    else row_pass(std::false_type{}, std::false_type{});
                 }
             }
         }
@@ -338,11 +474,35 @@ resize_kernel(ResizeLaunch L) {
 
 namespace {
 
+// Workgroups of this kernel instance the device holds at once, for an LDS
+// footprint (cached: the occupancy query is not free).
+template <typename K>
+int64_t resident_workgroups(K kernel, int lds_bytes) {
+    static std::mutex mu;
+    static std::map<std::pair<int, int>, int64_t> cache;  // (device, lds) -> workgroups
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return 0;
+    std::lock_guard<std::mutex> lk(mu);
+    auto it = cache.find({dev, lds_bytes});
+    if (it != cache.end()) return it->second;
+    int per_cu = 0, cus = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, kBlock, lds_bytes) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+        return 0;
+    const int64_t r = (int64_t)std::max(per_cu, 1) * std::max(cus, 1);
+    cache.emplace(std::make_pair(dev, lds_bytes), r);
+    return r;
+}
+
 template <int KIND, int CC, typename TIn, int OUT, int MODE>
-hipError_t launch_one(const ResizeLaunch& L, hipStream_t s) {
+hipError_t launch_one(ResizeLaunch L, hipStream_t s) {
+    auto kernel = resize_kernel<KIND, CC, TIn, OUT, MODE>;
+    const int64_t resident = resident_workgroups(kernel, L.lds_bytes);
+    if (resident <= 0) return hipErrorInvalidValue;
+    set_strips(L, resident);
     const int64_t blocks = (int64_t)L.n * L.src.planes * L.tiles_x * L.strips;
     if (blocks > 0x7FFFFFFF) return hipErrorInvalidValue;
-    hipLaunchKernelGGL((resize_kernel<KIND, CC, TIn, OUT, MODE>), dim3((unsigned)blocks), dim3(kBlock), L.lds_bytes, s, L);
+    hipLaunchKernelGGL(kernel, dim3((unsigned)blocks), dim3(kBlock), L.lds_bytes, s, L);
     return hipGetLastError();
 }
 

@@ -35,6 +35,7 @@ namespace {
 
 constexpr int kLdsBudget = 40 * 1024;   // per workgroup; 4 resident per CU
 constexpr int kMaxChunksPerThread = 8;  // register prefetch depth (uint4 per thread)
+constexpr int kWorkPerThread = 8;       // target output work items per thread per task
 
 struct Taps {
     int origin;   // first tap (row or column)
@@ -115,6 +116,7 @@ bool evaluate(const ResizeLaunch& L, const std::vector<Taps>& xt, const std::vec
     g.lds = (int)(a16(tile_w * 4) + a16((size_t)tile_w * xw) + 32 * 8 * 4 + a16(slots * 4) +
                   (size_t)slots * g.slot_stride);
     if (tile_h * taps > 64) return false;
+    if (L.dst.esize == 4 && (int64_t)tile_w * L.dst.cc > 4 * kResizeMaxChunksPerLane * kBlock) return false;
     if ((int64_t)slots * g.max_cpr > (int64_t)kMaxChunksPerThread * kBlock) return false;
     return g.lds <= kLdsBudget;
 }
@@ -156,7 +158,8 @@ int plan_resize(ResizeLaunch& L, hipStream_t stream) {
 
     const int force_h = env_int("VACV_RESIZE_TILE_H", 0);
     const int force_w = env_int("VACV_RESIZE_TILE_W", 0);
-    put(key, force_h); put(key, force_w);
+    const int work = std::max(1, env_int("VACV_RESIZE_WORK", kWorkPerThread));
+    put(key, force_h); put(key, force_w); put(key, work);
 
     std::lock_guard<std::mutex> lk(g_mu);
     auto it = g_plans.find(key);
@@ -173,12 +176,23 @@ int plan_resize(ResizeLaunch& L, hipStream_t stream) {
             const double sx = (double)L.src.w / L.dst.w;
             tile_w = std::min(L.dst.w, std::max(64, (int)(8192.0 / (sx * bp)) / 64 * 64));
         }
+        if (L.dst.esize == 4) {
+            // fp32 output: a tile row is at most kResizeMaxChunksPerLane
+            // 4-element chunks per lane (k_resize.hip); split evenly
+            const int max_w = std::max(4, (4 * kResizeMaxChunksPerLane * kBlock / L.dst.cc) / 4 * 4);
+            if (tile_w > max_w) {
+                const int nt = (L.dst.w + max_w - 1) / max_w;
+                tile_w = std::min(max_w, ((L.dst.w + nt - 1) / nt + 3) / 4 * 4);
+            }
+        }
         if (force_w > 0) tile_w = std::min(force_w, L.dst.w);
         Geometry g{};
         bool ok = false;
         for (;;) {
-            const int per_row = (tile_w * L.dst.cc + 3) / 4;
-            int th = std::max(1, std::min((8 * kBlock + per_row - 1) / per_row, 64 / taps));
+            // work items per output row: 4-pixel groups (byte output) or
+            // 4-element chunks (fp32 output), see k_resize.hip
+            const int per_row = L.dst.esize == 1 ? (tile_w + 3) / 4 : (tile_w * L.dst.cc + 3) / 4;
+            int th = std::max(1, std::min((work * kBlock + per_row - 1) / per_row, 64 / taps));
             if (force_h > 0) th = std::min(force_h, 64 / taps);
             th = std::min(th, L.dst.h);
             for (; th >= 1; --th)
@@ -203,6 +217,7 @@ int plan_resize(ResizeLaunch& L, hipStream_t stream) {
         const size_t o_tn = take((size_t)g.tiles_y * 4);
         const size_t o_tr = take((size_t)g.tiles_y * g.max_slots * 4);
         const size_t o_tc = take((size_t)g.tiles_y * cand_n * 4);
+        const size_t o_tf = take((size_t)g.tiles_y * 4);
         const size_t o_lut = take(lut ? (size_t)L.norm.c_total * 256 * 4 : 16);
         const size_t bytes = off;
         std::vector<unsigned char> img(bytes, 0);
@@ -258,6 +273,11 @@ int plan_resize(ResizeLaunch& L, hipStream_t stream) {
                         if (weight_nonzero(L, yt[y0 + t], j)) cand[t * taps + j] = yt[y0 + t].origin + j - lo;
             }
             I(o_tn)[ty] = ns;
+            int flags = 0;
+            for (int t = 0; t < ny; ++t)
+                for (int j = 0; j < taps; ++j)
+                    if (weight_nonzero(L, yt[y0 + t], j)) flags |= 1 << j;
+            I(o_tf)[ty] = flags;
         }
         if (lut)
             for (int k = 0; k < L.norm.c_total; ++k)
@@ -297,6 +317,7 @@ int plan_resize(ResizeLaunch& L, hipStream_t stream) {
         cp.offs.task_nslots = reinterpret_cast<const int*>(P(o_tn));
         cp.offs.task_rows = reinterpret_cast<const int*>(P(o_tr));
         cp.offs.task_cand = reinterpret_cast<const int*>(P(o_tc));
+        cp.offs.task_flags = reinterpret_cast<const int*>(P(o_tf));
         cp.offs.lut = lut ? reinterpret_cast<const float*>(P(o_lut)) : nullptr;
         it = g_plans.emplace(key, cp).first;
     }
@@ -311,15 +332,21 @@ int plan_resize(ResizeLaunch& L, hipStream_t stream) {
     L.slot_stride = g.slot_stride;
     L.lds_bytes = g.lds;
     L.plan = cp.offs;
-    // strips: enough workgroups for every CU to hold ~4, each streaming a
-    // contiguous run of row tiles of one (plane, tile column)
-    const int64_t columns = (int64_t)L.n * L.src.planes * g.tiles_x;
-    const int resident = std::max(1, std::min(8, (160 * 1024) / std::max(g.lds, 1)));
-    const int64_t target = env_int("VACV_RESIZE_WGS", 256 * resident);
-    int strips = (int)std::max<int64_t>(1, std::min<int64_t>(g.tiles_y, (target + columns - 1) / columns));
-    L.tasks_per_strip = (g.tiles_y + strips - 1) / strips;
-    L.strips = (g.tiles_y + L.tasks_per_strip - 1) / L.tasks_per_strip;
+    L.strips = 0;  // set_strips(), once the kernel's residency is known
     return VACV_OK;
+}
+
+// Strips: one wave of resident workgroups, each streaming a contiguous run
+// of row tiles of one (plane, tile column).  `resident` = workgroups the
+// chosen kernel instance fits on the whole device at once (its VGPR and LDS
+// use, from the occupancy API): a grid larger than that by a fraction would
+// run a mostly idle second round.
+void set_strips(ResizeLaunch& L, int64_t resident) {
+    const int64_t columns = (int64_t)L.n * L.src.planes * L.tiles_x;
+    const int64_t target = env_int("VACV_RESIZE_WGS", (int)std::max<int64_t>(1, resident));
+    const int strips = (int)std::max<int64_t>(1, std::min<int64_t>(L.tiles_y, target / std::max<int64_t>(columns, 1)));
+    L.tasks_per_strip = (L.tiles_y + strips - 1) / strips;
+    L.strips = (L.tiles_y + L.tasks_per_strip - 1) / L.tasks_per_strip;
 }
 
 int release_plans() {

@@ -233,6 +233,8 @@ int resize_impl(const vacv_image* src_d, const vacv_image* dst_d, int interpolat
     ResizeLaunch L{};
     L.src = geom(src);
     L.dst = geom(dst);
+    // the kernel addresses one plane through a 32-bit buffer resource
+    if (L.src.plane_bytes > kMaxPlaneBytes || L.dst.plane_bytes > kMaxPlaneBytes) return VACV_ERR_UNSUPPORTED;
     L.n = src.n;
     L.mode = mode;
     L.out = out_kind;

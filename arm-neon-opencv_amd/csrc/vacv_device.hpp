@@ -10,6 +10,17 @@
 
 namespace vacv {
 
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+// Cache-policy aux bits of the streaming buffer loads / stores (gfx950:
+// 1 = sc0, 2 = nt, 16 = sc1).  Source rows and outputs are touched once.
+#ifndef VACV_LOAD_AUX
+#define VACV_LOAD_AUX 0
+#endif
+#ifndef VACV_STORE_AUX
+#define VACV_STORE_AUX 0
+#endif
+
 // A raw buffer resource over [base16, base16 + bytes): loads past the end
 // return zeros instead of faulting, so a 16-byte staging load may overhang
 // the last row of a batch.  base16 is the 16-byte aligned-down plane base;
@@ -25,14 +36,23 @@ __device__ __forceinline__ Rsrc make_rsrc(const unsigned char* base, int64_t byt
     Rsrc s;
     s.delta = static_cast<uint32_t>(p - a);
     int64_t n = bytes + s.delta;
-    if (n > 0x7FFFFFF0LL) n = 0x7FFFFFF0LL;
+    if (n > kMaxPlaneBytes + 16) n = kMaxPlaneBytes + 16;  // callers check plane sizes (kMaxPlaneBytes)
     s.r = __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(a), (short)0, (int)n, 0x00020000);
     return s;
 }
 
 __device__ __forceinline__ uint4 load16(const Rsrc& s, uint32_t off_from_base16) {
-    auto v = __builtin_amdgcn_raw_buffer_load_b128(s.r, (int)off_from_base16, 0, 0);
+    auto v = __builtin_amdgcn_raw_buffer_load_b128(s.r, (int)off_from_base16, 0, VACV_LOAD_AUX);
     return *reinterpret_cast<uint4*>(&v);
+}
+
+
+// 16-byte store through a buffer resource.  Kept distinct from plain stores
+// on purpose: the compiler cannot merge it with a masked fallback path into
+// narrower stores, so a wave's 64 lanes write 1 KiB in one instruction.
+__device__ __forceinline__ void store16(const Rsrc& s, uint32_t off_from_base16, uint4 v) {
+    u32x4 d = {v.x, v.y, v.z, v.w};
+    __builtin_amdgcn_raw_buffer_store_b128(d, s.r, (int)off_from_base16, 0, VACV_STORE_AUX);
 }
 
 // Per-workgroup mean/stddev for channel ch of image img.

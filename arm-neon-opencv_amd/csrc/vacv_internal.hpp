@@ -11,6 +11,8 @@ namespace vacv {
 
 constexpr int kBlock = 256;         // threads per workgroup (4 waves)
 constexpr int kMaxC = VACV_MAX_CHANNELS;
+constexpr int kResizeMaxChunksPerLane = 1;        // fp32 resize: 4-element chunks per lane per row
+constexpr int64_t kMaxPlaneBytes = 0x7FFFFFF0LL;  // buffer-resource addressing limit of one plane
 
 // How a batch is walked: a "plane" is what one sampler pass sees -- a whole
 // NHWC image (cc = c interleaved channels) or one NCHW channel plane (cc = 1).
@@ -70,6 +72,7 @@ struct ResizePlanDev {
     const int* task_nslots;      // [tiles_y]
     const int* task_rows;        // [tiles_y][max_slots] source row of each LDS slot
     const int* task_cand;        // [tiles_y][tile_h*TAPS] slot of (row t, tap j) or -1 (zero weight)
+    const int* task_flags;       // [tiles_y] bit j: some row of the tile has a non-zero weight on tap j
     const float* lut;            // [c_total][256] normalised u8 values (host-constant mean/std) or null
 };
 
@@ -95,6 +98,7 @@ struct ResizeLaunch {
 
 // Fills tiles, strips and the cached device plan of L (host).
 int plan_resize(ResizeLaunch& L, hipStream_t s);
+void set_strips(ResizeLaunch& L, int64_t resident_workgroups);
 int release_plans();
 
 hipError_t launch_resize(const ResizeLaunch& L, hipStream_t s);

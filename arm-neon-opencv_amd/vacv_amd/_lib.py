@@ -94,10 +94,12 @@ def build(quiet: bool = True) -> None:
     subprocess.run(cmd, check=True)
 
 
-def load(path: Path = HIP_LIB) -> ctypes.CDLL:
+def load(path: Path = None) -> ctypes.CDLL:
     global _lib
     if _lib is not None:
         return _lib
+    if path is None:  # VACV_HIP_LIB: an alternative build of the same ABI (kernel experiments)
+        path = Path(os.environ.get("VACV_HIP_LIB", str(HIP_LIB)))
     if not path.exists():
         raise ImportError(
             f"{path} is missing: the vacv HIP library has not been built "

@@ -21,6 +21,8 @@ def main():
     ap.add_argument("--op", default="resize_normalize")
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--batch", type=int, default=0)
+    ap.add_argument("--sweep", default="",
+                    help="planner env knobs to sweep, e.g. 'VACV_RESIZE_WORK=2,4,8;VACV_RESIZE_TILE_H=0,4'")
     a = ap.parse_args()
     import torch
     import vacv_amd
@@ -79,11 +81,24 @@ def main():
         src = frames(n, 360, 640)
         cases["hwc_to_chw_640x360_u8"] = (lambda src=src: ops.change_layout(src, vacv_amd.NCHW),
                                           n * 640 * 360 * 6, n * 640 * 360)
+    import itertools
+    import os
+    knobs = [kv.split("=", 1) for kv in a.sweep.split(";") if kv]
+    combos = list(itertools.product(*[[(k, v) for v in vals.split(",")] for k, vals in knobs])) or [()]
+    for combo in combos:
+        for k, v in combo:
+            os.environ[k] = v
+        tag = " ".join(f"{k}={v}" for k, v in combo)
+        run_cases(cases, a.iters, tag)
+
+
+def run_cases(cases, iters, tag):
+    import torch
     for name, (fn, nbytes, px) in cases.items():
         for _ in range(3):
             fn()
         torch.cuda.synchronize()
-        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(a.iters)]
+        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(iters)]
         s = torch.cuda.current_stream()
         for e0, e1 in ev:
             e0.record(s)
@@ -92,7 +107,7 @@ def main():
         torch.cuda.synchronize()
         ms = sorted(e0.elapsed_time(e1) for e0, e1 in ev)
         med = ms[len(ms) // 2]
-        print(json.dumps({"case": name, "ms_median": round(med, 4), "ms_min": round(ms[0], 4),
+        print(json.dumps({"case": name, **({"knobs": tag} if tag else {}), "ms_median": round(med, 4), "ms_min": round(ms[0], 4),
                           "alg_GBps": round(nbytes / med / 1e6, 1), "frac_8TBps": round(nbytes / med / 1e6 / 8000, 4),
                           "Mpx_s": round(px / med / 1e3, 1)}), flush=True)
 
