@@ -162,6 +162,32 @@ def test_resize_normalize(ops, dev, oracle):
         assert_same(out[k], oracle.normalize(oracle.u8_to_f32(r), m, s), "resize_normalize auto")
 
 
+def test_resize_normalize_bench_batch(ops, dev, oracle):
+    """The bench workload at its full size (256 x 1080p, one launch): images
+    spread over the batch match the oracle bit for bit, every image equals the
+    kernel's own single-image result (batch invariance), and a stripe of the
+    batch has the oracle's checksum."""
+    import torch
+    g = torch.Generator(device=dev)
+    g.manual_seed(7)
+    src = torch.randint(0, 256, (256, 1080, 1920, 3), dtype=torch.uint8, device=dev, generator=g)
+    out = ops.resize_normalize(src, 640, 360, MEAN, STD)
+    torch.cuda.synchronize(dev)
+    for k in (0, 1, 77, 128, 255):
+        img = host(src[k])
+        want = oracle.normalize(oracle.u8_to_f32(oracle.resize_linear(img, 640, 360)), MEAN, STD)
+        assert_same(host(out[k]), want, f"bench batch image {k}")
+    for k in (3, 200):
+        single = ops.resize_normalize(src[k:k + 1], 640, 360, MEAN, STD)
+        assert torch.equal(single[0], out[k]), f"batch invariance {k}"
+    # u8 resize of the same batch: per-image checksums of a stripe vs the oracle
+    r8 = ops.resize(src, 640, 360)
+    for k in range(16, 24):
+        assert sha(host(r8[k])) == sha(oracle.resize_linear(host(src[k]), 640, 360)), f"u8 stripe {k}"
+    del src, out, r8
+    torch.cuda.empty_cache()
+
+
 # ---------------------------------------------------------------------------
 # warp affine
 

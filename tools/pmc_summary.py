@@ -1,7 +1,10 @@
 #!/usr/bin/env python3
 """Summarise rocprofv3 --pmc CSV passes per kernel (mean per dispatch).
 
-  python tools/pmc_summary.py gpurun_out/pmc_dir [kernel-substring ...]
+  python tools/pmc_summary.py gpurun_out/pmc_dir [kernel-substring ...] [--out file.json]
+With --out, the first matching kernel's corrected HBM bytes per launch are
+written as {"kernel", "hbm_bytes_per_launch", "fetch_bytes", "write_bytes",
+"counters"} (what bench.py reads as roofline.traffic).
 FETCH_SIZE / WRITE_SIZE are reported raw (KB, as rocprofv3 gives them) and
 as bytes with the gfx950 correction of MI355X_MICROARCH.md §HBM (FETCH_SIZE
 counts half of a 16-B/lane streaming read: x2)."""
@@ -13,8 +16,14 @@ import sys
 
 
 def main():
-    d = sys.argv[1]
-    keys = sys.argv[2:] or [""]
+    argv = sys.argv[1:]
+    out_path = None
+    if "--out" in argv:
+        i = argv.index("--out")
+        out_path = argv[i + 1]
+        del argv[i:i + 2]
+    d = argv[0]
+    keys = argv[1:] or [""]
     rows = collections.defaultdict(lambda: collections.defaultdict(list))
     for f in sorted(glob.glob(f"{d}/**/*counter_collection.csv", recursive=True)):
         for r in csv.DictReader(open(f)):
@@ -33,6 +42,14 @@ def main():
             m["write_bytes"] = m["WRITE_SIZE"] * 1024
         out[kname] = m
     print(json.dumps(out, indent=1))
+    if out_path and out:
+        kname, m = next(iter(out.items()))
+        rec = {"kernel": kname, "fetch_bytes": m.get("fetch_bytes_corrected"), "write_bytes": m.get("write_bytes"),
+               "hbm_bytes_per_launch": (m.get("fetch_bytes_corrected") or 0) + (m.get("write_bytes") or 0),
+               "correction": "FETCH_SIZE x 1024 x 2 (gfx950 16-B/lane streaming reads), WRITE_SIZE x 1024",
+               "counters": m}
+        with open(out_path, "w") as f:
+            json.dump(rec, f, indent=1)
 
 
 if __name__ == "__main__":
