@@ -1,0 +1,99 @@
+// Internal: per-device HIP streams and staging scratch for the C++ layer.
+// Not installed with the public headers.
+#ifndef VACV_HIP_CONTEXT_H
+#define VACV_HIP_CONTEXT_H
+
+#include <hip/hip_runtime_api.h>
+
+#include <cstddef>
+#include <vector>
+
+#include "../../../include/vacv_hip.h"
+#include "tensor.h"
+
+namespace vision {
+namespace detail {
+
+/// Throws std::runtime_error("<fn>: <reason>") when status != VACV_OK.
+void check(const char* fn, int status);
+void check_hip(const char* fn, hipError_t e);
+[[noreturn]] void fail(const char* fn, const char* why);
+
+/// The device an op on `t` runs on: its own for device tensors, else the
+/// calling thread's current HIP device.
+int compute_device(const Tensor& t);
+
+/// A stream plus grow-only HBM scratch slots on one device, leased from a
+/// process-wide pool for the duration of one operator call (so concurrent
+/// callers never share a stream or scratch).  Makes `device` current for the
+/// lease and restores the previous device afterwards.
+class Lease {
+public:
+    explicit Lease(int device);
+    ~Lease();
+    Lease(const Lease&) = delete;
+    Lease& operator=(const Lease&) = delete;
+
+    int device() const { return _device; }
+    hipStream_t stream() const;
+    /// HBM scratch of >= bytes in slot 0..kSlots-1 (contents undefined)
+    void* scratch(int slot, size_t bytes);
+    /// wait for everything queued on the stream; throws on a HIP error
+    void sync(const char* fn);
+
+    static constexpr int kSlots = 4;
+    struct Ctx;  // stream + scratch, defined in hip_context.cpp
+
+private:
+    Ctx* _ctx;
+    int _device;
+    int _prev;
+};
+
+/// Descriptor of a dense single image (n = 1) at `data`.
+vacv_image describe(const Tensor& t, void* data);
+inline vacv_image describe(const Tensor& t) { return describe(t, t.data); }
+
+/// One operator call: leases the compute device's stream, gives the kernels
+/// HBM views of every operand, and moves host operands across PCIe.
+///   in():  a device tensor is used in place; a host tensor is copied
+///          (hipMemcpyAsync, DMA from the pinned pool) into scratch.
+///   out(): creates `dst` with the anchor's placement (the reference's
+///          dst.create, tensor.cpp:512-540); a host dst gets a scratch HBM
+///          buffer whose bytes finish() copies back.
+///   finish(): queues the copies back and waits for the stream -- the
+///          reference's ops are synchronous and so are these.
+/// Inputs are kept alive (refcount) until finish(), so `dst` may alias `src`.
+class Staging {
+public:
+    Staging(const char* fn, const Tensor& anchor);
+    /// on an early exit (exception) waits for queued work before the kept
+    /// operands are released
+    ~Staging();
+    Staging(const Staging&) = delete;
+    Staging& operator=(const Staging&) = delete;
+    vacv_image in(const Tensor& t, int slot);
+    vacv_image out(Tensor& dst, int w, int h, int c, DType dtype, DLayout layout, int slot);
+    /// fail loudly on a non-OK status from the C ABI
+    void run(int status) { check(_fn, status); }
+    void finish();
+    hipStream_t stream() const { return _lease.stream(); }
+    int placement() const { return _placement; }
+
+private:
+    struct Copy {
+        void* host;
+        const void* dev;
+        size_t bytes;
+    };
+    const char* _fn;
+    int _placement;
+    Lease _lease;
+    std::vector<Tensor> _keep;
+    std::vector<Copy> _d2h;
+};
+
+}  // namespace detail
+}  // namespace vision
+
+#endif  // VACV_HIP_CONTEXT_H

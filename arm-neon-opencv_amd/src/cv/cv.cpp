@@ -1,0 +1,244 @@
+// va_cv:: over the C ABI (include/vacv_hip.h).  Each function reproduces the
+// reference operator's output-tensor contract (shape, dtype, layout via
+// dst.create) and hands the pixel work to the HIP kernels; detail::Staging
+// moves host operands across PCIe and leaves device operands in HBM.
+#include "cv.h"
+
+#include <cstring>
+#include <vector>
+
+#include "../common/hip_context.h"
+
+namespace va_cv {
+
+using namespace vision;
+using detail::fail;
+using detail::Staging;
+
+namespace {
+
+// Small host-side parameter vectors (mean / stddev / M) read from a Tensor of
+// FP32 values, wherever it lives.
+std::vector<float> host_floats(const char* fn, const Tensor& t, size_t want) {
+    if (t.dtype != FP32) fail(fn, "parameter tensors must be FP32");
+    if (t.size() != want) fail(fn, "parameter tensor has the wrong number of values");
+    const Tensor h = t.to_host();
+    std::vector<float> v(want);
+    std::memcpy(v.data(), h.data, want * sizeof(float));
+    return v;
+}
+
+// mean / stddev: (nullptr, nullptr) = per-image statistics.  `either_empty`
+// picks the rule of resize_normalize_opencv (resize_normalize.cpp:58: either
+// empty -> computed); otherwise both must be empty (normalize.cpp:98).
+struct Stats {
+    std::vector<float> mean, stdv;
+    const float* m() const { return mean.empty() ? nullptr : mean.data(); }
+    const float* s() const { return stdv.empty() ? nullptr : stdv.data(); }
+};
+
+Stats read_stats(const char* fn, const Tensor& mean, const Tensor& stddev, int c, bool either_empty) {
+    Stats st;
+    const bool me = mean.empty(), se = stddev.empty();
+    if (me && se) return st;
+    if (me || se) {
+        if (either_empty) return st;
+        fail(fn, "mean and stddev must both be given or both be empty");
+    }
+    // resize_normalize.cpp:82-84 / normalize.cpp: one value per channel
+    if ((int)mean.size() != c || (int)stddev.size() != c)
+        fail(fn, "The input mean or stddev channels is not matched with tensor dims");
+    st.mean = host_floats(fn, mean, c);
+    st.stdv = host_floats(fn, stddev, c);
+    return st;
+}
+
+DType resize_out_dtype(const char* fn, const Tensor& src, int interpolation) {
+    if (interpolation == INTER_LINEAR) {
+        if (src.dtype != INT8 && src.dtype != FP32) fail(fn, "INTER_LINEAR takes INT8 or FP32");
+        return src.dtype;
+    }
+    if (interpolation == INTER_CUBIC) {
+        if (src.dtype != INT8 && src.dtype != FP32) fail(fn, "INTER_CUBIC takes INT8 or FP32");
+        return FP32;  // INT8 cubic = fused widen to FP32 (reference: infinite recursion)
+    }
+    // resize.cpp:46-49 hands every other mode to OpenCV, which this build
+    // does not ship (the reference without OpenCV recurses forever)
+    fail(fn, "only INTER_LINEAR and INTER_CUBIC are supported");
+}
+
+std::vector<float> affine_of(const char* fn, const Tensor& M) { return host_floats(fn, M, 6); }
+
+void check_warp_modes(const char* fn, const Tensor& src, int flags, int borderMode) {
+    // warp_affine.cpp:114-118
+    if (src.dtype != INT8 && src.dtype != FP32) fail(fn, "warp_affine takes INT8 or FP32");
+    if (flags != INTER_LINEAR) fail(fn, "only INTER_LINEAR is supported");
+    if (borderMode != BORDER_CONSTANT) fail(fn, "only BORDER_CONSTANT is supported");
+}
+
+std::vector<float> rotation(float scale, float rot, const VScalar& aux) {
+    const double a[4] = {aux.v0, aux.v1, aux.v2, aux.v3};
+    std::vector<float> m(6);
+    detail::check("va_cv::warp_affine", vacv_rotation_matrix(scale, rot, a, m.data()));
+    return m;
+}
+
+void warp_into(const char* fn, const Tensor& src, Tensor& dst, const float* m, VSize dsize, int flags,
+               int borderMode, const VScalar& bv, bool normalize, const Stats* stats) {
+    check_warp_modes(fn, src, flags, borderMode);
+    if (dsize.w < 1 || dsize.h < 1) fail(fn, "dsize must be positive");
+    const double border[4] = {bv.v0, bv.v1, bv.v2, bv.v3};
+    Staging st(fn, src);
+    const vacv_image s = st.in(src, 0);
+    const vacv_image d = st.out(dst, dsize.w, dsize.h, src.c, normalize ? FP32 : src.dtype, src.layout, 1);
+    if (normalize) {
+        st.run(vacv_warp_affine_normalize(&s, &d, m, flags, borderMode, border, stats->m(), stats->s(),
+                                          st.stream()));
+    } else {
+        st.run(vacv_warp_affine(&s, &d, m, flags, borderMode, border, st.stream()));
+    }
+    st.finish();
+}
+
+int yuv_rows(const char* fn, const Tensor& src) {
+    if (src.dtype != INT8 || src.c != 1) fail(fn, "YUV420sp input must be a (w, h*3/2, 1) INT8 tensor");
+    return src.h / 3 * 2;  // cvt_color.cpp:152
+}
+
+void check_yuv_code(const char* fn, int code) {
+    if (code != COLOR_YUV2BGR_NV21 && code != COLOR_YUV2RGB_NV21 && code != COLOR_YUV2BGR_NV12 &&
+        code != COLOR_YUV2RGB_NV12)
+        fail(fn, "unsupported colour conversion code");
+}
+
+}  // namespace
+
+void resize(const Tensor& src, Tensor& dst, VSize dsize, double /*fx*/, double /*fy*/, int interpolation) {
+    static const char* fn = "va_cv::resize";
+    const DType out = resize_out_dtype(fn, src, interpolation);
+    if (dsize.w < 1 || dsize.h < 1) fail(fn, "dsize must be positive");
+    Staging st(fn, src);
+    const vacv_image s = st.in(src, 0);
+    const vacv_image d = st.out(dst, dsize.w, dsize.h, src.c, out, src.layout, 1);
+    st.run(vacv_resize(&s, &d, interpolation, VACV_LINEAR_REFERENCE, st.stream()));
+    st.finish();
+}
+
+void cvt_color(const Tensor& src, Tensor& dst, int code) {
+    static const char* fn = "va_cv::cvt_color";
+    check_yuv_code(fn, code);
+    const int h = yuv_rows(fn, src);
+    Staging st(fn, src);
+    const vacv_image s = st.in(src, 0);
+    const vacv_image d = st.out(dst, src.w, h, 3, INT8, NHWC, 1);
+    st.run(vacv_cvt_color(&s, &d, code, st.stream()));
+    st.finish();
+}
+
+void cvt_color_normalize(const Tensor& src, Tensor& dst, int code, const Tensor& mean, const Tensor& stddev) {
+    static const char* fn = "va_cv::cvt_color_normalize";
+    check_yuv_code(fn, code);
+    const int h = yuv_rows(fn, src);
+    const Stats stats = read_stats(fn, mean, stddev, 3, false);
+    Staging st(fn, src);
+    const vacv_image s = st.in(src, 0);
+    const vacv_image d = st.out(dst, src.w, h, 3, FP32, NHWC, 1);
+    st.run(vacv_cvt_color_normalize(&s, &d, code, stats.m(), stats.s(), st.stream()));
+    st.finish();
+}
+
+void normalize(const Tensor& src, Tensor& dst, const Tensor& mean, const Tensor& stddev) {
+    static const char* fn = "va_cv::normalize";
+    if (src.dtype != INT8 && src.dtype != FP32) fail(fn, "normalize takes INT8 or FP32");
+    const Stats stats = read_stats(fn, mean, stddev, src.c, false);
+    Staging st(fn, src);
+    const vacv_image s = st.in(src, 0);
+    const vacv_image d = st.out(dst, src.w, src.h, src.c, FP32, src.layout, 1);
+    st.run(vacv_normalize(&s, &d, stats.m(), stats.s(), st.stream()));
+    st.finish();
+}
+
+void mean_stddev(const Tensor& src, Tensor& mean, Tensor& stddev) {
+    static const char* fn = "va_cv::mean_stddev";
+    if (src.dtype != INT8 && src.dtype != FP32) fail(fn, "mean_stddev takes INT8 or FP32");
+    Staging st(fn, src);
+    const vacv_image s = st.in(src, 0);
+    const vacv_image m = st.out(mean, src.c, 1, 1, FP32, NCHW, 1);
+    const vacv_image d = st.out(stddev, src.c, 1, 1, FP32, NCHW, 2);
+    st.run(vacv_mean_stddev(&s, static_cast<float*>(m.data), static_cast<float*>(d.data), st.stream()));
+    st.finish();
+}
+
+void warp_affine(const Tensor& src, Tensor& dst, const Tensor& M, VSize dsize, int flags, int borderMode,
+                 const VScalar& borderValue) {
+    static const char* fn = "va_cv::warp_affine";
+    const std::vector<float> m = affine_of(fn, M);
+    warp_into(fn, src, dst, m.data(), dsize, flags, borderMode, borderValue, false, nullptr);
+}
+
+void warp_affine(const Tensor& src, Tensor& dst, float scale, float rot, VSize dsize, const VScalar& aux_param,
+                 int flags, int borderMode, const VScalar& borderValue) {
+    static const char* fn = "va_cv::warp_affine";
+    const std::vector<float> m = rotation(scale, rot, aux_param);
+    warp_into(fn, src, dst, m.data(), dsize, flags, borderMode, borderValue, false, nullptr);
+}
+
+void resize_normalize(const Tensor& src, Tensor& dst, VSize dsize, double /*fx*/, double /*fy*/, int interpolation,
+                      const Tensor& mean, const Tensor& stddev) {
+    static const char* fn = "va_cv::resize_normalize";
+    (void)resize_out_dtype(fn, src, interpolation);
+    if (dsize.w < 1 || dsize.h < 1) fail(fn, "dsize must be positive");
+    const Stats stats = read_stats(fn, mean, stddev, src.c, true);
+    Staging st(fn, src);
+    const vacv_image s = st.in(src, 0);
+    const vacv_image d = st.out(dst, dsize.w, dsize.h, src.c, FP32, src.layout, 1);
+    st.run(vacv_resize_normalize(&s, &d, interpolation, VACV_LINEAR_REFERENCE, stats.m(), stats.s(), st.stream()));
+    st.finish();
+}
+
+void warp_affine_normalize(const Tensor& src, Tensor& dst, const Tensor& M, VSize dsize, int flags, int borderMode,
+                           const VScalar& borderValue, const Tensor& mean, const Tensor& stddev) {
+    static const char* fn = "va_cv::warp_affine_normalize";
+    const std::vector<float> m = affine_of(fn, M);
+    const Stats stats = read_stats(fn, mean, stddev, src.c, false);
+    warp_into(fn, src, dst, m.data(), dsize, flags, borderMode, borderValue, true, &stats);
+}
+
+void warp_affine_normalize(const Tensor& src, Tensor& dst, float scale, float rot, VSize dsize,
+                           const VScalar& aux_param, int flags, int borderMode, const VScalar& borderValue,
+                           const Tensor& mean, const Tensor& stddev) {
+    static const char* fn = "va_cv::warp_affine_normalize";
+    const std::vector<float> m = rotation(scale, rot, aux_param);
+    const Stats stats = read_stats(fn, mean, stddev, src.c, false);
+    warp_into(fn, src, dst, m.data(), dsize, flags, borderMode, borderValue, true, &stats);
+}
+
+void crop(const Tensor& src, Tensor& dst, const VRect& rect) {
+    static const char* fn = "va_cv::crop";
+    // crop.cpp:128-131
+    const int left = static_cast<int>(rect.left);
+    const int top = static_cast<int>(rect.top);
+    const int cw = static_cast<int>(rect.width());
+    const int ch = static_cast<int>(rect.height());
+    if (cw < 1 || ch < 1 || left < 0 || top < 0 || left + cw > src.w || top + ch > src.h)
+        fail(fn, "rect must lie inside the image");  // the reference reads out of bounds
+    Staging st(fn, src);
+    const vacv_image s = st.in(src, 0);
+    const vacv_image d = st.out(dst, cw, ch, src.c, src.dtype, src.layout, 1);
+    st.run(vacv_crop(&s, &d, left, top, st.stream()));
+    st.finish();
+}
+
+void match_template(const Tensor&, const Tensor&, Tensor&, int) {
+    fail("va_cv::match_template", "not provided by the MI355X build (OpenCV-only in the reference)");
+}
+
+void minMaxIdx(const Tensor&, double*, double*, int*, int*, const Tensor&) {
+    fail("va_cv::minMaxIdx", "not provided by the MI355X build (OpenCV-only in the reference)");
+}
+
+void imencode(const Tensor&, std::vector<unsigned char>&, const char*) {
+    fail("va_cv::imencode", "not provided by the MI355X build (OpenCV-only in the reference)");
+}
+
+}  // namespace va_cv
