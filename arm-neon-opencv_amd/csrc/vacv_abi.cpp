@@ -12,6 +12,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdint>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <mutex>
@@ -266,7 +267,19 @@ int resize_impl(const vacv_image* src_d, const vacv_image* dst_d, int interpolat
     L.scale_yf = (float)src.h / (float)dst.h;
     L.scale_xd = (double)src.w / (double)dst.w;
     L.scale_yd = (double)src.h / (double)dst.h;
-    if ((st = plan_resize(L, s))) return st;
+    // resize_kernel with interleaved (address-ordered) tasks by default;
+    // VACV_RESIZE_INTERLEAVE=0 selects its strip order and VACV_RESIZE_ROWS=1
+    // the whole-row kernel, for A/B measurement
+    const char* il_env = std::getenv("VACV_RESIZE_INTERLEAVE");
+    L.interleave = !(il_env && il_env[0] == '0');
+    const char* rows_env = std::getenv("VACV_RESIZE_ROWS");
+    L.rows_mode = rows_env && rows_env[0] == '1';
+    if (L.rows_mode) {
+        st = plan_resize(L, s, 1);
+        if (st == VACV_ERR_UNSUPPORTED) L.rows_mode = 0;
+        else if (st) return st;
+    }
+    if (!L.rows_mode && (st = plan_resize(L, s, 0))) return st;
     return hip_status(launch_resize(L, s));
 }
 

@@ -13,12 +13,14 @@ namespace vacv {
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
 // Cache-policy aux bits of the streaming buffer loads / stores (gfx950:
-// 1 = sc0, 2 = nt, 16 = sc1).  Source rows and outputs are touched once.
+// 1 = sc0, 2 = nt, 16 = sc1).  Source rows and outputs are touched once:
+// non-temporal on both sides measured 2-7 % faster on the resize kernels
+// (profiles/r01_kbench.jsonl vs the nt sweep in DESIGN.md §3.1).
 #ifndef VACV_LOAD_AUX
-#define VACV_LOAD_AUX 0
+#define VACV_LOAD_AUX 2
 #endif
 #ifndef VACV_STORE_AUX
-#define VACV_STORE_AUX 0
+#define VACV_STORE_AUX 2
 #endif
 
 // A raw buffer resource over [base16, base16 + bytes): loads past the end
