@@ -4,6 +4,8 @@
 // alignment allows and falls back to narrower accesses only at row tails.
 #pragma clang fp contract(off)
 
+#include <cstdlib>
+
 #include "vacv_device.hpp"
 
 namespace vacv {
@@ -11,6 +13,8 @@ namespace {
 
 __device__ __forceinline__ int64_t gtid() { return (int64_t)blockIdx.x * blockDim.x + threadIdx.x; }
 __device__ __forceinline__ int64_t gstride() { return (int64_t)gridDim.x * blockDim.x; }
+
+constexpr int kColorPairs = 1;  // row pairs per wave in color_kernel (4 measured 15 % slower)
 
 int grid_for(int64_t work_items, int cap = 256 * 16) {
     int64_t g = (work_items + kBlock - 1) / kBlock;
@@ -129,6 +133,40 @@ __global__ void __launch_bounds__(kBlock) u8_to_f32_kernel(DtypeLaunch L) {
         reinterpret_cast<float*>(L.dst)[i] = (float)L.src[i];
 }
 
+// One dword of u8 in, one 16-byte float4 out per thread over a grid that
+// covers the buffer once, in order (the shape that streams fastest on MI355X,
+// tools/membench2.hip); non-temporal stores.  Needs 4-byte aligned u8 and
+// 16-byte aligned fp32; the last count % 4 elements go through the tail.
+__global__ void __launch_bounds__(kBlock) u8_to_f32_flat_kernel(DtypeLaunch L) {
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    const int64_t n4 = L.count >> 2;
+    if (i < n4) {
+        const uint32_t w = __builtin_nontemporal_load(reinterpret_cast<const uint32_t*>(L.src) + i);
+        const u32x4 f = {__float_as_uint((float)(w & 0xFF)), __float_as_uint((float)((w >> 8) & 0xFF)),
+                         __float_as_uint((float)((w >> 16) & 0xFF)), __float_as_uint((float)(w >> 24))};
+        __builtin_nontemporal_store(f, reinterpret_cast<u32x4*>(L.dst) + i);
+    } else if (i - n4 < (L.count & 3)) {
+        const int64_t e = (n4 << 2) + (i - n4);
+        reinterpret_cast<float*>(L.dst)[e] = (float)L.src[e];
+    }
+}
+
+__global__ void __launch_bounds__(kBlock) f32_to_u8_flat_kernel(DtypeLaunch L) {
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    const int64_t n4 = L.count >> 2;
+    if (i < n4) {
+        const u32x4 f = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(L.src) + i);
+        const uint32_t w = (uint32_t)f32_to_u8_neon(__uint_as_float(f.x)) |
+                           ((uint32_t)f32_to_u8_neon(__uint_as_float(f.y)) << 8) |
+                           ((uint32_t)f32_to_u8_neon(__uint_as_float(f.z)) << 16) |
+                           ((uint32_t)f32_to_u8_neon(__uint_as_float(f.w)) << 24);
+        __builtin_nontemporal_store(w, reinterpret_cast<uint32_t*>(L.dst) + i);
+    } else if (i - n4 < (L.count & 3)) {
+        const int64_t e = (n4 << 2) + (i - n4);
+        L.dst[e] = f32_to_u8_neon(reinterpret_cast<const float*>(L.src)[e]);
+    }
+}
+
 __global__ void __launch_bounds__(kBlock) f32_to_u8_kernel(DtypeLaunch L) {
     const int64_t n16 = L.count >> 4;
     for (int64_t i = gtid(); i < n16; i += gstride()) {
@@ -165,9 +203,18 @@ __global__ void __launch_bounds__(kBlock) color_kernel(ColorLaunch L) {
         }
         __syncthreads();
     }
+    // fp32 output: a wave's 64 lanes x 48 B of one row go out through LDS as
+    // three 1 KiB contiguous non-temporal stores (lane-strided 48-B stores
+    // measured 0.37 of the HBM roofline)
+    constexpr bool kXch = OUT != kOutSame;
+    __shared__ u32x4 xch[kXch ? 4 : 1][kXch ? 192 : 1];
     const int x0 = (blockIdx.x * blockDim.x + threadIdx.x) * 4;
-    const int yy = blockIdx.y * blockDim.y + threadIdx.y;  // row pair
-    if (x0 >= L.w || 2 * yy >= L.h) return;
+    if (x0 >= L.w) return;
+    const bool wave_full = (int)(blockIdx.x + 1) * 256 <= L.w;  // uniform: every lane has 4 pixels
+    // each wave takes kColorPairs row pairs (the block's table is built once)
+    for (int it = 0; it < kColorPairs; ++it) {
+    const int yy = (blockIdx.y * kColorPairs + it) * blockDim.y + threadIdx.y;  // row pair (wave-uniform)
+    if (2 * yy >= L.h) break;
 
     const unsigned char* yb = L.src + (int64_t)img * L.src_img;
     const unsigned char* y0p = yb + (int64_t)(2 * yy) * L.src_row + x0;
@@ -220,6 +267,28 @@ __global__ void __launch_bounds__(kBlock) color_kernel(ColorLaunch L) {
         unsigned char* dp = L.dst + (int64_t)img * L.dst_img + (int64_t)(2 * yy + r) * L.dst_row +
                             (int64_t)x0 * 3 * sizeof(TOut);
         constexpr int kBytes = 12 * (int)sizeof(TOut);
+        if constexpr (kXch) {
+            unsigned char* wbase = L.dst + (int64_t)img * L.dst_img + (int64_t)(2 * yy + r) * L.dst_row +
+                                   (int64_t)blockIdx.x * 256 * 12;
+            if (wave_full && (reinterpret_cast<uintptr_t>(wbase) & 15) == 0) {  // uniform
+                const int lane = threadIdx.x;
+                u32x4* w = xch[threadIdx.y];
+#pragma unroll
+                for (int b = 0; b < 3; ++b)
+                    w[lane * 3 + b] = u32x4{__float_as_uint(out[4 * b]), __float_as_uint(out[4 * b + 1]),
+                                            __float_as_uint(out[4 * b + 2]), __float_as_uint(out[4 * b + 3])};
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+                for (int b = 0; b < 3; ++b)
+                    __builtin_nontemporal_store(w[b * 64 + lane], reinterpret_cast<u32x4*>(wbase) + b * 64 + lane);
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();  // the next row reuses the exchange buffer
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                continue;
+            }
+        }
         if (valid == 4 && (kBytes % 16 == 0) && ((reinterpret_cast<uintptr_t>(dp) & 15) == 0)) {
 #pragma unroll
             for (int b = 0; b < kBytes / 16; ++b) reinterpret_cast<uint4*>(dp)[b] = reinterpret_cast<const uint4*>(out)[b];
@@ -232,6 +301,82 @@ __global__ void __launch_bounds__(kBlock) color_kernel(ColorLaunch L) {
             for (int e = 0; e < 12; ++e)
                 if (e < 3 * valid) o[e] = out[e];
         }
+    }
+    }  // row pairs
+}
+
+// --------------------------------------------------------------------------
+// YUV420sp -> BGR with an fp32 output (+ normalize), the BASELINE cfg3 path.
+// Output-stationary: one thread = one 16-byte output chunk (4 consecutive
+// elements of a row), chunks numbered in address order over the batch, so
+// every wave stores 1 KiB contiguously (non-temporal) and the grid sweeps
+// HBM in order.  The chunk's (at most two) pixels read their Y and chroma
+// bytes from the L1/L2-resident input rows; each input byte leaves HBM once.
+template <int OUT>
+__global__ void __launch_bounds__(kBlock) color_f32_kernel(ColorLaunch L, uint32_t cpo) {
+    const uint32_t g = blockIdx.x * kBlock + threadIdx.x;
+    const uint32_t r = g / cpo;  // image * h + y
+    if (r >= (uint32_t)L.n * L.h) return;
+    const int e0 = (int)(g - r * cpo) * 4;
+    const int img = (int)(r / L.h);
+    const int y = (int)r - img * L.h;
+    const int rl = 3 * L.w;
+
+    const unsigned char* yrow = L.src + (int64_t)img * L.src_img + (int64_t)y * L.src_row;
+    const unsigned char* uvrow = L.src + (int64_t)img * L.src_img + (int64_t)(L.h + (y >> 1)) * L.src_row;
+    const int p0 = e0 / 3;
+    const int p1 = min((e0 + 3) / 3, L.w - 1);
+    int bgr[2][3];
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+        const int px = q ? p1 : p0;
+        const int pair = px & ~1;
+        const int Y = yrow[px];
+        const int a = uvrow[pair], b = uvrow[pair + 1];
+        const Chroma ch = chroma_terms(L.v_first ? b : a, L.v_first ? a : b);  // (u, v)
+        const int R = clamp_u8(Y + ch.ra), G = clamp_u8(Y - ch.ga), B = clamp_u8(Y + ch.ba);
+        bgr[q][0] = L.rgb ? R : B;
+        bgr[q][1] = G;
+        bgr[q][2] = L.rgb ? B : R;
+    }
+    float m[3] = {0.f, 0.f, 0.f}, sd[3] = {1.f, 1.f, 1.f};
+    if (OUT == kOutNorm) {
+#pragma unroll
+        for (int k = 0; k < 3; ++k) norm_params(L.norm, img, k, m[k], sd[k]);
+    }
+    float o[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int e = min(e0 + i, rl - 1);
+        const int px = e / 3;
+        const int k = e - px * 3;
+        const int q = px != p0;
+        const int v = q ? (k == 0 ? bgr[1][0] : (k == 1 ? bgr[1][1] : bgr[1][2]))
+                        : (k == 0 ? bgr[0][0] : (k == 1 ? bgr[0][1] : bgr[0][2]));
+        if (OUT == kOutNorm) {
+            const float mk = k == 0 ? m[0] : (k == 1 ? m[1] : m[2]);
+            const double d = (double)((float)v - mk);
+            if (L.norm.mode == 1 && ((L.norm.mul_ok >> k) & 1u)) {
+                // host-verified exact for every u8 value (NormSpec.mul_ok)
+                o[i] = (float)(d * (k == 0 ? L.norm.inv[0] : (k == 1 ? L.norm.inv[1] : L.norm.inv[2])));
+            } else {
+                const float sk = k == 0 ? sd[0] : (k == 1 ? sd[1] : sd[2]);
+                o[i] = (float)(d / ((double)sk + 1e-6));  // normalize_naive.cpp:84-87
+            }
+        } else {
+            o[i] = (float)v;
+        }
+    }
+    unsigned char* drow = L.dst + (int64_t)img * L.dst_img + (int64_t)y * L.dst_row;
+    float* dp = reinterpret_cast<float*>(drow) + e0;
+    if (e0 + 4 <= rl && (reinterpret_cast<uintptr_t>(dp) & 15) == 0) {
+        __builtin_nontemporal_store(u32x4{__float_as_uint(o[0]), __float_as_uint(o[1]), __float_as_uint(o[2]),
+                                          __float_as_uint(o[3])},
+                                    reinterpret_cast<u32x4*>(dp));
+    } else {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+            if (e0 + i < rl) dp[i] = o[i];
     }
 }
 
@@ -461,6 +606,15 @@ hipError_t launch_layout(const LayoutLaunch& L, hipStream_t s) {
 }
 
 hipError_t launch_dtype(const DtypeLaunch& L, hipStream_t s) {
+    const uintptr_t a8 = reinterpret_cast<uintptr_t>(L.to_f32 ? L.src : L.dst);
+    const uintptr_t a32 = reinterpret_cast<uintptr_t>(L.to_f32 ? L.dst : L.src);
+    const int64_t threads = (L.count >> 2) + (L.count & 3);
+    if ((a8 & 3) == 0 && (a32 & 15) == 0 && threads <= (int64_t)0x7FFFFFFF * kBlock) {
+        const unsigned blocks = (unsigned)((threads + kBlock - 1) / kBlock);
+        if (L.to_f32) hipLaunchKernelGGL(u8_to_f32_flat_kernel, dim3(blocks), dim3(kBlock), 0, s, L);
+        else hipLaunchKernelGGL(f32_to_u8_flat_kernel, dim3(blocks), dim3(kBlock), 0, s, L);
+        return hipGetLastError();
+    }
     const int g = grid_for(L.count / 16 + 1);
     if (L.to_f32) hipLaunchKernelGGL(u8_to_f32_kernel, dim3(g), dim3(kBlock), 0, s, L);
     else hipLaunchKernelGGL(f32_to_u8_kernel, dim3(g), dim3(kBlock), 0, s, L);
@@ -468,8 +622,17 @@ hipError_t launch_dtype(const DtypeLaunch& L, hipStream_t s) {
 }
 
 hipError_t launch_color(const ColorLaunch& L, hipStream_t s) {
+    const uint32_t cpo = (uint32_t)((3LL * L.w + 3) / 4);
+    const uint64_t chunks = (uint64_t)cpo * L.n * L.h;
+    const char* env = std::getenv("VACV_COLOR_CHUNKS");
+    if (L.out != kOutSame && chunks < (1ull << 32) - kBlock && env && env[0] == '1') {  // opt-in: measured slower (VALU-bound)
+        const uint32_t blocks = (uint32_t)((chunks + kBlock - 1) / kBlock);
+        if (L.out == kOutF32) hipLaunchKernelGGL(color_f32_kernel<kOutF32>, dim3(blocks), dim3(kBlock), 0, s, L, cpo);
+        else hipLaunchKernelGGL(color_f32_kernel<kOutNorm>, dim3(blocks), dim3(kBlock), 0, s, L, cpo);
+        return hipGetLastError();
+    }
     dim3 block(64, 4);
-    dim3 grid((L.w / 4 + 64) / 64, (L.h / 2 + 3) / 4, L.n);
+    dim3 grid((L.w / 4 + 64) / 64, (L.h / 2 + 4 * kColorPairs - 1) / (4 * kColorPairs), L.n);
     if (L.out == kOutSame) hipLaunchKernelGGL(color_kernel<kOutSame>, grid, block, 0, s, L);
     else if (L.out == kOutF32) hipLaunchKernelGGL(color_kernel<kOutF32>, grid, block, 0, s, L);
     else hipLaunchKernelGGL(color_kernel<kOutNorm>, grid, block, 0, s, L);

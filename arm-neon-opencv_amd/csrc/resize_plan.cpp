@@ -35,7 +35,7 @@ namespace {
 
 constexpr int kLdsBudget = 40 * 1024;   // per workgroup; 4 resident per CU
 constexpr int kMaxChunksPerThread = 8;  // register prefetch depth (uint4 per thread)
-constexpr int kWorkPerThread = 8;       // target output work items per thread per task
+constexpr int kWorkPerThread = 16;      // target output work items per thread per task (capped by LDS / prefetch registers)
 
 struct Taps {
     int origin;   // first tap (row or column)

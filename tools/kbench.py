@@ -95,7 +95,7 @@ def main():
 def run_cases(cases, iters, tag):
     import torch
     for name, (fn, nbytes, px) in cases.items():
-        for _ in range(3):
+        for _ in range(10):  # clocks settle before the timed launches
             fn()
         torch.cuda.synchronize()
         ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(iters)]
