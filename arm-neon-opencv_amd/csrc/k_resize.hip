@@ -88,23 +88,32 @@ struct Sampler<kLinearFixed, CC, uint8_t, MODE> {
     static constexpr int ES = 1;
     template <bool TWO>
     __device__ __forceinline__ static int at(const unsigned char* rows, int off, XW xw, const RowTaps& r) {
-        const int a0 = (int)(short)(xw & 0xFFFFu), a1 = (int)(short)(xw >> 16);
+        // The column weights a0, a1 and row weights wA, wB are SATURATE_CAST
+        // values of (1-f)*2048 and f*2048 with f in [0, 1], i.e. in
+        // [0, 2048]: xw = {a0, a1} is a u16 pair, the row sums tl*a0 + tr*a1
+        // (< 2^24) are one packed dot product (v_dot2_u32_u16), and every
+        // further product is an exact full-rate 24-bit multiply.
+        typedef unsigned short us2 __attribute__((ext_vector_type(2)));
+        const us2 wx = __builtin_bit_cast(us2, xw);
         const unsigned char* pa = rows + r.rb[0] + off;
         const unsigned char* pb = rows + r.rb[1] + off;
-        const int tl = pa[0], tr = pa[CC];
-        int bl = 0, br = 0;
-        if (TWO) { bl = pb[0]; br = pb[CC]; }
-        const int wA = r.w[0], wB = r.w[1];
+        const uint32_t top = (uint32_t)pa[0] | ((uint32_t)pa[CC] << 16);
+        uint32_t bot = 0;
+        if (TWO) bot = (uint32_t)pb[0] | ((uint32_t)pb[CC] << 16);
+        const uint32_t ht = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, top), wx, 0u, false);
+        const uint32_t hb = TWO ? __builtin_amdgcn_udot2(__builtin_bit_cast(us2, bot), wx, 0u, false) : 0u;
+        const uint32_t wA = (uint32_t)r.w[0], wB = (uint32_t)r.w[1];
         if (MODE == VACV_LINEAR_REFERENCE) {
-            // resize_naive.cpp:61-64: (Sum S*wx*wy) >> 22, stored as a byte.
-            // With one vertical tap (wB == 0) the sum factors exactly in int32.
-            if (TWO) return ((tl * a0 * wA + bl * a0 * wB + tr * a1 * wA + br * a1 * wB) >> 22) & 0xFF;
-            return (((tl * a0 + tr * a1) * wA) >> 22) & 0xFF;
+            // resize_naive.cpp:61-64: (Sum S*wx*wy) >> 22, stored as a byte;
+            // (tl*a0 + tr*a1)*wA + (bl*a0 + br*a1)*wB is the same int32 value
+            // (all terms >= 0, total <= 255*2049^2 < 2^31)
+            if (TWO) return (int)(((__umul24(ht, wA) + __umul24(hb, wB)) >> 22) & 0xFF);
+            return (int)((__umul24(ht, wA) >> 22) & 0xFF);
         }
         // resize_neon.cpp:103,122-123 (int16 rows), :150-167 (vertical)
-        const int h0 = (int)(short)((tl * a0 + tr * a1) >> 4);
-        const int h1 = (int)(short)((bl * a0 + br * a1) >> 4);
-        return clamp_u8((((h0 * wA) >> 16) + ((h1 * wB) >> 16) + 2) >> 2);
+        const int h0 = (int)(short)(ht >> 4);
+        const int h1 = (int)(short)(hb >> 4);
+        return clamp_u8((((h0 * (int)wA) >> 16) + ((h1 * (int)wB) >> 16) + 2) >> 2);
     }
 };
 

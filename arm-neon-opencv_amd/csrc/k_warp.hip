@@ -8,10 +8,20 @@
 // tap is outside [0,w-2]x[0,h-2]; u8 weights SAT((1-f)*2048) and 2048-that;
 // value (Sum S*wx*wy) >> 22.  Skipped pixels get the border value here.
 //
-// One thread = 4 consecutive output pixels of one row (vector stores); a
-// 64x4-thread block covers a 256x4 output tile so the source footprint of a
-// block is compact (L1/L2 reuse of the gathered taps).
+// A wave owns 256 consecutive output pixels of one row; lane l samples
+// pixels l, l+64, l+128, l+192 (so each gather instruction covers 64
+// consecutive pixels: ~20 source cache lines under a rotation instead of
+// 64), re-assembles the row segment in LDS and writes it with 16-byte
+// stores.  Taps: one unaligned 8-byte buffer load per source row, packed
+// u16 dot products for the fixed-point sum.  Blocks are ordered so each XCD
+// walks a contiguous range (its L2 keeps the shared source rows).
+// Measured alternative, kept out: staging each tile's source bounding box in
+// LDS (coalesced 16-B loads) ran 1.2-1.9x slower at 1280x720 rot15 -- the
+// box overlap between tiles and the per-tile barrier cost more than the
+// gathers it saves.
 #pragma clang fp contract(off)
+
+#include <cstdlib>
 
 #include "vacv_device.hpp"
 
@@ -22,16 +32,28 @@ constexpr int kPx = 4;
 
 template <int CC, typename TIn, int OUT>
 __global__ void __launch_bounds__(kBlock)
-warp_kernel(WarpLaunch L) {
+warp_kernel(WarpLaunch L, int gx, int gy, int total) {
     using TOut = typename std::conditional<(OUT == kOutSame), TIn, float>::type;
     constexpr bool kLut = std::is_same<TIn, uint8_t>::value && (OUT == kOutNorm);
+    constexpr int kRowBytes = 64 * kPx * CC * (int)sizeof(TOut);  // one wave's output row segment
     __shared__ float lut[kLut ? 256 * CC : 1];
+    __shared__ __attribute__((aligned(16))) unsigned char xch[4][kRowBytes];
 
-    const int pidx = blockIdx.z;
+    // XCD-aware block order: workgroup b runs on XCD b % 8, and each XCD
+    // walks one contiguous range of (plane, row band, column) blocks, so the
+    // rotated source rows that neighbouring blocks share stay in one L2
+    // (measured: scattered blocks fetched 3.7x the source bytes past L2)
+    const int per_xcd = (total + 7) / 8;
+    const int id = (int)(blockIdx.x % 8) * per_xcd + (int)(blockIdx.x / 8);
+    if (id >= total) return;  // uniform
+    const int pidx = id / (gx * gy);
+    const int rem = id - pidx * gx * gy;
+    const int by = rem / gx, bx = rem - by * gx;
     const int img = pidx / L.src.planes;
     const int plane = pidx - img * L.src.planes;
-    const int y = blockIdx.y * 4 + threadIdx.y;
-    const int x0 = (blockIdx.x * 64 + threadIdx.x) * kPx;
+    const int lane = threadIdx.x;
+    const int y = by * 4 + threadIdx.y;  // wave-uniform
+    const int xw = bx * 64 * kPx;        // the wave's first pixel
 
     float nmean[CC], nstd[CC];
     if (OUT == kOutNorm) {
@@ -46,20 +68,27 @@ warp_kernel(WarpLaunch L) {
         }
         __syncthreads();
     }
-    if (y >= L.dst.h || x0 >= L.dst.w) return;
+    if (y >= L.dst.h) return;  // whole wave
 
     const unsigned char* sp = L.src.base + (int64_t)img * L.src.img_pitch + (int64_t)plane * L.src.plane_pitch;
-    unsigned char* dp = const_cast<unsigned char*>(L.dst.base) + (int64_t)img * L.dst.img_pitch +
-                        (int64_t)plane * L.dst.plane_pitch + (int64_t)y * L.dst.row_pitch +
-                        (int64_t)x0 * CC * sizeof(TOut);
     const int64_t rp = L.src.row_pitch;
     const float fy_row = L.inv[1] * (float)y;
     const float gy_row = L.inv[4] * (float)y;
+    const Rsrc srs = make_rsrc(sp, L.src.plane_bytes);
+    const uint32_t slimit = (uint32_t)L.src.plane_bytes + srs.delta;
+    const uint32_t rp32 = (rp < (1 << 24) && L.src.h < (1 << 24)) ? (uint32_t)rp : 0u;  // 24-bit row offsets
+    TOut* xrow = reinterpret_cast<TOut*>(xch[threadIdx.y]);
 
-    TOut out[kPx * CC];
+    // Lane l samples pixels xw + q*64 + l: each wave gather instruction then
+    // reads 64 CONSECUTIVE output pixels, whose rotated source footprint spans
+    // ~20 cache lines instead of 64 (4 adjacent pixels per lane put every lane
+    // on its own source row).  The row segment is re-assembled in LDS and
+    // written as contiguous 16-byte stores.
 #pragma unroll
     for (int q = 0; q < kPx; ++q) {
-        const int x = x0 + q;
+        const int x = xw + q * 64 + lane;
+        if (x >= L.dst.w) continue;
+        TOut* o = xrow + (q * 64 + lane) * CC;
         // warp_affine_naive.cpp:23-24: (m0*x + m1*y) + m2, all float
         const float fx = L.inv[0] * (float)x + fy_row + L.inv[2];
         const float fy = L.inv[3] * (float)x + gy_row + L.inv[5];
@@ -70,10 +99,10 @@ warp_kernel(WarpLaunch L) {
 #pragma unroll
             for (int k = 0; k < CC; ++k) {
                 if (OUT == kOutNorm) {
-                    out[q * CC + k] = kLut ? (TOut)lut[k * 256 + (int)L.border[k]]
-                                           : (TOut)normalize_value(L.border[k], nmean[k], nstd[k]);
+                    o[k] = kLut ? (TOut)lut[k * 256 + (int)L.border[k]]
+                                : (TOut)normalize_value(L.border[k], nmean[k], nstd[k]);
                 } else {
-                    out[q * CC + k] = (TOut)L.border[k];
+                    o[k] = (TOut)L.border[k];
                 }
             }
             continue;
@@ -81,55 +110,97 @@ warp_kernel(WarpLaunch L) {
         const unsigned char* r0 = sp + (int64_t)sy * rp + (int64_t)sx * CC * sizeof(TIn);
         const unsigned char* r1 = r0 + rp;
         if (std::is_same<TIn, uint8_t>::value) {
-            const int wy0 = sat_short_away((1.f - ay) * 2048.f), wy1 = 2048 - wy0;
-            const int wx0 = sat_short_away((1.f - ax) * 2048.f), wx1 = 2048 - wx0;
+            // SATURATE_CAST_SHORT of a value in (0, 2048]: the +0.5f branch, no clamp
+            const int wy0 = (int)((1.f - ay) * 2048.f + 0.5f), wy1 = 2048 - wy0;
+            const int wx0 = (int)((1.f - ax) * 2048.f + 0.5f), wx1 = 2048 - wx0;
+            // the 2*CC tap bytes of each row in ONE (unaligned) buffer load;
+            // a load past the plane's end (its last pixel) falls back to bytes
+            uint32_t a0 = 0, a1 = 0, c0 = 0, c1 = 0;
+            const uint32_t o0 = (rp32 ? __umul24((uint32_t)sy, rp32) : (uint32_t)((int64_t)sy * rp)) +
+                                (uint32_t)(sx * CC) + srs.delta;
+            const uint32_t o1 = o0 + (uint32_t)rp;
+            if (CC <= 4 && o1 + 8u <= slimit) {
+                auto a = __builtin_amdgcn_raw_buffer_load_b64(srs.r, (int)o0, 0, 0);
+                auto c = __builtin_amdgcn_raw_buffer_load_b64(srs.r, (int)o1, 0, 0);
+                a0 = a[0]; a1 = a[1]; c0 = c[0]; c1 = c[1];
+            } else {
+#pragma unroll
+                for (int e = 0; e < 2 * CC && e < 8; ++e) {
+                    if (e < 4) { a0 |= (uint32_t)r0[e] << (8 * e); c0 |= (uint32_t)r1[e] << (8 * e); }
+                    else { a1 |= (uint32_t)r0[e] << (8 * (e - 4)); c1 |= (uint32_t)r1[e] << (8 * (e - 4)); }
+                }
+            }
+            // warp_affine_naive.cpp:50-54 as (tl*wx0 + tr*wx1)*wy0 + (bl*wx0 +
+            // br*wx1)*wy1: the same int32 value (exact, no overflow: <= 255*2^22),
+            // as one packed u16 dot product per row (v_dot2_u32_u16, tap pair
+            // gathered by v_perm_b32) and two full-rate 24-bit multiplies
+            typedef unsigned short us2 __attribute__((ext_vector_type(2)));
+            const us2 wx = __builtin_bit_cast(us2, (uint32_t)wx0 | ((uint32_t)wx1 << 16));
 #pragma unroll
             for (int k = 0; k < CC; ++k) {
-                const int tl = r0[k], tr = r0[CC + k], bl = r1[k], br = r1[CC + k];
-                // warp_affine_naive.cpp:50-54
-                const int v = ((tl * wx0 * wy0 + bl * wx0 * wy1 + tr * wx1 * wy0 + br * wx1 * wy1) >> 22) & 0xFF;
-                if (OUT == kOutSame) out[q * CC + k] = (TOut)v;
-                else if (OUT == kOutF32) out[q * CC + k] = (TOut)(float)v;
-                else out[q * CC + k] = (TOut)lut[k * 256 + v];
+                uint32_t top, bot;
+                if (CC <= 4) {
+                    const uint32_t sel = (uint32_t)k | (0x0Cu << 8) | ((uint32_t)(CC + k) << 16) | (0x0Cu << 24);
+                    top = __builtin_amdgcn_perm(a1, a0, sel);
+                    bot = __builtin_amdgcn_perm(c1, c0, sel);
+                } else {
+                    top = (uint32_t)r0[k] | ((uint32_t)r0[CC + k] << 16);
+                    bot = (uint32_t)r1[k] | ((uint32_t)r1[CC + k] << 16);
+                }
+                const uint32_t ht = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, top), wx, 0u, false);
+                const uint32_t hb = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, bot), wx, 0u, false);
+                const int v = (int)((__umul24(ht, (uint32_t)wy0) + __umul24(hb, (uint32_t)wy1)) >> 22);
+                if (OUT == kOutSame) o[k] = (TOut)v;
+                else if (OUT == kOutF32) o[k] = (TOut)(float)v;
+                else o[k] = (TOut)lut[k * 256 + v];
             }
         } else {
-            const float y0 = 1.f - ay, y1 = ay, xa = 1.f - ax, xb = ax;
+            const float yy0 = 1.f - ay, yy1 = ay, xa = 1.f - ax, xb = ax;
             const float* f0 = reinterpret_cast<const float*>(r0);
             const float* f1 = reinterpret_cast<const float*>(r1);
 #pragma unroll
             for (int k = 0; k < CC; ++k) {
                 // warp_affine_naive.cpp:98-102, left to right
-                float v = f0[k] * xa * y0;
-                v += f1[k] * xa * y1;
-                v += f0[CC + k] * xb * y0;
-                v += f1[CC + k] * xb * y1;
+                float v = f0[k] * xa * yy0;
+                v += f1[k] * xa * yy1;
+                v += f0[CC + k] * xb * yy0;
+                v += f1[CC + k] * xb * yy1;
                 if (OUT == kOutNorm) v = normalize_value(v, nmean[k], nstd[k]);
-                out[q * CC + k] = (TOut)v;
+                o[k] = (TOut)v;
             }
         }
     }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 
-    const int valid = min(kPx, L.dst.w - x0);
-    constexpr int kBytes = kPx * CC * (int)sizeof(TOut);
-    if (valid == kPx && (kBytes % 16 == 0) && ((reinterpret_cast<uintptr_t>(dp) & 15) == 0)) {
-#pragma unroll
-        for (int b = 0; b < kBytes / 16; ++b) reinterpret_cast<uint4*>(dp)[b] = reinterpret_cast<const uint4*>(out)[b];
-    } else if (valid == kPx && (kBytes % 4 == 0) && ((reinterpret_cast<uintptr_t>(dp) & 3) == 0)) {
-#pragma unroll
-        for (int b = 0; b < kBytes / 4; ++b) reinterpret_cast<uint32_t*>(dp)[b] = reinterpret_cast<const uint32_t*>(out)[b];
+    // ---- the wave's row segment, LDS -> HBM in 16-byte chunks ------------------
+    const int vbytes = min(64 * kPx, L.dst.w - xw) * CC * (int)sizeof(TOut);
+    unsigned char* drow = const_cast<unsigned char*>(L.dst.base) + (int64_t)img * L.dst.img_pitch +
+                          (int64_t)plane * L.dst.plane_pitch + (int64_t)y * L.dst.row_pitch +
+                          (int64_t)xw * CC * sizeof(TOut);
+    const unsigned char* xs = xch[threadIdx.y];
+    if ((reinterpret_cast<uintptr_t>(drow) & 15) == 0) {  // uniform
+        for (int c = lane; c * 16 < vbytes; c += 64) {
+            if (c * 16 + 16 <= vbytes) {
+                __builtin_nontemporal_store(*reinterpret_cast<const u32x4*>(xs + 16 * c),
+                                            reinterpret_cast<u32x4*>(drow) + c);
+            } else {
+                for (int e = c * 16; e < vbytes; ++e) drow[e] = xs[e];
+            }
+        }
     } else {
-        TOut* o = reinterpret_cast<TOut*>(dp);
-#pragma unroll
-        for (int e = 0; e < kPx * CC; ++e)
-            if (e < valid * CC) o[e] = out[e];
+        for (int e = lane; e < vbytes; e += 64) drow[e] = xs[e];
     }
 }
 
 template <int CC, typename TIn, int OUT>
 hipError_t launch_one(const WarpLaunch& L, hipStream_t s) {
-    dim3 block(64, 4);
-    dim3 grid((L.dst.w + 64 * kPx - 1) / (64 * kPx), (L.dst.h + 3) / 4, L.n * L.src.planes);
-    hipLaunchKernelGGL((warp_kernel<CC, TIn, OUT>), grid, block, 0, s, L);
+    const int gx = (L.dst.w + 64 * kPx - 1) / (64 * kPx), gy = (L.dst.h + 3) / 4;
+    const int64_t total = (int64_t)gx * gy * L.n * L.src.planes;
+    if (total >= 0x7FFFFFF0LL) return hipErrorInvalidValue;
+    const int64_t blocks = (total + 7) / 8 * 8;
+    hipLaunchKernelGGL((warp_kernel<CC, TIn, OUT>), dim3((unsigned)blocks), dim3(64, 4), 0, s, L, gx, gy, (int)total);
     return hipGetLastError();
 }
 
