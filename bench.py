@@ -44,6 +44,8 @@ def parse():
     ap.add_argument("--batch", type=int, default=256, help="images per GPU")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget of the CPU baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--graph", action="store_true",
+                    help="replay the step from a captured HIP graph (measured no faster than eager launches)")
     return ap.parse_args()
 
 
@@ -124,10 +126,35 @@ def main():
     dst = torch.empty((B, H_OUT, W_OUT, C), dtype=torch.float32, device=dev)
     stream = torch.cuda.current_stream(dev)
 
-    def step():
+    def launch():
         ops.resize_normalize(src, W_OUT, H_OUT, MEAN, STD, out=dst, stream=stream)
 
     for _ in range(args.warmup):
+        launch()  # also builds and caches the resize plan (a one-time upload)
+    torch.cuda.synchronize(dev)
+
+    # One step = one vacv_resize_normalize launch over the whole batch.  With
+    # --graph it is captured once into a HIP graph and replayed (every replay
+    # runs the full kernel); the default launches it from Python each step.
+    graph = None
+    if args.graph:
+        try:
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                ops.resize_normalize(src, W_OUT, H_OUT, MEAN, STD, out=dst)
+            graph = g
+            stream = torch.cuda.current_stream(dev)
+        except Exception as e:  # capture unsupported: eager launches
+            print(f"bench: graph capture failed ({e}); eager launches", file=sys.stderr)
+            graph = None
+
+    def step():
+        if graph is not None:
+            graph.replay()
+        else:
+            launch()
+
+    for _ in range(3):
         step()
     torch.cuda.synchronize(dev)
 

@@ -5,6 +5,8 @@
 #      bench line below carries it as roofline.traffic)
 #   2. bench.py (the driver's command) -> gpurun_out/bench.json
 #   3. rocprofv3 --kernel-trace --stats over the same bench.py command
+#   4. tools/kbench.py over every operator (HIP events) and its rocprofv3
+#      --kernel-trace --stats summary
 # Every GPU step has its own time limit; the script stops at the first failure.
 set -o pipefail
 R=$(pwd)
@@ -24,3 +26,9 @@ timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/prof_bench"
     -- python3 "$R/bench.py" > gpurun_out/prof_bench.log 2>&1 || exit $?
 tail -1 gpurun_out/prof_bench.log
 find gpurun_out/prof_bench -name "*kernel_stats.csv" -exec head -5 {} \;
+step kbench
+timeout -k 10 300 python3 tools/kbench.py --op all --iters 30 > gpurun_out/kbench.jsonl 2> gpurun_out/kbench.err || exit $?
+step kbench_stats
+timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/prof_kbench" -o kbench --output-format csv \
+    -- python3 "$R/tools/kbench.py" --op all --iters 30 > gpurun_out/prof_kbench.log 2>&1 || exit $?
+find gpurun_out/prof_kbench -name "*kernel_stats.csv" -exec cat {} \;
