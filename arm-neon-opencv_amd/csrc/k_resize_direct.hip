@@ -1,0 +1,308 @@
+// k_resize_direct.hip -- u8 bilinear resize (all three fixed-point modes)
+// with u8 / fp32 / normalised-fp32 output, as per-pixel gathers straight from
+// HBM/L2: no LDS staging of source rows, no planner tables, no barriers.
+//
+// Reference arithmetic (the same as resize_kernel<kLinearFixed>, k_resize.hip):
+//   taps  fixed_tap() = resize_naive.cpp:19-45 (REFERENCE), resize_neon.cpp:
+//         17-78 (NEON, OPENCV half-even), shared host/device code
+//   blend resize_naive.cpp:61-64  (Sum S*wx*wy) >> 22        (REFERENCE)
+//         resize_neon.cpp:103-167 int16 rows, (h*w >> 16) + 2 >> 2 (NEON/OPENCV)
+//   epilogue u8 -> fp32 and normalize_naive.cpp:74-90 (resize_normalize.cpp:
+//         33-107 = resize, convertTo fp32, (x - mean) / (std + 1e-6))
+//
+// Shape.  Output pixels of one plane are numbered row-major; a wave owns PXL*64
+// consecutive pixels -- rows are crossed freely, so every wave is full
+// whatever the output width.  Lane l samples pixels p0 + 64q + l: each gather
+// instruction reads 64 consecutive output pixels' taps (one contiguous run of
+// a source row, ~9 bytes apart at a 3x downscale).  Per pixel and weighted tap
+// row ONE unaligned 8-byte buffer load brings both horizontal taps of all
+// CC <= 4 channels.  A row with a zero vertical weight is never read: when no
+// output row has two weighted taps (ONE_ROW: the host checks, e.g. an exact
+// 3x downscale) a pixel gathers one row only and the lane takes 8 pixels, so
+// a CU keeps twice the bytes in flight for the same registers.  Outputs are
+// re-assembled in LDS, 256 pixels at a time, and leave as 16-byte
+// non-temporal stores: one store instruction writes 1 KiB of contiguous output.
+#pragma clang fp contract(off)
+
+#include <cstdlib>
+
+#include "vacv_device.hpp"
+
+namespace vacv {
+namespace {
+
+constexpr int kGroupPx = 256;  // pixels per LDS exchange round (4 per lane)
+
+// Pixels per lane: 8 when one tap row is gathered and the kernel still fits
+// 64 VGPRs (8 waves per SIMD) at 8, else 4 (measured: spills otherwise).
+constexpr int direct_pxl(int cc, int out, bool one_row) {
+    return one_row && (cc < 4 || out == kOutSame) ? 8 : 4;
+}
+
+typedef unsigned short us2 __attribute__((ext_vector_type(2)));
+
+// One channel of one output pixel from its packed tap pairs.  A zero weight
+// contributes exactly 0 in both formulas, so a skipped row is bot = 0, wB = 0.
+template <int MODE>
+__device__ __forceinline__ int blend_fixed(uint32_t top, uint32_t bot, us2 wx, uint32_t wA, uint32_t wB) {
+    const uint32_t ht = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, top), wx, 0u, false);
+    const uint32_t hb = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, bot), wx, 0u, false);
+    if (MODE == VACV_LINEAR_REFERENCE) {
+        // (tl*a0 + tr*a1)*wA + (bl*a0 + br*a1)*wB: the reference's int32 sum
+        // (terms >= 0, total <= 255*2049^2 < 2^31), 24-bit multiplies exact
+        return (int)(((__umul24(ht, wA) + __umul24(hb, wB)) >> 22) & 0xFFu);
+    }
+    const int h0 = (int)(short)(ht >> 4);
+    const int h1 = (int)(short)(hb >> 4);
+    return clamp_u8((((h0 * (int)wA) >> 16) + ((h1 * (int)wB) >> 16) + 2) >> 2);
+}
+
+// fixed_tap() of the kernel.  REFERENCE mode: the coordinate
+// (float)(((double)d + 0.5) * (double)scale_f - 0.5) is computed as ONE fp32
+// fma, which is bit-identical: d + 0.5 (d < 2^23) and scale_f have 24-bit
+// significands, so the product is exact in double and so is the - 0.5; the
+// double path therefore rounds the exact value once to float -- exactly what
+// fmaf does.  The rest is fixed_tap's own float arithmetic.
+template <int MODE>
+__device__ __forceinline__ FixedTap tap_of(int d, int n_in, int n_out, float scale_f, double scale_d) {
+    if (MODE != VACV_LINEAR_REFERENCE) return fixed_tap(d, n_in, n_out, scale_f, scale_d, MODE);
+    const float c = __builtin_fmaf((float)d + 0.5f, scale_f, -0.5f);
+    const LinearTap t = linear_tap(c, n_in);
+    FixedTap r;
+    r.i = t.i;
+    r.w0 = sat_short_away((1.f - t.f) * 2048.f);
+    r.w1 = sat_short_away(t.f * 2048.f);
+    return r;
+}
+
+template <int CC, int OUT, int MODE, bool ONE_ROW>
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8)))
+resize_direct_kernel(ResizeLaunch L, int blocks_per_plane, int total, int xcd) {
+    using TOut = typename std::conditional<(OUT == kOutSame), uint8_t, float>::type;
+    // pixels per lane (4-channel fp32 output at 8 would spill under 64 VGPRs)
+    constexpr int PXL = direct_pxl(CC, OUT, ONE_ROW);
+    constexpr int NR = ONE_ROW ? 1 : 2;                // gathered rows per pixel
+    constexpr int kWavePx = 64 * PXL;
+    constexpr int kOutPx = CC * (int)sizeof(TOut);    // output bytes per pixel
+    __shared__ __attribute__((aligned(16))) unsigned char xch[4][kGroupPx * kOutPx];
+
+    // xcd: workgroup b runs on XCD b % 8; give each XCD one contiguous eighth
+    // of the work so source rows shared by neighbouring workgroups (two-tap
+    // rows) are fetched into one L2 only
+    const int per_xcd = (total + 7) >> 3;
+    const int id = xcd ? (int)(blockIdx.x & 7) * per_xcd + (int)(blockIdx.x >> 3) : (int)blockIdx.x;
+    if (id >= total) return;  // uniform
+    const int pidx = id / blocks_per_plane;  // image * planes + plane
+    const int blk = id - pidx * blocks_per_plane;
+    const int W = L.dst.w;
+    const int P = W * L.dst.h;                            // output pixels per plane
+    const int p0 = (blk * 4 + (int)threadIdx.y) * kWavePx;
+    if (p0 >= P) return;  // whole wave
+    const int npx = min(kWavePx, P - p0);
+    const int lane = threadIdx.x;
+    const int img = pidx / L.src.planes;
+    const int plane = pidx - img * L.src.planes;
+
+    const unsigned char* sp = L.src.base + (int64_t)img * L.src.img_pitch + (int64_t)plane * L.src.plane_pitch;
+    const Rsrc srs = make_rsrc(sp, L.src.plane_bytes);
+    const uint32_t slimit = (uint32_t)L.src.plane_bytes + srs.delta;
+    const int64_t rp = L.src.row_pitch;
+    const uint32_t rp32 = (uint32_t)rp;  // plane_bytes < 2^31 (kMaxPlaneBytes): every row offset fits
+
+    // ---- taps and gathers: every load of the lane issued before any blend ---
+    const int y_first = p0 / W;  // wave-uniform
+    const int x_first = p0 - y_first * W;
+    uint32_t tap[PXL][NR][2];    // the 8 bytes at each gathered tap row
+    uint32_t wxp[PXL], wyp[PXL]; // {a0, a1} and {wA, wB} as u16 pairs
+    // vertical taps: a wave of an output at least kWavePx wide touches at most
+    // two rows, whose taps are computed once (uniform); narrower outputs
+    // compute them per pixel
+    const bool wide = W >= kWavePx;
+    const FixedTap ty0 = tap_of<MODE>(y_first, L.src.h, L.dst.h, L.scale_yf, L.scale_yd);
+    const FixedTap ty1 = tap_of<MODE>(min(y_first + 1, L.dst.h - 1), L.src.h, L.dst.h, L.scale_yf, L.scale_yd);
+#pragma unroll
+    for (int q = 0; q < PXL; ++q) {
+        const int d = x_first + q * 64 + lane;  // < W + kWavePx
+        const int dy = wide ? (d >= W ? 1 : 0) : d / W;
+        const int y = y_first + dy;
+        const int x = d - dy * W;
+#pragma unroll
+        for (int r = 0; r < NR; ++r) tap[q][r][0] = tap[q][r][1] = 0u;
+        wxp[q] = wyp[q] = 0u;
+        if (q * 64 + lane >= npx) continue;
+        const FixedTap tx = tap_of<MODE>(x, L.src.w, W, L.scale_xf, L.scale_xd);
+        FixedTap ty;
+        if (wide) {
+            ty.i = dy ? ty1.i : ty0.i;
+            ty.w0 = dy ? ty1.w0 : ty0.w0;
+            ty.w1 = dy ? ty1.w1 : ty0.w1;
+        } else {
+            ty = tap_of<MODE>(y, L.src.h, L.dst.h, L.scale_yf, L.scale_yd);
+        }
+        if (ONE_ROW && ty.w0 == 0) { ty.i += 1; ty.w0 = ty.w1; ty.w1 = 0; }  // the weighted row as row A
+        wxp[q] = (uint32_t)tx.w0 | ((uint32_t)tx.w1 << 16);
+        wyp[q] = (uint32_t)ty.w0 | ((uint32_t)ty.w1 << 16);
+        const uint32_t oa = (uint32_t)ty.i * rp32 + (uint32_t)(tx.i * CC) + srs.delta;
+        const uint32_t ob = oa + rp32;
+        if ((ONE_ROW ? oa : ob) + 8u <= slimit) {
+            if (ONE_ROW || ty.w0) {
+                auto v = __builtin_amdgcn_raw_buffer_load_b64(srs.r, (int)oa, 0, VACV_LOAD_AUX);
+                tap[q][0][0] = v[0]; tap[q][0][1] = v[1];
+            }
+            if (!ONE_ROW && ty.w1) {
+                auto v = __builtin_amdgcn_raw_buffer_load_b64(srs.r, (int)ob, 0, VACV_LOAD_AUX);
+                tap[q][NR - 1][0] = v[0]; tap[q][NR - 1][1] = v[1];
+            }
+        } else {
+            // the plane's last pixels: an 8-byte load overhanging the end of
+            // the buffer would read as zeros, so take the 2*CC bytes singly
+            const unsigned char* r0 = sp + (int64_t)ty.i * rp + (int64_t)tx.i * CC;
+#pragma unroll
+            for (int e = 0; e < 2 * CC; ++e) {
+                tap[q][0][e >> 2] |= (ty.w0 ? (uint32_t)r0[e] : 0u) << (8 * (e & 3));
+                if (!ONE_ROW) tap[q][NR - 1][e >> 2] |= (ty.w1 ? (uint32_t)r0[rp + e] : 0u) << (8 * (e & 3));
+            }
+        }
+    }
+
+    ChanNorm cn[CC] = {};
+    if (OUT == kOutNorm) {
+#pragma unroll
+        for (int k = 0; k < CC; ++k) cn[k] = chan_norm(L.norm, img, CC == 1 ? plane % L.norm.c_total : k);
+    }
+
+    unsigned char* dp = const_cast<unsigned char*>(L.dst.base) + (int64_t)img * L.dst.img_pitch +
+                        (int64_t)plane * L.dst.plane_pitch;
+    const uint32_t out_row = (uint32_t)W * kOutPx;  // dense bytes of one output row
+    const uint32_t rowp = (uint32_t)L.dst.row_pitch;
+    const bool dense = L.dst.row_pitch == (int64_t)out_row;
+    const bool chunked = (reinterpret_cast<uintptr_t>(dp) & 15) == 0 && (L.dst.row_pitch & 15) == 0 &&
+                         (dense || (out_row & 15) == 0);  // 16-byte chunks never straddle rows
+    const Rsrc rd = make_rsrc(dp, L.dst.plane_bytes);
+    TOut* xrow = reinterpret_cast<TOut*>(xch[threadIdx.y]);
+    const unsigned char* xs = xch[threadIdx.y];
+
+#pragma unroll
+    for (int g = 0; g < PXL / 4; ++g) {
+        // ---- blend 256 pixels into the wave's LDS buffer ---------------------
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int q = g * 4 + j;
+            const us2 wx = __builtin_bit_cast(us2, wxp[q]);
+            const uint32_t wA = wyp[q] & 0xFFFFu, wB = wyp[q] >> 16;
+            TOut* o = xrow + (j * 64 + lane) * CC;
+#pragma unroll
+            for (int k = 0; k < CC; ++k) {
+                // tap pair (byte k, byte CC + k) -> u16 lanes {lo, hi} (v_perm_b32)
+                const uint32_t sel = (uint32_t)k | (0x0Cu << 8) | ((uint32_t)(CC + k) << 16) | (0x0Cu << 24);
+                const uint32_t top = __builtin_amdgcn_perm(tap[q][0][1], tap[q][0][0], sel);
+                const uint32_t bot = ONE_ROW ? 0u : __builtin_amdgcn_perm(tap[q][NR - 1][1], tap[q][NR - 1][0], sel);
+                const int v = blend_fixed<MODE>(top, bot, wx, wA, wB);
+                if (OUT == kOutSame) o[k] = (TOut)v;
+                else if (OUT == kOutF32) o[k] = (TOut)(float)v;
+                else o[k] = (TOut)normalize_u8v(cn[k], v);
+            }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+
+        // ---- LDS -> HBM: dense byte b of the plane's output lives at row
+        // b / out_row, column byte b % out_row ---------------------------------
+        const int gp = npx - g * kGroupPx;  // valid pixels of this round (uniform)
+        if (gp > 0) {
+            // 32-bit offsets: the plane is < 2^31 bytes (kMaxPlaneBytes)
+            const uint32_t vbytes = (uint32_t)(min(gp, kGroupPx) * kOutPx);
+            const uint32_t b0 = (uint32_t)(p0 + g * kGroupPx) * kOutPx;  // 16-byte aligned (256 | p0)
+            if (chunked) {
+                for (uint32_t c = lane; c * 16 < vbytes; c += 64) {
+                    const uint32_t b = b0 + 16 * c;
+                    uint32_t off = b;
+                    if (!dense) {
+                        const uint32_t r = b / out_row;
+                        off = r * rowp + (b - r * out_row);
+                    }
+                    if (c * 16 + 16 <= vbytes) {
+                        store16(rd, off + rd.delta, *reinterpret_cast<const uint4*>(xs + 16 * c));
+                    } else {
+                        for (uint32_t e = c * 16; e < vbytes; ++e) dp[off + (e - c * 16)] = xs[e];
+                    }
+                }
+            } else {
+                for (uint32_t e = lane; e < vbytes; e += 64) {
+                    const uint32_t b = b0 + e;
+                    const uint32_t r = b / out_row;
+                    dp[r * rowp + (b - r * out_row)] = xs[e];
+                }
+            }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+}
+
+template <int CC, int OUT, int MODE, bool ONE_ROW>
+hipError_t launch_one(const ResizeLaunch& L, hipStream_t s) {
+    constexpr int kBlockPx = 4 * 64 * direct_pxl(CC, OUT, ONE_ROW);
+    const int64_t P = (int64_t)L.dst.w * L.dst.h;
+    const int64_t per_plane = (P + kBlockPx - 1) / kBlockPx;
+    const int64_t total = per_plane * L.n * L.src.planes;
+    if (P >= 0x7FFFFFFF - kBlockPx || total > 0x7FFFFFF0LL) return hipErrorInvalidValue;
+    // XCD-contiguous order only where neighbouring workgroups share source
+    // rows (two-tap rows); one-tap rows stream fastest in plain address order
+    // (measured 0.222 vs 0.233 ms on the headline; VACV_DIRECT_XCD overrides)
+    const char* env = std::getenv("VACV_DIRECT_XCD");
+    const int xcd = env ? std::atoi(env) : (ONE_ROW ? 0 : 1);
+    const int64_t blocks = xcd ? (total + 7) / 8 * 8 : total;
+    hipLaunchKernelGGL((resize_direct_kernel<CC, OUT, MODE, ONE_ROW>), dim3((unsigned)blocks), dim3(64, 4), 0, s,
+                       L, (int)per_plane, (int)total, xcd);
+    return hipGetLastError();
+}
+
+template <int OUT, int MODE, bool ONE_ROW>
+hipError_t launch_cc(const ResizeLaunch& L, hipStream_t s) {
+    switch (L.src.cc) {
+        case 1: return launch_one<1, OUT, MODE, ONE_ROW>(L, s);
+        case 2: return launch_one<2, OUT, MODE, ONE_ROW>(L, s);
+        case 3: return launch_one<3, OUT, MODE, ONE_ROW>(L, s);
+        case 4: return launch_one<4, OUT, MODE, ONE_ROW>(L, s);
+        default: return hipErrorInvalidValue;
+    }
+}
+
+template <int OUT, bool ONE_ROW>
+hipError_t launch_mode(const ResizeLaunch& L, hipStream_t s) {
+    switch (L.mode) {
+        case VACV_LINEAR_REFERENCE: return launch_cc<OUT, VACV_LINEAR_REFERENCE, ONE_ROW>(L, s);
+        case VACV_LINEAR_NEON: return launch_cc<OUT, VACV_LINEAR_NEON, ONE_ROW>(L, s);
+        default: return launch_cc<OUT, VACV_LINEAR_OPENCV, ONE_ROW>(L, s);
+    }
+}
+
+template <int OUT>
+hipError_t launch_rows(const ResizeLaunch& L, bool one_row, hipStream_t s) {
+    return one_row ? launch_mode<OUT, true>(L, s) : launch_mode<OUT, false>(L, s);
+}
+
+}  // namespace
+
+bool resize_one_tap_rows(const ResizeLaunch& L) {
+    // no output row has two non-zero vertical weights (the kernel's taps, on
+    // the host)
+    for (int y = 0; y < L.dst.h; ++y) {
+        const FixedTap t = fixed_tap(y, L.src.h, L.dst.h, L.scale_yf, L.scale_yd, L.mode);
+        if (t.w0 != 0 && t.w1 != 0) return false;
+    }
+    return true;
+}
+
+hipError_t launch_resize_direct(const ResizeLaunch& L, hipStream_t s) {
+    if (L.kind != kLinearFixed) return hipErrorInvalidValue;
+    const bool one_row = resize_one_tap_rows(L);
+    if (L.out == kOutSame) return launch_rows<kOutSame>(L, one_row, s);
+    if (L.out == kOutF32) return launch_rows<kOutF32>(L, one_row, s);
+    return launch_rows<kOutNorm>(L, one_row, s);
+}
+
+}  // namespace vacv

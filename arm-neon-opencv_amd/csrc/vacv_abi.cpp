@@ -267,9 +267,19 @@ int resize_impl(const vacv_image* src_d, const vacv_image* dst_d, int interpolat
     L.scale_yf = (float)src.h / (float)dst.h;
     L.scale_xd = (double)src.w / (double)dst.w;
     L.scale_yd = (double)src.h / (double)dst.h;
-    // resize_kernel with interleaved (address-ordered) tasks by default;
+    // u8 bilinear whose output rows each weight ONE source row (downscales by
+    // an integer factor >= 2, e.g. the 1080p -> 640x360 headline): the
+    // per-pixel gather kernel (k_resize_direct.hip).  Elsewhere the staged
+    // kernel measured faster (1280x720: 0.63 vs 0.69 ms).  VACV_RESIZE_DIRECT
+    // = 0 never / 2 always uses the gather kernel, for A/B tests.
+    // Otherwise resize_kernel with interleaved (address-ordered) tasks;
     // VACV_RESIZE_INTERLEAVE=0 selects its strip order and VACV_RESIZE_ROWS=1
-    // the whole-row kernel, for A/B measurement
+    // the whole-row kernel.
+    const char* direct_env = std::getenv("VACV_RESIZE_DIRECT");
+    const int direct = direct_env ? std::atoi(direct_env) : 1;
+    if (L.kind == kLinearFixed && L.src.cc <= 4 && dst.w < (1 << 23) && dst.h < (1 << 23) &&
+        (direct == 2 || (direct == 1 && resize_one_tap_rows(L))))
+        return hip_status(launch_resize_direct(L, s));
     const char* il_env = std::getenv("VACV_RESIZE_INTERLEAVE");
     L.interleave = !(il_env && il_env[0] == '0');
     const char* rows_env = std::getenv("VACV_RESIZE_ROWS");

@@ -107,6 +107,10 @@ void set_strips(ResizeLaunch& L, int64_t resident_workgroups);
 int release_plans();
 
 hipError_t launch_resize(const ResizeLaunch& L, hipStream_t s);
+// u8 bilinear as per-pixel gathers (k_resize_direct.hip); needs no plan.
+// resize_one_tap_rows: no output row of L has two weighted source rows.
+hipError_t launch_resize_direct(const ResizeLaunch& L, hipStream_t s);
+bool resize_one_tap_rows(const ResizeLaunch& L);
 
 struct WarpLaunch {
     PlaneGeom src;

@@ -71,8 +71,12 @@ SIZES = [((23, 37), 1), ((48, 64), 3), ((61, 97), 3), ((5, 7), 3), ((16, 16), 4)
 OUTS = [(20, 11), (33, 29), (111, 40), (7, 5), (2, 2), (160, 90), (1, 1), (300, 7)]
 
 
+@pytest.mark.parametrize("direct", ["1", "2"])
 @pytest.mark.parametrize("mode", [0, 1, 2])
-def test_resize_linear_u8_hwc(ops, dev, oracle, mode):
+def test_resize_linear_u8_hwc(ops, dev, oracle, mode, direct, monkeypatch):
+    # direct "1": the default dispatch (gather kernel for one-tap-row
+    # geometries, staged kernel otherwise); "2": the gather kernel everywhere
+    monkeypatch.setenv("VACV_RESIZE_DIRECT", direct)
     for i, ((h, w), c) in enumerate(SIZES):
         imgs = [synthetic_image(100 * i + k, h, w, c) for k in range(3)]
         src = to_dev(batch(imgs) if c > 1 else batch(imgs)[..., None], dev)
@@ -138,6 +142,48 @@ def test_resize_full_size_batch(ops, dev, oracle):
     got = host(ops.resize(view, 77, 55))
     want = oracle.resize_linear(np.ascontiguousarray(synthetic_image(99, 200, 300, 3)[10:150, 20:220]), 77, 55)
     assert_same(got, want, "pitched")
+
+
+def test_resize_u8_kernels_agree_and_pitched_out(ops, dev, oracle, monkeypatch):
+    """u8 bilinear with one weighted source row per output row runs on the
+    per-pixel gather kernel (k_resize_direct.hip), the rest on the LDS-staged
+    strip kernel; VACV_RESIZE_DIRECT=2 forces the gather kernel for every
+    geometry and 0 the strip kernel.  Both must give identical bytes / floats
+    at full size (one-tap and two-tap geometries), and the gather kernel must
+    honour a pitched (sub-window) destination in every store path: 16-byte
+    chunks mapped per row (row bytes a multiple of 16) and the byte
+    fallback."""
+    import torch
+    imgs = [synthetic_image(60 + k, 1080, 1920, 3) for k in range(2)]
+    src = to_dev(batch(imgs), dev)
+    for wo, ho in [(640, 360), (1280, 720), (333, 129), (64, 1000)]:
+        for mode in (0, 1, 2):
+            monkeypatch.setenv("VACV_RESIZE_DIRECT", "2")
+            a8 = ops.resize(src, wo, ho, mode=mode)
+            an = ops.resize_normalize(src, wo, ho, MEAN, STD, mode=mode)
+            monkeypatch.setenv("VACV_RESIZE_DIRECT", "0")
+            b8 = ops.resize(src, wo, ho, mode=mode)
+            bn = ops.resize_normalize(src, wo, ho, MEAN, STD, mode=mode)
+            monkeypatch.delenv("VACV_RESIZE_DIRECT")
+            assert torch.equal(a8, b8), f"u8 kernels differ {wo}x{ho} mode {mode}"
+            assert torch.equal(an, bn), f"normalize kernels differ {wo}x{ho} mode {mode}"
+    small = synthetic_image(61, 97, 151, 3)
+    s = to_dev(small[None], dev)
+    monkeypatch.setenv("VACV_RESIZE_DIRECT", "2")
+    for wo, ho, dt in [(80, 50, torch.uint8), (77, 55, torch.uint8), (64, 31, torch.float32), (41, 23, torch.float32)]:
+        big = torch.zeros((1, ho + 9, wo + 24, 3), dtype=dt, device=dev)
+        view = big[:, 4:4 + ho, 8:8 + wo]
+        if dt == torch.uint8:
+            ops.resize(s, wo, ho, out=view)
+            want = oracle.resize_linear(small, wo, ho)
+        else:
+            ops.resize_normalize(s, wo, ho, MEAN, STD, out=view)
+            want = oracle.normalize(oracle.u8_to_f32(oracle.resize_linear(small, wo, ho)), MEAN, STD)
+        got = host(big)
+        assert_same(got[0, 4:4 + ho, 8:8 + wo], want, f"pitched out {wo}x{ho} {dt}")
+        rim = got.copy()
+        rim[0, 4:4 + ho, 8:8 + wo] = 0
+        assert not rim.any(), f"pitched out {wo}x{ho}: wrote outside the window"
 
 
 def test_resize_normalize(ops, dev, oracle):

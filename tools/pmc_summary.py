@@ -31,7 +31,7 @@ def main():
             k = next((k for k in keys if k in name), None)
             if k is None:
                 continue
-            short = name.split("(")[0][-90:]
+            short = name.replace("(anonymous namespace)::", "").split("(")[0][-90:]
             rows[short][r["Counter_Name"]].append(float(r["Counter_Value"]))
     out = {}
     for kname, cnt in rows.items():

@@ -16,7 +16,7 @@ step() { echo "=== $1 $(date +%T)"; }
 step pmc
 timeout -k 10 400 rocprofv3 -i "$R/tools/pmc_bench.txt" -d "$R/gpurun_out/pmc_bench" -o pmc --output-format csv \
     -- python3 "$R/bench.py" --steps 5 --warmup 2 --no-cpu-baseline > gpurun_out/pmc_bench.log 2>&1 || exit $?
-python3 tools/pmc_summary.py gpurun_out/pmc_bench resize_kernel --out gpurun_out/pmc_resize_normalize.json > gpurun_out/pmc_summary.txt || exit 1
+python3 tools/pmc_summary.py gpurun_out/pmc_bench resize_ --out gpurun_out/pmc_resize_normalize.json > gpurun_out/pmc_summary.txt || exit 1
 cp gpurun_out/pmc_resize_normalize.json profiles/pmc_resize_normalize.json
 step bench
 timeout -k 10 300 python3 bench.py > gpurun_out/bench.json 2> gpurun_out/bench.err || exit $?
