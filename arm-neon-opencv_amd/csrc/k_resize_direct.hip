@@ -15,8 +15,8 @@
 // whatever the output width.  Lane l samples pixels p0 + 64q + l: each gather
 // instruction reads 64 consecutive output pixels' taps (one contiguous run of
 // a source row, ~9 bytes apart at a 3x downscale).  Per pixel and weighted tap
-// row ONE unaligned 8-byte buffer load brings both horizontal taps of all
-// CC <= 4 channels.  A row with a zero vertical weight is never read: when no
+// row ONE unaligned 8-byte buffer load (load_taps, vacv_device.hpp) brings
+// both horizontal taps of all CC <= 4 channels.  A row with a zero vertical weight is never read: when no
 // output row has two weighted taps (ONE_ROW: the host checks, e.g. an exact
 // 3x downscale) a pixel gathers one row only and the lane takes 8 pixels, so
 // a CU keeps twice the bytes in flight for the same registers.  Outputs are
@@ -144,15 +144,9 @@ resize_direct_kernel(ResizeLaunch L, int blocks_per_plane, int total, int xcd) {
         wyp[q] = (uint32_t)ty.w0 | ((uint32_t)ty.w1 << 16);
         const uint32_t oa = (uint32_t)ty.i * rp32 + (uint32_t)(tx.i * CC) + srs.delta;
         const uint32_t ob = oa + rp32;
-        if ((ONE_ROW ? oa : ob) + 8u <= slimit) {
-            if (ONE_ROW || ty.w0) {
-                auto v = __builtin_amdgcn_raw_buffer_load_b64(srs.r, (int)oa, 0, VACV_LOAD_AUX);
-                tap[q][0][0] = v[0]; tap[q][0][1] = v[1];
-            }
-            if (!ONE_ROW && ty.w1) {
-                auto v = __builtin_amdgcn_raw_buffer_load_b64(srs.r, (int)ob, 0, VACV_LOAD_AUX);
-                tap[q][NR - 1][0] = v[0]; tap[q][NR - 1][1] = v[1];
-            }
+        if ((ONE_ROW ? oa : ob) + 8u <= slimit) {  // the unaligned 8 bytes in range
+            if (ONE_ROW || ty.w0) load_taps<CC, false, VACV_LOAD_AUX>(srs, oa, tap[q][0][0], tap[q][0][1]);
+            if (!ONE_ROW && ty.w1) load_taps<CC, false, VACV_LOAD_AUX>(srs, ob, tap[q][NR - 1][0], tap[q][NR - 1][1]);
         } else {
             // the plane's last pixels: an 8-byte load overhanging the end of
             // the buffer would read as zeros, so take the 2*CC bytes singly

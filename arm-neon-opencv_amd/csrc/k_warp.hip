@@ -12,7 +12,8 @@
 // pixels l, l+64, l+128, l+192 (so each gather instruction covers 64
 // consecutive pixels: ~20 source cache lines under a rotation instead of
 // 64), re-assembles the row segment in LDS and writes it with 16-byte
-// stores.  Taps: one unaligned 8-byte buffer load per source row, packed
+// stores.  Taps: one dword-aligned 8/12-byte buffer load per source row
+// (load_taps, vacv_device.hpp), packed
 // u16 dot products for the fixed-point sum.  Blocks are ordered so each XCD
 // walks a contiguous range (its L2 keeps the shared source rows).
 // Measured alternative, kept out: staging each tile's source bounding box in
@@ -113,16 +114,15 @@ warp_kernel(WarpLaunch L, int gx, int gy, int total) {
             // SATURATE_CAST_SHORT of a value in (0, 2048]: the +0.5f branch, no clamp
             const int wy0 = (int)((1.f - ay) * 2048.f + 0.5f), wy1 = 2048 - wy0;
             const int wx0 = (int)((1.f - ax) * 2048.f + 0.5f), wx1 = 2048 - wx0;
-            // the 2*CC tap bytes of each row in ONE (unaligned) buffer load;
+            // the 2*CC tap bytes of each row in ONE dword-aligned buffer load;
             // a load past the plane's end (its last pixel) falls back to bytes
             uint32_t a0 = 0, a1 = 0, c0 = 0, c1 = 0;
             const uint32_t o0 = (rp32 ? __umul24((uint32_t)sy, rp32) : (uint32_t)((int64_t)sy * rp)) +
                                 (uint32_t)(sx * CC) + srs.delta;
             const uint32_t o1 = o0 + (uint32_t)rp;
-            if (CC <= 4 && o1 + 8u <= slimit) {
-                auto a = __builtin_amdgcn_raw_buffer_load_b64(srs.r, (int)o0, 0, 0);
-                auto c = __builtin_amdgcn_raw_buffer_load_b64(srs.r, (int)o1, 0, 0);
-                a0 = a[0]; a1 = a[1]; c0 = c[0]; c1 = c[1];
+            if (CC <= 4 && (o1 & ~3u) + 4u * kTapDwords<CC, true> <= slimit) {
+                load_taps<CC, true, 0>(srs, o0, a0, a1);
+                load_taps<CC, true, 0>(srs, o1, c0, c1);
             } else {
 #pragma unroll
                 for (int e = 0; e < 2 * CC && e < 8; ++e) {
@@ -218,6 +218,7 @@ hipError_t launch_cc(const WarpLaunch& L, hipStream_t s) {
 }  // namespace
 
 hipError_t launch_warp(const WarpLaunch& L, hipStream_t s) {
+    if (warp_tile_applies(L)) return launch_warp_tile(L, s);
     if (L.src.esize == 1) {
         if (L.out == kOutSame) return launch_cc<uint8_t, kOutSame>(L, s);
         if (L.out == kOutF32) return launch_cc<uint8_t, kOutF32>(L, s);

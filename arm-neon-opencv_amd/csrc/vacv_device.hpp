@@ -57,6 +57,39 @@ __device__ __forceinline__ void store16(const Rsrc& s, uint32_t off_from_base16,
     __builtin_amdgcn_raw_buffer_store_b128(d, s.r, (int)off_from_base16, 0, VACV_STORE_AUX);
 }
 
+// The 2*CC tap bytes of a bilinear pixel (left tap's CC bytes, right tap's
+// CC bytes) starting at buffer byte offset `off`, as bytes 0.. of (lo, hi).
+// Two forms, each the faster one for its access pattern (kbench, MI355X):
+//  * dword-aligned (b64 for CC <= 2, b96 for CC 3-4) and byte-shifted in
+//    registers: the warp's rotated gathers, 0.34 -> 0.31 ms;
+//  * one unaligned b64: lane-consecutive resize gathers 9 bytes apart, where
+//    the aligned form was 10-20 % slower (0.220 -> 0.241 ms headline).
+// The caller guarantees off + 8 <= size (unaligned) or
+// (off & ~3) + 4 * kTapDwords<CC, true> <= size (aligned).
+template <int CC, bool ALIGNED>
+constexpr uint32_t kTapDwords = (!ALIGNED || CC <= 2) ? 2u : 3u;
+
+template <int CC, bool ALIGNED, int AUX>
+__device__ __forceinline__ void load_taps(const Rsrc& rs, uint32_t off, uint32_t& lo, uint32_t& hi) {
+    if constexpr (!ALIGNED) {
+        const auto v = __builtin_amdgcn_raw_buffer_load_b64(rs.r, (int)off, 0, AUX);
+        lo = v[0];
+        hi = v[1];
+        return;
+    }
+    const int a = (int)(off & ~3u);
+    const uint32_t sh = off & 3u;
+    if constexpr (CC <= 2) {
+        const auto v = __builtin_amdgcn_raw_buffer_load_b64(rs.r, a, 0, AUX);
+        lo = __builtin_amdgcn_alignbyte(v[1], v[0], sh);
+        hi = 0u;  // 2*CC <= 4 bytes: lo holds them all
+    } else {
+        const auto v = __builtin_amdgcn_raw_buffer_load_b96(rs.r, a, 0, AUX);
+        lo = __builtin_amdgcn_alignbyte(v[1], v[0], sh);
+        hi = __builtin_amdgcn_alignbyte(v[2], v[1], sh);
+    }
+}
+
 // Per-workgroup mean/stddev for channel ch of image img.
 __device__ __forceinline__ void norm_params(const NormSpec& ns, int img, int ch, float& m, float& s) {
     if (ns.mode == 2) {

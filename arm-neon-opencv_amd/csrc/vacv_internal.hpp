@@ -122,6 +122,9 @@ struct WarpLaunch {
     NormSpec norm;
 };
 hipError_t launch_warp(const WarpLaunch& L, hipStream_t s);
+// u8 warp with each tile's source box staged in LDS (k_warp_tile.hip)
+bool warp_tile_applies(const WarpLaunch& L);
+hipError_t launch_warp_tile(const WarpLaunch& L, hipStream_t s);
 
 struct CopyLaunch {                // crop / clone: row copies
     PlaneGeom src;                 // base already offset to the crop origin

@@ -287,6 +287,48 @@ def test_warp_affine_config_and_harness(ops, dev, oracle, golden):
     assert_same(got[1], want, "warp_affine_normalize")
 
 
+def test_warp_tile_and_gather_kernels_agree(ops, dev, oracle, monkeypatch):
+    """VACV_WARP_TILE=1 runs u8 warps on the LDS-staged tile kernel
+    (k_warp_tile.hip, opt-in: measured slower) when the tile's source box fits
+    its LDS budget; the default is the per-pixel gather kernel (k_warp.hip).
+    Identical outputs at full size for rotations,
+    flips, shears, strong down-scales (box over budget: the gather kernel),
+    fused normalisation, NCHW planes and a pitched destination."""
+    import torch
+    from vacv_amd import NCHW
+    imgs = np.stack([synthetic_image(80 + k, 720, 1280, 3) for k in range(2)])
+    src = to_dev(imgs, dev)
+    mats = [ops.rotation_matrix(0.9, 15.0, (640, 360, 640, 360)),
+            ops.rotation_matrix(1.7, -130.0, (640, 360, 500, 300)),
+            np.array([-1, 0, 1279, 0, 1, 0], np.float32),            # horizontal flip
+            np.array([1.3, 0.2, 100.0, -0.1, 1.45, 50.0], np.float32),  # shear + up-scale
+            np.array([0.25, 0.0, 0.0, 0.0, 0.25, 0.0], np.float32),   # 4x down: box over budget
+            np.array([1, 0, 0.5, 0, 1, -0.25], np.float32)]
+    for m in mats:
+        for wo, ho in [(1280, 720), (333, 211)]:
+            monkeypatch.setenv("VACV_WARP_TILE", "1")
+            a = ops.warp_affine(src, m, wo, ho)
+            an = ops.warp_affine_normalize(src, m, wo, ho, MEAN, STD)
+            monkeypatch.setenv("VACV_WARP_TILE", "0")
+            b = ops.warp_affine(src, m, wo, ho)
+            bn = ops.warp_affine_normalize(src, m, wo, ho, MEAN, STD)
+            monkeypatch.delenv("VACV_WARP_TILE")
+            assert torch.equal(a, b), f"warp kernels differ {m.tolist()} {wo}x{ho}"
+            assert torch.equal(an, bn), f"warp normalize kernels differ {m.tolist()} {wo}x{ho}"
+    monkeypatch.setenv("VACV_WARP_TILE", "1")
+    chw = to_dev(np.ascontiguousarray(imgs.transpose(0, 3, 1, 2)), dev)
+    got = host(ops.warp_affine(chw, mats[0], 300, 200, layout=NCHW))
+    for k in range(3):
+        assert_same(got[1, k], oracle.warp_affine(np.ascontiguousarray(imgs[1, ..., k]), mats[0], 300, 200), "tile chw")
+    big = torch.zeros((1, 130, 230, 3), dtype=torch.uint8, device=dev)
+    view = big[:, 3:123, 5:205]
+    ops.warp_affine(src[:1], mats[1], 200, 120, out=view)
+    g = host(big)
+    assert_same(g[0, 3:123, 5:205], oracle.warp_affine(imgs[0], mats[1], 200, 120), "tile pitched out")
+    g[0, 3:123, 5:205] = 0
+    assert not g.any(), "tile kernel wrote outside the window"
+
+
 # ---------------------------------------------------------------------------
 # colour
 
