@@ -8,11 +8,14 @@
 // tap is outside [0,w-2]x[0,h-2]; u8 weights SAT((1-f)*2048) and 2048-that;
 // value (Sum S*wx*wy) >> 22.  Skipped pixels get the border value here.
 //
-// A wave owns 256 consecutive output pixels of one row; lane l samples
-// pixels l, l+64, l+128, l+192 (so each gather instruction covers 64
-// consecutive pixels: ~20 source cache lines under a rotation instead of
-// 64), re-assembles the row segment in LDS and writes it with 16-byte
-// stores.  Taps: one dword-aligned 8/12-byte buffer load per source row
+// A workgroup owns a 64*kPx x 4 output tile.  Each gather instruction
+// samples an LW x (64/LW) block of output pixels: LW = 64 (one row segment
+// per instruction) by default, 16 (16 x 4 blocks, a more compact rotated
+// footprint: measured no faster) via VACV_WARP_LW.  kPx = 8 lane blocks per
+// wave for byte output (VACV_WARP_PX overrides): more gathers in flight per
+// wave, and the per-workgroup setup spread over twice the pixels (0.30 ->
+// 0.28 ms at 720p rot15); 4 for fp32 output.  The tile is re-assembled in LDS and each wave writes one of its
+// rows with 16-byte stores.  Taps: one dword-aligned 8/12-byte buffer load per source row
 // (load_taps, vacv_device.hpp), packed
 // u16 dot products for the fixed-point sum.  Blocks are ordered so each XCD
 // walks a contiguous range (its L2 keeps the shared source rows).
@@ -29,11 +32,12 @@
 namespace vacv {
 namespace {
 
-constexpr int kPx = 4;
 
-template <int CC, typename TIn, int OUT>
+template <int CC, typename TIn, int OUT, int LW, int kPx>
 __global__ void __launch_bounds__(kBlock)
 warp_kernel(WarpLaunch L, int gx, int gy, int total) {
+    constexpr int LH = 64 / LW;  // rows of one lane block; the tile is 4 rows
+    static_assert(LW * LH == 64 && LH <= 4, "lane block");
     using TOut = typename std::conditional<(OUT == kOutSame), TIn, float>::type;
     constexpr bool kLut = std::is_same<TIn, uint8_t>::value && (OUT == kOutNorm);
     constexpr int kRowBytes = 64 * kPx * CC * (int)sizeof(TOut);  // one wave's output row segment
@@ -53,8 +57,12 @@ warp_kernel(WarpLaunch L, int gx, int gy, int total) {
     const int img = pidx / L.src.planes;
     const int plane = pidx - img * L.src.planes;
     const int lane = threadIdx.x;
-    const int y = by * 4 + threadIdx.y;  // wave-uniform
-    const int xw = bx * 64 * kPx;        // the wave's first pixel
+    const int xw = bx * 64 * kPx;        // the tile's first column
+    // wave (wx, wy) of the tile's LH x (4/LH) wave grid covers kPx lane blocks
+    // side by side: columns [cx0, cx0 + kPx*LW), rows [ry0, ry0 + LH)
+    const int cx0 = (int)(threadIdx.y % LH) * kPx * LW + lane % LW;
+    const int ry = (int)(threadIdx.y / LH) * LH + lane / LW;  // tile row of this lane
+    const int y = by * 4 + ry;
 
     float nmean[CC], nstd[CC];
     if (OUT == kOutNorm) {
@@ -69,7 +77,6 @@ warp_kernel(WarpLaunch L, int gx, int gy, int total) {
         }
         __syncthreads();
     }
-    if (y >= L.dst.h) return;  // whole wave
 
     const unsigned char* sp = L.src.base + (int64_t)img * L.src.img_pitch + (int64_t)plane * L.src.plane_pitch;
     const int64_t rp = L.src.row_pitch;
@@ -78,18 +85,18 @@ warp_kernel(WarpLaunch L, int gx, int gy, int total) {
     const Rsrc srs = make_rsrc(sp, L.src.plane_bytes);
     const uint32_t slimit = (uint32_t)L.src.plane_bytes + srs.delta;
     const uint32_t rp32 = (rp < (1 << 24) && L.src.h < (1 << 24)) ? (uint32_t)rp : 0u;  // 24-bit row offsets
-    TOut* xrow = reinterpret_cast<TOut*>(xch[threadIdx.y]);
+    TOut* xrow = reinterpret_cast<TOut*>(xch[ry]);
 
-    // Lane l samples pixels xw + q*64 + l: each wave gather instruction then
-    // reads 64 CONSECUTIVE output pixels, whose rotated source footprint spans
-    // ~20 cache lines instead of 64 (4 adjacent pixels per lane put every lane
-    // on its own source row).  The row segment is re-assembled in LDS and
-    // written as contiguous 16-byte stores.
+    // pass q samples the lane block at tile columns cx0 + q*LW (+ lane % LW).
+    // With LW = 64 each gather instruction reads 64 CONSECUTIVE output
+    // pixels, whose rotated source footprint spans ~20 cache lines instead of
+    // 64 (adjacent pixels per lane would put every lane on its own row).
 #pragma unroll
     for (int q = 0; q < kPx; ++q) {
-        const int x = xw + q * 64 + lane;
-        if (x >= L.dst.w) continue;
-        TOut* o = xrow + (q * 64 + lane) * CC;
+        const int cx = cx0 + q * LW;
+        const int x = xw + cx;
+        if (x >= L.dst.w || y >= L.dst.h) continue;
+        TOut* o = xrow + cx * CC;
         // warp_affine_naive.cpp:23-24: (m0*x + m1*y) + m2, all float
         const float fx = L.inv[0] * (float)x + fy_row + L.inv[2];
         const float fy = L.inv[3] * (float)x + gy_row + L.inv[5];
@@ -170,14 +177,14 @@ warp_kernel(WarpLaunch L, int gx, int gy, int total) {
             }
         }
     }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    __syncthreads();
 
-    // ---- the wave's row segment, LDS -> HBM in 16-byte chunks ------------------
+    // ---- wave r writes tile row r, LDS -> HBM in 16-byte chunks ----------------
+    const int yo = by * 4 + (int)threadIdx.y;
+    if (yo >= L.dst.h) return;
     const int vbytes = min(64 * kPx, L.dst.w - xw) * CC * (int)sizeof(TOut);
     unsigned char* drow = const_cast<unsigned char*>(L.dst.base) + (int64_t)img * L.dst.img_pitch +
-                          (int64_t)plane * L.dst.plane_pitch + (int64_t)y * L.dst.row_pitch +
+                          (int64_t)plane * L.dst.plane_pitch + (int64_t)yo * L.dst.row_pitch +
                           (int64_t)xw * CC * sizeof(TOut);
     const unsigned char* xs = xch[threadIdx.y];
     if ((reinterpret_cast<uintptr_t>(drow) & 15) == 0) {  // uniform
@@ -194,14 +201,38 @@ warp_kernel(WarpLaunch L, int gx, int gy, int total) {
     }
 }
 
-template <int CC, typename TIn, int OUT>
-hipError_t launch_one(const WarpLaunch& L, hipStream_t s) {
+// lane block width (64: one row segment per gather instruction, 16: 16 x 4
+// blocks) and lane blocks per wave (8 or 4): A/B measurement knobs
+int warp_lane_width() {
+    const char* env = std::getenv("VACV_WARP_LW");
+    return (env && std::atoi(env) == 16) ? 16 : 64;
+}
+// default: 8 for byte output (0.283 vs 0.304 ms at 720p rot15), 4 for fp32
+// output (0.538 vs 0.614 ms: 8 blocks double the LDS row buffers and halve
+// the resident workgroups)
+int warp_blocks_per_wave(bool byte_out) {
+    const char* env = std::getenv("VACV_WARP_PX");
+    if (env && (std::atoi(env) == 4 || std::atoi(env) == 8)) return std::atoi(env);
+    return byte_out ? 8 : 4;
+}
+
+template <int CC, typename TIn, int OUT, int LW, int kPx>
+hipError_t launch_px(const WarpLaunch& L, hipStream_t s) {
     const int gx = (L.dst.w + 64 * kPx - 1) / (64 * kPx), gy = (L.dst.h + 3) / 4;
     const int64_t total = (int64_t)gx * gy * L.n * L.src.planes;
     if (total >= 0x7FFFFFF0LL) return hipErrorInvalidValue;
     const int64_t blocks = (total + 7) / 8 * 8;
-    hipLaunchKernelGGL((warp_kernel<CC, TIn, OUT>), dim3((unsigned)blocks), dim3(64, 4), 0, s, L, gx, gy, (int)total);
+    hipLaunchKernelGGL((warp_kernel<CC, TIn, OUT, LW, kPx>), dim3((unsigned)blocks), dim3(64, 4), 0, s, L, gx, gy,
+                       (int)total);
     return hipGetLastError();
+}
+
+template <int CC, typename TIn, int OUT>
+hipError_t launch_one(const WarpLaunch& L, hipStream_t s) {
+    const bool wide = warp_blocks_per_wave(OUT == kOutSame && sizeof(TIn) == 1) == 8;
+    if (warp_lane_width() == 64)
+        return wide ? launch_px<CC, TIn, OUT, 64, 8>(L, s) : launch_px<CC, TIn, OUT, 64, 4>(L, s);
+    return wide ? launch_px<CC, TIn, OUT, 16, 8>(L, s) : launch_px<CC, TIn, OUT, 16, 4>(L, s);
 }
 
 template <typename TIn, int OUT>

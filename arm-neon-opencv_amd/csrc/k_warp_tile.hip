@@ -9,18 +9,19 @@
 // here (the reference leaves them untouched).  The per-pixel
 // arithmetic is warp_kernel's (k_warp.hip), bit for bit.
 //
-// Why staging: warp_kernel gathers each tap row with one 8-byte load per lane,
-// and PMC shows the texture data path at ~1 lane per clock per CU (TD_TD_BUSY
-// ~95 % of the kernel, TA ~85 %): the kernel is bound by per-lane gathers, not
-// HBM.  Here a workgroup owns a 64 x 16 output tile, loads the tile's source
-// bounding box (a parallelogram's box, a few KB) with coalesced 16-byte
-// loads -- ~0.4 lane-loads per output pixel instead of 2 --
-// and reads the taps from LDS (two aligned 8-byte LDS reads per tap row,
-// v_alignbyte to the tap's byte offset).  Pixels whose taps fall outside the
-// box (only possible through rounding at the box edge, or non-finite
-// matrices) take warp_kernel's global gather, so correctness never depends on
-// the box computation.  Outputs leave through a per-wave LDS exchange as
-// 16-byte non-temporal stores.
+// Why staging: warp_kernel gathers each tap row with one 8/12-byte load per
+// lane; adjacent lanes' windows overlap but are not contiguous, so the
+// texture path processes them about one lane per clock per CU (TA/TD busy
+// ~90 % of the kernel): the gather kernel is bound by per-lane address
+// processing, not HBM.  Here a workgroup owns a 64 x TH output tile and
+// stages the tile's source bounding box into LDS with CONTIGUOUS lane loads
+// (lane i loads pixels 4i..4i+3 of a box row: CC dwords, 4-byte aligned),
+// widening every pixel to one LDS dword.  A tap pair is then two aligned
+// LDS dwords (ds_read2), so the sampler spends ~2 LDS instructions per
+// output pixel and no byte alignment.  Pixels whose taps fall outside the
+// box (rounding at its edge, non-finite matrices) take warp_kernel's global
+// gather, so correctness never depends on the box computation.  Outputs
+// leave through a per-wave LDS exchange as 16-byte non-temporal stores.
 #pragma clang fp contract(off)
 
 #include <cmath>
@@ -31,56 +32,65 @@
 namespace vacv {
 namespace {
 
-constexpr int kTW = 64;   // tile width (one pixel per lane)
-constexpr int kTH = 16;   // tile height (4 rows per wave)
-constexpr int kBoxBudget = 24 * 1024;  // LDS bytes for the staged box
+constexpr int kTW = 64;                  // tile width (one pixel per lane)
+constexpr int kBoxBudget = 40 * 1024;    // LDS bytes for the staged box
+
+// Tile height: a multiple of 16 (each wave samples TH/4 rows, 4 at a time).
+// 48 by default: at 1280x720 rot15 a 64 x 48 tile's box is ~1.7x its
+// footprint, and 720 rows split into whole tiles.
+int tile_height() {
+    const char* env = std::getenv("VACV_WARP_TH");
+    const int v = env ? std::atoi(env) : 48;
+    return (v >= 16 && v <= 128 && v % 16 == 0) ? v : 48;
+}
 
 // Box geometry every tile of this launch fits (host and device agree):
-// width/height in pixels and the LDS row stride in bytes.
+// width/height in pixels and the LDS row stride in dwords (one per pixel).
 struct BoxCap {
     int w, h, stride;
 };
 
-__host__ __device__ inline BoxCap box_cap(const float inv[6], int cc) {
+__host__ __device__ inline BoxCap box_cap(const float inv[6], int th) {
     // the tile's source footprint spans |m0|*(TW-1) + |m1|*(TH-1) in x (and
     // the same with m3, m4 in y); +6 covers the floor, the second tap, the
     // one-pixel margins and rounding
-    const float ex = fabsf(inv[0]) * (kTW - 1) + fabsf(inv[1]) * (kTH - 1);
-    const float ey = fabsf(inv[3]) * (kTW - 1) + fabsf(inv[4]) * (kTH - 1);
+    const float ex = fabsf(inv[0]) * (kTW - 1) + fabsf(inv[1]) * (th - 1);
+    const float ey = fabsf(inv[3]) * (kTW - 1) + fabsf(inv[4]) * (th - 1);
     BoxCap b{0, 0, 0};
     if (!(ex < 4096.f && ey < 4096.f)) return b;  // also NaN
     b.w = (int)ex + 6;
     b.h = (int)ey + 6;
-    int stride = ((b.w * cc + 15 + 16) + 15) & ~15;  // head (<16) + chunk overhang
-    if ((stride & 255) == 0) stride += 16;           // rows on different LDS banks
+    int stride = (b.w + 3 + 4 + 3) & ~3;  // align-down head (<4) + the last chunk's overhang
+    if (stride % 32 == 0) stride += 4;    // successive rows on different banks
     b.stride = stride;
     return b;
 }
 
-// 8 bytes at LDS byte address a (two aligned 8-byte reads + byte align)
-__device__ __forceinline__ void lds_tap8(const unsigned char* lds, uint32_t a, uint32_t& lo, uint32_t& hi) {
-    const uint32_t a8 = a & ~7u;
-    const uint2 p = *reinterpret_cast<const uint2*>(lds + a8);
-    const uint2 q = *reinterpret_cast<const uint2*>(lds + a8 + 8);
-    const uint32_t s = a & 7u;
-    if (s < 4) {
-        lo = __builtin_amdgcn_alignbyte(p.y, p.x, s);
-        hi = __builtin_amdgcn_alignbyte(q.x, p.y, s);
+template <int CC>
+__device__ __forceinline__ void widen4(const uint32_t* w, uint32_t* px) {
+    if constexpr (CC == 1) {
+        px[0] = w[0]; px[1] = w[0] >> 8; px[2] = w[0] >> 16; px[3] = w[0] >> 24;
+    } else if constexpr (CC == 2) {
+        px[0] = w[0]; px[1] = w[0] >> 16; px[2] = w[1]; px[3] = w[1] >> 16;
+    } else if constexpr (CC == 3) {
+        px[0] = w[0];
+        px[1] = __builtin_amdgcn_alignbyte(w[1], w[0], 3);
+        px[2] = __builtin_amdgcn_alignbyte(w[2], w[1], 2);
+        px[3] = w[2] >> 8;
     } else {
-        lo = __builtin_amdgcn_alignbyte(q.x, p.y, s - 4);
-        hi = __builtin_amdgcn_alignbyte(q.y, q.x, s - 4);
+        px[0] = w[0]; px[1] = w[1]; px[2] = w[2]; px[3] = w[3];
     }
 }
 
 template <int CC, int OUT>
 __global__ void __launch_bounds__(kBlock)
-warp_tile_kernel(WarpLaunch L, BoxCap cap, int tiles_x, int tiles_y, int total) {
+warp_tile_kernel(WarpLaunch L, BoxCap cap, int th, int tiles_x, int tiles_y, int total) {
     using TOut = typename std::conditional<(OUT == kOutSame), uint8_t, float>::type;
     constexpr bool kLut = OUT == kOutNorm;
     constexpr int kRowOut = kTW * CC * (int)sizeof(TOut);  // bytes of one tile row
     __shared__ float lut[kLut ? 256 * CC : 1];
     __shared__ __attribute__((aligned(16))) unsigned char xch[4][4 * kRowOut];
-    extern __shared__ __attribute__((aligned(16))) unsigned char box[];
+    extern __shared__ __attribute__((aligned(16))) uint32_t box[];
 
     // XCD-contiguous tile order (block b runs on XCD b % 8): neighbouring
     // tiles share box rows, so they should share an L2
@@ -94,7 +104,7 @@ warp_tile_kernel(WarpLaunch L, BoxCap cap, int tiles_x, int tiles_y, int total) 
     const int plane = pidx - img * L.src.planes;
     const int tid = (int)(threadIdx.y * 64 + threadIdx.x);
     const int lane = threadIdx.x, wave = threadIdx.y;
-    const int X0 = tx * kTW, Y0 = ty * kTH;
+    const int X0 = tx * kTW, Y0 = ty * th;
 
     if (kLut) {
         for (int i = tid; i < 256 * CC; i += kBlock) {
@@ -110,13 +120,14 @@ warp_tile_kernel(WarpLaunch L, BoxCap cap, int tiles_x, int tiles_y, int total) 
     const uint32_t slimit = (uint32_t)L.src.plane_bytes + srs.delta;
     const uint32_t rp32 = (uint32_t)L.src.row_pitch;  // plane < 2^31 bytes
     const int Ws = L.src.w, Hs = L.src.h;
+    const int Yend = min(Y0 + th, L.dst.h);
 
     // ---- the tile's source box (uniform) from its corner coordinates --------
     float fx_min = INFINITY, fx_max = -INFINITY, fy_min = INFINITY, fy_max = -INFINITY;
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
         const float x = (float)(X0 + ((c & 1) ? kTW - 1 : 0));
-        const float y = (float)(Y0 + ((c & 2) ? kTH - 1 : 0));
+        const float y = (float)(Y0 + ((c & 2) ? th - 1 : 0));
         const float fx = L.inv[0] * x + L.inv[1] * y + L.inv[2];
         const float fy = L.inv[3] * x + L.inv[4] * y + L.inv[5];
         fx_min = fminf(fx_min, fx); fx_max = fmaxf(fx_max, fx);
@@ -130,181 +141,210 @@ warp_tile_kernel(WarpLaunch L, BoxCap cap, int tiles_x, int tiles_y, int total) 
         by1 = min(Hs - 1, (int)floorf(fy_max) + 2);
     }
     if (bx1 - bx0 + 1 > cap.w || by1 - by0 + 1 > cap.h) { bx1 = bx0 - 1; by1 = by0 - 1; }  // nothing staged
+    const int bxa = bx0 & ~3;  // chunks start on 4-pixel boundaries: 4-byte aligned loads
     const int nrows = max(0, by1 - by0 + 1);
-    const int ncols = max(0, bx1 - bx0 + 1);
+    const int cpr = bx1 >= bx0 ? (bx1 - bxa) / 4 + 1 : 0;  // 4-pixel chunks per row
 
-    // ---- stage it: 16-byte chunks, row heads aligned down --------------------
-    const int cpr = ncols > 0 ? (ncols * CC + 15 + 15) / 16 : 0;  // chunks per row (head < 16)
-    auto chunk = [&](int i) {
+    // ---- stage it: lane-contiguous CC-dword loads, one LDS dword per pixel ---
+    // Every load of a pass is issued before any is consumed (no branch between
+    // them), so a tile costs one HBM/L2 round trip.  A chunk that crosses the
+    // plane's end reads as zeros from the buffer resource and is re-read byte
+    // by byte afterwards.
+    auto addr = [&](int i) {
         const int r = i / cpr, c = i - r * cpr;
-        const uint32_t a = (((uint32_t)(by0 + r) * rp32 + srs.delta + (uint32_t)(bx0 * CC)) & ~15u) + 16u * c;
-        uint4 v;
-        if (a + 16u <= slimit) {
-            // default cache policy: neighbouring tiles re-read these lines from L2
-            auto t = __builtin_amdgcn_raw_buffer_load_b128(srs.r, (int)a, 0, 0);
-            v = *reinterpret_cast<uint4*>(&t);
-        } else {
-            uint32_t w[4] = {0, 0, 0, 0};  // the chunk crossing the plane's end
-            for (int b = 0; b < 16; ++b)
-                if (a + b < slimit)
-                    w[b >> 2] |= (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(srs.r, (int)(a + b), 0, 0) << (8 * (b & 3));
-            v = make_uint4(w[0], w[1], w[2], w[3]);
-        }
-        return v;
+        return (uint32_t)(by0 + r) * rp32 + srs.delta + (uint32_t)((bxa + 4 * c) * CC);
     };
+    auto load_chunk = [&](uint32_t a, uint32_t* w) {
+        // default cache policy: neighbouring tiles re-read these lines from L2
+        if constexpr (CC == 1) {
+            w[0] = __builtin_amdgcn_raw_buffer_load_b32(srs.r, (int)a, 0, 0);
+        } else if constexpr (CC == 2) {
+            auto t = __builtin_amdgcn_raw_buffer_load_b64(srs.r, (int)a, 0, 0);
+            w[0] = t[0]; w[1] = t[1];
+        } else if constexpr (CC == 3) {
+            auto t = __builtin_amdgcn_raw_buffer_load_b96(srs.r, (int)a, 0, 0);
+            w[0] = t[0]; w[1] = t[1]; w[2] = t[2];
+        } else {
+            auto t = __builtin_amdgcn_raw_buffer_load_b128(srs.r, (int)a, 0, 0);
+            w[0] = t[0]; w[1] = t[1]; w[2] = t[2]; w[3] = t[3];
+        }
+    };
+    constexpr int kInFlight = 6;
     const int nchunks = nrows * cpr;
-    for (int i = tid; i < nchunks; i += 2 * kBlock) {  // two loads in flight per thread
-        const int i2 = i + kBlock;
-        const uint4 v0 = chunk(i);
-        uint4 v1 = make_uint4(0, 0, 0, 0);
-        if (i2 < nchunks) v1 = chunk(i2);
-        *reinterpret_cast<uint4*>(box + (i / cpr) * cap.stride + 16 * (i % cpr)) = v0;
-        if (i2 < nchunks) *reinterpret_cast<uint4*>(box + (i2 / cpr) * cap.stride + 16 * (i2 % cpr)) = v1;
+    for (int i0 = tid; i0 < nchunks; i0 += kInFlight * kBlock) {
+        uint32_t w[kInFlight][CC], a[kInFlight];
+#pragma unroll
+        for (int j = 0; j < kInFlight; ++j) {
+            a[j] = i0 + j * kBlock < nchunks ? addr(i0 + j * kBlock) : 0u;
+            load_chunk(a[j], w[j]);
+        }
+#pragma unroll
+        for (int j = 0; j < kInFlight; ++j) {
+            const int i = i0 + j * kBlock;
+            if (i < nchunks) {
+                if (a[j] + 4u * CC > slimit) {  // the chunk crossing the plane's end
+#pragma unroll
+                    for (int d = 0; d < CC; ++d) w[j][d] = 0;
+                    for (int e = 0; e < 4 * CC; ++e)
+                        if (a[j] + e < slimit)
+                            w[j][e >> 2] |= (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(srs.r, (int)(a[j] + e), 0, 0)
+                                            << (8 * (e & 3));
+                }
+                uint32_t px[4];
+                widen4<CC>(w[j], px);
+                *reinterpret_cast<uint4*>(box + (i / cpr) * cap.stride + 4 * (i % cpr)) =
+                    make_uint4(px[0], px[1], px[2], px[3]);
+            }
+        }
     }
     __syncthreads();
 
-    // ---- sample: wave w takes tile rows 4w..4w+3, lane = column -------------
+    // ---- sample: wave w takes rows [Y0 + w*th/4, +th/4), 4 at a time --------
     TOut* xo = reinterpret_cast<TOut*>(xch[wave]);
     const int x = X0 + lane;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        const int y = Y0 + wave * 4 + q;
-        TOut* o = xo + (q * kTW + lane) * CC;
-        if (x >= L.dst.w || y >= L.dst.h) continue;
-        // warp_affine_naive.cpp:23-24: (m0*x + m1*y) + m2, all float
-        const float fx = L.inv[0] * (float)x + L.inv[1] * (float)y + L.inv[2];
-        const float fy = L.inv[3] * (float)x + L.inv[4] * (float)y + L.inv[5];
-        int sx = 0, sy = 0;
-        float ax = 0.f, ay = 0.f;
-        if (!(affine_tap(fy, Hs, sy, ay) && affine_tap(fx, Ws, sx, ax))) {
-#pragma unroll
-            for (int k = 0; k < CC; ++k) {
-                if (OUT == kOutNorm) o[k] = lut[k * 256 + (int)L.border[k]];
-                else o[k] = (TOut)L.border[k];
-            }
-            continue;
-        }
-        const int wy0 = (int)((1.f - ay) * 2048.f + 0.5f), wy1 = 2048 - wy0;
-        const int wx0 = (int)((1.f - ax) * 2048.f + 0.5f), wx1 = 2048 - wx0;
-        uint32_t a0, a1, c0, c1;
-        if (sx >= bx0 && sx + 1 <= bx1 && sy >= by0 && sy + 1 <= by1) {
-            const int r = sy - by0;
-            const uint32_t head = ((uint32_t)sy * rp32 + srs.delta + (uint32_t)(bx0 * CC)) & 15u;
-            const uint32_t la = (uint32_t)(r * cap.stride) + head + (uint32_t)((sx - bx0) * CC);
-            const uint32_t headb = ((uint32_t)(sy + 1) * rp32 + srs.delta + (uint32_t)(bx0 * CC)) & 15u;
-            const uint32_t lb = (uint32_t)((r + 1) * cap.stride) + headb + (uint32_t)((sx - bx0) * CC);
-            lds_tap8(box, la, a0, a1);
-            lds_tap8(box, lb, c0, c1);
-        } else {
-            // outside the staged box (rounding at its edge): gather as warp_kernel
-            const uint32_t o0 = (uint32_t)sy * rp32 + (uint32_t)(sx * CC) + srs.delta;
-            const uint32_t o1 = o0 + rp32;
-            a0 = a1 = c0 = c1 = 0u;
-            if (o1 + 8u <= slimit) {
-                auto va = __builtin_amdgcn_raw_buffer_load_b64(srs.r, (int)o0, 0, 0);
-                auto vc = __builtin_amdgcn_raw_buffer_load_b64(srs.r, (int)o1, 0, 0);
-                a0 = va[0]; a1 = va[1]; c0 = vc[0]; c1 = vc[1];
-            } else {
-                const unsigned char* r0 = sp + (int64_t)sy * L.src.row_pitch + (int64_t)sx * CC;
-                for (int e = 0; e < 2 * CC && e < 8; ++e) {
-                    const uint32_t ta = r0[e], tb = r0[L.src.row_pitch + e];
-                    if (e < 4) { a0 |= ta << (8 * e); c0 |= tb << (8 * e); }
-                    else { a1 |= ta << (8 * (e - 4)); c1 |= tb << (8 * (e - 4)); }
-                }
-            }
-        }
-        // warp_affine_naive.cpp:50-54 as (tl*wx0 + tr*wx1)*wy0 + (bl*wx0 +
-        // br*wx1)*wy1: the same int32 value (exact: <= 255*2^22)
-        typedef unsigned short us2 __attribute__((ext_vector_type(2)));
-        const us2 wx = __builtin_bit_cast(us2, (uint32_t)wx0 | ((uint32_t)wx1 << 16));
-#pragma unroll
-        for (int k = 0; k < CC; ++k) {
-            const uint32_t sel = (uint32_t)k | (0x0Cu << 8) | ((uint32_t)(CC + k) << 16) | (0x0Cu << 24);
-            const uint32_t top = __builtin_amdgcn_perm(a1, a0, sel);
-            const uint32_t bot = __builtin_amdgcn_perm(c1, c0, sel);
-            const uint32_t ht = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, top), wx, 0u, false);
-            const uint32_t hb = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, bot), wx, 0u, false);
-            const int v = (int)((__umul24(ht, (uint32_t)wy0) + __umul24(hb, (uint32_t)wy1)) >> 22);
-            if (OUT == kOutSame) o[k] = (TOut)v;
-            else if (OUT == kOutF32) o[k] = (TOut)(float)v;
-            else o[k] = lut[k * 256 + v];
-        }
-    }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-
-    // ---- the wave's 4 row segments, LDS -> HBM ------------------------------------
     const int nx = min(kTW, L.dst.w - X0);
     const int vbytes = nx * CC * (int)sizeof(TOut);
     unsigned char* dbase = const_cast<unsigned char*>(L.dst.base) + (int64_t)img * L.dst.img_pitch +
                            (int64_t)plane * L.dst.plane_pitch + (int64_t)X0 * CC * sizeof(TOut);
-    const unsigned char* xs = xch[wave];
     const bool aligned = ((reinterpret_cast<uintptr_t>(dbase) | (uintptr_t)L.dst.row_pitch) & 15) == 0;
-    const int rows = max(0, min(4, L.dst.h - (Y0 + wave * 4)));
-    if (aligned) {
-        const int cpr_o = (vbytes + 15) / 16;
-        for (int i = lane; i < rows * cpr_o; i += 64) {
-            const int q = i / cpr_o, c = i - q * cpr_o;
-            unsigned char* drow = dbase + (int64_t)(Y0 + wave * 4 + q) * L.dst.row_pitch;
-            const unsigned char* s = xs + q * kRowOut;
-            if (16 * c + 16 <= vbytes) {
-                __builtin_nontemporal_store(*reinterpret_cast<const u32x4*>(s + 16 * c),
-                                            reinterpret_cast<u32x4*>(drow) + c);
+    typedef unsigned short us2 __attribute__((ext_vector_type(2)));
+    const float fxc = L.inv[0] * (float)x, fyc = L.inv[3] * (float)x;
+
+    for (int yg = Y0 + wave * (th / 4); yg < min(Y0 + (wave + 1) * (th / 4), Yend); yg += 4) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int y = yg + q;
+            TOut* o = xo + (q * kTW + lane) * CC;
+            if (x >= L.dst.w || y >= Yend) continue;
+            // warp_affine_naive.cpp:23-24: (m0*x + m1*y) + m2, all float
+            const float fx = fxc + L.inv[1] * (float)y + L.inv[2];
+            const float fy = fyc + L.inv[4] * (float)y + L.inv[5];
+            int sx = 0, sy = 0;
+            float ax = 0.f, ay = 0.f;
+            if (!(affine_tap(fy, Hs, sy, ay) && affine_tap(fx, Ws, sx, ax))) {
+#pragma unroll
+                for (int k = 0; k < CC; ++k) {
+                    if (OUT == kOutNorm) o[k] = lut[k * 256 + (int)L.border[k]];
+                    else o[k] = (TOut)L.border[k];
+                }
+                continue;
+            }
+            const int wy0 = (int)((1.f - ay) * 2048.f + 0.5f), wy1 = 2048 - wy0;
+            const int wx0 = (int)((1.f - ax) * 2048.f + 0.5f), wx1 = 2048 - wx0;
+            uint32_t a0, a1, c0, c1;
+            if (sx >= bx0 && sx + 1 <= bx1 && sy >= by0 && sy + 1 <= by1) {
+                const uint32_t* t = box + (sy - by0) * cap.stride + (sx - bxa);
+                a0 = t[0]; a1 = t[1]; c0 = t[cap.stride]; c1 = t[cap.stride + 1];
             } else {
-                for (int e = 16 * c; e < vbytes; ++e) drow[e] = s[e];
+                // outside the staged box (rounding at its edge): gather the
+                // 2*CC tap bytes of both rows, one pixel per dword
+                const unsigned char* r0 = sp + (int64_t)sy * L.src.row_pitch + (int64_t)sx * CC;
+                a0 = a1 = c0 = c1 = 0u;
+                for (int e = 0; e < CC; ++e) {
+                    a0 |= (uint32_t)r0[e] << (8 * e);
+                    a1 |= (uint32_t)r0[CC + e] << (8 * e);
+                    c0 |= (uint32_t)r0[L.src.row_pitch + e] << (8 * e);
+                    c1 |= (uint32_t)r0[L.src.row_pitch + CC + e] << (8 * e);
+                }
+            }
+            // warp_affine_naive.cpp:50-54 as (tl*wx0 + tr*wx1)*wy0 + (bl*wx0 +
+            // br*wx1)*wy1: the same int32 value (exact: <= 255*2^22)
+            const us2 wx = __builtin_bit_cast(us2, (uint32_t)wx0 | ((uint32_t)wx1 << 16));
+#pragma unroll
+            for (int k = 0; k < CC; ++k) {
+                const uint32_t sel = (uint32_t)k | (0x0Cu << 8) | ((uint32_t)(4 + k) << 16) | (0x0Cu << 24);
+                const uint32_t top = __builtin_amdgcn_perm(a1, a0, sel);
+                const uint32_t bot = __builtin_amdgcn_perm(c1, c0, sel);
+                const uint32_t ht = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, top), wx, 0u, false);
+                const uint32_t hb = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, bot), wx, 0u, false);
+                const int v = (int)((__umul24(ht, (uint32_t)wy0) + __umul24(hb, (uint32_t)wy1)) >> 22);
+                if (OUT == kOutSame) o[k] = (TOut)v;
+                else if (OUT == kOutF32) o[k] = (TOut)(float)v;
+                else o[k] = lut[k * 256 + v];
             }
         }
-    } else {
-        for (int i = lane; i < rows * vbytes; i += 64) {
-            const int q = i / vbytes, e = i - q * vbytes;
-            dbase[(int64_t)(Y0 + wave * 4 + q) * L.dst.row_pitch + e] = xs[q * kRowOut + e];
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+
+        // ---- the wave's 4 row segments, LDS -> HBM ------------------------------
+        const int rows = max(0, min(4, Yend - yg));
+        const unsigned char* xs = xch[wave];
+        if (aligned) {
+            const int cpr_o = (vbytes + 15) / 16;
+            for (int i = lane; i < rows * cpr_o; i += 64) {
+                const int q = i / cpr_o, c = i - q * cpr_o;
+                unsigned char* drow = dbase + (int64_t)(yg + q) * L.dst.row_pitch;
+                const unsigned char* s = xs + q * kRowOut;
+                if (16 * c + 16 <= vbytes) {
+                    __builtin_nontemporal_store(*reinterpret_cast<const u32x4*>(s + 16 * c),
+                                                reinterpret_cast<u32x4*>(drow) + c);
+                } else {
+                    for (int e = 16 * c; e < vbytes; ++e) drow[e] = s[e];
+                }
+            }
+        } else {
+            for (int i = lane; i < rows * vbytes; i += 64) {
+                const int q = i / vbytes, e = i - q * vbytes;
+                dbase[(int64_t)(yg + q) * L.dst.row_pitch + e] = xs[q * kRowOut + e];
+            }
         }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     }
 }
 
 template <int CC, int OUT>
-hipError_t launch_one(const WarpLaunch& L, const BoxCap& cap, hipStream_t s) {
-    const int tiles_x = (L.dst.w + kTW - 1) / kTW, tiles_y = (L.dst.h + kTH - 1) / kTH;
+hipError_t launch_one(const WarpLaunch& L, const BoxCap& cap, int th, hipStream_t s) {
+    const int tiles_x = (L.dst.w + kTW - 1) / kTW, tiles_y = (L.dst.h + th - 1) / th;
     const int64_t total = (int64_t)tiles_x * tiles_y * L.n * L.src.planes;
     if (total >= 0x7FFFFFF0LL) return hipErrorInvalidValue;
     const int64_t blocks = (total + 7) / 8 * 8;
-    const size_t lds = (size_t)cap.h * cap.stride + 16;  // +16: the last tap read's window
-    hipLaunchKernelGGL((warp_tile_kernel<CC, OUT>), dim3((unsigned)blocks), dim3(64, 4), lds, s, L, cap, tiles_x,
-                       tiles_y, (int)total);
+    const size_t lds = (size_t)cap.h * cap.stride * 4 + 16;  // +16: the last tap pair past the last row
+    hipLaunchKernelGGL((warp_tile_kernel<CC, OUT>), dim3((unsigned)blocks), dim3(64, 4), lds, s, L, cap, th,
+                       tiles_x, tiles_y, (int)total);
     return hipGetLastError();
 }
 
 template <int OUT>
-hipError_t launch_cc(const WarpLaunch& L, const BoxCap& cap, hipStream_t s) {
+hipError_t launch_cc(const WarpLaunch& L, const BoxCap& cap, int th, hipStream_t s) {
     switch (L.src.cc) {
-        case 1: return launch_one<1, OUT>(L, cap, s);
-        case 2: return launch_one<2, OUT>(L, cap, s);
-        case 3: return launch_one<3, OUT>(L, cap, s);
-        case 4: return launch_one<4, OUT>(L, cap, s);
+        case 1: return launch_one<1, OUT>(L, cap, th, s);
+        case 2: return launch_one<2, OUT>(L, cap, th, s);
+        case 3: return launch_one<3, OUT>(L, cap, th, s);
+        case 4: return launch_one<4, OUT>(L, cap, th, s);
         default: return hipErrorInvalidValue;
     }
 }
 
 }  // namespace
 
-// Opt-in (VACV_WARP_TILE=1), for A/B measurement: u8 warps whose tile
-// footprint fits the LDS budget.  Measured slower than warp_kernel at 720p
-// rot15 (0.395 vs 0.315 ms): the per-pixel LDS address / byte-align work and
-// the staging barrier cost more than the gathers saved.
+// Opt-in (VACV_WARP_TILE=1), for A/B measurement: u8 warps whose tile box
+// fits the LDS budget and whose source rows are 4-byte aligned (the staging
+// loads are dword loads).  Measured slower than warp_kernel at 720p rot15
+// (0.357 vs 0.283 ms u8 out; 0.599 vs 0.538 ms normalized): PMC shows ~10x
+// the gather kernel's LDS bank-conflict cycles (the rotated tap reads of 64
+// lanes spread over ~18 box rows) and no drop in texture-path busy time,
+// which counts outstanding requests rather than a throughput limit
+// (DESIGN.md 3.3).
 bool warp_tile_applies(const WarpLaunch& L) {
     const char* env = std::getenv("VACV_WARP_TILE");
     if (!(env && env[0] == '1')) return false;
     if (L.src.esize != 1 || L.src.cc > 4) return false;
-    const BoxCap cap = box_cap(L.inv, L.src.cc);
-    return cap.w > 0 && (int64_t)cap.h * cap.stride <= kBoxBudget;
+    const uint64_t al = reinterpret_cast<uintptr_t>(L.src.base) | (uint64_t)L.src.row_pitch |
+                        (uint64_t)L.src.img_pitch | (uint64_t)L.src.plane_pitch;
+    if (al & 3) return false;
+    const BoxCap cap = box_cap(L.inv, tile_height());
+    return cap.w > 0 && (int64_t)cap.h * cap.stride * 4 + 16 <= kBoxBudget;
 }
 
 hipError_t launch_warp_tile(const WarpLaunch& L, hipStream_t s) {
-    const BoxCap cap = box_cap(L.inv, L.src.cc);
-    if (L.out == kOutSame) return launch_cc<kOutSame>(L, cap, s);
-    if (L.out == kOutF32) return launch_cc<kOutF32>(L, cap, s);
-    return launch_cc<kOutNorm>(L, cap, s);
+    const int th = tile_height();
+    const BoxCap cap = box_cap(L.inv, th);
+    if (L.out == kOutSame) return launch_cc<kOutSame>(L, cap, th, s);
+    if (L.out == kOutF32) return launch_cc<kOutF32>(L, cap, th, s);
+    return launch_cc<kOutNorm>(L, cap, th, s);
 }
 
 }  // namespace vacv

@@ -290,7 +290,9 @@ def test_warp_affine_config_and_harness(ops, dev, oracle, golden):
 def test_warp_tile_and_gather_kernels_agree(ops, dev, oracle, monkeypatch):
     """VACV_WARP_TILE=1 runs u8 warps on the LDS-staged tile kernel
     (k_warp_tile.hip, opt-in: measured slower) when the tile's source box fits
-    its LDS budget; the default is the per-pixel gather kernel (k_warp.hip).
+    its LDS budget and the source rows are 4-byte aligned; the default is the
+    per-pixel gather kernel (k_warp.hip).  VACV_WARP_LW / VACV_WARP_PX switch
+    the gather kernel's lane blocks (64 x 1 or 16 x 4; 4 or 8 per wave).
     Identical outputs at full size for rotations,
     flips, shears, strong down-scales (box over budget: the gather kernel),
     fused normalisation, NCHW planes and a pitched destination."""
@@ -312,9 +314,24 @@ def test_warp_tile_and_gather_kernels_agree(ops, dev, oracle, monkeypatch):
             monkeypatch.setenv("VACV_WARP_TILE", "0")
             b = ops.warp_affine(src, m, wo, ho)
             bn = ops.warp_affine_normalize(src, m, wo, ho, MEAN, STD)
-            monkeypatch.delenv("VACV_WARP_TILE")
             assert torch.equal(a, b), f"warp kernels differ {m.tolist()} {wo}x{ho}"
             assert torch.equal(an, bn), f"warp normalize kernels differ {m.tolist()} {wo}x{ho}"
+            for lw, px in (("16", "4"), ("16", "8"), ("64", "4")):
+                monkeypatch.setenv("VACV_WARP_LW", lw)
+                monkeypatch.setenv("VACV_WARP_PX", px)
+                assert torch.equal(ops.warp_affine(src, m, wo, ho), b), f"gather LW={lw} PX={px}"
+                assert torch.equal(ops.warp_affine_normalize(src, m, wo, ho, MEAN, STD), bn), f"gather LW={lw} PX={px} norm"
+            monkeypatch.delenv("VACV_WARP_LW")
+            monkeypatch.delenv("VACV_WARP_PX")
+            monkeypatch.delenv("VACV_WARP_TILE")
+    for c in (1, 2, 4):  # every staged pixel width, odd sizes, both kernels vs the oracle
+        im = synthetic_image(90 + c, 97, 143, c)
+        for m in mats[:2]:
+            for flag in ("1", "0"):
+                monkeypatch.setenv("VACV_WARP_TILE", flag)
+                got = host(ops.warp_affine(to_dev(im.reshape(1, 97, 143, c), dev), m, 121, 83))[0]
+                assert_same(got.reshape(83, 121, c), oracle.warp_affine(im, m, 121, 83).reshape(83, 121, c),
+                            f"warp c={c} tile={flag}")
     monkeypatch.setenv("VACV_WARP_TILE", "1")
     chw = to_dev(np.ascontiguousarray(imgs.transpose(0, 3, 1, 2)), dev)
     got = host(ops.warp_affine(chw, mats[0], 300, 200, layout=NCHW))
