@@ -1,0 +1,302 @@
+// k_yuv_resize.hip -- YUV420sp (NV21 / NV12) -> BGR -> u8 bilinear resize
+// -> (u8 | fp32 | normalised fp32), NHWC or NCHW, in one pass over HBM.
+//
+// This is the camera-frame-to-model-input step: the
+// reference's callers run it as three or four separate passes,
+//   CvtColor::nv_to_bgr_naive        cvt_color.cpp:39-135 (decode)
+//   ResizeNaive::resize_naive_inter_linear_u8  resize_naive.cpp:10-68
+//   Tensor::change_dtype + NormalizeNaive::normalize_naive_*
+//                                    tensor.cpp:459-502, normalize_naive.cpp:74-90
+//   Tensor::change_layout (HWC -> CHW)  tensor.cpp:393-457
+// each writing a full-size intermediate.  Here every output pixel decodes
+// only the (at most) four source pixels its bilinear taps weight, straight
+// from the NV21 planes, so the decoded BGR frame never exists: HBM traffic
+// is the weighted Y and chroma rows plus the output.
+//
+// Exactness.  A tap pixel is decoded with the reference's integer formula
+// (chroma_terms, vacv_semantics.hpp) to the same u8 BGR triple
+// nv_to_bgr_naive writes, and the blend is the u8 resize's fixed point
+// (blend_fixed / tap_of, vacv_device.hpp) on those bytes; the result is
+// therefore bit-identical to decode -> resize -> convert -> normalize ->
+// change_layout.  Rows with a zero vertical weight are never read (they
+// contribute exactly 0 in every mode).
+//
+// Shape.  Output pixels of an image are numbered row-major; wave v of
+// workgroup b owns the 256 pixels from p0 = (4b + v)*256 and lane l samples
+// p0 + 64j + l (j < 4), so each gather instruction reads one contiguous run
+// of a source row.  Per source row a pixel issues two dword gathers: 4 Y
+// bytes at the left tap (2 used) and 4 chroma bytes covering both taps' VU
+// pairs (clamped so the read never leaves the row).  When no output row
+// weights two source rows (ONE_ROW, checked on the host) only one row is
+// gathered; otherwise both rows always are (a zero weight multiplies exactly).
+// Results are re-assembled in LDS (plane-major for NCHW) and leave as 16-byte
+// non-temporal stores, 1 KiB of contiguous output per store instruction.
+#pragma clang fp contract(off)
+
+#include <type_traits>
+
+#include "vacv_device.hpp"
+
+namespace vacv {
+namespace {
+
+// Pixels per lane: 8 when one source row is gathered per pixel (twice the
+// bytes in flight for the same registers), else 4.
+constexpr int yuv_pxl(bool one_row) { return one_row ? 8 : 4; }
+
+// One decoded pixel, cvt_color.cpp:69-88: R = Y + ra, G = Y - ga, B = Y + ba,
+// clamped; packed as bytes {B, G, R} of a dword.
+__device__ __forceinline__ uint32_t decode_bgr(int y, const Chroma& c) {
+    const uint32_t b = (uint32_t)clamp_u8(y + c.ba);
+    const uint32_t g = (uint32_t)clamp_u8(y - c.ga);
+    const uint32_t r = (uint32_t)clamp_u8(y + c.ra);
+    return b | (g << 8) | (r << 16);
+}
+
+// Raw gathers of one weighted source row sy for a pixel whose left tap is
+// column tx: 4 Y bytes at tx (2 used) and 4 chroma bytes holding the VU
+// pairs of columns tx and tx + 1 (one pair when tx is even), read from an
+// even column no later than w - 4 so the dword never leaves the row.
+// w >= 4 and even, tx <= w - 2.
+struct RowTaps {
+    uint32_t y, c;   // raw dwords
+};
+
+// Where the two taps' VU pairs sit in RowTaps::c: bits 0-7 = bit shift of
+// the left tap's pair (0 or 16), bit 8 = the right tap's pair is the next one.
+__device__ __forceinline__ uint32_t chroma_sel(int w, int tx) {
+    const int ca = tx & ~1;
+    return 8u * (uint32_t)(ca - min(ca, w - 4)) | ((uint32_t)(tx & 1) << 8);
+}
+
+__device__ __forceinline__ void gather_row(const Rsrc& rs, uint32_t rp, uint32_t uvbase, int w, int sy, int tx,
+                                           RowTaps& t) {
+    t.y = __builtin_amdgcn_raw_buffer_load_b32(rs.r, (int)((uint32_t)sy * rp + (uint32_t)tx + rs.delta), 0,
+                                               VACV_LOAD_AUX);
+    const int ca = tx & ~1;
+    const int c0 = min(ca, w - 4);
+    t.c = __builtin_amdgcn_raw_buffer_load_b32(rs.r, (int)(uvbase + (uint32_t)(sy >> 1) * rp + (uint32_t)c0 + rs.delta),
+                                               0, VACV_LOAD_AUX);
+}
+
+// Decode the row's two tap pixels: lo = left {B,G,R}, hi = right.
+__device__ __forceinline__ void decode_row(const RowTaps& t, uint32_t cs, int v_first, uint32_t& lo, uint32_t& hi) {
+    const uint32_t sa = cs & 0xFFu;
+    const uint32_t sb = sa + ((cs >> 8) << 4);
+    const int a0 = (int)((t.c >> sa) & 0xFFu), a1 = (int)((t.c >> (sa + 8)) & 0xFFu);
+    const int b0 = (int)((t.c >> sb) & 0xFFu), b1 = (int)((t.c >> (sb + 8)) & 0xFFu);
+    // cvt_color.cpp:68-69: _v = vu[x_num], _u = vu[y_num]; NV21 stores V first
+    const Chroma ka = v_first ? chroma_terms(a1, a0) : chroma_terms(a0, a1);
+    const Chroma kb = v_first ? chroma_terms(b1, b0) : chroma_terms(b0, b1);
+    lo = decode_bgr((int)(t.y & 0xFFu), ka);
+    hi = decode_bgr((int)((t.y >> 8) & 0xFFu), kb);
+}
+
+// Output pixels per wave and per LDS exchange round (4 per lane).
+constexpr int kGroupPx = 256;
+
+// Waves per SIMD the register budget is set for: the normalised one-row
+// kernel needs ~70 VGPRs at 8 pixels per lane (64 would spill).
+constexpr int yuv_waves(int out, bool one_row) { return (one_row && out == kOutNorm) ? 6 : 8; }
+
+template <int OUT, int MODE, bool CHW, bool ONE_ROW>
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(yuv_waves(OUT, ONE_ROW))))
+yuv_resize_kernel(YuvResizeLaunch L) {
+    using TOut = typename std::conditional<(OUT == kOutSame), uint8_t, float>::type;
+    constexpr int kES = (int)sizeof(TOut);
+    constexpr int NR = ONE_ROW ? 1 : 2;
+    constexpr int PXL = yuv_pxl(ONE_ROW);
+    constexpr int kWavePx = 64 * PXL;
+    constexpr int kSpan = kGroupPx * kES * (CHW ? 1 : 3);  // bytes one round writes per plane
+    __shared__ __attribute__((aligned(16))) unsigned char xch[4][3 * kGroupPx * kES];
+
+    const int img = blockIdx.y;
+    const int P = L.wo * L.ho;
+    const int p0 = ((int)blockIdx.x * 4 + (int)threadIdx.y) * kWavePx;
+    if (p0 >= P) return;  // whole wave
+    const int npx = min(kWavePx, P - p0);
+    const int lane = threadIdx.x;
+
+    const unsigned char* sp = L.src + (int64_t)img * L.src_img;
+    const Rsrc rs = make_rsrc(sp, L.src_bytes);
+    const uint32_t rp = (uint32_t)L.src_row;
+    const uint32_t uvbase = (uint32_t)L.h * rp;
+
+    // ---- gathers: lane l takes pixels p0 + 64j + l, so one gather
+    // instruction reads a contiguous run of a source row; every load is
+    // issued before any decode ------------------------------------------------
+    RowTaps t[PXL][NR];
+    // wyp = {wA, wB} as u16; ONE_ROW keeps chroma_sel in the (zero) wB half
+    uint32_t wxp[PXL], wyp[PXL], csel[ONE_ROW ? 1 : PXL];
+    // vertical taps: when the output is at least a wave's pixels wide a wave
+    // touches at most two output rows, whose taps are computed once
+    const int W = L.wo;
+    const int y_first = p0 / W;  // wave-uniform
+    const int x_first = p0 - y_first * W;
+    const bool wide = W >= kWavePx;
+    FixedTap ty0 = tap_of<MODE>(y_first, L.h, L.ho, L.scale_yf, L.scale_yd);
+    FixedTap ty1 = tap_of<MODE>(min(y_first + 1, L.ho - 1), L.h, L.ho, L.scale_yf, L.scale_yd);
+    if (ONE_ROW && ty0.w0 == 0) { ty0.i += 1; ty0.w0 = ty0.w1; ty0.w1 = 0; }  // the weighted row as row A
+    if (ONE_ROW && ty1.w0 == 0) { ty1.i += 1; ty1.w0 = ty1.w1; ty1.w1 = 0; }
+#pragma unroll
+    for (int j = 0; j < PXL; ++j) {
+#pragma unroll
+        for (int r = 0; r < NR; ++r) t[j][r].y = t[j][r].c = 0u;
+        wxp[j] = wyp[j] = 0u;
+        if (!ONE_ROW) csel[j] = 0u;
+        if (j * 64 + lane >= npx) continue;
+        const int d = x_first + j * 64 + lane;  // < W + kWavePx
+        const int dy = wide ? (d >= W ? 1 : 0) : d / W;
+        const int x = d - dy * W;
+        const FixedTap tx = tap_of<MODE>(x, L.w, W, L.scale_xf, L.scale_xd);
+        FixedTap ty;
+        if (wide) {
+            ty.i = dy ? ty1.i : ty0.i;
+            ty.w0 = dy ? ty1.w0 : ty0.w0;
+            ty.w1 = dy ? ty1.w1 : ty0.w1;
+        } else {
+            ty = tap_of<MODE>(y_first + dy, L.h, L.ho, L.scale_yf, L.scale_yd);
+            if (ONE_ROW && ty.w0 == 0) { ty.i += 1; ty.w0 = ty.w1; ty.w1 = 0; }
+        }
+        wxp[j] = (uint32_t)tx.w0 | ((uint32_t)tx.w1 << 16);
+        const uint32_t cs = chroma_sel(L.w, tx.i);
+        wyp[j] = (uint32_t)ty.w0 | ((ONE_ROW ? cs : (uint32_t)ty.w1) << 16);
+        if (!ONE_ROW) csel[j] = cs;
+        // both rows of a two-row pixel are always read (rows i, i + 1 exist);
+        // a zero weight multiplies them out exactly
+        gather_row(rs, rp, uvbase, L.w, ty.i, tx.i, t[j][0]);
+        if (!ONE_ROW) gather_row(rs, rp, uvbase, L.w, ty.i + 1, tx.i, t[j][NR - 1]);
+    }
+
+    ChanNorm cn[3] = {};
+    if (OUT == kOutNorm) {
+#pragma unroll
+        for (int k = 0; k < 3; ++k) cn[k] = chan_norm(L.norm, img, k);
+    }
+
+    unsigned char* dimg = L.dst + (int64_t)img * L.dst_img;
+    const uint32_t out_row = (uint32_t)L.wo * kES * (CHW ? 1 : 3);  // dense bytes of one output row
+    const uint32_t rowp = (uint32_t)L.dst_row;
+    const bool dense = L.dst_row == (int64_t)out_row;
+    TOut* xo = reinterpret_cast<TOut*>(xch[threadIdx.y]);
+
+#pragma unroll
+    for (int g = 0; g < PXL / 4; ++g) {
+        // ---- decode + blend 256 pixels into the wave's LDS buffer:
+        // plane-major for NCHW ([k][256]), pixel-major for NHWC ([256][3]) ---
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) {
+            const int j = g * 4 + jj;
+            uint32_t px[2][2];
+            const uint32_t cs = ONE_ROW ? wyp[j] >> 16 : csel[j];
+            decode_row(t[j][0], cs, L.v_first, px[0][0], px[0][1]);
+            if (ONE_ROW) px[1][0] = px[1][1] = 0u;
+            else decode_row(t[j][NR - 1], cs, L.v_first, px[1][0], px[1][1]);
+            const us2 wx = __builtin_bit_cast(us2, wxp[j]);
+            const uint32_t wA = wyp[j] & 0xFFFFu, wB = ONE_ROW ? 0u : wyp[j] >> 16;
+            const int q = jj * 64 + lane;
+#pragma unroll
+            for (int k = 0; k < 3; ++k) {
+                // byte of the decoded triple: B,G,R = 0,1,2; RGB output reverses
+                const uint32_t bsel = L.rgb ? 2u - (uint32_t)k : (uint32_t)k;
+                // {left, right} bytes -> u16 lanes (v_perm_b32)
+                const uint32_t ps = bsel | (0x0Cu << 8) | ((bsel + 4u) << 16) | (0x0Cu << 24);
+                const uint32_t top = __builtin_amdgcn_perm(px[0][1], px[0][0], ps);
+                const uint32_t bot = __builtin_amdgcn_perm(px[1][1], px[1][0], ps);
+                const int v = blend_fixed<MODE>(top, bot, wx, wA, wB);
+                TOut ov;
+                if (OUT == kOutSame) ov = (TOut)v;
+                else if (OUT == kOutF32) ov = (TOut)(float)v;
+                else ov = (TOut)normalize_u8v(cn[k], v);
+                xo[CHW ? k * kGroupPx + q : q * 3 + k] = ov;
+            }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+
+        // ---- LDS -> HBM: dense byte b of a plane's output lives at row
+        // b / out_row, column byte b % out_row --------------------------------
+        const int gp = npx - g * kGroupPx;  // valid pixels of this round (uniform)
+        if (gp > 0) {
+            const uint32_t vbytes = (uint32_t)min(gp, kGroupPx) * kES * (CHW ? 1 : 3);
+            const uint32_t b0 = (uint32_t)(p0 + g * kGroupPx) * kES * (CHW ? 1 : 3);
+#pragma unroll
+            for (int k = 0; k < (CHW ? 3 : 1); ++k) {
+                unsigned char* dp = dimg + (int64_t)k * L.dst_plane;
+                const unsigned char* xs = xch[threadIdx.y] + k * kSpan;
+                const bool chunked = (reinterpret_cast<uintptr_t>(dp) & 15) == 0 && (L.dst_row & 15) == 0 &&
+                                     (dense || (out_row & 15) == 0);  // 16-byte chunks never straddle rows
+                if (chunked) {
+                    for (uint32_t c = lane; c * 16 < vbytes; c += 64) {
+                        const uint32_t b = b0 + 16 * c;
+                        uint32_t off = b;
+                        if (!dense) {
+                            const uint32_t r = b / out_row;
+                            off = r * rowp + (b - r * out_row);
+                        }
+                        if (c * 16 + 16 <= vbytes) {
+                            __builtin_nontemporal_store(*reinterpret_cast<const u32x4*>(xs + 16 * c),
+                                                        reinterpret_cast<u32x4*>(dp + off));
+                        } else {
+                            for (uint32_t e = c * 16; e < vbytes; ++e) dp[off + (e - c * 16)] = xs[e];
+                        }
+                    }
+                } else {
+                    for (uint32_t e = lane; e < vbytes; e += 64) {
+                        const uint32_t b = b0 + e;
+                        const uint32_t r = b / out_row;
+                        dp[(int64_t)r * rowp + (b - r * out_row)] = xs[e];
+                    }
+                }
+            }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+}
+
+template <int OUT, int MODE, bool CHW>
+hipError_t launch_rows_t(const YuvResizeLaunch& L, bool one_row, dim3 grid, hipStream_t s) {
+    if (one_row) hipLaunchKernelGGL((yuv_resize_kernel<OUT, MODE, CHW, true>), grid, dim3(64, 4), 0, s, L);
+    else hipLaunchKernelGGL((yuv_resize_kernel<OUT, MODE, CHW, false>), grid, dim3(64, 4), 0, s, L);
+    return hipGetLastError();
+}
+
+template <int OUT, int MODE>
+hipError_t launch_layout_t(const YuvResizeLaunch& L, bool one_row, dim3 grid, hipStream_t s) {
+    return L.chw ? launch_rows_t<OUT, MODE, true>(L, one_row, grid, s)
+                 : launch_rows_t<OUT, MODE, false>(L, one_row, grid, s);
+}
+
+template <int OUT>
+hipError_t launch_mode_t(const YuvResizeLaunch& L, bool one_row, dim3 grid, hipStream_t s) {
+    switch (L.mode) {
+        case VACV_LINEAR_REFERENCE: return launch_layout_t<OUT, VACV_LINEAR_REFERENCE>(L, one_row, grid, s);
+        case VACV_LINEAR_NEON: return launch_layout_t<OUT, VACV_LINEAR_NEON>(L, one_row, grid, s);
+        default: return launch_layout_t<OUT, VACV_LINEAR_OPENCV>(L, one_row, grid, s);
+    }
+}
+
+}  // namespace
+
+hipError_t launch_yuv_resize(const YuvResizeLaunch& L, hipStream_t s) {
+    // the host (vacv_abi.cpp) has checked: w, h even, w >= 4, h >= 2, the
+    // image's bytes fit one buffer resource, wo*ho < 2^31 - 2048, n <= 65535
+    const int64_t P = (int64_t)L.wo * L.ho;
+    // no output row weights two source rows (e.g. an integer downscale >= 2):
+    // gather one row per pixel (the taps are the u8 resize's, resize_one_tap_rows)
+    bool one_row = true;
+    for (int y = 0; y < L.ho && one_row; ++y) {
+        const FixedTap t = fixed_tap(y, L.h, L.ho, L.scale_yf, L.scale_yd, L.mode);
+        one_row = !(t.w0 != 0 && t.w1 != 0);
+    }
+    const int64_t block_px = 4 * 64 * yuv_pxl(one_row);
+    const dim3 grid((unsigned)((P + block_px - 1) / block_px), (unsigned)L.n);
+    if (L.out == kOutSame) return launch_mode_t<kOutSame>(L, one_row, grid, s);
+    if (L.out == kOutF32) return launch_mode_t<kOutF32>(L, one_row, grid, s);
+    return launch_mode_t<kOutNorm>(L, one_row, grid, s);
+}
+
+}  // namespace vacv

@@ -354,6 +354,16 @@ int warp_impl(const vacv_image* src_d, const vacv_image* dst_d, const float m[6]
     return hip_status(launch_warp(L, s));
 }
 
+int color_code(int code, int& v_first, int& rgb) {
+    switch (code) {
+        case VACV_COLOR_YUV2BGR_NV21: v_first = 1; rgb = 0; return VACV_OK;
+        case VACV_COLOR_YUV2RGB_NV21: v_first = 1; rgb = 1; return VACV_OK;
+        case VACV_COLOR_YUV2BGR_NV12: v_first = 0; rgb = 0; return VACV_OK;
+        case VACV_COLOR_YUV2RGB_NV12: v_first = 0; rgb = 1; return VACV_OK;
+        default: return VACV_ERR_UNSUPPORTED;
+    }
+}
+
 int color_impl(const vacv_image* src_d, const vacv_image* dst_d, int code, int out_kind, const NormSpec* ns,
                hipStream_t s) {
     Img src, dst;
@@ -361,13 +371,7 @@ int color_impl(const vacv_image* src_d, const vacv_image* dst_d, int code, int o
     if (st) return st;
     if ((st = load(dst_d, dst))) return st;
     int v_first, rgb;
-    switch (code) {
-        case VACV_COLOR_YUV2BGR_NV21: v_first = 1; rgb = 0; break;
-        case VACV_COLOR_YUV2RGB_NV21: v_first = 1; rgb = 1; break;
-        case VACV_COLOR_YUV2BGR_NV12: v_first = 0; rgb = 0; break;
-        case VACV_COLOR_YUV2RGB_NV12: v_first = 0; rgb = 1; break;
-        default: return VACV_ERR_UNSUPPORTED;
-    }
+    if ((st = color_code(code, v_first, rgb))) return st;
     if (src.dtype != VACV_INT8 || src.c != 1) return VACV_ERR_INVALID_ARG;
     const int h = src.h / 3 * 2;  // cvt_color.cpp:152
     if (src.w % 2 || h % 2 || h < 2 || src.h != h / 2 * 3) return VACV_ERR_INVALID_ARG;
@@ -390,6 +394,56 @@ int color_impl(const vacv_image* src_d, const vacv_image* dst_d, int code, int o
     L.out = out_kind;
     if (ns) L.norm = *ns;
     return hip_status(launch_color(L, s));
+}
+
+// YUV420sp -> BGR -> bilinear resize (-> fp32 / normalize) in one kernel
+// (k_yuv_resize.hip).  dst = (wo, ho, 3) NHWC or NCHW, INT8 (out_kind
+// kOutSame) or FP32.
+int yuv_resize_impl(const vacv_image* src_d, const vacv_image* dst_d, int code, int interpolation, int mode,
+                    int out_kind, const NormSpec* ns, hipStream_t s) {
+    Img src, dst;
+    int st = load(src_d, src);
+    if (st) return st;
+    if ((st = load(dst_d, dst))) return st;
+    int v_first, rgb;
+    if ((st = color_code(code, v_first, rgb))) return st;
+    if (interpolation != VACV_INTER_LINEAR) return VACV_ERR_UNSUPPORTED;
+    if (mode < VACV_LINEAR_REFERENCE || mode > VACV_LINEAR_OPENCV) return VACV_ERR_INVALID_ARG;
+    if (src.dtype != VACV_INT8 || src.c != 1 || src.layout != VACV_NHWC) return VACV_ERR_INVALID_ARG;
+    const int h = src.h / 3 * 2;  // cvt_color.cpp:152
+    // w >= 4: the chroma gather reads 4 bytes within the row
+    if (src.w % 2 || h % 2 || h < 2 || src.w < 4 || src.h != h / 2 * 3) return VACV_ERR_INVALID_ARG;
+    if (dst.c != 3 || dst.n != src.n) return VACV_ERR_INVALID_ARG;
+    const int want = out_kind == kOutSame ? VACV_INT8 : VACV_FP32;
+    if (dst.dtype != want) return VACV_ERR_INVALID_ARG;
+    const int64_t src_bytes = src.row * (src.h - 1) + src.w;
+    const int64_t P = (int64_t)dst.w * dst.h;
+    if (src_bytes > kMaxPlaneBytes || P > 0x7FFFFFFFLL - 1024 || src.n > 65535) return VACV_ERR_UNSUPPORTED;
+    YuvResizeLaunch L{};
+    L.src = src.data;
+    L.src_img = src.batch;
+    L.src_row = src.row;
+    L.src_bytes = src_bytes;
+    L.dst = dst.data;
+    L.dst_img = dst.batch;
+    L.dst_row = dst.row;
+    L.dst_plane = dst.plane;
+    L.n = src.n;
+    L.w = src.w;
+    L.h = h;
+    L.wo = dst.w;
+    L.ho = dst.h;
+    L.v_first = v_first;
+    L.rgb = rgb;
+    L.chw = dst.layout == VACV_NCHW;
+    L.mode = mode;
+    L.out = out_kind;
+    L.scale_xf = (float)L.w / (float)L.wo;
+    L.scale_yf = (float)L.h / (float)L.ho;
+    L.scale_xd = (double)L.w / (double)L.wo;
+    L.scale_yd = (double)L.h / (double)L.ho;
+    if (ns) L.norm = *ns;
+    return hip_status(launch_yuv_resize(L, s));
 }
 
 // Shape of the fp32 output viewed as its own image (for the auto-stats passes).
@@ -442,6 +496,16 @@ struct ColorCtx {
 int color_pass(const void* c, int out, const NormSpec* ns, hipStream_t s) {
     const ColorCtx* k = static_cast<const ColorCtx*>(c);
     return color_impl(k->src, k->dst, k->code, out, ns, s);
+}
+
+struct YuvResizeCtx {
+    const vacv_image* src;
+    const vacv_image* dst;
+    int code, interpolation, mode;
+};
+int yuv_resize_pass(const void* c, int out, const NormSpec* ns, hipStream_t s) {
+    const YuvResizeCtx* k = static_cast<const YuvResizeCtx*>(c);
+    return yuv_resize_impl(k->src, k->dst, k->code, k->interpolation, k->mode, out, ns, s);
 }
 
 }  // namespace
@@ -680,6 +744,19 @@ int vacv_cvt_color_normalize(const vacv_image* src, const vacv_image* dst, int c
                              const float* stddev, void* stream) {
     ColorCtx c{src, dst, code};
     return fused_normalize(dst, mean, stddev, (hipStream_t)stream, color_pass, &c);
+}
+
+int vacv_cvt_color_resize(const vacv_image* src, const vacv_image* dst, int code, int interpolation, int mode,
+                          void* stream) {
+    if (!dst) return VACV_ERR_INVALID_ARG;
+    const int out = dst->dtype == VACV_FP32 ? kOutF32 : kOutSame;
+    return yuv_resize_impl(src, dst, code, interpolation, mode, out, nullptr, (hipStream_t)stream);
+}
+
+int vacv_cvt_color_resize_normalize(const vacv_image* src, const vacv_image* dst, int code, int interpolation,
+                                    int mode, const float* mean, const float* stddev, void* stream) {
+    YuvResizeCtx c{src, dst, code, interpolation, mode};
+    return fused_normalize(dst, mean, stddev, (hipStream_t)stream, yuv_resize_pass, &c);
 }
 
 int vacv_stream_synchronize(void* stream) {

@@ -127,6 +127,44 @@ __device__ __forceinline__ float normalize_f(const ChanNorm& c, float x) {
     return normalize_value(x, c.mean, c.stdv);
 }
 
+// ---- u8 bilinear fixed point (k_resize_direct.hip, k_yuv_resize.hip) ----
+
+typedef unsigned short us2 __attribute__((ext_vector_type(2)));
+
+// One channel of one output pixel from its packed tap pairs.  A zero weight
+// contributes exactly 0 in both formulas, so a skipped row is bot = 0, wB = 0.
+template <int MODE>
+__device__ __forceinline__ int blend_fixed(uint32_t top, uint32_t bot, us2 wx, uint32_t wA, uint32_t wB) {
+    const uint32_t ht = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, top), wx, 0u, false);
+    const uint32_t hb = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, bot), wx, 0u, false);
+    if (MODE == VACV_LINEAR_REFERENCE) {
+        // (tl*a0 + tr*a1)*wA + (bl*a0 + br*a1)*wB: the reference's int32 sum
+        // (terms >= 0, total <= 255*2049^2 < 2^31), 24-bit multiplies exact
+        return (int)(((__umul24(ht, wA) + __umul24(hb, wB)) >> 22) & 0xFFu);
+    }
+    const int h0 = (int)(short)(ht >> 4);
+    const int h1 = (int)(short)(hb >> 4);
+    return clamp_u8((((h0 * (int)wA) >> 16) + ((h1 * (int)wB) >> 16) + 2) >> 2);
+}
+
+// fixed_tap() of the kernel.  REFERENCE mode: the coordinate
+// (float)(((double)d + 0.5) * (double)scale_f - 0.5) is computed as ONE fp32
+// fma, which is bit-identical: d + 0.5 (d < 2^23) and scale_f have 24-bit
+// significands, so the product is exact in double and so is the - 0.5; the
+// double path therefore rounds the exact value once to float -- exactly what
+// fmaf does.  The rest is fixed_tap's own float arithmetic.
+template <int MODE>
+__device__ __forceinline__ FixedTap tap_of(int d, int n_in, int n_out, float scale_f, double scale_d) {
+    if (MODE != VACV_LINEAR_REFERENCE) return fixed_tap(d, n_in, n_out, scale_f, scale_d, MODE);
+    const float c = __builtin_fmaf((float)d + 0.5f, scale_f, -0.5f);
+    const LinearTap t = linear_tap(c, n_in);
+    FixedTap r;
+    r.i = t.i;
+    r.w0 = sat_short_away((1.f - t.f) * 2048.f);
+    r.w1 = sat_short_away(t.f * 2048.f);
+    return r;
+}
+
 template <typename T>
 __device__ __forceinline__ T wave_sum(T v) {
 #pragma unroll

@@ -164,6 +164,28 @@ struct ColorLaunch {
 };
 hipError_t launch_color(const ColorLaunch& L, hipStream_t s);
 
+// YUV420sp -> BGR -> u8 bilinear resize (-> fp32 / normalised fp32), NHWC or
+// NCHW output: the model-input pipeline of SURVEY.md §8(f)2 in one pass
+// (k_yuv_resize.hip).
+struct YuvResizeLaunch {
+    const unsigned char* src;      // Y plane of image 0
+    int64_t src_img, src_row;      // bytes
+    int64_t src_bytes;             // readable bytes of one image (Y + chroma planes)
+    unsigned char* dst;
+    int64_t dst_img, dst_row, dst_plane;  // bytes; dst_plane used for NCHW
+    int n, w, h;                   // decoded BGR size
+    int wo, ho;                    // output size
+    int v_first;                   // NV21
+    int rgb;                       // swap output channel order
+    int chw;                       // 1: NCHW planar output, 0: NHWC
+    int mode;                      // VACV_LINEAR_*
+    int out;                       // kOutSame (u8) / kOutF32 / kOutNorm
+    float scale_xf, scale_yf;
+    double scale_xd, scale_yd;
+    NormSpec norm;
+};
+hipError_t launch_yuv_resize(const YuvResizeLaunch& L, hipStream_t s);
+
 struct NormLaunch {                // elementwise normalize
     PlaneGeom src;
     PlaneGeom dst;

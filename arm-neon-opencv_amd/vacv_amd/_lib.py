@@ -78,6 +78,8 @@ SIGNATURES = {
     "vacv_resize_normalize": ([_IMG, _IMG, _I, _I, _FP, _FP, _P], _I),
     "vacv_warp_affine_normalize": ([_IMG, _IMG, _FP, _I, _I, _DP, _FP, _FP, _P], _I),
     "vacv_cvt_color_normalize": ([_IMG, _IMG, _I, _FP, _FP, _P], _I),
+    "vacv_cvt_color_resize": ([_IMG, _IMG, _I, _I, _I, _P], _I),
+    "vacv_cvt_color_resize_normalize": ([_IMG, _IMG, _I, _I, _I, _FP, _FP, _P], _I),
     "vacv_stream_synchronize": ([_P], _I),
     "vacv_release_workspace": ([], _I),
 }

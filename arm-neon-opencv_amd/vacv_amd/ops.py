@@ -254,6 +254,42 @@ def cvt_color_normalize(yuv: torch.Tensor, code: int = L.COLOR_YUV2BGR_NV21, mea
     return out if yuv.dim() == 3 else out[0]
 
 
+def cvt_color_resize(yuv: torch.Tensor, w: int, h: int, code: int = L.COLOR_YUV2BGR_NV21, layout: int = NHWC,
+                     dtype: torch.dtype = torch.uint8, mode: int = LINEAR_REFERENCE, out=None,
+                     stream=None) -> torch.Tensor:
+    """cvt_color -> resize(INTER_LINEAR) [-> change_dtype(FP32)] [-> change_layout]
+    (cvt_color.cpp:39-157, resize_naive.cpp:10-68) in one kernel:
+    (n, h_in*3/2, w_in) u8 -> (n, h, w, 3) NHWC or (n, 3, h, w) NCHW."""
+    y4 = yuv if yuv.dim() == 3 else yuv.unsqueeze(0)
+    n = y4.shape[0]
+    if out is None:
+        shape = (n, h, w, 3) if layout == NHWC else (n, 3, h, w)
+        out = torch.empty(shape, dtype=dtype, device=yuv.device)
+    check("vacv_cvt_color_resize",
+          L.load().vacv_cvt_color_resize(ctypes.byref(_yuv_desc(y4)), ctypes.byref(describe(out, layout)), code,
+                                         INTER_LINEAR, mode, _stream(stream)))
+    return out if yuv.dim() == 3 else out[0]
+
+
+def cvt_color_resize_normalize(yuv: torch.Tensor, w: int, h: int, mean=None, std=None,
+                               code: int = L.COLOR_YUV2BGR_NV21, layout: int = NCHW, mode: int = LINEAR_REFERENCE,
+                               out=None, stream=None) -> torch.Tensor:
+    """The camera-frame -> model-input step: cvt_color, resize, convert to
+    fp32, normalize((x - mean) / (std + 1e-6)), change_layout -- one kernel.
+    Default layout NCHW (planar fp32).  mean/std None = per-image stats of
+    the resized image (two passes)."""
+    y4 = yuv if yuv.dim() == 3 else yuv.unsqueeze(0)
+    n = y4.shape[0]
+    if out is None:
+        shape = (n, h, w, 3) if layout == NHWC else (n, 3, h, w)
+        out = torch.empty(shape, dtype=torch.float32, device=yuv.device)
+    (ma, mp), (sa, sp) = _meanstd(mean, std, 3)
+    check("vacv_cvt_color_resize_normalize",
+          L.load().vacv_cvt_color_resize_normalize(ctypes.byref(_yuv_desc(y4)), ctypes.byref(describe(out, layout)),
+                                                   code, INTER_LINEAR, mode, mp, sp, _stream(stream)))
+    return out if yuv.dim() == 3 else out[0]
+
+
 # ---------------------------------------------------------------------------
 # normalize / statistics
 

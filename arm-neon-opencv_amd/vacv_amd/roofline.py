@@ -80,3 +80,13 @@ def resize_bytes(w_in: int, h_in: int, c: int, w_out: int, h_out: int, in_esize:
                  cubic: bool = False, mode: int = 0) -> int:
     rows = weighted_rows_cubic(h_in, h_out) if cubic else weighted_rows_linear(h_in, h_out, mode)
     return rows * w_in * c * in_esize + w_out * h_out * c * out_esize
+
+
+def yuv_resize_bytes(w_in: int, h_in: int, w_out: int, h_out: int, out_esize: int = 4, mode: int = 0) -> int:
+    """B_alg of the fused YUV420sp -> BGR -> resize kernel: every weighted Y row,
+    every chroma row (one per Y row pair) that a weighted Y row needs, and the
+    3-channel output."""
+    i, w0, w1 = linear_row_weights(h_in, h_out, mode)
+    rows = set(i[w0 != 0].tolist()) | set((i[w1 != 0] + 1).tolist())
+    chroma = {r >> 1 for r in rows}
+    return (len(rows) + len(chroma)) * w_in + w_out * h_out * 3 * out_esize

@@ -184,6 +184,27 @@ int vacv_warp_affine_normalize(const vacv_image* src, const vacv_image* dst, con
 int vacv_cvt_color_normalize(const vacv_image* src, const vacv_image* dst, int code,
                              const float* mean, const float* stddev, void* stream);
 
+/* Camera frame -> model input in ONE pass: YUV420sp
+ * decode, u8 bilinear resize, and optionally convert + normalize, with NHWC
+ * or NCHW (planar, the model-input layout) output.  Bit-identical to the
+ * reference's chain
+ *   CvtColor::cvt_color (cvt_color.cpp:39-157)
+ *   -> Resize::resize INTER_LINEAR u8 (resize_naive.cpp:10-68; `mode` as in
+ *      vacv_resize)
+ *   -> Tensor::change_dtype FP32 + Normalize::normalize
+ *      (tensor.cpp:459-502, normalize_naive.cpp:74-90)
+ *   -> Tensor::change_layout(NCHW) (tensor.cpp:393-457)
+ * without materialising the decoded frame.  src = (w, h*3/2, 1) INT8, w and
+ * h even, w >= 4; dst = (wo, ho, 3), any wo/ho >= 1, NHWC or NCHW.
+ * interpolation must be INTER_LINEAR.
+ *  vacv_cvt_color_resize:           dst INT8 (u8 BGR/RGB) or FP32 (widened)
+ *  vacv_cvt_color_resize_normalize: dst FP32; NULL mean and stddev = per-image
+ *                                   statistics of the resized image. */
+int vacv_cvt_color_resize(const vacv_image* src, const vacv_image* dst, int code, int interpolation,
+                          int mode, void* stream);
+int vacv_cvt_color_resize_normalize(const vacv_image* src, const vacv_image* dst, int code, int interpolation,
+                                    int mode, const float* mean, const float* stddev, void* stream);
+
 /* ---- runtime ---------------------------------------------------------- */
 
 /* Block until all work this library queued on `stream` has finished. */

@@ -381,6 +381,81 @@ def test_cvt_color_pipeline_digests(ops, dev, oracle, golden):
 
 
 # ---------------------------------------------------------------------------
+# fused camera frame -> model input
+
+def _yuv_chain(oracle, yuv, w, h, v_first, rgb, mode, mean=None, std=None, chw=False, u8=False):
+    """The reference's own chain, step by step, on the oracle: cvt_color ->
+    resize INTER_LINEAR u8 -> change_dtype FP32 -> normalize -> change_layout."""
+    r = oracle.resize_linear(oracle.yuv420sp_to_bgr(yuv, v_first=v_first, rgb=rgb), w, h, mode)
+    if not u8:
+        r = oracle.u8_to_f32(r)
+        if mean is not None:
+            r = oracle.normalize(r, mean, std)
+    return oracle.hwc_to_chw(r) if chw else r
+
+
+@pytest.mark.parametrize("v_first,rgb", [(True, False), (False, True)])
+def test_cvt_color_resize(ops, dev, oracle, v_first, rgb):
+    import vacv_amd as V
+    code = {(True, False): V.COLOR_YUV2BGR_NV21, (False, True): V.COLOR_YUV2RGB_NV12}[(v_first, rgb)]
+    rng = np.random.default_rng(29)
+    cases = [((36, 50), (17, 11)), ((144, 176), (64, 48)), ((120, 160), (224, 224)), ((1080, 1920), (640, 360)),
+             ((1080, 1920), (224, 224)), ((4, 4), (3, 5)), ((360, 640), (640, 360))]
+    for (h, w), (wo, ho) in cases:
+        yuv = np.stack([rng.integers(0, 256, (h * 3 // 2, w), dtype=np.uint8) for _ in range(2)])
+        ydev = to_dev(yuv, dev)
+        for mode in (0, 1, 2):
+            got = host(ops.cvt_color_resize(ydev, wo, ho, code, mode=mode))
+            for k in range(2):
+                assert_same(got[k], _yuv_chain(oracle, yuv[k], wo, ho, v_first, rgb, mode, u8=True),
+                            f"u8 nhwc {h}x{w}->{wo}x{ho} mode {mode}")
+        got = host(ops.cvt_color_resize(ydev, wo, ho, code, layout=V.NCHW))
+        for k in range(2):
+            assert_same(got[k], _yuv_chain(oracle, yuv[k], wo, ho, v_first, rgb, 0, chw=True, u8=True), "u8 nchw")
+        got = host(ops.cvt_color_resize(ydev, wo, ho, code, dtype=__import__("torch").float32))
+        for k in range(2):
+            assert_same(got[k], _yuv_chain(oracle, yuv[k], wo, ho, v_first, rgb, 0), "f32 nhwc")
+        for layout, chw in ((V.NCHW, True), (V.NHWC, False)):
+            got = host(ops.cvt_color_resize_normalize(ydev, wo, ho, MEAN, STD, code, layout=layout))
+            for k in range(2):
+                assert_same(got[k], _yuv_chain(oracle, yuv[k], wo, ho, v_first, rgb, 0, MEAN, STD, chw=chw),
+                            f"normalize {'nchw' if chw else 'nhwc'} {h}x{w}->{wo}x{ho}")
+        # auto statistics: per-image exact stats of the resized image
+        got = host(ops.cvt_color_resize_normalize(ydev, wo, ho, code=code))
+        for k in range(2):
+            r = _yuv_chain(oracle, yuv[k], wo, ho, v_first, rgb, 0, u8=True)
+            m, s = oracle.mean_stddev_exact(r)
+            want = oracle.hwc_to_chw(oracle.normalize(oracle.u8_to_f32(r), m, s))
+            assert_same(got[k], want, "auto stats")
+
+
+def test_cvt_color_resize_batch_and_pitch(ops, dev, oracle):
+    """Full-size batch (64 x NV21 1080p -> 224x224 CHW fp32, one launch): images
+    across the batch match the oracle chain; a pitched NCHW destination (a
+    slice of a wider buffer) gets the same values."""
+    import torch
+    import vacv_amd as V
+    g = torch.Generator(device=dev)
+    g.manual_seed(11)
+    yuv = torch.randint(0, 256, (64, 1620, 1920), dtype=torch.uint8, device=dev, generator=g)
+    out = ops.cvt_color_resize_normalize(yuv, 224, 224, MEAN, STD)
+    for k in (0, 31, 63):
+        want = _yuv_chain(oracle, host(yuv[k]), 224, 224, True, False, 0, MEAN, STD, chw=True)
+        assert_same(host(out[k]), want, f"batch image {k}")
+    big = torch.full((2, 3, 230, 240), -7.0, dtype=torch.float32, device=dev)
+    view = big[:, :, 3:227, 5:229]
+    ops.cvt_color_resize_normalize(yuv[:2], 224, 224, MEAN, STD, out=view)
+    assert torch.equal(view, out[:2])
+    assert bool((big[:, :, :3] == -7.0).all()) and bool((big[:, :, :, :5] == -7.0).all())
+    # the fused op equals the unfused GPU chain (cvt_color, resize_normalize, layout)
+    bgr = ops.cvt_color(yuv[:4])
+    chain = ops.change_layout(ops.resize_normalize(bgr, 224, 224, MEAN, STD), V.NCHW)
+    assert torch.equal(chain, out[:4])
+    del yuv, out, big
+    torch.cuda.empty_cache()
+
+
+# ---------------------------------------------------------------------------
 # normalize / stats
 
 def test_normalize_and_stats(ops, dev, oracle):

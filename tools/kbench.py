@@ -67,6 +67,26 @@ def main():
         o = torch.empty((n, 1080, 1920, 3), dtype=torch.float32, device=dev)
         cases["nv21_bgr_normalize_1080p"] = (lambda yuv=yuv, o=o: ops.cvt_color_normalize(yuv, mean=MEAN, std=STD, out=o),
                                              n * (1920 * 1620 + 1920 * 1080 * 12), n * 1920 * 1080)
+    if a.op in ("yuv_resize", "all"):
+        from vacv_amd.roofline import yuv_resize_bytes
+        n = a.batch or 256
+        yuv = torch.randint(0, 256, (n, 1620, 1920), dtype=torch.uint8, device=dev, generator=g)
+        o1 = torch.empty((n, 3, 360, 640), dtype=torch.float32, device=dev)
+        o2 = torch.empty((n, 3, 224, 224), dtype=torch.float32, device=dev)
+        cases["nv21_resize_normalize_1080p_640x360_chw"] = (
+            lambda yuv=yuv, o1=o1: ops.cvt_color_resize_normalize(yuv, 640, 360, MEAN, STD, out=o1),
+            n * yuv_resize_bytes(1920, 1080, 640, 360), n * 1920 * 1080)
+        o3 = torch.empty((n, 360, 640, 3), dtype=torch.float32, device=dev)
+        cases["nv21_resize_normalize_1080p_640x360_hwc"] = (
+            lambda yuv=yuv, o3=o3: ops.cvt_color_resize_normalize(yuv, 640, 360, MEAN, STD, layout=vacv_amd.NHWC, out=o3),
+            n * yuv_resize_bytes(1920, 1080, 640, 360), n * 1920 * 1080)
+        o4 = torch.empty((n, 360, 640, 3), dtype=torch.uint8, device=dev)
+        cases["nv21_resize_1080p_640x360_u8"] = (
+            lambda yuv=yuv, o4=o4: ops.cvt_color_resize(yuv, 640, 360, out=o4),
+            n * yuv_resize_bytes(1920, 1080, 640, 360, out_esize=1), n * 1920 * 1080)
+        cases["nv21_resize_normalize_1080p_224_chw"] = (
+            lambda yuv=yuv, o2=o2: ops.cvt_color_resize_normalize(yuv, 224, 224, MEAN, STD, out=o2),
+            n * yuv_resize_bytes(1920, 1080, 224, 224), n * 1920 * 1080)
     if a.op in ("cubic", "all"):
         n = a.batch or 128
         src = frames(n, 1440, 2560)
