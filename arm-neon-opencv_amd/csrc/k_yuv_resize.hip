@@ -44,15 +44,6 @@ namespace {
 // bytes in flight for the same registers), else 4.
 constexpr int yuv_pxl(bool one_row) { return one_row ? 8 : 4; }
 
-// One decoded pixel, cvt_color.cpp:69-88: R = Y + ra, G = Y - ga, B = Y + ba,
-// clamped; packed as bytes {B, G, R} of a dword.
-__device__ __forceinline__ uint32_t decode_bgr(int y, const Chroma& c) {
-    const uint32_t b = (uint32_t)clamp_u8(y + c.ba);
-    const uint32_t g = (uint32_t)clamp_u8(y - c.ga);
-    const uint32_t r = (uint32_t)clamp_u8(y + c.ra);
-    return b | (g << 8) | (r << 16);
-}
-
 // Raw gathers of one weighted source row sy for a pixel whose left tap is
 // column tx: 4 Y bytes at tx (2 used) and 4 chroma bytes holding the VU
 // pairs of columns tx and tx + 1 (one pair when tx is even), read from an
@@ -62,34 +53,63 @@ struct RowTaps {
     uint32_t y, c;   // raw dwords
 };
 
-// Where the two taps' VU pairs sit in RowTaps::c: bits 0-7 = bit shift of
-// the left tap's pair (0 or 16), bit 8 = the right tap's pair is the next one.
+// Where the two taps' VU pairs sit in RowTaps::c: bits 0-1 = byte index of
+// the left tap's pair (0 or 2), bits 2-3 = the right tap's (equal when tx is
+// even, the next pair when odd).
 __device__ __forceinline__ uint32_t chroma_sel(int w, int tx) {
     const int ca = tx & ~1;
-    return 8u * (uint32_t)(ca - min(ca, w - 4)) | ((uint32_t)(tx & 1) << 8);
+    const uint32_t a = (uint32_t)(ca - min(ca, w - 4));
+    return a | ((a + 2u * (uint32_t)(tx & 1)) << 2);
 }
 
-__device__ __forceinline__ void gather_row(const Rsrc& rs, uint32_t rp, uint32_t uvbase, int w, int sy, int tx,
-                                           RowTaps& t) {
-    t.y = __builtin_amdgcn_raw_buffer_load_b32(rs.r, (int)((uint32_t)sy * rp + (uint32_t)tx + rs.delta), 0,
-                                               VACV_LOAD_AUX);
+// yo / co: byte offsets (from the 16-byte aligned base) of the Y row and of
+// its chroma row.
+__device__ __forceinline__ void gather_row(const Rsrc& rs, uint32_t yo, uint32_t co, int w, int tx, RowTaps& t) {
+    t.y = __builtin_amdgcn_raw_buffer_load_b32(rs.r, (int)(yo + (uint32_t)tx), 0, VACV_LOAD_AUX);
     const int ca = tx & ~1;
     const int c0 = min(ca, w - 4);
-    t.c = __builtin_amdgcn_raw_buffer_load_b32(rs.r, (int)(uvbase + (uint32_t)(sy >> 1) * rp + (uint32_t)c0 + rs.delta),
-                                               0, VACV_LOAD_AUX);
+    t.c = __builtin_amdgcn_raw_buffer_load_b32(rs.r, (int)(co + (uint32_t)c0), 0, VACV_LOAD_AUX);
 }
 
-// Decode the row's two tap pixels: lo = left {B,G,R}, hi = right.
-__device__ __forceinline__ void decode_row(const RowTaps& t, uint32_t cs, int v_first, uint32_t& lo, uint32_t& hi) {
-    const uint32_t sa = cs & 0xFFu;
-    const uint32_t sb = sa + ((cs >> 8) << 4);
-    const int a0 = (int)((t.c >> sa) & 0xFFu), a1 = (int)((t.c >> (sa + 8)) & 0xFFu);
-    const int b0 = (int)((t.c >> sb) & 0xFFu), b1 = (int)((t.c >> (sb + 8)) & 0xFFu);
-    // cvt_color.cpp:68-69: _v = vu[x_num], _u = vu[y_num]; NV21 stores V first
-    const Chroma ka = v_first ? chroma_terms(a1, a0) : chroma_terms(a0, a1);
-    const Chroma kb = v_first ? chroma_terms(b1, b0) : chroma_terms(b0, b1);
-    lo = decode_bgr((int)(t.y & 0xFFu), ka);
-    hi = decode_bgr((int)((t.y >> 8) & 0xFFu), kb);
+struct RowOffs {
+    uint32_t y0, c0, y1, c1;  // rows i and i + 1 of a vertical tap
+};
+__device__ __forceinline__ RowOffs row_offs(int i, uint32_t rp, uint32_t uvbase, uint32_t delta) {
+    RowOffs o;
+    o.y0 = (uint32_t)i * rp + delta;
+    o.y1 = o.y0 + rp;
+    o.c0 = uvbase + (uint32_t)(i >> 1) * rp + delta;
+    o.c1 = uvbase + (uint32_t)((i + 1) >> 1) * rp + delta;
+    return o;
+}
+
+typedef short s16x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ s16x2 clamp_u8x2(s16x2 v) {
+    return __builtin_elementwise_max(__builtin_elementwise_min(v, (s16x2)(short)255), (s16x2)(short)0);
+}
+
+// Decode the row's two tap pixels, cvt_color.cpp:66-88, on packed 16-bit
+// pairs {left, right}: every intermediate of the reference's int arithmetic
+// fits in int16 (|179(v-128)|, |44(u-128) + 91(v-128)|, |227(u-128)| < 2^15,
+// Y + term in [-227, 481]), >> is arithmetic as in the reference, so each
+// lane is exact.  Out: B, G, R as u16 pairs {left, right} -- the layout the
+// blend's v_dot2_u32_u16 takes.
+__device__ __forceinline__ void decode_row(const RowTaps& t, uint32_t cs, int v_first, uint32_t& bp, uint32_t& gp,
+                                           uint32_t& rp) {
+    // v_perm selectors: byte (a + vi) -> lane 0, byte (b + vi) -> lane 1, 0x0C = 0
+    const uint32_t base = (cs & 3u) | ((cs >> 2) << 16) | 0x0C000C00u;
+    const uint32_t vo = v_first ? 0u : 0x00010001u;  // NV21: V first in a pair
+    const s16x2 V = __builtin_bit_cast(s16x2, __builtin_amdgcn_perm(0u, t.c, base + vo));
+    const s16x2 U = __builtin_bit_cast(s16x2, __builtin_amdgcn_perm(0u, t.c, base + (0x00010001u - vo)));
+    const s16x2 Y = __builtin_bit_cast(s16x2, __builtin_amdgcn_perm(0u, t.y, 0x0C010C00u));
+    const s16x2 vm = V - (short)128, um = U - (short)128;
+    const s16x2 ra = (vm * (short)179) >> (short)7;
+    const s16x2 ga = (um * (short)44 + vm * (short)91) >> (short)7;
+    const s16x2 ba = (um * (short)227) >> (short)7;
+    bp = __builtin_bit_cast(uint32_t, clamp_u8x2(Y + ba));
+    gp = __builtin_bit_cast(uint32_t, clamp_u8x2(Y - ga));
+    rp = __builtin_bit_cast(uint32_t, clamp_u8x2(Y + ra));
 }
 
 // Output pixels per wave and per LDS exchange round (4 per lane).
@@ -138,6 +158,18 @@ yuv_resize_kernel(YuvResizeLaunch L) {
     FixedTap ty1 = tap_of<MODE>(min(y_first + 1, L.ho - 1), L.h, L.ho, L.scale_yf, L.scale_yd);
     if (ONE_ROW && ty0.w0 == 0) { ty0.i += 1; ty0.w0 = ty0.w1; ty0.w1 = 0; }  // the weighted row as row A
     if (ONE_ROW && ty1.w0 == 0) { ty1.i += 1; ty1.w0 = ty1.w1; ty1.w1 = 0; }
+    // wave-uniform; readfirstlane keeps them scalar (otherwise LLVM folds
+    // the per-pixel select of two products into a per-pixel multiply)
+    RowOffs ro0 = row_offs(ty0.i, rp, uvbase, rs.delta);
+    RowOffs ro1 = row_offs(ty1.i, rp, uvbase, rs.delta);
+    ro0.y0 = __builtin_amdgcn_readfirstlane(ro0.y0);
+    ro0.c0 = __builtin_amdgcn_readfirstlane(ro0.c0);
+    ro0.y1 = __builtin_amdgcn_readfirstlane(ro0.y1);
+    ro0.c1 = __builtin_amdgcn_readfirstlane(ro0.c1);
+    ro1.y0 = __builtin_amdgcn_readfirstlane(ro1.y0);
+    ro1.c0 = __builtin_amdgcn_readfirstlane(ro1.c0);
+    ro1.y1 = __builtin_amdgcn_readfirstlane(ro1.y1);
+    ro1.c1 = __builtin_amdgcn_readfirstlane(ro1.c1);
 #pragma unroll
     for (int j = 0; j < PXL; ++j) {
 #pragma unroll
@@ -147,16 +179,22 @@ yuv_resize_kernel(YuvResizeLaunch L) {
         if (j * 64 + lane >= npx) continue;
         const int d = x_first + j * 64 + lane;  // < W + kWavePx
         const int dy = wide ? (d >= W ? 1 : 0) : d / W;
-        const int x = d - dy * W;
+        const int x = wide ? (dy ? d - W : d) : d - dy * W;
         const FixedTap tx = tap_of<MODE>(x, L.w, W, L.scale_xf, L.scale_xd);
         FixedTap ty;
+        RowOffs ro;
         if (wide) {
             ty.i = dy ? ty1.i : ty0.i;
             ty.w0 = dy ? ty1.w0 : ty0.w0;
             ty.w1 = dy ? ty1.w1 : ty0.w1;
+            ro.y0 = dy ? ro1.y0 : ro0.y0;
+            ro.c0 = dy ? ro1.c0 : ro0.c0;
+            ro.y1 = dy ? ro1.y1 : ro0.y1;
+            ro.c1 = dy ? ro1.c1 : ro0.c1;
         } else {
             ty = tap_of<MODE>(y_first + dy, L.h, L.ho, L.scale_yf, L.scale_yd);
             if (ONE_ROW && ty.w0 == 0) { ty.i += 1; ty.w0 = ty.w1; ty.w1 = 0; }
+            ro = row_offs(ty.i, rp, uvbase, rs.delta);
         }
         wxp[j] = (uint32_t)tx.w0 | ((uint32_t)tx.w1 << 16);
         const uint32_t cs = chroma_sel(L.w, tx.i);
@@ -164,8 +202,8 @@ yuv_resize_kernel(YuvResizeLaunch L) {
         if (!ONE_ROW) csel[j] = cs;
         // both rows of a two-row pixel are always read (rows i, i + 1 exist);
         // a zero weight multiplies them out exactly
-        gather_row(rs, rp, uvbase, L.w, ty.i, tx.i, t[j][0]);
-        if (!ONE_ROW) gather_row(rs, rp, uvbase, L.w, ty.i + 1, tx.i, t[j][NR - 1]);
+        gather_row(rs, ro.y0, ro.c0, L.w, tx.i, t[j][0]);
+        if (!ONE_ROW) gather_row(rs, ro.y1, ro.c1, L.w, tx.i, t[j][NR - 1]);
     }
 
     ChanNorm cn[3] = {};
@@ -187,22 +225,21 @@ yuv_resize_kernel(YuvResizeLaunch L) {
 #pragma unroll
         for (int jj = 0; jj < 4; ++jj) {
             const int j = g * 4 + jj;
-            uint32_t px[2][2];
+            uint32_t pa[3], pb[3] = {0u, 0u, 0u};  // rows A/B: B, G, R as u16 pairs {left, right}
             const uint32_t cs = ONE_ROW ? wyp[j] >> 16 : csel[j];
-            decode_row(t[j][0], cs, L.v_first, px[0][0], px[0][1]);
-            if (ONE_ROW) px[1][0] = px[1][1] = 0u;
-            else decode_row(t[j][NR - 1], cs, L.v_first, px[1][0], px[1][1]);
+            decode_row(t[j][0], cs, L.v_first, pa[0], pa[1], pa[2]);
+            if (!ONE_ROW) decode_row(t[j][NR - 1], cs, L.v_first, pb[0], pb[1], pb[2]);
+            if (L.rgb) {  // output order R, G, B
+                const uint32_t x0 = pa[0], x1 = pb[0];
+                pa[0] = pa[2]; pa[2] = x0;
+                pb[0] = pb[2]; pb[2] = x1;
+            }
             const us2 wx = __builtin_bit_cast(us2, wxp[j]);
             const uint32_t wA = wyp[j] & 0xFFFFu, wB = ONE_ROW ? 0u : wyp[j] >> 16;
             const int q = jj * 64 + lane;
 #pragma unroll
             for (int k = 0; k < 3; ++k) {
-                // byte of the decoded triple: B,G,R = 0,1,2; RGB output reverses
-                const uint32_t bsel = L.rgb ? 2u - (uint32_t)k : (uint32_t)k;
-                // {left, right} bytes -> u16 lanes (v_perm_b32)
-                const uint32_t ps = bsel | (0x0Cu << 8) | ((bsel + 4u) << 16) | (0x0Cu << 24);
-                const uint32_t top = __builtin_amdgcn_perm(px[0][1], px[0][0], ps);
-                const uint32_t bot = __builtin_amdgcn_perm(px[1][1], px[1][0], ps);
+                const uint32_t top = pa[k], bot = pb[k];
                 const int v = blend_fixed<MODE>(top, bot, wx, wA, wB);
                 TOut ov;
                 if (OUT == kOutSame) ov = (TOut)v;

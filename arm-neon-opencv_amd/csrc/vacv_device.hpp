@@ -160,8 +160,10 @@ __device__ __forceinline__ FixedTap tap_of(int d, int n_in, int n_out, float sca
     const LinearTap t = linear_tap(c, n_in);
     FixedTap r;
     r.i = t.i;
-    r.w0 = sat_short_away((1.f - t.f) * 2048.f);
-    r.w1 = sat_short_away(t.f * 2048.f);
+    // sat_short_away of a value in [0, 2048]: the clamp and the sign test
+    // are no-ops (t.f is in [0, 1])
+    r.w0 = (int)((1.f - t.f) * 2048.f + 0.5f);
+    r.w1 = (int)(t.f * 2048.f + 0.5f);
     return r;
 }
 
