@@ -58,6 +58,10 @@ def main():
         m = ops.rotation_matrix(0.9, 15.0, (640, 360, 640, 360))
         cases["warp_720p_rot15_u8"] = (lambda src=src, m=m, o=o: ops.warp_affine(src, m, 1280, 720, out=o), n * 2 * 1280 * 720 * 3,
                                        n * 1280 * 720)
+        for rot in (0.0, 5.0, 45.0):
+            mr = ops.rotation_matrix(0.9, rot, (640, 360, 640, 360))
+            cases[f"warp_720p_rot{int(rot)}_u8"] = (lambda src=src, m=mr, o=o: ops.warp_affine(src, m, 1280, 720, out=o),
+                                                   n * 2 * 1280 * 720 * 3, n * 1280 * 720)
         of = torch.empty((n, 720, 1280, 3), dtype=torch.float32, device=dev)
         cases["warp_normalize_720p_rot15"] = (lambda src=src, m=m, of=of: ops.warp_affine_normalize(src, m, 1280, 720, MEAN, STD, out=of),
                                               n * 5 * 1280 * 720 * 3, n * 1280 * 720)
