@@ -1,0 +1,221 @@
+// k_cubic_direct.hip -- Keys cubic resize (A = -0.75) of u8 images to fp32
+// (optionally normalised) as per-pixel gathers: no LDS staging of source
+// rows, no planner tables, no barriers.  The u8 -> fp32 conversion the
+// reference requires before its cubic (resize.cpp:89-98, App. C) is fused.
+//
+// Reference arithmetic (as resize_kernel<kCubic>, k_resize.hip):
+//   taps   cubic_tap() = resize_naive.cpp:130-185 (coefficients, replicate
+//          folding), shared host/device code
+//   rows   h_r = S[-1]*a0 + S[0]*a1 + S[1]*a2 + S[2]*a3  (resize_naive.cpp:325-328)
+//   value  h_0*b0 + h_1*b1 + h_2*b2 + h_3*b3             (resize_naive.cpp:349-351)
+//   all fp32, left to right, no contraction (-ffp-contract=off).
+//
+// Shape.  Output pixels of one plane are numbered row-major; a wave owns 128
+// consecutive ones and lane l samples pixels p0 + 64j + l (j < 2), so one
+// gather instruction reads the taps of 64 consecutive output pixels.  Per
+// pixel and tap row ONE dword-aligned 16-byte buffer load brings the four
+// horizontal taps of all CC <= 3 channels (4*CC + 3 <= 16 bytes).  The
+// vertical taps of the (at most two) output rows a wave touches are computed
+// once per wave.  Results are re-assembled in LDS and leave as 16-byte
+// non-temporal stores.
+#pragma clang fp contract(off)
+
+#include <cstdlib>
+
+#include "vacv_device.hpp"
+
+namespace vacv {
+namespace {
+
+constexpr int kPxl = 2;               // pixels per lane
+constexpr int kWavePx = 64 * kPxl;    // 128 output pixels per wave
+
+// 32 tap dwords per lane plus coefficients: ~70-90 VGPRs for CC >= 2 (64
+// spills; 80 still spills the normalised 3-channel kernel)
+constexpr int cubic_waves(int cc, int out) { return cc == 1 ? 8 : (cc == 3 && out == kOutNorm ? 5 : 6); }
+
+template <int CC, int OUT>
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(cubic_waves(CC, OUT))))
+cubic_direct_kernel(ResizeLaunch L, int blocks_per_plane) {
+    __shared__ __attribute__((aligned(16))) float xch[4][kWavePx * CC];
+
+    const int pidx = blockIdx.x / blocks_per_plane;  // image * planes + plane
+    const int blk = blockIdx.x - pidx * blocks_per_plane;
+    const int W = L.dst.w;
+    const int P = W * L.dst.h;
+    const int p0 = (blk * 4 + (int)threadIdx.y) * kWavePx;
+    if (p0 >= P) return;  // whole wave
+    const int npx = min(kWavePx, P - p0);
+    const int lane = threadIdx.x;
+    const int img = pidx / L.src.planes;
+    const int plane = pidx - img * L.src.planes;
+
+    const unsigned char* sp = L.src.base + (int64_t)img * L.src.img_pitch + (int64_t)plane * L.src.plane_pitch;
+    const Rsrc srs = make_rsrc(sp, L.src.plane_bytes);
+    const uint32_t slimit = (uint32_t)L.src.plane_bytes + srs.delta;
+    const uint32_t rp = (uint32_t)L.src.row_pitch;  // plane < 2^31 bytes (kMaxPlaneBytes)
+
+    const int y_first = p0 / W;  // wave-uniform
+    const int x_first = p0 - y_first * W;
+    const bool wide = W >= kWavePx;
+    const CubicTap ty0 = cubic_tap(y_first, L.src.h, L.scale_yd);
+    const CubicTap ty1 = cubic_tap(min(y_first + 1, L.dst.h - 1), L.src.h, L.scale_yd);
+
+    // ---- gathers: the 16 bytes at (row ty.i - 1 + r, column tx.i - 1) ------
+    uint32_t ch[kPxl][4][4];
+#pragma unroll
+    for (int j = 0; j < kPxl; ++j) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) ch[j][r][0] = ch[j][r][1] = ch[j][r][2] = ch[j][r][3] = 0u;
+        if (j * 64 + lane >= npx) continue;
+        const int d = x_first + j * 64 + lane;
+        const int dy = wide ? (d >= W ? 1 : 0) : d / W;
+        const int x = wide ? (dy ? d - W : d) : d - dy * W;
+        const int tyi = wide ? (dy ? ty1.i : ty0.i) : cubic_tap(y_first + dy, L.src.h, L.scale_yd).i;
+        const int txi = cubic_tap(x, L.src.w, L.scale_xd).i;
+        const uint32_t o0 = (uint32_t)(tyi - 1) * rp + (uint32_t)((txi - 1) * CC) + srs.delta;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const uint32_t a4 = (o0 + (uint32_t)r * rp) & ~3u;
+            if (a4 + 16u <= slimit) {
+                const auto v = __builtin_amdgcn_raw_buffer_load_b128(srs.r, (int)a4, 0, VACV_LOAD_AUX);
+                ch[j][r][0] = v[0];
+                ch[j][r][1] = v[1];
+                ch[j][r][2] = v[2];
+                ch[j][r][3] = v[3];
+            } else {  // the plane's last bytes: an overhanging load would read zeros
+                const unsigned char* b = sp + ((int64_t)a4 - (int64_t)srs.delta);
+#pragma unroll
+                for (int e = 0; e < 16; ++e)
+                    if (a4 + (uint32_t)e < slimit) ch[j][r][e >> 2] |= (uint32_t)b[e] << (8 * (e & 3));
+            }
+        }
+    }
+
+    ChanNorm cn[CC] = {};
+    if (OUT == kOutNorm) {
+#pragma unroll
+        for (int k = 0; k < CC; ++k) cn[k] = chan_norm(L.norm, img, CC == 1 ? plane % L.norm.c_total : k);
+    }
+
+    // ---- blend into the wave's LDS buffer (coefficients recomputed here so
+    // they do not hold registers across the loads) ------------------------------
+    float* xo = xch[threadIdx.y];
+#pragma unroll
+    for (int j = 0; j < kPxl; ++j) {
+        if (j * 64 + lane >= npx) continue;
+        const int d = x_first + j * 64 + lane;
+        const int dy = wide ? (d >= W ? 1 : 0) : d / W;
+        const int x = wide ? (dy ? d - W : d) : d - dy * W;
+        CubicTap ty;
+        if (wide) {
+            ty.i = dy ? ty1.i : ty0.i;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) ty.c[q] = dy ? ty1.c[q] : ty0.c[q];
+        } else {
+            ty = cubic_tap(y_first + dy, L.src.h, L.scale_yd);
+        }
+        const CubicTap tx = cubic_tap(x, L.src.w, L.scale_xd);
+        const uint32_t o0 = (uint32_t)(ty.i - 1) * rp + (uint32_t)((tx.i - 1) * CC) + srs.delta;
+        float h[4][CC];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const uint32_t sh = (o0 + (uint32_t)r * rp) & 3u;
+            const uint32_t w0 = __builtin_amdgcn_alignbyte(ch[j][r][1], ch[j][r][0], sh);
+            const uint32_t w1 = __builtin_amdgcn_alignbyte(ch[j][r][2], ch[j][r][1], sh);
+            const uint32_t w2 = __builtin_amdgcn_alignbyte(ch[j][r][3], ch[j][r][2], sh);
+            const uint32_t wv[3] = {w0, w1, w2};
+#pragma unroll
+            for (int k = 0; k < CC; ++k) {
+                float s[4];
+#pragma unroll
+                for (int m = 0; m < 4; ++m) {
+                    const int e = m * CC + k;  // byte of the 4*CC tap bytes
+                    s[m] = (float)((wv[e >> 2] >> (8 * (e & 3))) & 0xFFu);
+                }
+                // resize_naive.cpp:325-328
+                h[r][k] = s[0] * tx.c[0] + s[1] * tx.c[1] + s[2] * tx.c[2] + s[3] * tx.c[3];
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < CC; ++k) {
+            // resize_naive.cpp:349-351
+            float v = h[0][k] * ty.c[0] + h[1][k] * ty.c[1] + h[2][k] * ty.c[2] + h[3][k] * ty.c[3];
+            if (OUT == kOutNorm) v = normalize_f(cn[k], v);
+            xo[(j * 64 + lane) * CC + k] = v;
+        }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+
+    // ---- LDS -> HBM: dense byte b of the plane's output lives at row
+    // b / out_row, column byte b % out_row --------------------------------------
+    unsigned char* dp = const_cast<unsigned char*>(L.dst.base) + (int64_t)img * L.dst.img_pitch +
+                        (int64_t)plane * L.dst.plane_pitch;
+    const uint32_t out_row = (uint32_t)W * CC * 4u;
+    const uint32_t rowp = (uint32_t)L.dst.row_pitch;
+    const bool dense = L.dst.row_pitch == (int64_t)out_row;
+    const bool chunked = (reinterpret_cast<uintptr_t>(dp) & 15) == 0 && (L.dst.row_pitch & 15) == 0 &&
+                         (dense || (out_row & 15) == 0);  // 16-byte chunks never straddle rows
+    const uint32_t vbytes = (uint32_t)npx * CC * 4u;
+    const uint32_t b0 = (uint32_t)p0 * CC * 4u;
+    const unsigned char* xs = reinterpret_cast<const unsigned char*>(xch[threadIdx.y]);
+    if (chunked) {
+        for (uint32_t c = lane; c * 16 < vbytes; c += 64) {
+            const uint32_t b = b0 + 16 * c;
+            uint32_t off = b;
+            if (!dense) {
+                const uint32_t r = b / out_row;
+                off = r * rowp + (b - r * out_row);
+            }
+            if (c * 16 + 16 <= vbytes) {
+                __builtin_nontemporal_store(*reinterpret_cast<const u32x4*>(xs + 16 * c),
+                                            reinterpret_cast<u32x4*>(dp + off));
+            } else {
+                for (uint32_t e = c * 16; e < vbytes; ++e) dp[off + (e - c * 16)] = xs[e];
+            }
+        }
+    } else {
+        for (uint32_t e = lane; e < vbytes; e += 64) {
+            const uint32_t b = b0 + e;
+            const uint32_t r = b / out_row;
+            dp[(int64_t)r * rowp + (b - r * out_row)] = xs[e];
+        }
+    }
+}
+
+template <int CC>
+hipError_t launch_cc(const ResizeLaunch& L, hipStream_t s) {
+    constexpr int kBlockPx = 4 * kWavePx;
+    const int64_t P = (int64_t)L.dst.w * L.dst.h;
+    const int64_t per_plane = (P + kBlockPx - 1) / kBlockPx;
+    const int64_t total = per_plane * L.n * L.src.planes;
+    if (P >= 0x7FFFFFFF - kBlockPx || total > 0x7FFFFFF0LL) return hipErrorInvalidValue;
+    if (L.out == kOutNorm)
+        hipLaunchKernelGGL((cubic_direct_kernel<CC, kOutNorm>), dim3((unsigned)total), dim3(64, 4), 0, s, L,
+                           (int)per_plane);
+    else
+        hipLaunchKernelGGL((cubic_direct_kernel<CC, kOutF32>), dim3((unsigned)total), dim3(64, 4), 0, s, L,
+                           (int)per_plane);
+    return hipGetLastError();
+}
+
+}  // namespace
+
+bool cubic_direct_applies(const ResizeLaunch& L) {
+    const char* env = std::getenv("VACV_CUBIC_DIRECT");
+    if (env && env[0] == '0') return false;
+    return L.kind == kCubic && L.src.esize == 1 && L.src.cc <= 3 && (L.out == kOutF32 || L.out == kOutNorm);
+}
+
+hipError_t launch_cubic_direct(const ResizeLaunch& L, hipStream_t s) {
+    switch (L.src.cc) {
+        case 1: return launch_cc<1>(L, s);
+        case 2: return launch_cc<2>(L, s);
+        case 3: return launch_cc<3>(L, s);
+        default: return hipErrorInvalidValue;
+    }
+}
+
+}  // namespace vacv

@@ -280,6 +280,9 @@ int resize_impl(const vacv_image* src_d, const vacv_image* dst_d, int interpolat
     if (L.kind == kLinearFixed && L.src.cc <= 4 && dst.w < (1 << 23) && dst.h < (1 << 23) &&
         (direct == 2 || (direct == 1 && resize_one_tap_rows(L))))
         return hip_status(launch_resize_direct(L, s));
+    // u8 cubic (fused widen to fp32), c <= 3 interleaved: per-pixel gathers
+    // (k_cubic_direct.hip); VACV_CUBIC_DIRECT=0 selects the staged kernel
+    if (cubic_direct_applies(L)) return hip_status(launch_cubic_direct(L, s));
     const char* il_env = std::getenv("VACV_RESIZE_INTERLEAVE");
     L.interleave = !(il_env && il_env[0] == '0');
     const char* rows_env = std::getenv("VACV_RESIZE_ROWS");

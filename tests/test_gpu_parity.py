@@ -128,6 +128,38 @@ def test_resize_cubic(ops, dev, oracle):
             assert_same(got[k], oracle.resize_cubic(chw[k], 31, 17), "cubic chw")
 
 
+def test_cubic_direct_and_staged_agree(ops, dev, oracle, monkeypatch):
+    """u8 cubic runs on the per-pixel gather kernel (k_cubic_direct.hip) unless
+    VACV_CUBIC_DIRECT=0 selects the staged kernel (k_resize.hip).  Both are
+    the reference's arithmetic, so they agree bit for bit: BASELINE cfg5 at
+    full size (2560x1440 -> 224x224, batch 6), normalized, a pitched source,
+    NCHW planes and an upscale; image 0 is also checked against the oracle."""
+    import torch
+    from vacv_amd import INTER_CUBIC, NCHW
+    imgs = np.stack([synthetic_image(90 + k, 1440, 2560, 3) for k in range(6)])
+    src = to_dev(imgs, dev)
+    big = torch.zeros((2, 1450, 2600, 3), dtype=torch.uint8, device=dev)
+    big[:, 3:1443, 7:2567] = src[:2]
+    view = big[:, 3:1443, 7:2567]
+    cases = [lambda: ops.resize(src, 224, 224, interpolation=INTER_CUBIC),
+             lambda: ops.resize_normalize(src, 224, 224, MEAN, STD, interpolation=INTER_CUBIC),
+             lambda: ops.resize(view, 300, 171, interpolation=INTER_CUBIC),
+             lambda: ops.resize(src[:1, :100, :90], 250, 333, interpolation=INTER_CUBIC),
+             lambda: ops.resize(ops.change_layout(src[:2], NCHW), 97, 61, interpolation=INTER_CUBIC, layout=NCHW)]
+    for i, fn in enumerate(cases):
+        monkeypatch.setenv("VACV_CUBIC_DIRECT", "1")
+        a = fn()
+        monkeypatch.setenv("VACV_CUBIC_DIRECT", "0")
+        b = fn()
+        torch.cuda.synchronize(dev)
+        assert torch.equal(a, b), f"case {i}: {(a != b).sum().item()} values differ"
+    monkeypatch.delenv("VACV_CUBIC_DIRECT")
+    got = host(ops.resize(src[:1], 224, 224, interpolation=INTER_CUBIC))[0]
+    assert_same(got, oracle.resize_cubic(oracle.u8_to_f32(imgs[0]), 224, 224), "cfg5 image 0 vs oracle")
+    del src, big
+    torch.cuda.empty_cache()
+
+
 def test_resize_full_size_batch(ops, dev, oracle):
     """BASELINE cfg2 at full size: 1920x1080 -> 640x360 / 1280x720, batch of 3,
     plus a pitched source (a sub-window of a wider buffer)."""
