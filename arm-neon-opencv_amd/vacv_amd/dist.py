@@ -35,6 +35,16 @@ def allreduce_sums(local_sums: torch.Tensor, local_count: float, group=None) -> 
     return buf[:-1].reshape(local_sums.shape), float(buf[-1].item())
 
 
+def allreduce_sums_async(local_sums: torch.Tensor, local_count: float, group=None):
+    """allreduce_sums without a host round trip: the count stays a device
+    tensor, so a step that all-reduces its statistics never synchronises."""
+    buf = torch.cat([local_sums.reshape(-1).to(torch.float64),
+                     torch.full((1,), float(local_count), dtype=torch.float64, device=local_sums.device)])
+    if dist.is_available() and dist.is_initialized():
+        dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=group)
+    return buf[:-1].reshape(local_sums.shape), buf[-1]
+
+
 def stats_from_moments(sums: torch.Tensor, count: float) -> Tuple[torch.Tensor, torch.Tensor]:
     """Host-side twin of vacv_stats_from_sums (same formula) for any device."""
     s = sums.reshape(-1, 2).to(torch.float64)

@@ -8,6 +8,17 @@ the reference's arithmetic, mean (103.94,116.78,123.68) / std
 One step = one vacv_resize_normalize call over the whole per-GPU batch (one
 kernel launch: resize_direct_kernel, k_resize_direct.hip).  Metric = input-frame Mpixels/s over all GPUs ("at 1080p").
 
+Other BASELINE configs (--workload; the default is the headline above):
+  warp          cfg4: warp_affine INTER_LINEAR 1280x720x3 u8, scale 0.9, rot 15,
+                aux (640,360,640,360), 128 frames per GPU (1024 over 8 GPUs)
+  cvt_normalize cfg3: NV21 1920x1620 -> BGR 1920x1080x3 fp32 normalised, 256 per GPU
+  cubic_stats   cfg5: INTER_CUBIC 2560x1440x3 u8 -> 224x224x3 fp32 (128 per GPU),
+                then the GLOBAL per-channel mean/stddev of the whole sharded
+                batch: exact sums per rank + one RCCL all-reduce per step
+  yuv_resize    SURVEY 8(f)2: NV21 1080p -> 640x360 planar (NCHW) fp32 normalised,
+                decode + resize + normalize + layout in one kernel, 256 per GPU
+The roofline covers the step's dominant kernel (HIP events around it alone).
+
 Multi-GPU: torchrun one process per GPU; images are independent, so each rank
 owns its own batch (weak scaling) and there is no data-path collective.
 Timing: barrier + synchronize around exactly --steps steps, max over ranks.
@@ -44,7 +55,9 @@ def parse():
     # 50 warmup launches (~12 ms): measured 0.2225 ms/launch after 50 or 200
     # warmups vs 0.2285 after 10 (the GPU's clocks settle under the load)
     ap.add_argument("--warmup", type=int, default=50)
-    ap.add_argument("--batch", type=int, default=256, help="images per GPU")
+    ap.add_argument("--workload", default="resize_normalize",
+                    choices=["resize_normalize", "warp", "cvt_normalize", "cubic_stats", "yuv_resize"])
+    ap.add_argument("--batch", type=int, default=0, help="images per GPU (0: the workload's default)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget of the CPU baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--graph", action="store_true",
@@ -59,30 +72,69 @@ def ensure_built():
     vacv_amd._lib.load()
 
 
-def cpu_baseline(budget_s: float):
-    """The reference's own naive path on the host, on a bounded sample:
-    first on 1 thread, then batch-parallel with one image per thread on up
-    to 16 threads (the GPU box's CPU share; ctypes releases the GIL, so the
-    reference's loops run concurrently).  SURVEY.md 8(d) asks for both; the
-    multi-core figure is the reported baseline."""
+def cpu_case(workload: str):
+    """(one(img), inputs, input pixels per image, kind, what) of the reference's
+    own CPU path for a workload: oracle/_ref (the reference's loops compiled
+    from its sources) where present, else the C restatement (oracle/)."""
     import numpy as np
-    from concurrent.futures import ThreadPoolExecutor
     sys.path.insert(0, str(REPO / "oracle"))
     from oracle import Oracle, Reference, synthetic_image
     mean = np.array(MEAN, np.float32)
     std = np.array(STD, np.float32)
-    imgs = [synthetic_image(1000 + k, H_IN, W_IN, C) for k in range(4)]
-    if Reference.available():
-        R, kind = Reference(), "reference"
+    O = Oracle()
+    R = Reference() if Reference.available() else None
+    kind = "reference" if R else "port"
+    if workload == "warp":
+        imgs = [synthetic_image(1000 + k, 720, 1280, 3) for k in range(4)]
+        m = O.rotation_matrix(0.9, 15.0, (640, 360, 640, 360))
+        inv = O.invert_affine(m)
+        if R:
+            def one(img):  # warp_affine.cpp:121-133 inverse, warp_affine_naive.cpp:9-62
+                return R.warp_affine_inv(img, inv, 1280, 720)
+        else:
+            def one(img):
+                return O.warp_affine(img, m, 1280, 720)
+        return one, imgs, 1280 * 720, kind, "warp_affine_naive 1280x720 rot15 scale0.9"
+    if workload in ("cvt_normalize", "yuv_resize"):
+        imgs = [O.bgr2nv21(synthetic_image(1000 + k, 1080, 1920, 3)) for k in range(4)]
+        to_bgr = R.nv21_to_bgr if R else O.yuv420sp_to_bgr
+        rs = R.resize_linear if R else O.resize_linear
+        norm = R.normalize if R else O.normalize
+        if workload == "cvt_normalize":
+            def one(yuv):  # cvt_color.cpp:39-135, tensor.cpp:477-481, normalize_naive.cpp:74-90
+                return norm(to_bgr(yuv).astype(np.float32), mean, std)
+            return one, imgs, 1920 * 1080, kind, "nv_to_bgr_naive 1080p + u8->fp32 + normalize"
 
+        def one(yuv):  # + resize_naive.cpp:10-68 and the HWC->CHW of tensor.cpp:160-182
+            return O.hwc_to_chw(norm(rs(to_bgr(yuv), 640, 360).astype(np.float32), mean, std))
+        return one, imgs, 1920 * 1080, kind, "nv_to_bgr_naive 1080p + resize_naive 640x360 + normalize + hwc_to_chw"
+    if workload == "cubic_stats":
+        imgs = [synthetic_image(1000 + k, 1440, 2560, 3) for k in range(2)]
+        cubic = R.resize_cubic if R else O.resize_cubic
+        stats = R.mean_stddev if R else O.mean_stddev_ref
+
+        def one(img):  # tensor.cpp:477-481, resize_naive.cpp:130-569, normalize_naive.cpp:7-48
+            return stats(cubic(img.astype(np.float32), 224, 224))
+        return one, imgs, 2560 * 1440, kind, "u8->fp32 2560x1440 + cubic 224x224 + mean_stddev"
+    imgs = [synthetic_image(1000 + k, H_IN, W_IN, C) for k in range(4)]
+    if R:
         def one(img):
             r = R.resize_linear(img, W_OUT, H_OUT)           # resize_naive.cpp:10-68
             return R.normalize(r.astype(np.float32), mean, std)  # tensor.cpp:477-481 + normalize_naive.cpp:74-90
     else:
-        O, kind = Oracle(), "port"
-
         def one(img):
             return O.normalize(O.u8_to_f32(O.resize_linear(img, W_OUT, H_OUT)), mean, std)
+    return one, imgs, W_IN * H_IN, kind, "1920x1080x3 u8 frames, resize_naive 640x360 + u8->fp32 + normalize"
+
+
+def cpu_baseline(budget_s: float, workload: str = "resize_normalize"):
+    """The reference's own CPU path of the workload on the host, on a bounded
+    sample: first on 1 thread, then batch-parallel with one image per thread
+    on up to 16 threads (the GPU box's CPU share; ctypes releases the GIL, so
+    the reference's loops run concurrently).  SURVEY.md 8(d) asks for both;
+    the multi-core figure is the reported baseline."""
+    from concurrent.futures import ThreadPoolExecutor
+    one, imgs, px, kind, what = cpu_case(workload)
 
     def run(threads, seconds):
         def worker(t):
@@ -102,25 +154,91 @@ def cpu_baseline(budget_s: float):
     n1, el1 = run(1, budget_s * 0.4)
     threads = max(1, min(16, os.cpu_count() or 1))
     nt, elt = run(threads, budget_s * 0.6)
-    v1 = n1 * W_IN * H_IN / el1 / 1e6
-    vt = nt * W_IN * H_IN / elt / 1e6
+    v1 = n1 * px / el1 / 1e6
+    vt = nt * px / elt / 1e6
     return {"value": round(vt, 3), "unit": "Mpixels/s", "cores": threads, "kind": kind,
             "value_1_core": round(v1, 3),
-            "sample": f"synthetic 1920x1080x3 u8 frames, resize_naive 640x360 + u8->fp32 + normalize: "
-                      f"{nt} frames on {threads} threads (one frame per thread) in {elt:.1f} s; "
+            "sample": f"synthetic {what}: {nt} frames on {threads} threads (one frame per thread) in {elt:.1f} s; "
                       f"{n1} frames on 1 thread in {el1:.1f} s"}
 
 
-def pmc_traffic():
+def pmc_traffic(workload: str = "resize_normalize"):
     """Corrected HBM bytes per launch from the committed rocprofv3 PMC passes
-    (profiles/pmc_resize_normalize.json, written by tools/pmc_summary.py)."""
-    p = PROFILES / "pmc_resize_normalize.json"
+    (profiles/pmc_<workload>.json, written by tools/pmc_summary.py)."""
+    p = PROFILES / f"pmc_{workload}.json"
     if not p.exists():
         return None
     try:
         return json.loads(p.read_text()).get("hbm_bytes_per_launch")
     except Exception:
         return None
+
+
+def make_workload(name: str, batch: int, dev, rank: int, world: int, ops) -> dict:
+    """Inputs resident in HBM, the step's launches and the roofline terms of
+    one BASELINE config.  b_alg = algorithmic bytes of the dominant kernel per
+    launch; px = input-frame pixels per image."""
+    import torch
+    from vacv_amd.roofline import resize_bytes, yuv_resize_bytes
+    g = torch.Generator(device=dev)
+    g.manual_seed(1234 + rank)
+
+    def u8(*shape):
+        return torch.randint(0, 256, shape, dtype=torch.uint8, device=dev, generator=g)
+
+    if name == "warp":
+        B = batch or 128
+        src = u8(B, 720, 1280, 3)
+        dst = torch.empty_like(src)
+        m = ops.rotation_matrix(0.9, 15.0, (640, 360, 640, 360))
+        return {"batch": B, "px": 1280 * 720, "b_alg": B * 2 * 1280 * 720 * 3, "kernel": "warp_kernel",
+                "frame": "1280x720x3", "output": "1280x720x3 u8",
+                "desc": "warp_affine INTER_LINEAR BORDER_CONSTANT 1280x720x3 u8, scale 0.9 rot 15 aux (640,360,640,360)",
+                "main": lambda stream=None: ops.warp_affine(src, m, 1280, 720, out=dst, stream=stream)}
+    if name == "cvt_normalize":
+        B = batch or 256
+        yuv = u8(B, 1620, 1920)
+        dst = torch.empty((B, 1080, 1920, 3), dtype=torch.float32, device=dev)
+        return {"batch": B, "px": 1920 * 1080, "b_alg": B * (1920 * 1620 + 1920 * 1080 * 12), "kernel": "color_kernel",
+                "frame": "NV21 1920x1620", "output": "1920x1080x3 fp32",
+                "desc": "cvt_color YUV2BGR_NV21 1080p + normalize(mean/std) -> 1920x1080x3 fp32, one pass",
+                "main": lambda stream=None: ops.cvt_color_normalize(yuv, mean=MEAN, std=STD, out=dst, stream=stream)}
+    if name == "yuv_resize":
+        B = batch or 256
+        yuv = u8(B, 1620, 1920)
+        dst = torch.empty((B, 3, 360, 640), dtype=torch.float32, device=dev)
+        return {"batch": B, "px": 1920 * 1080, "b_alg": B * yuv_resize_bytes(1920, 1080, 640, 360),
+                "kernel": "yuv_resize_kernel", "frame": "NV21 1920x1620", "output": "3x360x640 fp32 (NCHW)",
+                "desc": "cvt_color NV21 -> resize INTER_LINEAR 640x360 -> normalize -> NCHW, one kernel",
+                "main": lambda stream=None: ops.cvt_color_resize_normalize(yuv, 640, 360, MEAN, STD, out=dst,
+                                                                           stream=stream)}
+    if name == "cubic_stats":
+        from vacv_amd import INTER_CUBIC
+        from vacv_amd import dist as vdist
+        B = batch or 128
+        src = u8(B, 1440, 2560, 3)
+        dst = torch.empty((B, 224, 224, 3), dtype=torch.float32, device=dev)
+        stats = {}
+
+        def extra(stream=None):
+            # the global mean/stddev of the whole sharded batch: exact per-rank
+            # sums, ONE all-reduce of 7 doubles over RCCL, identical on every rank
+            sums = ops.channel_sums(dst, per_image=False)[0]
+            total, count = vdist.allreduce_sums_async(sums, float(B) * 224 * 224)
+            stats["mean"], stats["std"] = vdist.stats_from_moments(total, count)
+        return {"batch": B, "px": 2560 * 1440, "b_alg": B * resize_bytes(2560, 1440, 3, 224, 224, 1, 4, cubic=True),
+                "kernel": "cubic_direct_kernel", "frame": "2560x1440x3", "output": "224x224x3 fp32 + global mean/std",
+                "desc": "resize INTER_CUBIC 2560x1440x3 u8 -> 224x224x3 fp32 + global mean_stddev (RCCL all-reduce)",
+                "main": lambda stream=None: ops.resize(src, 224, 224, interpolation=INTER_CUBIC, out=dst, stream=stream),
+                "extra": extra}
+    B = batch or 256
+    src = u8(B, H_IN, W_IN, C)
+    dst = torch.empty((B, H_OUT, W_OUT, C), dtype=torch.float32, device=dev)
+    return {"batch": B, "px": W_IN * H_IN, "b_alg": resize_bytes(W_IN, H_IN, C, W_OUT, H_OUT, 1, 4) * B,
+            "kernel": "resize_direct_kernel", "frame": "1920x1080x3", "output": "640x360x3 fp32",
+            "desc": "resize_normalize INTER_LINEAR 1920x1080x3 u8 NHWC -> 640x360x3 fp32 "
+                    "(reference arithmetic) + per-channel normalize",
+            "main": lambda stream=None: ops.resize_normalize(src, W_OUT, H_OUT, MEAN, STD, out=dst, stream=stream)}
 
 
 def main():
@@ -139,31 +257,29 @@ def main():
 
     ensure_built()
     from vacv_amd import ops
-    from vacv_amd.roofline import HBM_PEAK_GBS, resize_bytes
+    from vacv_amd.roofline import HBM_PEAK_GBS
 
-    B = args.batch
-    g = torch.Generator(device=dev)
-    g.manual_seed(1234 + rank)
-    src = torch.randint(0, 256, (B, H_IN, W_IN, C), dtype=torch.uint8, device=dev, generator=g)
-    dst = torch.empty((B, H_OUT, W_OUT, C), dtype=torch.float32, device=dev)
+    wl = make_workload(args.workload, args.batch, dev, rank, world, ops)
+    B = wl["batch"]
     stream = torch.cuda.current_stream(dev)
-
-    def launch():
-        ops.resize_normalize(src, W_OUT, H_OUT, MEAN, STD, out=dst, stream=stream)
+    launch = wl["main"]       # the dominant kernel (timed alone for the roofline)
+    extra = wl.get("extra")   # the rest of the step (e.g. cfg5's stats + all-reduce)
 
     for _ in range(args.warmup):
         launch()  # also builds and caches the resize plan (a one-time upload)
+        if extra:
+            extra()
     torch.cuda.synchronize(dev)
 
     # One step = one vacv_resize_normalize launch over the whole batch.  With
     # --graph it is captured once into a HIP graph and replayed (every replay
     # runs the full kernel); the default launches it from Python each step.
     graph = None
-    if args.graph:
+    if args.graph and not extra:
         try:
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g):
-                ops.resize_normalize(src, W_OUT, H_OUT, MEAN, STD, out=dst)
+                wl["main"](stream=torch.cuda.current_stream(dev))
             graph = g
             stream = torch.cuda.current_stream(dev)
         except Exception as e:  # capture unsupported: eager launches
@@ -190,6 +306,8 @@ def main():
         ev[i][0].record(stream)
         step()
         ev[i][1].record(stream)
+        if extra:
+            extra()
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -203,14 +321,14 @@ def main():
     ms_per_step = elapsed * 1e3 / args.steps
 
     n_img = B * world
-    value = n_img * W_IN * H_IN / (ms_per_step / 1e3) / 1e6
-    b_alg = resize_bytes(W_IN, H_IN, C, W_OUT, H_OUT, 1, 4) * B  # per launch (one GPU's batch)
+    value = n_img * wl["px"] / (ms_per_step / 1e3) / 1e6
+    b_alg = wl["b_alg"]  # per launch (one GPU's batch)
     achieved = b_alg / (kern_ms / 1e3) / 1e9
-    traffic = pmc_traffic()
+    traffic = pmc_traffic(args.workload)
 
     out = None
     if rank == 0:
-        cpu = None if args.no_cpu_baseline else cpu_baseline(args.cpu_seconds)
+        cpu = None if args.no_cpu_baseline else cpu_baseline(args.cpu_seconds, args.workload)
         out = {
             "metric": "Mpixels/sec per op (resize/warp/normalize) at 1080p; achieved HBM GB/s vs peak",
             "value": round(value, 2),
@@ -224,13 +342,11 @@ def main():
             "vs_baseline": None,
             "dtype": "u8",
             "data": "synthetic (torch.randint u8 frames resident in HBM)",
-            "config": {"workload": "resize_normalize INTER_LINEAR 1920x1080x3 u8 NHWC -> 640x360x3 fp32 "
-                                   "(reference arithmetic) + per-channel normalize",
-                       "global_batch": n_img, "batch_per_gpu": B, "parallelism": f"dp{world}",
-                       "frame": "1920x1080x3", "output": "640x360x3 fp32"},
+            "config": {"workload": wl["desc"], "global_batch": n_img, "batch_per_gpu": B,
+                       "parallelism": f"dp{world}", "frame": wl["frame"], "output": wl["output"]},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                         "kernel_ms": round(kern_ms, 4), "alg_bytes_per_launch": b_alg},
+                         "kernel": wl["kernel"], "kernel_ms": round(kern_ms, 4), "alg_bytes_per_launch": b_alg},
             "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)

@@ -39,7 +39,7 @@ def _worker(rank, world, port, images, out_q):
         sys.path.insert(0, p)
     import torch.distributed as dist
     from oracle import Oracle
-    from vacv_amd.dist import allreduce_sums, shard_range, stats_from_moments
+    from vacv_amd.dist import allreduce_sums, allreduce_sums_async, shard_range, stats_from_moments
     dist.init_process_group("gloo", rank=rank, world_size=world)
     b, e = shard_range(len(images), rank, world)
     O = Oracle()
@@ -50,6 +50,10 @@ def _worker(rank, world, port, images, out_q):
     h, w = images[0].shape[:2]
     total, count = allreduce_sums(torch.from_numpy(local), float((e - b) * h * w))
     mean, std = stats_from_moments(total, count)
+    # the no-sync variant bench.py's cubic_stats step uses: identical results
+    ta, ca = allreduce_sums_async(torch.from_numpy(local), float((e - b) * h * w))
+    ma, sa = stats_from_moments(ta, ca)
+    assert float(ca) == count and torch.equal(ma, mean) and torch.equal(sa, std)
     out_q.put((rank, mean.numpy(), std.numpy(), count))
     dist.destroy_process_group()
 
