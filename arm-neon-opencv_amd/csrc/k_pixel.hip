@@ -522,24 +522,35 @@ __global__ void __launch_bounds__(kBlock) channel_sums_kernel(SumsLaunch L) {
 }
 
 // sums[g][c][2] from partials, fixed order: image-major, then plane, block.
-__global__ void stats_reduce_kernel(SumsLaunch L, int cc) {
+// One workgroup per (group, channel, moment): thread t sums partials t,
+// t + 256, ... in order, then a fixed LDS tree -- the same order on every run
+// (deterministic), and parallel: a whole-batch sum over n * blocks partials
+// took 262 us as one sequential loop per output (cfg5, n = 128).
+__global__ void __launch_bounds__(kBlock) stats_reduce_kernel(SumsLaunch L, int cc) {
+    __shared__ double red[kBlock];
     const int c = L.c;
-    const int groups = L.per_image ? L.n : 1;
-    const int idx = blockIdx.x * blockDim.x + threadIdx.x;
-    if (idx >= groups * c * 2) return;
+    const int idx = blockIdx.x;  // < groups * c * 2
     const int g = idx / (2 * c);
     const int r = idx - g * 2 * c;
     const int ch = r >> 1, mom = r & 1;
     const int plane = (cc == 1) ? ch : 0;  // NCHW: channel = plane
     const int k = (cc == 1) ? 0 : ch;
     const int img_lo = L.per_image ? g : 0, img_hi = L.per_image ? g + 1 : L.n;
+    const int64_t terms = (int64_t)(img_hi - img_lo) * L.blocks_per_image;
     double acc = 0.0;
-    for (int img = img_lo; img < img_hi; ++img) {
+    for (int64_t t = threadIdx.x; t < terms; t += kBlock) {
+        const int img = img_lo + (int)(t / L.blocks_per_image);
+        const int b = (int)(t - (int64_t)(img - img_lo) * L.blocks_per_image);
         const int64_t pidx = (int64_t)img * L.src.planes + plane;
-        for (int b = 0; b < L.blocks_per_image; ++b)
-            acc += L.partials[((pidx * L.blocks_per_image) + b) * (2 * cc) + 2 * k + mom];
+        acc += L.partials[((pidx * L.blocks_per_image) + b) * (2 * cc) + 2 * k + mom];
     }
-    L.sums[idx] = acc;
+    red[threadIdx.x] = acc;
+    __syncthreads();
+    for (int h = kBlock / 2; h > 0; h >>= 1) {
+        if ((int)threadIdx.x < h) red[threadIdx.x] += red[threadIdx.x + h];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) L.sums[idx] = red[0];
 }
 
 __global__ void stats_kernel(const double* sums, int groups, int c, double count, float* mean, float* stddev) {
@@ -560,7 +571,7 @@ hipError_t launch_sums_cc(const SumsLaunch& L, hipStream_t s) {
     if (e != hipSuccess) return e;
     const int groups = L.per_image ? L.n : 1;
     const int work = groups * L.c * 2;
-    hipLaunchKernelGGL(stats_reduce_kernel, dim3((work + 255) / 256), dim3(256), 0, s, L, CC);
+    hipLaunchKernelGGL(stats_reduce_kernel, dim3(work), dim3(kBlock), 0, s, L, CC);
     return hipGetLastError();
 }
 

@@ -214,7 +214,6 @@ def make_workload(name: str, batch: int, dev, rank: int, world: int, ops) -> dic
                                                                            stream=stream)}
     if name == "cubic_stats":
         from vacv_amd import INTER_CUBIC
-        from vacv_amd import dist as vdist
         B = batch or 128
         src = u8(B, 1440, 2560, 3)
         dst = torch.empty((B, 224, 224, 3), dtype=torch.float32, device=dev)
@@ -222,10 +221,12 @@ def make_workload(name: str, batch: int, dev, rank: int, world: int, ops) -> dic
 
         def extra(stream=None):
             # the global mean/stddev of the whole sharded batch: exact per-rank
-            # sums, ONE all-reduce of 7 doubles over RCCL, identical on every rank
-            sums = ops.channel_sums(dst, per_image=False)[0]
-            total, count = vdist.allreduce_sums_async(sums, float(B) * 224 * 224)
-            stats["mean"], stats["std"] = vdist.stats_from_moments(total, count)
+            # sums (vacv_channel_sums), ONE all-reduce of 6 doubles over RCCL,
+            # vacv_stats_from_sums -- identical on every rank, no host sync
+            sums = ops.channel_sums(dst, per_image=False)  # (1, c, 2) fp64
+            if world > 1:
+                torch.distributed.all_reduce(sums, op=torch.distributed.ReduceOp.SUM)
+            stats["mean"], stats["std"] = ops.stats_from_sums(sums, float(B) * world * 224 * 224)
         return {"batch": B, "px": 2560 * 1440, "b_alg": B * resize_bytes(2560, 1440, 3, 224, 224, 1, 4, cubic=True),
                 "kernel": "cubic_direct_kernel", "frame": "2560x1440x3", "output": "224x224x3 fp32 + global mean/std",
                 "desc": "resize INTER_CUBIC 2560x1440x3 u8 -> 224x224x3 fp32 + global mean_stddev (RCCL all-reduce)",
