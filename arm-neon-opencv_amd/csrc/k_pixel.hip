@@ -191,17 +191,14 @@ __global__ void __launch_bounds__(kBlock) f32_to_u8_kernel(DtypeLaunch L) {
 template <int OUT>
 __global__ void __launch_bounds__(kBlock) color_kernel(ColorLaunch L) {
     using TOut = typename std::conditional<(OUT == kOutSame), uint8_t, float>::type;
-    constexpr bool kLut = (OUT == kOutNorm);
-    __shared__ float lut[kLut ? 3 * 256 : 1];
-
+    // normalisation in registers (normalize_u8v: the host-verified fp64
+    // multiply, else the reference's divide); a per-workgroup 768-entry LDS
+    // table cost 3 fp64 divides per thread and a barrier for 8 pixels
     const int img = blockIdx.z;
-    if (kLut) {
-        for (int i = threadIdx.y * blockDim.x + threadIdx.x; i < 3 * 256; i += kBlock) {
-            float m, s;
-            norm_params(L.norm, img, i >> 8, m, s);
-            lut[i] = normalize_value((float)(i & 255), m, s);
-        }
-        __syncthreads();
+    ChanNorm cn[3] = {};
+    if (OUT == kOutNorm) {
+#pragma unroll
+        for (int k = 0; k < 3; ++k) cn[k] = chan_norm(L.norm, img, k);
     }
     // fp32 output: a wave's 64 lanes x 48 B of one row go out through LDS as
     // three 1 KiB contiguous non-temporal stores (lane-strided 48-B stores
@@ -261,7 +258,9 @@ __global__ void __launch_bounds__(kBlock) color_kernel(ColorLaunch L) {
             } else if (OUT == kOutF32) {
                 out[3 * j + 0] = (TOut)(float)c0; out[3 * j + 1] = (TOut)(float)G; out[3 * j + 2] = (TOut)(float)c2;
             } else {
-                out[3 * j + 0] = lut[c0]; out[3 * j + 1] = lut[256 + G]; out[3 * j + 2] = lut[512 + c2];
+                out[3 * j + 0] = normalize_u8v(cn[0], c0);
+                out[3 * j + 1] = normalize_u8v(cn[1], G);
+                out[3 * j + 2] = normalize_u8v(cn[2], c2);
             }
         }
         unsigned char* dp = L.dst + (int64_t)img * L.dst_img + (int64_t)(2 * yy + r) * L.dst_row +
