@@ -39,9 +39,11 @@ warp_kernel(WarpLaunch L, int gx, int gy, int total) {
     constexpr int LH = 64 / LW;  // rows of one lane block; the tile is 4 rows
     static_assert(LW * LH == 64 && LH <= 4, "lane block");
     using TOut = typename std::conditional<(OUT == kOutSame), TIn, float>::type;
-    constexpr bool kLut = std::is_same<TIn, uint8_t>::value && (OUT == kOutNorm);
+    // u8 normalisation in registers (normalize_u8v); a per-workgroup LDS
+    // table cost 3 fp64 divides per thread and a barrier (NV21 kernel: 0.58 ->
+    // 0.71 of the roofline without it)
+    constexpr bool kU8Norm = std::is_same<TIn, uint8_t>::value && (OUT == kOutNorm);
     constexpr int kRowBytes = 64 * kPx * CC * (int)sizeof(TOut);  // one wave's output row segment
-    __shared__ float lut[kLut ? 256 * CC : 1];
     __shared__ __attribute__((aligned(16))) unsigned char xch[4][kRowBytes];
 
     // XCD-aware block order: workgroup b runs on XCD b % 8, and each XCD
@@ -69,13 +71,10 @@ warp_kernel(WarpLaunch L, int gx, int gy, int total) {
 #pragma unroll
         for (int k = 0; k < CC; ++k) norm_params(L.norm, img, CC == 1 ? plane : k, nmean[k], nstd[k]);
     }
-    if (kLut) {
-        const int tid = threadIdx.y * 64 + threadIdx.x;
-        for (int i = tid; i < 256 * CC; i += kBlock) {
-            const int k = i >> 8;
-            lut[i] = normalize_value((float)(i & 255), nmean[k], nstd[k]);
-        }
-        __syncthreads();
+    ChanNorm cn[CC] = {};
+    if (kU8Norm) {
+#pragma unroll
+        for (int k = 0; k < CC; ++k) cn[k] = chan_norm(L.norm, img, CC == 1 ? plane : k);
     }
 
     const unsigned char* sp = L.src.base + (int64_t)img * L.src.img_pitch + (int64_t)plane * L.src.plane_pitch;
@@ -107,7 +106,7 @@ warp_kernel(WarpLaunch L, int gx, int gy, int total) {
 #pragma unroll
             for (int k = 0; k < CC; ++k) {
                 if (OUT == kOutNorm) {
-                    o[k] = kLut ? (TOut)lut[k * 256 + (int)L.border[k]]
+                    o[k] = kU8Norm ? (TOut)normalize_u8v(cn[k], (int)L.border[k])
                                 : (TOut)normalize_value(L.border[k], nmean[k], nstd[k]);
                 } else {
                     o[k] = (TOut)L.border[k];
@@ -159,7 +158,7 @@ warp_kernel(WarpLaunch L, int gx, int gy, int total) {
                 const int v = (int)((__umul24(ht, (uint32_t)wy0) + __umul24(hb, (uint32_t)wy1)) >> 22);
                 if (OUT == kOutSame) o[k] = (TOut)v;
                 else if (OUT == kOutF32) o[k] = (TOut)(float)v;
-                else o[k] = (TOut)lut[k * 256 + v];
+                else o[k] = (TOut)normalize_u8v(cn[k], v);
             }
         } else {
             const float yy0 = 1.f - ay, yy1 = ay, xa = 1.f - ax, xb = ax;
