@@ -74,6 +74,7 @@ SIGNATURES = {
     "vacv_normalize": ([_IMG, _IMG, _FP, _FP, _P], _I),
     "vacv_channel_sums": ([_IMG, _P, _I, _P], _I),
     "vacv_stats_from_sums": ([_P, _I, _I, _D, _P, _P, _P], _I),
+    "vacv_resize_channel_sums": ([_IMG, _IMG, _I, _I, _P, _I, _P], _I),
     "vacv_mean_stddev": ([_IMG, _P, _P, _P], _I),
     "vacv_resize_normalize": ([_IMG, _IMG, _I, _I, _FP, _FP, _P], _I),
     "vacv_warp_affine_normalize": ([_IMG, _IMG, _FP, _I, _I, _DP, _FP, _FP, _P], _I),

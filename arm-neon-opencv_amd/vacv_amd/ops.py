@@ -316,6 +316,24 @@ def channel_sums(src: torch.Tensor, per_image: bool = True, layout: int = NHWC, 
     return out
 
 
+def resize_channel_sums(src: torch.Tensor, w: int, h: int, interpolation: int = INTER_LINEAR,
+                        mode: int = LINEAR_REFERENCE, per_image: bool = True, layout: int = NHWC, out=None,
+                        stream=None) -> Tuple[torch.Tensor, torch.Tensor]:
+    """resize() and channel_sums() of its output in one pass where the kernel
+    fuses them (u8 -> fp32 INTER_CUBIC).  Returns (resized, sums)."""
+    s4 = _as4d(src, layout)
+    if out is None:
+        dt = torch.float32 if (interpolation == INTER_CUBIC or src.dtype == torch.float32) else src.dtype
+        out = _empty_like_shape(s4, layout, w, h, dt, False, src.dim())
+    o4 = _as4d(out, layout)
+    c = o4.shape[3] if layout == NHWC else o4.shape[1]
+    sums = torch.empty((o4.shape[0] if per_image else 1, c, 2), dtype=torch.float64, device=src.device)
+    check("vacv_resize_channel_sums",
+          L.load().vacv_resize_channel_sums(ctypes.byref(describe(s4, layout)), ctypes.byref(describe(o4, layout)),
+                                            interpolation, mode, sums.data_ptr(), int(per_image), _stream(stream)))
+    return out, sums
+
+
 def stats_from_sums(sums: torch.Tensor, count: float, stream=None) -> Tuple[torch.Tensor, torch.Tensor]:
     sums = sums.contiguous()
     groups, c = sums.shape[0], sums.shape[1]

@@ -221,9 +221,10 @@ def make_workload(name: str, batch: int, dev, rank: int, world: int, ops) -> dic
 
         def extra(stream=None):
             # the global mean/stddev of the whole sharded batch: exact per-rank
-            # sums (vacv_channel_sums), ONE all-reduce of 6 doubles over RCCL,
-            # vacv_stats_from_sums -- identical on every rank, no host sync
-            sums = ops.channel_sums(dst, per_image=False)  # (1, c, 2) fp64
+            # sums (vacv_channel_sums), ONE all-reduce of the (c, 2) fp64 sums
+            # over RCCL, vacv_stats_from_sums -- identical on every rank, no
+            # host sync
+            sums = ops.channel_sums(dst, per_image=False)
             if world > 1:
                 torch.distributed.all_reduce(sums, op=torch.distributed.ReduceOp.SUM)
             stats["mean"], stats["std"] = ops.stats_from_sums(sums, float(B) * world * 224 * 224)

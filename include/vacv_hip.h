@@ -154,6 +154,13 @@ int vacv_normalize(const vacv_image* src, const vacv_image* dst,
  * partials the multi-GPU path all-reduces over RCCL. */
 int vacv_channel_sums(const vacv_image* src, double* sums, int per_image, void* stream);
 
+/* vacv_resize followed by vacv_channel_sums of its output: the statistics
+ * half of BASELINE cfg5 (resize + mean_stddev, normalize_naive.cpp:7-72 on
+ * the resized image); on several GPUs the sums are what one all-reduce
+ * merges.  dst must be dense. */
+int vacv_resize_channel_sums(const vacv_image* src, const vacv_image* dst, int interpolation, int mode,
+                             double* sums, int per_image, void* stream);
+
 /* mean = S1/count, stddev = sqrt(max(S2/count - mean^2, 0)) per group and
  * channel, on the device: sums[groups][c][2] -> mean/stddev[groups][c]. */
 int vacv_stats_from_sums(const double* sums, int groups, int c, double count,

@@ -160,6 +160,37 @@ def test_cubic_direct_and_staged_agree(ops, dev, oracle, monkeypatch):
     torch.cuda.empty_cache()
 
 
+def test_resize_channel_sums(ops, dev, oracle):
+    """vacv_resize_channel_sums: the resize output is unchanged and the sums
+    equal vacv_channel_sums of that output (the bound in the asserts allows a
+    fused epilogue's other fp64 summation order).  The batch statistic of
+    cfg5 (2560x1440 -> 224x224 cubic) at full size."""
+    import torch
+    from vacv_amd import INTER_CUBIC, NCHW
+    imgs = np.stack([synthetic_image(300 + k, 1440, 2560, 3) for k in range(4)])
+    src = to_dev(imgs, dev)
+    for per_image in (True, False):
+        out, sums = ops.resize_channel_sums(src, 224, 224, INTER_CUBIC, per_image=per_image)
+        ref = ops.resize(src, 224, 224, interpolation=INTER_CUBIC)
+        assert torch.equal(out, ref)
+        want = ops.channel_sums(ref, per_image=per_image)
+        torch.cuda.synchronize(dev)
+        rel = ((sums - want).abs() / want.abs().clamp(min=1.0)).max().item()
+        assert rel <= 1e-12, rel  # |d| <= 1e-12 relative (fp64 summation order)
+    # NCHW planes and odd sizes
+    chw = ops.change_layout(src[:2, :301, :257].contiguous(), NCHW)
+    out, sums = ops.resize_channel_sums(chw, 61, 37, INTER_CUBIC, layout=NCHW)
+    want = ops.channel_sums(out, layout=NCHW)
+    torch.cuda.synchronize(dev)
+    assert ((sums - want).abs() / want.abs().clamp(min=1.0)).max().item() <= 1e-12
+    # u8 bilinear: identical to the two calls
+    out, sums = ops.resize_channel_sums(src, 640, 360)
+    assert torch.equal(out, ops.resize(src, 640, 360))
+    assert torch.equal(sums, ops.channel_sums(out))
+    del src
+    torch.cuda.empty_cache()
+
+
 def test_resize_full_size_batch(ops, dev, oracle):
     """BASELINE cfg2 at full size: 1920x1080 -> 640x360 / 1280x720, batch of 3,
     plus a pitched source (a sub-window of a wider buffer)."""
