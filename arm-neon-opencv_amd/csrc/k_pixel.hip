@@ -471,25 +471,58 @@ __global__ void __launch_bounds__(kBlock) channel_sums_kernel(SumsLaunch L) {
 #pragma unroll
         for (int k = 0; k < CC; ++k) { s1[k] += a1[k]; s2[k] += a2[k]; }
     } else {
-        for (int64_t c = c_begin + threadIdx.x; c < c_end; c += kBlock) {
-            const float4* p = reinterpret_cast<const float4*>(base + c * kChunk);
+        // fp32: lane-consecutive float4 loads (1 KiB per wave instruction).
+        // Block ranges and wave steps are multiples of 192 float4s, so the
+        // channel of element j of load m (float4 192k + 64m + lane) is
+        // (lane + m + j) % 3 for CC = 3 (4 = 1 mod 3) and j % CC otherwise:
+        // accumulate by the lane-relative slot, un-rotate once at the end.
+        const int64_t n4 = L.scalar_only ? 0 : elems / 4;
+        const int64_t groups = (n4 + 191) / 192;
+        const int64_t g_per_block = (groups + gridDim.x - 1) / gridDim.x;
+        const int64_t g_begin = blockIdx.x * g_per_block;
+        const int64_t g_end = min(groups, g_begin + g_per_block);
+        const int wave = threadIdx.x >> 6, ln = threadIdx.x & 63;
+        typedef float f32x4_t __attribute__((ext_vector_type(4)));
+        const f32x4_t* b4 = reinterpret_cast<const f32x4_t*>(base);
+        double r1[CC], r2[CC];
 #pragma unroll
-            for (int q = 0; q < 4 * CC; ++q) {
-                const float4 v = p[q];
-                const float f[4] = {v.x, v.y, v.z, v.w};
+        for (int k = 0; k < CC; ++k) { r1[k] = 0.0; r2[k] = 0.0; }
+        for (int64_t g = g_begin + wave; g < g_end; g += kBlock / 64) {
+            f32x4_t v[3];
+#pragma unroll
+            for (int m = 0; m < 3; ++m) {
+                const int64_t i = g * 192 + 64 * m + ln;
+                v[m] = i < n4 ? __builtin_nontemporal_load(b4 + i) : f32x4_t{0.f, 0.f, 0.f, 0.f};
+            }
+#pragma unroll
+            for (int m = 0; m < 3; ++m) {
+                const float f[4] = {v[m][0], v[m][1], v[m][2], v[m][3]};
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
-                    const int k = (q * 4 + j) % CC;
+                    const int slot = CC == 3 ? (m + j) % 3 : j % CC;
                     const double d = f[j];
-                    s1[k] += d;
-                    s2[k] += d * d;
+                    r1[slot] += d;
+                    r2[slot] += d * d;
+                }
+            }
+        }
+        // slot -> channel: (slot + lane) % 3 for CC = 3, the identity otherwise
+        const int rot = CC == 3 ? ln % 3 : 0;
+#pragma unroll
+        for (int k = 0; k < CC; ++k) {
+#pragma unroll
+            for (int sl = 0; sl < CC; ++sl) {
+                if (CC == 3 ? ((sl + rot) % 3 == k) : (sl == k)) {
+                    s1[k] += r1[sl];
+                    s2[k] += r2[sl];
                 }
             }
         }
     }
     // tail elements (all of them on a misaligned plane), split over blocks
     {
-        const int64_t t0 = nchunks * kChunk, tn = elems - t0;
+        const int64_t t0 = sizeof(TIn) == 1 ? nchunks * kChunk : (L.scalar_only ? 0 : elems / 4 * 4);
+        const int64_t tn = elems - t0;
         const int64_t tper = (tn + gridDim.x - 1) / gridDim.x;
         const int64_t tb = t0 + blockIdx.x * tper, te = min(elems, tb + tper);
         for (int64_t e = tb + threadIdx.x; e < te; e += kBlock) {
