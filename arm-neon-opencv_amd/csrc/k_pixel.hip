@@ -618,6 +618,63 @@ hipError_t launch_sums_t(const SumsLaunch& L, hipStream_t s) {
     }
 }
 
+// --------------------------------------------------------------------------
+// INTER_NEAREST resize (cv::resize -> resizeNN of the pinned OpenCV 2.4,
+// which the reference hands every mode but LINEAR/CUBIC to, resize.cpp:44-49):
+// sx = min(floor(x * ifx), w - 1), ifx = 1 / ((double)w_out / w_in), the same
+// for y.  One thread per output pixel (all cc channels); a workgroup row is
+// one output row, so sy is uniform.  Optional widen / normalize epilogue.
+template <typename TIn, int OUT>
+__global__ void __launch_bounds__(kBlock) nearest_kernel(ResizeLaunch L) {
+    using TOut = typename std::conditional<(OUT == kOutSame), TIn, float>::type;
+    const int x = blockIdx.x * kBlock + threadIdx.x;
+    const int y = blockIdx.y;
+    const int pidx = blockIdx.z;  // image * planes + plane
+    if (x >= L.dst.w) return;
+    const int img = pidx / L.src.planes;
+    const int plane = pidx - img * L.src.planes;
+    int sx = (int)floor((double)x * L.scale_xd);
+    int sy = (int)floor((double)y * L.scale_yd);
+    sx = min(sx, L.src.w - 1);
+    sy = min(sy, L.src.h - 1);
+    const int cc = L.src.cc;
+    const TIn* sp = reinterpret_cast<const TIn*>(L.src.base + (int64_t)img * L.src.img_pitch +
+                                                 (int64_t)plane * L.src.plane_pitch + (int64_t)sy * L.src.row_pitch) +
+                    (int64_t)sx * cc;
+    TOut* dp = reinterpret_cast<TOut*>(const_cast<unsigned char*>(L.dst.base) + (int64_t)img * L.dst.img_pitch +
+                                       (int64_t)plane * L.dst.plane_pitch + (int64_t)y * L.dst.row_pitch) +
+               (int64_t)x * cc;
+    for (int k = 0; k < cc; ++k) {
+        const TIn v = sp[k];
+        if (OUT == kOutSame) {
+            dp[k] = (TOut)v;
+        } else if (OUT == kOutF32) {
+            dp[k] = (TOut)(float)v;
+        } else {
+            const ChanNorm cn = chan_norm(L.norm, img, cc == 1 ? plane % L.norm.c_total : k);
+            dp[k] = (TOut)(std::is_same<TIn, uint8_t>::value ? normalize_u8v(cn, (int)v) : normalize_f(cn, (float)v));
+        }
+    }
+}
+
+template <typename TIn>
+hipError_t launch_nearest_t(const ResizeLaunch& L, hipStream_t s) {
+    const dim3 grid((L.dst.w + kBlock - 1) / kBlock, L.dst.h, L.n * L.src.planes);
+    if (L.out == kOutSame) hipLaunchKernelGGL((nearest_kernel<TIn, kOutSame>), grid, dim3(kBlock), 0, s, L);
+    else if (L.out == kOutF32) hipLaunchKernelGGL((nearest_kernel<TIn, kOutF32>), grid, dim3(kBlock), 0, s, L);
+    else hipLaunchKernelGGL((nearest_kernel<TIn, kOutNorm>), grid, dim3(kBlock), 0, s, L);
+    return hipGetLastError();
+}
+
+}  // namespace
+
+hipError_t launch_resize_nearest(const ResizeLaunch& L, hipStream_t s) {
+    if (L.dst.h > 65535 || (int64_t)L.n * L.src.planes > 65535) return hipErrorInvalidValue;
+    return L.src.esize == 1 ? launch_nearest_t<uint8_t>(L, s) : launch_nearest_t<float>(L, s);
+}
+
+namespace {
+
 }  // namespace
 
 hipError_t launch_row_copy(const CopyLaunch& L, hipStream_t s) {

@@ -260,6 +260,17 @@ int resize_impl(const vacv_image* src_d, const vacv_image* dst_d, int interpolat
         L.kind = kCubic;
         if (L.out == kOutSame && src.dtype == VACV_INT8) L.out = kOutF32;
         if (L.out == kOutF32 && src.dtype == VACV_FP32) L.out = kOutSame;
+    } else if (interpolation == VACV_INTER_NEAREST) {
+        // resize.cpp:44-49 hands it to cv::resize (recursing forever without
+        // OpenCV); OpenCV 2.4's resizeNN semantics
+        if (src.dtype != VACV_INT8 && src.dtype != VACV_FP32) return VACV_ERR_UNSUPPORTED;
+        L.out = out_kind;
+        if (src.dtype == VACV_FP32 && L.out == kOutF32) L.out = kOutSame;
+        const int want = L.out == kOutSame ? src.dtype : VACV_FP32;
+        if (dst.dtype != want) return VACV_ERR_INVALID_ARG;
+        L.scale_xd = 1. / ((double)dst.w / src.w);  // ifx, as cv::resize computes it
+        L.scale_yd = 1. / ((double)dst.h / src.h);
+        return hip_status(launch_resize_nearest(L, s));
     } else {
         return VACV_ERR_UNSUPPORTED;  // resize.cpp:46-49 recurses forever for other modes
     }

@@ -111,6 +111,8 @@ hipError_t launch_resize(const ResizeLaunch& L, hipStream_t s);
 // resize_one_tap_rows: no output row of L has two weighted source rows.
 hipError_t launch_resize_direct(const ResizeLaunch& L, hipStream_t s);
 bool resize_one_tap_rows(const ResizeLaunch& L);
+// INTER_NEAREST (OpenCV 2.4 resizeNN): scale_xd / scale_yd carry ifx / ify
+hipError_t launch_resize_nearest(const ResizeLaunch& L, hipStream_t s);
 // u8 -> fp32 cubic as per-pixel gathers (k_cubic_direct.hip); needs no plan
 bool cubic_direct_applies(const ResizeLaunch& L);
 hipError_t launch_cubic_direct(const ResizeLaunch& L, hipStream_t s);

@@ -110,6 +110,9 @@ int vacv_change_dtype(const vacv_image* src, const vacv_image* dst, void* stream
  *  INTER_LINEAR: INT8->INT8 (mode = VACV_LINEAR_*), FP32->FP32.
  *  INTER_CUBIC:  FP32->FP32 and INT8->FP32 (the u8->fp32 conversion the
  *                reference requires before cubic, fused).
+ *  INTER_NEAREST: INT8->INT8, FP32->FP32 with OpenCV 2.4's resizeNN
+ *                semantics, which the reference delegates to cv::resize
+ *                (resize.cpp:44-49): sx = min(floor(x / (w_out / w_in)), w_in - 1).
  * NHWC channels 1..4; NCHW any c (per plane, as resize.cpp:72-88). */
 int vacv_resize(const vacv_image* src, const vacv_image* dst, int interpolation, int mode, void* stream);
 

@@ -73,6 +73,7 @@ class Oracle:
             ("oracle_resize_linear_u8", [_P, _I, _I, _I, _P, _I, _I, _I], None),
             ("oracle_resize_linear_f32", [_P, _I, _I, _I, _P, _I, _I], None),
             ("oracle_resize_cubic_f32", [_P, _I, _I, _I, _P, _I, _I], None),
+            ("oracle_resize_nearest", [_P, _I, _I, _I, _I, _P, _I, _I], None),
             ("oracle_warp_affine_u8", [_P, _I, _I, _I, _P, _I, _I, _P], None),
             ("oracle_warp_affine_f32", [_P, _I, _I, _I, _P, _I, _I, _P], None),
             ("oracle_yuv420sp_to_bgr", [_P, _P, _I, _I, _I, _I], None),
@@ -130,6 +131,14 @@ class Oracle:
         else:
             assert img.dtype == np.float32
             self.lib.oracle_resize_linear_f32(_ptr(img), w, h, c, _ptr(out), w_out, h_out)
+        return out
+
+    def resize_nearest(self, img, w_out, h_out):
+        """OpenCV 2.4 resizeNN restated (parity unpinned, vacv_oracle.c)."""
+        img = np.ascontiguousarray(img)
+        w, h, c = _shape(img)
+        out = _out(h_out, w_out, c, img.dtype)
+        self.lib.oracle_resize_nearest(_ptr(img), w, h, c, img.dtype.itemsize, _ptr(out), w_out, h_out)
         return out
 
     def resize_cubic(self, img, w_out, h_out):

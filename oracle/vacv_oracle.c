@@ -192,6 +192,32 @@ void oracle_resize_linear_u8(const uint8_t* src, int w_in, int h_in, int cc,
     free(xo); free(xa); free(xb); free(yo); free(ya); free(yb);
 }
 
+/* INTER_NEAREST.  The reference has no nearest loop of its own: Resize::resize
+ * hands every mode but LINEAR/CUBIC to resize_opencv (resize.cpp:44-49),
+ * i.e. cv::resize of the pinned OpenCV 2.4.13.4 (CMakeLists.txt:23).  Its
+ * published algorithm (imgwarp.cpp, cv::resize -> resizeNN), restated:
+ * inv_scale = (double)dsize / ssize, ifx = 1. / inv_scale, and
+ *   sx = min(cvFloor(x * ifx), w_in - 1),  sy = min(cvFloor(y * ify), h_in - 1);
+ * a same-size resize is a copy (cv::resize's dsize == ssize shortcut, which
+ * the formula reproduces).  PARITY UNPINNED: no reference entry runs this
+ * path here (OpenCV's binaries are not loaded) and its tests hold no nearest
+ * output (test_resize.cpp passes INTER_NEAREST as fx).
+ * esize bytes per element, cc interleaved channels. */
+void oracle_resize_nearest(const void* src, int w_in, int h_in, int cc, int esize,
+                           void* dst, int w_out, int h_out) {
+    const double ifx = 1. / ((double)w_out / w_in), ify = 1. / ((double)h_out / h_in);
+    const size_t px = (size_t)cc * esize;
+    for (int y = 0; y < h_out; ++y) {
+        int sy = (int)floor(y * ify);
+        if (sy > h_in - 1) sy = h_in - 1;
+        for (int x = 0; x < w_out; ++x) {
+            int sx = (int)floor(x * ifx);
+            if (sx > w_in - 1) sx = w_in - 1;
+            memcpy((char*)dst + ((size_t)y * w_out + x) * px, (const char*)src + ((size_t)sy * w_in + sx) * px, px);
+        }
+    }
+}
+
 /* fp32 bilinear, resize_naive.cpp:70-128; value summed lt,lb,rt,rb. */
 void oracle_resize_linear_f32(const float* src, int w_in, int h_in, int cc,
                               float* dst, int w_out, int h_out) {

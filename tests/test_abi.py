@@ -69,7 +69,7 @@ def test_argument_validation_without_device(lib):
     assert lib.vacv_resize(ctypes.byref(small_pitch), ctypes.byref(good), 1, 0, None) == -1
     dst = VacvImage(0x2000, 1, 4, 4, 3, 2, 1, 0, 0, 0)
     assert lib.vacv_crop(ctypes.byref(good), ctypes.byref(dst), 6, 0, None) == -1      # rect outside
-    assert lib.vacv_resize(ctypes.byref(good), ctypes.byref(dst), 0, 0, None) == -2    # INTER_NEAREST
+    assert lib.vacv_resize(ctypes.byref(good), ctypes.byref(dst), 3, 0, None) == -2    # INTER_AREA
     assert lib.vacv_resize(ctypes.byref(good), ctypes.byref(dst), 1, 7, None) == -1    # bad mode
     m = (ctypes.c_float * 6)(1, 0, 0, 0, 1, 0)
     assert lib.vacv_warp_affine(ctypes.byref(good), ctypes.byref(dst), m, 1, 1, None, None) == -2  # REPLICATE

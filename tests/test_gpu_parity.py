@@ -191,6 +191,38 @@ def test_resize_channel_sums(ops, dev, oracle):
     torch.cuda.empty_cache()
 
 
+def test_resize_nearest(ops, dev, oracle):
+    """INTER_NEAREST (OpenCV 2.4 resizeNN semantics, parity unpinned -- see
+    oracle/vacv_oracle.c): u8 and fp32, NHWC c = 1..4 and NCHW, down- and
+    upscales, same size (a copy), the normalize epilogue, a pitched source."""
+    import torch
+    from vacv_amd import INTER_NEAREST, NCHW
+    rng = np.random.default_rng(31)
+    for i, ((h, w), c) in enumerate(SIZES + [((1080, 1920), 3)]):
+        img = synthetic_image(600 + i, h, w, c)
+        img = img if c > 1 else img[..., None]
+        f = (img.astype(np.float32) + rng.standard_normal(img.shape).astype(np.float32)).astype(np.float32)
+        for wo, ho in OUTS + [(w, h), (640, 360), (3 * w, 2 * h)]:
+            sq = (lambda a: a) if c > 1 else (lambda a: a[..., 0])
+            got = host(ops.resize(to_dev(img[None], dev), wo, ho, interpolation=INTER_NEAREST))[0]
+            assert_same(sq(got), oracle.resize_nearest(sq(img), wo, ho), f"nearest u8 {h}x{w}x{c}->{ho}x{wo}")
+            gotf = host(ops.resize(to_dev(f[None], dev), wo, ho, interpolation=INTER_NEAREST))[0]
+            assert_same(sq(gotf), oracle.resize_nearest(sq(f), wo, ho), f"nearest f32 {h}x{w}x{c}->{ho}x{wo}")
+        chw = np.ascontiguousarray(img.transpose(2, 0, 1))
+        got = host(ops.resize(to_dev(chw[None], dev), 33, 21, interpolation=INTER_NEAREST, layout=NCHW))[0]
+        for k in range(c):
+            assert_same(got[k], oracle.resize_nearest(chw[k], 33, 21), "nearest chw")
+        if c == 3:
+            got = host(ops.resize_normalize(to_dev(img[None], dev), 50, 40, MEAN, STD, interpolation=INTER_NEAREST))[0]
+            want = oracle.normalize(oracle.u8_to_f32(oracle.resize_nearest(img, 50, 40)), MEAN, STD)
+            assert_same(got, want, "nearest normalize")
+    big = torch.zeros((1, 80, 90, 3), dtype=torch.uint8, device=dev)
+    img = synthetic_image(5, 61, 77, 3)
+    big[0, 7:68, 3:80] = to_dev(img, dev)
+    got = host(ops.resize(big[:, 7:68, 3:80], 30, 20, interpolation=INTER_NEAREST))[0]
+    assert_same(got, oracle.resize_nearest(img, 30, 20), "nearest pitched")
+
+
 def test_resize_full_size_batch(ops, dev, oracle):
     """BASELINE cfg2 at full size: 1920x1080 -> 640x360 / 1280x720, batch of 3,
     plus a pitched source (a sub-window of a wider buffer)."""
@@ -611,7 +643,7 @@ def test_error_statuses(ops, dev):
         ops.crop(x, (4, 4, 12, 12))           # rect outside the image
     assert e.value.status == V._lib.ERR_INVALID_ARG
     with pytest.raises(V.VacvError) as e:
-        ops.resize(x, 4, 4, interpolation=V.INTER_NEAREST)
+        ops.resize(x, 4, 4, interpolation=3)  # INTER_AREA
     assert e.value.status == V._lib.ERR_UNSUPPORTED
     with pytest.raises(V.VacvError) as e:
         ops.warp_affine(x, np.eye(2, 3, dtype=np.float32), 8, 8, border_mode=V.BORDER_REPLICATE)

@@ -163,3 +163,21 @@ def test_live_cross_check_random(oracle):
                       rng.uniform(-0.5, 0.5), rng.uniform(0.3, 2), rng.uniform(-20, 20)], np.float32)
         inv = oracle.invert_affine(m)
         assert np.array_equal(oracle.warp_affine(img, m, wo, ho), R.warp_affine_inv(img, inv, wo, ho))
+
+
+def test_resize_nearest_restatement(oracle):
+    """OpenCV 2.4 resizeNN as restated in oracle/vacv_oracle.c (parity
+    unpinned: no reference entry or fixture covers nearest): an integer
+    downscale picks every k-th pixel, same size is a copy, an upscale
+    repeats pixels, and indices never pass the last row/column."""
+    import numpy as np
+    from oracle import synthetic_image
+    img = synthetic_image(3, 30, 40, 3)
+    assert np.array_equal(oracle.resize_nearest(img, 20, 10), img[::3, ::2])
+    assert np.array_equal(oracle.resize_nearest(img, 40, 30), img)
+    up = oracle.resize_nearest(img, 80, 60)
+    assert np.array_equal(up[::2, ::2], img) and np.array_equal(up[1::2, 1::2], img)
+    odd = oracle.resize_nearest(img, 7, 11)
+    xs = [min(int(np.floor(x * (1.0 / (7 / 40)))), 39) for x in range(7)]
+    ys = [min(int(np.floor(y * (1.0 / (11 / 30)))), 29) for y in range(11)]
+    assert np.array_equal(odd, img[ys][:, xs])
