@@ -12,9 +12,10 @@
 // samples an LW x (64/LW) block of output pixels: LW = 64 (one row segment
 // per instruction) by default, 16 (16 x 4 blocks, a more compact rotated
 // footprint: measured no faster) via VACV_WARP_LW.  kPx = 8 lane blocks per
-// wave for byte output (VACV_WARP_PX overrides): more gathers in flight per
-// wave, and the per-workgroup setup spread over twice the pixels (0.30 ->
-// 0.28 ms at 720p rot15); 4 for fp32 output.  The tile is re-assembled in LDS and each wave writes one of its
+// wave for byte output (10 when that pads the output width less, e.g. 1280;
+// VACV_WARP_PX overrides): more gathers in flight per wave, and the
+// per-workgroup setup spread over twice the pixels (0.30 -> 0.28 -> 0.27 ms
+// at 720p rot15); 4 for fp32 output.  The tile is re-assembled in LDS and each wave writes one of its
 // rows with 16-byte stores.  Taps: one dword-aligned 8/12-byte buffer load per source row
 // (load_taps, vacv_device.hpp), packed
 // u16 dot products for the fixed-point sum.  Blocks are ordered so each XCD
@@ -206,13 +207,18 @@ int warp_lane_width() {
     const char* env = std::getenv("VACV_WARP_LW");
     return (env && std::atoi(env) == 16) ? 16 : 64;
 }
-// default: 8 for byte output (0.283 vs 0.304 ms at 720p rot15), 4 for fp32
+// default: 8 or 10 lane blocks per wave for byte output, whichever pads the
+// output width less (1280: 10 -> 2 tiles of 640 exactly, 0.271 ms, vs 8 ->
+// 2.5 tiles, 0.281 ms at 720p rot15; 8 vs 4: 0.283 vs 0.304), 4 for fp32
 // output (0.538 vs 0.614 ms: 8 blocks double the LDS row buffers and halve
-// the resident workgroups)
-int warp_blocks_per_wave(bool byte_out) {
+// the resident workgroups).  VACV_WARP_PX = 4, 5, 8 or 10 overrides.
+int warp_blocks_per_wave(bool byte_out, int w) {
     const char* env = std::getenv("VACV_WARP_PX");
-    if (env && (std::atoi(env) == 4 || std::atoi(env) == 8)) return std::atoi(env);
-    return byte_out ? 8 : 4;
+    if (env && (std::atoi(env) == 4 || std::atoi(env) == 5 || std::atoi(env) == 8 || std::atoi(env) == 10))
+        return std::atoi(env);
+    if (!byte_out) return 4;
+    const auto pad = [w](int k) { return (w + 64 * k - 1) / (64 * k) * (64 * k) - w; };
+    return pad(10) < pad(8) ? 10 : 8;
 }
 
 template <int CC, typename TIn, int OUT, int LW, int kPx>
@@ -228,9 +234,13 @@ hipError_t launch_px(const WarpLaunch& L, hipStream_t s) {
 
 template <int CC, typename TIn, int OUT>
 hipError_t launch_one(const WarpLaunch& L, hipStream_t s) {
-    const bool wide = warp_blocks_per_wave(OUT == kOutSame && sizeof(TIn) == 1) == 8;
-    if (warp_lane_width() == 64)
+    const int bpw = warp_blocks_per_wave(OUT == kOutSame && sizeof(TIn) == 1, L.dst.w);
+    const bool wide = bpw >= 8;
+    if (warp_lane_width() == 64) {
+        if (bpw == 10) return launch_px<CC, TIn, OUT, 64, 10>(L, s);
+        if (bpw == 5) return launch_px<CC, TIn, OUT, 64, 5>(L, s);
         return wide ? launch_px<CC, TIn, OUT, 64, 8>(L, s) : launch_px<CC, TIn, OUT, 64, 4>(L, s);
+    }
     return wide ? launch_px<CC, TIn, OUT, 16, 8>(L, s) : launch_px<CC, TIn, OUT, 16, 4>(L, s);
 }
 
