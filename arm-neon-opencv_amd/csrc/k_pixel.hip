@@ -666,11 +666,81 @@ hipError_t launch_nearest_t(const ResizeLaunch& L, hipStream_t s) {
     return hipGetLastError();
 }
 
+// --------------------------------------------------------------------------
+// INTER_AREA at an integer scale (cv::resize -> resizeAreaFast_ of the pinned
+// OpenCV 2.4, the other mode the reference hands to OpenCV, resize.cpp:44-49;
+// the reference's own area attempt, src_deprecated/img_resize_inter_area.cpp,
+// stops after building the same ofs/xofs tables).  Output pixel (x, y) is the
+// mean of the area_x * area_y block at (x * area_x, y * area_y), summed in
+// OpenCV's order (block rows, then columns; four taps grouped per add as its
+// CV_ENABLE_UNROLLED loop does, which only matters for fp32) and scaled by
+// the fp32 1/area; u8 rounds half to even (saturate_cast = lrint on the ARM
+// build).  One thread per output pixel; a wave reads 64 * area_x * cc
+// contiguous elements per block row.
+template <typename TIn, int OUT>
+__global__ void __launch_bounds__(kBlock) area_fast_kernel(ResizeLaunch L) {
+    using TOut = typename std::conditional<(OUT == kOutSame), TIn, float>::type;
+    using TSum = typename std::conditional<std::is_same<TIn, uint8_t>::value, int, float>::type;
+    const int x = blockIdx.x * kBlock + threadIdx.x;
+    const int y = blockIdx.y;
+    const int pidx = blockIdx.z;
+    if (x >= L.dst.w) return;
+    const int img = pidx / L.src.planes;
+    const int plane = pidx - img * L.src.planes;
+    const int cc = L.src.cc, ax = L.area_x, ay = L.area_y, area = ax * ay;
+    const unsigned char* row0 = L.src.base + (int64_t)img * L.src.img_pitch + (int64_t)plane * L.src.plane_pitch +
+                                (int64_t)y * ay * L.src.row_pitch;
+    TOut* dp = reinterpret_cast<TOut*>(const_cast<unsigned char*>(L.dst.base) + (int64_t)img * L.dst.img_pitch +
+                                       (int64_t)plane * L.dst.plane_pitch + (int64_t)y * L.dst.row_pitch) +
+               (int64_t)x * cc;
+    for (int k = 0; k < cc; ++k) {
+        // tap t of the block: row t / ax, column t % ax (OpenCV's ofs table)
+        auto tap = [&](int t) -> TSum {
+            const int r = t / ax, col = t - r * ax;
+            const TIn* sp = reinterpret_cast<const TIn*>(row0 + (int64_t)r * L.src.row_pitch);
+            return (TSum)sp[((int64_t)x * ax + col) * cc + k];
+        };
+        TSum sum = 0;
+        int t = 0;
+        for (; t <= area - 4; t += 4) sum = sum + (((tap(t) + tap(t + 1)) + tap(t + 2)) + tap(t + 3));
+        for (; t < area; ++t) sum = sum + tap(t);
+        const float m = __fmul_rn((float)sum, L.area_scale);
+        TIn v;
+        if (std::is_same<TIn, uint8_t>::value) v = (TIn)(int)rintf(m);
+        else v = (TIn)m;
+        if (OUT == kOutSame) {
+            dp[k] = (TOut)v;
+        } else if (OUT == kOutF32) {
+            dp[k] = (TOut)(float)v;
+        } else {
+            const ChanNorm cn = chan_norm(L.norm, img, cc == 1 ? plane % L.norm.c_total : k);
+            dp[k] = (TOut)(std::is_same<TIn, uint8_t>::value ? normalize_u8v(cn, (int)v) : normalize_f(cn, (float)v));
+        }
+    }
+}
+
+template <typename TIn>
+hipError_t launch_area_t(const ResizeLaunch& L, hipStream_t s) {
+    const dim3 grid((L.dst.w + kBlock - 1) / kBlock, L.dst.h, L.n * L.src.planes);
+    if (L.out == kOutSame) hipLaunchKernelGGL((area_fast_kernel<TIn, kOutSame>), grid, dim3(kBlock), 0, s, L);
+    else if (L.out == kOutF32) hipLaunchKernelGGL((area_fast_kernel<TIn, kOutF32>), grid, dim3(kBlock), 0, s, L);
+    else hipLaunchKernelGGL((area_fast_kernel<TIn, kOutNorm>), grid, dim3(kBlock), 0, s, L);
+    return hipGetLastError();
+}
+
 }  // namespace
 
 hipError_t launch_resize_nearest(const ResizeLaunch& L, hipStream_t s) {
     if (L.dst.h > 65535 || (int64_t)L.n * L.src.planes > 65535) return hipErrorInvalidValue;
     return L.src.esize == 1 ? launch_nearest_t<uint8_t>(L, s) : launch_nearest_t<float>(L, s);
+}
+
+hipError_t launch_resize_area(const ResizeLaunch& L, hipStream_t s) {
+    if (L.dst.h > 65535 || (int64_t)L.n * L.src.planes > 65535) return hipErrorInvalidValue;
+    if (L.area_x < 1 || L.area_y < 1 || (int64_t)L.dst.w * L.area_x != L.src.w ||
+        (int64_t)L.dst.h * L.area_y != L.src.h)
+        return hipErrorInvalidValue;  // the kernel reads exactly the source extent
+    return L.src.esize == 1 ? launch_area_t<uint8_t>(L, s) : launch_area_t<float>(L, s);
 }
 
 namespace {

@@ -10,6 +10,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cfloat>
 #include <cmath>
 #include <cstdint>
 #include <cstdlib>
@@ -271,6 +272,26 @@ int resize_impl(const vacv_image* src_d, const vacv_image* dst_d, int interpolat
         L.scale_xd = 1. / ((double)dst.w / src.w);  // ifx, as cv::resize computes it
         L.scale_yd = 1. / ((double)dst.h / src.h);
         return hip_status(launch_resize_nearest(L, s));
+    } else if (interpolation == VACV_INTER_AREA) {
+        // resize.cpp:44-49 hands it to cv::resize; OpenCV 2.4 takes
+        // resizeAreaFast_ when both scales are integers to within DBL_EPSILON
+        // (imgwarp.cpp: scale = 1 / ((double)dsize / ssize), is_area_fast).
+        // Fractional downscales (its resizeArea tables) and upscales (its
+        // bilinear fallback) are not built here.
+        if (src.dtype != VACV_INT8 && src.dtype != VACV_FP32) return VACV_ERR_UNSUPPORTED;
+        L.out = out_kind;
+        if (src.dtype == VACV_FP32 && L.out == kOutF32) L.out = kOutSame;
+        const int want = L.out == kOutSame ? src.dtype : VACV_FP32;
+        if (dst.dtype != want) return VACV_ERR_INVALID_ARG;
+        const double sx = 1. / ((double)dst.w / src.w), sy = 1. / ((double)dst.h / src.h);
+        const double ix = std::nearbyint(sx), iy = std::nearbyint(sy);
+        if (ix < 1 || iy < 1 || std::fabs(sx - ix) >= DBL_EPSILON || std::fabs(sy - iy) >= DBL_EPSILON)
+            return VACV_ERR_UNSUPPORTED;
+        L.area_x = (int)ix;
+        L.area_y = (int)iy;
+        if ((int64_t)dst.w * L.area_x != src.w || (int64_t)dst.h * L.area_y != src.h) return VACV_ERR_UNSUPPORTED;
+        L.area_scale = 1.f / (float)(L.area_x * L.area_y);
+        return hip_status(launch_resize_area(L, s));
     } else {
         return VACV_ERR_UNSUPPORTED;  // resize.cpp:46-49 recurses forever for other modes
     }

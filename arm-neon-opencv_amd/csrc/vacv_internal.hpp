@@ -95,6 +95,8 @@ struct ResizeLaunch {
     int tasks_per_strip;         // row tiles per workgroup (software-pipelined)
     int rows_mode;               // 1: resize_rows_kernel (whole output rows, one tile per workgroup)
     int interleave;              // resize_kernel: 1 = tasks grid-stride in address order, 0 = strips
+    int area_x, area_y;          // INTER_AREA integer block (launch_resize_area)
+    float area_scale;            // INTER_AREA: 1.f / (area_x * area_y)
     ResizePlanDev plan;
     NormSpec norm;
 };
@@ -113,6 +115,8 @@ hipError_t launch_resize_direct(const ResizeLaunch& L, hipStream_t s);
 bool resize_one_tap_rows(const ResizeLaunch& L);
 // INTER_NEAREST (OpenCV 2.4 resizeNN): scale_xd / scale_yd carry ifx / ify
 hipError_t launch_resize_nearest(const ResizeLaunch& L, hipStream_t s);
+// INTER_AREA at an integer scale (OpenCV 2.4 resizeAreaFast_): area_x/y, area_scale
+hipError_t launch_resize_area(const ResizeLaunch& L, hipStream_t s);
 // u8 -> fp32 cubic as per-pixel gathers (k_cubic_direct.hip); needs no plan
 bool cubic_direct_applies(const ResizeLaunch& L);
 hipError_t launch_cubic_direct(const ResizeLaunch& L, hipStream_t s);

@@ -67,9 +67,15 @@ DType resize_out_dtype(const char* fn, const Tensor& src, int interpolation) {
         if (src.dtype != INT8 && src.dtype != FP32) fail(fn, "INTER_NEAREST takes INT8 or FP32");
         return src.dtype;
     }
+    if (interpolation == INTER_AREA) {
+        // resize.cpp:46-49 hands it to cv::resize; OpenCV 2.4's resizeAreaFast_
+        // (integer downscales; the C ABI rejects other scales)
+        if (src.dtype != INT8 && src.dtype != FP32) fail(fn, "INTER_AREA takes INT8 or FP32");
+        return src.dtype;
+    }
     // every other mode goes to OpenCV in the reference, which this build
     // does not ship (the reference without OpenCV recurses forever)
-    fail(fn, "only INTER_NEAREST, INTER_LINEAR and INTER_CUBIC are supported");
+    fail(fn, "only INTER_NEAREST, INTER_LINEAR, INTER_CUBIC and INTER_AREA are supported");
 }
 
 std::vector<float> affine_of(const char* fn, const Tensor& M) { return host_floats(fn, M, 6); }

@@ -6,7 +6,7 @@ compute happens in lib/libvacv_hip.so (hand-written gfx950 kernels).
 """
 from . import _lib
 from ._lib import (BORDER_CONSTANT, BORDER_REPLICATE, COLOR_YUV2BGR_NV12, COLOR_YUV2BGR_NV21, COLOR_YUV2RGB_NV12, COLOR_YUV2RGB_NV21,
-                   FP16, FP32, FP64, INT8, INTER_CUBIC, INTER_LINEAR, INTER_NEAREST, LINEAR_NEON, LINEAR_OPENCV,
+                   FP16, FP32, FP64, INT8, INTER_AREA, INTER_CUBIC, INTER_LINEAR, INTER_NEAREST, LINEAR_NEON, LINEAR_OPENCV,
                    LINEAR_REFERENCE, NCHW, NHWC, VacvError, build)
 
 __all__ = ["ops", "dist", "build", "VacvError"]

@@ -48,7 +48,7 @@ enum { VACV_FP32 = 0, VACV_FP16 = 1, VACV_INT8 = 2 /* unsigned bytes */, VACV_FP
 /* vision::DLayout (tensor.h:21-24) */
 enum { VACV_NCHW = 0, VACV_NHWC = 1 };
 /* va_cv::VInterMode (cv.h:27-35) */
-enum { VACV_INTER_NEAREST = 0, VACV_INTER_LINEAR = 1, VACV_INTER_CUBIC = 2 };
+enum { VACV_INTER_NEAREST = 0, VACV_INTER_LINEAR = 1, VACV_INTER_CUBIC = 2, VACV_INTER_AREA = 3 };
 /* va_cv::VBorderMode (cv.h:38-48) */
 enum { VACV_BORDER_CONSTANT = 0, VACV_BORDER_REPLICATE = 1 };
 /* va_cv::InputImageFormat (cv.h:62-74) */
@@ -113,6 +113,10 @@ int vacv_change_dtype(const vacv_image* src, const vacv_image* dst, void* stream
  *  INTER_NEAREST: INT8->INT8, FP32->FP32 with OpenCV 2.4's resizeNN
  *                semantics, which the reference delegates to cv::resize
  *                (resize.cpp:44-49): sx = min(floor(x / (w_out / w_in)), w_in - 1).
+ *  INTER_AREA:   INT8->INT8, FP32->FP32 at integer downscales only (OpenCV
+ *                2.4's resizeAreaFast_, also behind resize.cpp:44-49): the mean
+ *                of each (w_in/w_out) x (h_in/h_out) block, u8 rounded half to
+ *                even.  Other scales: VACV_ERR_UNSUPPORTED.
  * NHWC channels 1..4; NCHW any c (per plane, as resize.cpp:72-88). */
 int vacv_resize(const vacv_image* src, const vacv_image* dst, int interpolation, int mode, void* stream);
 

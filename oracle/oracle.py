@@ -74,6 +74,7 @@ class Oracle:
             ("oracle_resize_linear_f32", [_P, _I, _I, _I, _P, _I, _I], None),
             ("oracle_resize_cubic_f32", [_P, _I, _I, _I, _P, _I, _I], None),
             ("oracle_resize_nearest", [_P, _I, _I, _I, _I, _P, _I, _I], None),
+            ("oracle_resize_area", [_P, _I, _I, _I, _I, _P, _I, _I], None),
             ("oracle_warp_affine_u8", [_P, _I, _I, _I, _P, _I, _I, _P], None),
             ("oracle_warp_affine_f32", [_P, _I, _I, _I, _P, _I, _I, _P], None),
             ("oracle_yuv420sp_to_bgr", [_P, _P, _I, _I, _I, _I], None),
@@ -139,6 +140,16 @@ class Oracle:
         w, h, c = _shape(img)
         out = _out(h_out, w_out, c, img.dtype)
         self.lib.oracle_resize_nearest(_ptr(img), w, h, c, img.dtype.itemsize, _ptr(out), w_out, h_out)
+        return out
+
+    def resize_area(self, img, w_out, h_out):
+        """OpenCV 2.4 resizeAreaFast_ restated (integer downscales only;
+        parity unpinned, vacv_oracle.c)."""
+        img = np.ascontiguousarray(img)
+        w, h, c = _shape(img)
+        assert w % w_out == 0 and h % h_out == 0, "integer downscales only"
+        out = _out(h_out, w_out, c, img.dtype)
+        self.lib.oracle_resize_area(_ptr(img), w, h, c, img.dtype.itemsize, _ptr(out), w_out, h_out)
         return out
 
     def resize_cubic(self, img, w_out, h_out):

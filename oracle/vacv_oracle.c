@@ -218,6 +218,55 @@ void oracle_resize_nearest(const void* src, int w_in, int h_in, int cc, int esiz
     }
 }
 
+/* INTER_AREA at an integer downscale.  Like nearest, the reference hands it
+ * to cv::resize (resize.cpp:44-49); its own attempt,
+ * src_deprecated/img_resize_inter_area.cpp:21-55, builds OpenCV's ofs/xofs
+ * tables and stops.  OpenCV 2.4.13.4's published algorithm (imgwarp.cpp,
+ * resizeAreaFast_ without a vector op, as on the ARM build), restated: with
+ * ax = w_in / w_out, ay = h_in / h_out exact integers, output (x, y, k) is
+ *   sum over the block rows r, columns q (taps grouped 4 per add as its
+ *   CV_ENABLE_UNROLLED loop) of src(x*ax + q, y*ay + r, k), times 1.f/(ax*ay)
+ *   in fp32; u8 rounds half to even (saturate_cast<uchar> = lrint).
+ * PARITY UNPINNED: no reference entry runs this path here and its tests hold
+ * no area output.  esize 1 (u8, int sum) or 4 (fp32, float sum). */
+void oracle_resize_area(const void* src, int w_in, int h_in, int cc, int esize,
+                        void* dst, int w_out, int h_out) {
+    const int ax = w_in / w_out, ay = h_in / h_out, area = ax * ay;
+    const float scale = 1.f / (float)area;
+    for (int y = 0; y < h_out; ++y)
+        for (int x = 0; x < w_out; ++x)
+            for (int k = 0; k < cc; ++k) {
+                int isum = 0;
+                float fsum = 0.f;
+                int t = 0;
+                for (; t <= area - 4; t += 4) {
+                    int iv[4];
+                    float fv[4];
+                    for (int j = 0; j < 4; ++j) {
+                        const int r = (t + j) / ax, q = (t + j) % ax;
+                        const size_t i = ((size_t)(y * ay + r) * w_in + (size_t)x * ax + q) * cc + k;
+                        if (esize == 1) iv[j] = ((const uint8_t*)src)[i];
+                        else fv[j] = ((const float*)src)[i];
+                    }
+                    if (esize == 1) isum += iv[0] + iv[1] + iv[2] + iv[3];
+                    else fsum += ((fv[0] + fv[1]) + fv[2]) + fv[3];
+                }
+                for (; t < area; ++t) {
+                    const int r = t / ax, q = t % ax;
+                    const size_t i = ((size_t)(y * ay + r) * w_in + (size_t)x * ax + q) * cc + k;
+                    if (esize == 1) isum += ((const uint8_t*)src)[i];
+                    else fsum += ((const float*)src)[i];
+                }
+                const size_t o = ((size_t)y * w_out + x) * cc + k;
+                if (esize == 1) {
+                    const float m = (float)isum * scale;
+                    ((uint8_t*)dst)[o] = (uint8_t)lrintf(m);
+                } else {
+                    ((float*)dst)[o] = fsum * scale;
+                }
+            }
+}
+
 /* fp32 bilinear, resize_naive.cpp:70-128; value summed lt,lb,rt,rb. */
 void oracle_resize_linear_f32(const float* src, int w_in, int h_in, int cc,
                               float* dst, int w_out, int h_out) {

@@ -40,6 +40,8 @@ void oracle_resize_linear_f32(const float* src, int w_in, int h_in, int cc,
                               float* dst, int w_out, int h_out);
 void oracle_resize_nearest(const void* src, int w_in, int h_in, int cc, int esize,
                            void* dst, int w_out, int h_out);
+void oracle_resize_area(const void* src, int w_in, int h_in, int cc, int esize,
+                        void* dst, int w_out, int h_out);
 void oracle_resize_cubic_f32(const float* src, int w_in, int h_in, int cc,
                              float* dst, int w_out, int h_out);
 void oracle_warp_affine_u8(const uint8_t* src, int w_in, int h_in, int cc,

@@ -528,9 +528,24 @@ Result tensor_semantics_case() {
     // unsupported combinations fail loudly
     try {
         Tensor o;
-        va_cv::resize(img, o, VSize(10, 10), 0, 0, INTER_AREA);
-        err += "INTER_AREA did not throw; ";
+        va_cv::resize(img, o, VSize(7, 7), 0, 0, INTER_AREA);
+        err += "fractional INTER_AREA did not throw; ";
     } catch (const std::runtime_error&) {
+    }
+    {
+        // integer INTER_AREA (OpenCV 2.4 resizeAreaFast_): 2x2 block means
+        Tensor o;
+        va_cv::resize(img, o, VSize(160, 90), 0, 0, INTER_AREA);
+        const uint8_t* s = static_cast<const uint8_t*>(img.data);
+        const uint8_t* d = static_cast<const uint8_t*>(o.data);
+        for (int y = 0; y < 90; y += 7)
+            for (int x = 0; x < 160; x += 5)
+                for (int k = 0; k < 3; ++k) {
+                    const int sum = s[((2 * y) * 320 + 2 * x) * 3 + k] + s[((2 * y) * 320 + 2 * x + 1) * 3 + k] +
+                                    s[((2 * y + 1) * 320 + 2 * x) * 3 + k] + s[((2 * y + 1) * 320 + 2 * x + 1) * 3 + k];
+                    const int want_v = (int)std::nearbyint((float)sum * 0.25f);  // half to even
+                    if (d[(y * 160 + x) * 3 + k] != want_v) { err += "INTER_AREA value; "; y = 90; x = 160; break; }
+                }
     }
     try {
         Tensor o;

@@ -223,6 +223,45 @@ def test_resize_nearest(ops, dev, oracle):
     assert_same(got, oracle.resize_nearest(img, 30, 20), "nearest pitched")
 
 
+def test_resize_area(ops, dev, oracle):
+    """INTER_AREA at integer downscales (OpenCV 2.4 resizeAreaFast_, parity
+    unpinned -- see oracle/vacv_oracle.c): u8 (half-to-even rounding) and fp32
+    (OpenCV's four-tap summation order, bit-exact), NHWC c = 1..4 and NCHW,
+    block sizes 1x1 .. 7x5 incl. areas that are not a multiple of 4, the
+    widen / normalize epilogues, a pitched source, and BASELINE's 1080p frame
+    at 1/2 and 1/3."""
+    import torch
+    from vacv_amd import INTER_AREA, NCHW
+    rng = np.random.default_rng(37)
+    for i, ((h, w), c) in enumerate([((60, 84), 1), ((60, 84), 2), ((60, 84), 3), ((60, 84), 4),
+                                     ((1080, 1920), 3)]):
+        img = synthetic_image(700 + i, h, w, c)
+        img = img if c > 1 else img[..., None]
+        f = (img.astype(np.float32) + rng.standard_normal(img.shape).astype(np.float32)).astype(np.float32)
+        sq = (lambda a: a) if c > 1 else (lambda a: a[..., 0])
+        blocks = [(2, 2), (3, 3)] if h == 1080 else [(1, 1), (2, 2), (3, 2), (4, 4), (7, 5), (6, 3), (12, 1)]
+        for ax, ay in blocks:
+            wo, ho = w // ax, h // ay
+            got = host(ops.resize(to_dev(img[None], dev), wo, ho, interpolation=INTER_AREA))[0]
+            assert_same(sq(got), oracle.resize_area(sq(img), wo, ho), f"area u8 {h}x{w}x{c}/{ax}x{ay}")
+            gotf = host(ops.resize(to_dev(f[None], dev), wo, ho, interpolation=INTER_AREA))[0]
+            assert_same(sq(gotf), oracle.resize_area(sq(f), wo, ho), f"area f32 {h}x{w}x{c}/{ax}x{ay}")
+        if c == 3:
+            chw = np.ascontiguousarray(img.transpose(2, 0, 1))
+            got = host(ops.resize(to_dev(chw[None], dev), w // 3, h // 2, interpolation=INTER_AREA, layout=NCHW))[0]
+            for k in range(c):
+                assert_same(got[k], oracle.resize_area(chw[k], w // 3, h // 2), "area chw")
+            got = host(ops.resize_normalize(to_dev(img[None], dev), w // 2, h // 2, MEAN, STD,
+                                            interpolation=INTER_AREA))[0]
+            want = oracle.normalize(oracle.u8_to_f32(oracle.resize_area(img, w // 2, h // 2)), MEAN, STD)
+            assert_same(got, want, "area normalize")
+    big = torch.zeros((1, 80, 90, 3), dtype=torch.uint8, device=dev)
+    img = synthetic_image(6, 60, 78, 3)
+    big[0, 7:67, 3:81] = to_dev(img, dev)
+    got = host(ops.resize(big[:, 7:67, 3:81], 26, 20, interpolation=INTER_AREA))[0]
+    assert_same(got, oracle.resize_area(img, 26, 20), "area pitched")
+
+
 def test_resize_full_size_batch(ops, dev, oracle):
     """BASELINE cfg2 at full size: 1920x1080 -> 640x360 / 1280x720, batch of 3,
     plus a pitched source (a sub-window of a wider buffer)."""
@@ -643,8 +682,12 @@ def test_error_statuses(ops, dev):
         ops.crop(x, (4, 4, 12, 12))           # rect outside the image
     assert e.value.status == V._lib.ERR_INVALID_ARG
     with pytest.raises(V.VacvError) as e:
-        ops.resize(x, 4, 4, interpolation=3)  # INTER_AREA
+        ops.resize(x, 4, 4, interpolation=4)  # INTER_LANCZOS4
     assert e.value.status == V._lib.ERR_UNSUPPORTED
+    for wo, ho in [(3, 3), (16, 16), (4, 3)]:  # INTER_AREA: fractional scales, upscales
+        with pytest.raises(V.VacvError) as e:
+            ops.resize(x, wo, ho, interpolation=V.INTER_AREA)
+        assert e.value.status == V._lib.ERR_UNSUPPORTED
     with pytest.raises(V.VacvError) as e:
         ops.warp_affine(x, np.eye(2, 3, dtype=np.float32), 8, 8, border_mode=V.BORDER_REPLICATE)
     assert e.value.status == V._lib.ERR_UNSUPPORTED

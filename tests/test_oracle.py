@@ -181,3 +181,24 @@ def test_resize_nearest_restatement(oracle):
     xs = [min(int(np.floor(x * (1.0 / (7 / 40)))), 39) for x in range(7)]
     ys = [min(int(np.floor(y * (1.0 / (11 / 30)))), 29) for y in range(11)]
     assert np.array_equal(odd, img[ys][:, xs])
+
+
+def test_resize_area_restatement(oracle):
+    """OpenCV 2.4 resizeAreaFast_ as restated in oracle/vacv_oracle.c (parity
+    unpinned), against an independent numpy statement: u8 = rint_half_even(
+    fp32(block sum) * fp32(1/area)); fp32 = the block mean with OpenCV's
+    grouping (exact here: small-integer fp32 inputs sum exactly)."""
+    import numpy as np
+    from oracle import synthetic_image
+    img = synthetic_image(4, 30, 42, 3)
+    for ax, ay in [(1, 1), (2, 2), (3, 2), (6, 5), (7, 3)]:
+        wo, ho = 42 // ax, 30 // ay
+        blk = img.reshape(ho, ay, wo, ax, 3).astype(np.int64).sum(axis=(1, 3))
+        want = np.rint(blk.astype(np.float32) * np.float32(1.0 / (ax * ay))).astype(np.uint8)
+        assert np.array_equal(oracle.resize_area(img, wo, ho), want), (ax, ay)
+        f = img.astype(np.float32)
+        wantf = blk.astype(np.float32) * np.float32(np.float32(1) / np.float32(ax * ay))
+        assert np.array_equal(oracle.resize_area(f, wo, ho), wantf), (ax, ay)
+    # ties round to even: a 2x1 block of (1, 2) averages 1.5 -> 2, (2, 3) -> 2
+    tie = np.array([[[1], [2], [2], [3]]], np.uint8).reshape(1, 4)
+    assert oracle.resize_area(tie, 2, 1).tolist() == [[2, 2]]

@@ -51,6 +51,22 @@ def main():
                                             n * resize_bytes(1920, 1080, 3, 640, 360, 1, 1), n * 1920 * 1080)
         cases["resize_1080p_1280x720_u8"] = (lambda src=src, o2=o2: ops.resize(src, 1280, 720, out=o2),
                                              n * resize_bytes(1920, 1080, 3, 1280, 720, 1, 1), n * 1920 * 1080)
+    if a.op in ("resize_other", "all"):
+        # INTER_NEAREST / INTER_AREA (OpenCV-delegated modes): read the frame, write the output
+        n = a.batch or 256
+        src = frames(n, 1080, 1920)
+        o3 = torch.empty((n, 360, 640, 3), dtype=torch.uint8, device=dev)
+        o2 = torch.empty((n, 540, 960, 3), dtype=torch.uint8, device=dev)
+        cases["area_1080p_640x360_u8"] = (
+            lambda src=src, o=o3: ops.resize(src, 640, 360, interpolation=vacv_amd.INTER_AREA, out=o),
+            n * (1920 * 1080 * 3 + 640 * 360 * 3), n * 1920 * 1080)
+        cases["area_1080p_960x540_u8"] = (
+            lambda src=src, o=o2: ops.resize(src, 960, 540, interpolation=vacv_amd.INTER_AREA, out=o),
+            n * (1920 * 1080 * 3 + 960 * 540 * 3), n * 1920 * 1080)
+        # nearest reads one pixel in (1920/640)^2 = 9 (whole 64 B lines of them, all of 1 in 3 rows)
+        cases["nearest_1080p_640x360_u8"] = (
+            lambda src=src, o=o3: ops.resize(src, 640, 360, interpolation=vacv_amd.INTER_NEAREST, out=o),
+            n * (360 * 1920 * 3 + 640 * 360 * 3), n * 1920 * 1080)
     if a.op in ("warp", "all"):
         n = a.batch or 128
         src = frames(n, 720, 1280)
