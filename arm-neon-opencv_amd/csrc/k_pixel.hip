@@ -719,6 +719,84 @@ __global__ void __launch_bounds__(kBlock) area_fast_kernel(ResizeLaunch L) {
     }
 }
 
+// u8 INTER_AREA by column sums.  An integer sum does not depend on its order,
+// so a workgroup takes one output row segment of TW pixels: its threads read
+// the ay source rows of the segment as coalesced dwords (a wave reads 256 B per
+// instruction), sum each byte column over the ay rows in registers, and park
+// the column sums in LDS; then one thread per output element adds its ax
+// column sums, rounds and stores (adjacent bytes per lane).  Needs a dword
+// aligned source (checked on the host); bit-identical to area_fast_kernel.
+constexpr int kAreaSeg = 4096;  // source bytes per segment row (16 KiB of LDS sums)
+template <int OUT>
+__global__ void __launch_bounds__(kBlock) area_u8_colsum_kernel(ResizeLaunch L, int tw) {
+    using TOut = typename std::conditional<(OUT == kOutSame), uint8_t, float>::type;
+    __shared__ int colsum[kAreaSeg];
+    const int y = blockIdx.y;
+    const int pidx = blockIdx.z;
+    const int img = pidx / L.src.planes;
+    const int plane = pidx - img * L.src.planes;
+    const int cc = L.src.cc, ax = L.area_x, ay = L.area_y;
+    const int x0 = blockIdx.x * tw;
+    const int pw = min(tw, L.dst.w - x0);          // output pixels in this segment
+    const int seg = pw * ax * cc;                  // source bytes per row in this segment
+    const int row_bytes = L.src.w * cc;
+    const int b0 = x0 * ax * cc;                   // multiple of 4 (tw % 4 == 0)
+    const unsigned char* row0 = L.src.base + (int64_t)img * L.src.img_pitch + (int64_t)plane * L.src.plane_pitch +
+                                (int64_t)y * ay * L.src.row_pitch + b0;
+    for (int j = threadIdx.x; j * 4 < seg; j += kBlock) {
+        int s0 = 0, s1 = 0, s2 = 0, s3 = 0;
+        if (b0 + j * 4 + 4 <= row_bytes) {
+            for (int r = 0; r < ay; ++r) {
+                const uint32_t v = *reinterpret_cast<const uint32_t*>(row0 + (int64_t)r * L.src.row_pitch + j * 4);
+                s0 += v & 0xff;
+                s1 += (v >> 8) & 0xff;
+                s2 += (v >> 16) & 0xff;
+                s3 += v >> 24;
+            }
+        } else {  // the row's last partial dword
+            for (int r = 0; r < ay; ++r) {
+                const unsigned char* p = row0 + (int64_t)r * L.src.row_pitch + j * 4;
+                const int lim = row_bytes - (b0 + j * 4);
+                s0 += p[0];
+                if (lim > 1) s1 += p[1];
+                if (lim > 2) s2 += p[2];
+            }
+        }
+        *reinterpret_cast<int4*>(&colsum[j * 4]) = make_int4(s0, s1, s2, s3);
+    }
+    __syncthreads();
+    TOut* dp = reinterpret_cast<TOut*>(const_cast<unsigned char*>(L.dst.base) + (int64_t)img * L.dst.img_pitch +
+                                       (int64_t)plane * L.dst.plane_pitch + (int64_t)y * L.dst.row_pitch) +
+               (int64_t)x0 * cc;
+    for (int e = threadIdx.x; e < pw * cc; e += kBlock) {
+        const int xl = e / cc, k = e - xl * cc;
+        const int* cs = colsum + xl * ax * cc + k;
+        int sum = 0;
+        for (int q = 0; q < ax; ++q) sum += cs[q * cc];
+        const uint8_t v = (uint8_t)(int)rintf(__fmul_rn((float)sum, L.area_scale));
+        if (OUT == kOutSame) {
+            dp[e] = v;
+        } else if (OUT == kOutF32) {
+            dp[e] = (float)v;
+        } else {
+            const ChanNorm cn = chan_norm(L.norm, img, cc == 1 ? plane % L.norm.c_total : k);
+            dp[e] = normalize_u8v(cn, (int)v);
+        }
+    }
+}
+
+hipError_t launch_area_u8_colsum(const ResizeLaunch& L, hipStream_t s) {
+    const int per_px = L.area_x * L.src.cc;
+    const int tw_max = (kAreaSeg / per_px) & ~3;
+    const int nblk = (L.dst.w + tw_max - 1) / tw_max;
+    const int tw = ((L.dst.w + nblk - 1) / nblk + 3) & ~3;  // even segments, x0 * per_px stays dword aligned
+    const dim3 grid(nblk, L.dst.h, L.n * L.src.planes);
+    if (L.out == kOutSame) hipLaunchKernelGGL((area_u8_colsum_kernel<kOutSame>), grid, dim3(kBlock), 0, s, L, tw);
+    else if (L.out == kOutF32) hipLaunchKernelGGL((area_u8_colsum_kernel<kOutF32>), grid, dim3(kBlock), 0, s, L, tw);
+    else hipLaunchKernelGGL((area_u8_colsum_kernel<kOutNorm>), grid, dim3(kBlock), 0, s, L, tw);
+    return hipGetLastError();
+}
+
 template <typename TIn>
 hipError_t launch_area_t(const ResizeLaunch& L, hipStream_t s) {
     const dim3 grid((L.dst.w + kBlock - 1) / kBlock, L.dst.h, L.n * L.src.planes);
@@ -740,7 +818,14 @@ hipError_t launch_resize_area(const ResizeLaunch& L, hipStream_t s) {
     if (L.area_x < 1 || L.area_y < 1 || (int64_t)L.dst.w * L.area_x != L.src.w ||
         (int64_t)L.dst.h * L.area_y != L.src.h)
         return hipErrorInvalidValue;  // the kernel reads exactly the source extent
-    return L.src.esize == 1 ? launch_area_t<uint8_t>(L, s) : launch_area_t<float>(L, s);
+    if (L.src.esize == 1) {
+        const bool aligned = ((reinterpret_cast<uintptr_t>(L.src.base) | (uintptr_t)L.src.img_pitch |
+                               (uintptr_t)L.src.plane_pitch | (uintptr_t)L.src.row_pitch) & 3) == 0;
+        if (aligned && L.area_x * L.src.cc <= 1024 && !std::getenv("VACV_AREA_PER_PIXEL"))
+            return launch_area_u8_colsum(L, s);
+        return launch_area_t<uint8_t>(L, s);
+    }
+    return launch_area_t<float>(L, s);
 }
 
 namespace {
