@@ -5,6 +5,7 @@
 #pragma clang fp contract(off)
 
 #include <cstdlib>
+#include <cstring>
 
 #include "vacv_device.hpp"
 
@@ -727,9 +728,10 @@ __global__ void __launch_bounds__(kBlock) area_fast_kernel(ResizeLaunch L) {
 // column sums, rounds and stores (adjacent bytes per lane).  Needs a dword
 // aligned source (checked on the host); bit-identical to area_fast_kernel.
 constexpr int kAreaSeg = 4096;  // source bytes per segment row (16 KiB of LDS sums)
-template <int OUT>
+template <int OUT, int VB>  // VB: source bytes per thread per row (4 or 16)
 __global__ void __launch_bounds__(kBlock) area_u8_colsum_kernel(ResizeLaunch L, int tw) {
     using TOut = typename std::conditional<(OUT == kOutSame), uint8_t, float>::type;
+    using TV = typename std::conditional<(VB == 16), uint4, uint32_t>::type;
     __shared__ int colsum[kAreaSeg];
     const int y = blockIdx.y;
     const int pidx = blockIdx.z;
@@ -740,29 +742,32 @@ __global__ void __launch_bounds__(kBlock) area_u8_colsum_kernel(ResizeLaunch L, 
     const int pw = min(tw, L.dst.w - x0);          // output pixels in this segment
     const int seg = pw * ax * cc;                  // source bytes per row in this segment
     const int row_bytes = L.src.w * cc;
-    const int b0 = x0 * ax * cc;                   // multiple of 4 (tw % 4 == 0)
+    const int b0 = x0 * ax * cc;                   // multiple of VB (host picks tw)
     const unsigned char* row0 = L.src.base + (int64_t)img * L.src.img_pitch + (int64_t)plane * L.src.plane_pitch +
                                 (int64_t)y * ay * L.src.row_pitch + b0;
-    for (int j = threadIdx.x; j * 4 < seg; j += kBlock) {
-        int s0 = 0, s1 = 0, s2 = 0, s3 = 0;
-        if (b0 + j * 4 + 4 <= row_bytes) {
+    for (int j = threadIdx.x; j * VB < seg; j += kBlock) {
+        int acc[VB];
+#pragma unroll
+        for (int i = 0; i < VB; ++i) acc[i] = 0;
+        if (b0 + (j + 1) * VB <= row_bytes) {
             for (int r = 0; r < ay; ++r) {
-                const uint32_t v = *reinterpret_cast<const uint32_t*>(row0 + (int64_t)r * L.src.row_pitch + j * 4);
-                s0 += v & 0xff;
-                s1 += (v >> 8) & 0xff;
-                s2 += (v >> 16) & 0xff;
-                s3 += v >> 24;
+                const TV t = *reinterpret_cast<const TV*>(row0 + (int64_t)r * L.src.row_pitch + j * VB);
+                const uint32_t* w = reinterpret_cast<const uint32_t*>(&t);
+#pragma unroll
+                for (int i = 0; i < VB; ++i) acc[i] += (w[i >> 2] >> (8 * (i & 3))) & 0xff;
             }
-        } else {  // the row's last partial dword
+        } else {  // the row's last partial chunk
+            const int lim = row_bytes - (b0 + j * VB);
             for (int r = 0; r < ay; ++r) {
-                const unsigned char* p = row0 + (int64_t)r * L.src.row_pitch + j * 4;
-                const int lim = row_bytes - (b0 + j * 4);
-                s0 += p[0];
-                if (lim > 1) s1 += p[1];
-                if (lim > 2) s2 += p[2];
+                const unsigned char* p = row0 + (int64_t)r * L.src.row_pitch + j * VB;
+#pragma unroll
+                for (int i = 0; i < VB; ++i)
+                    if (i < lim) acc[i] += p[i];
             }
         }
-        *reinterpret_cast<int4*>(&colsum[j * 4]) = make_int4(s0, s1, s2, s3);
+#pragma unroll
+        for (int i = 0; i < VB; i += 4)
+            *reinterpret_cast<int4*>(&colsum[j * VB + i]) = make_int4(acc[i], acc[i + 1], acc[i + 2], acc[i + 3]);
     }
     __syncthreads();
     TOut* dp = reinterpret_cast<TOut*>(const_cast<unsigned char*>(L.dst.base) + (int64_t)img * L.dst.img_pitch +
@@ -785,16 +790,22 @@ __global__ void __launch_bounds__(kBlock) area_u8_colsum_kernel(ResizeLaunch L, 
     }
 }
 
-hipError_t launch_area_u8_colsum(const ResizeLaunch& L, hipStream_t s) {
-    const int per_px = L.area_x * L.src.cc;
-    const int tw_max = (kAreaSeg / per_px) & ~3;
-    const int nblk = (L.dst.w + tw_max - 1) / tw_max;
-    const int tw = ((L.dst.w + nblk - 1) / nblk + 3) & ~3;  // even segments, x0 * per_px stays dword aligned
-    const dim3 grid(nblk, L.dst.h, L.n * L.src.planes);
-    if (L.out == kOutSame) hipLaunchKernelGGL((area_u8_colsum_kernel<kOutSame>), grid, dim3(kBlock), 0, s, L, tw);
-    else if (L.out == kOutF32) hipLaunchKernelGGL((area_u8_colsum_kernel<kOutF32>), grid, dim3(kBlock), 0, s, L, tw);
-    else hipLaunchKernelGGL((area_u8_colsum_kernel<kOutNorm>), grid, dim3(kBlock), 0, s, L, tw);
+template <int VB>
+hipError_t launch_area_u8_colsum_t(const ResizeLaunch& L, hipStream_t s, int tw, dim3 grid) {
+    if (L.out == kOutSame) hipLaunchKernelGGL((area_u8_colsum_kernel<kOutSame, VB>), grid, dim3(kBlock), 0, s, L, tw);
+    else if (L.out == kOutF32) hipLaunchKernelGGL((area_u8_colsum_kernel<kOutF32, VB>), grid, dim3(kBlock), 0, s, L, tw);
+    else hipLaunchKernelGGL((area_u8_colsum_kernel<kOutNorm, VB>), grid, dim3(kBlock), 0, s, L, tw);
     return hipGetLastError();
+}
+
+// vb: the source's alignment (4 or 16); segments of tw pixels start vb-aligned
+hipError_t launch_area_u8_colsum(const ResizeLaunch& L, hipStream_t s, int vb) {
+    const int per_px = L.area_x * L.src.cc;
+    const int tw_max = (kAreaSeg / per_px) & ~(vb - 1);
+    const int nblk = (L.dst.w + tw_max - 1) / tw_max;
+    const int tw = ((L.dst.w + nblk - 1) / nblk + vb - 1) & ~(vb - 1);
+    const dim3 grid(nblk, L.dst.h, L.n * L.src.planes);
+    return vb == 16 ? launch_area_u8_colsum_t<16>(L, s, tw, grid) : launch_area_u8_colsum_t<4>(L, s, tw, grid);
 }
 
 template <typename TIn>
@@ -819,10 +830,12 @@ hipError_t launch_resize_area(const ResizeLaunch& L, hipStream_t s) {
         (int64_t)L.dst.h * L.area_y != L.src.h)
         return hipErrorInvalidValue;  // the kernel reads exactly the source extent
     if (L.src.esize == 1) {
-        const bool aligned = ((reinterpret_cast<uintptr_t>(L.src.base) | (uintptr_t)L.src.img_pitch |
-                               (uintptr_t)L.src.plane_pitch | (uintptr_t)L.src.row_pitch) & 3) == 0;
-        if (aligned && L.area_x * L.src.cc <= 1024 && !std::getenv("VACV_AREA_PER_PIXEL"))
-            return launch_area_u8_colsum(L, s);
+        const uintptr_t bits = reinterpret_cast<uintptr_t>(L.src.base) | (uintptr_t)L.src.img_pitch |
+                               (uintptr_t)L.src.plane_pitch | (uintptr_t)L.src.row_pitch;
+        const char* env = std::getenv("VACV_AREA_KERNEL");  // "pixel" / "dword": A/B knobs
+        const int vb = (bits & 15) == 0 && L.area_x * L.src.cc <= 256 ? 16 : (bits & 3) == 0 ? 4 : 0;
+        if (vb && L.area_x * L.src.cc <= 1024 && !(env && !std::strcmp(env, "pixel")))
+            return launch_area_u8_colsum(L, s, env && !std::strcmp(env, "dword") ? 4 : vb);
         return launch_area_t<uint8_t>(L, s);
     }
     return launch_area_t<float>(L, s);
