@@ -729,11 +729,13 @@ __global__ void __launch_bounds__(kBlock) area_fast_kernel(ResizeLaunch L) {
 // aligned source (checked on the host); bit-identical to area_fast_kernel.
 constexpr int kAreaSeg = 4096;  // source bytes per segment row (16 KiB of LDS sums)
 template <int OUT, int VB>  // VB: source bytes per thread per row (4 or 16)
-__global__ void __launch_bounds__(kBlock) area_u8_colsum_kernel(ResizeLaunch L, int tw) {
+__global__ void __launch_bounds__(kBlock) area_u8_colsum_kernel(ResizeLaunch L, int tw, int rows) {
     using TOut = typename std::conditional<(OUT == kOutSame), uint8_t, float>::type;
     using TV = typename std::conditional<(VB == 16), uint4, uint32_t>::type;
     __shared__ int colsum[kAreaSeg];
-    const int y = blockIdx.y;
+    const int y_end = min(L.dst.h, (int)(blockIdx.y + 1) * rows);
+    for (int y = blockIdx.y * rows; y < y_end; ++y) {
+    if (y != (int)blockIdx.y * rows) __syncthreads();  // colsum of the previous row is consumed
     const int pidx = blockIdx.z;
     const int img = pidx / L.src.planes;
     const int plane = pidx - img * L.src.planes;
@@ -788,13 +790,14 @@ __global__ void __launch_bounds__(kBlock) area_u8_colsum_kernel(ResizeLaunch L, 
             dp[e] = normalize_u8v(cn, (int)v);
         }
     }
+    }
 }
 
 template <int VB>
-hipError_t launch_area_u8_colsum_t(const ResizeLaunch& L, hipStream_t s, int tw, dim3 grid) {
-    if (L.out == kOutSame) hipLaunchKernelGGL((area_u8_colsum_kernel<kOutSame, VB>), grid, dim3(kBlock), 0, s, L, tw);
-    else if (L.out == kOutF32) hipLaunchKernelGGL((area_u8_colsum_kernel<kOutF32, VB>), grid, dim3(kBlock), 0, s, L, tw);
-    else hipLaunchKernelGGL((area_u8_colsum_kernel<kOutNorm, VB>), grid, dim3(kBlock), 0, s, L, tw);
+hipError_t launch_area_u8_colsum_t(const ResizeLaunch& L, hipStream_t s, int tw, int rows, dim3 grid) {
+    if (L.out == kOutSame) hipLaunchKernelGGL((area_u8_colsum_kernel<kOutSame, VB>), grid, dim3(kBlock), 0, s, L, tw, rows);
+    else if (L.out == kOutF32) hipLaunchKernelGGL((area_u8_colsum_kernel<kOutF32, VB>), grid, dim3(kBlock), 0, s, L, tw, rows);
+    else hipLaunchKernelGGL((area_u8_colsum_kernel<kOutNorm, VB>), grid, dim3(kBlock), 0, s, L, tw, rows);
     return hipGetLastError();
 }
 
@@ -804,8 +807,11 @@ hipError_t launch_area_u8_colsum(const ResizeLaunch& L, hipStream_t s, int vb) {
     const int tw_max = (kAreaSeg / per_px) & ~(vb - 1);
     const int nblk = (L.dst.w + tw_max - 1) / tw_max;
     const int tw = ((L.dst.w + nblk - 1) / nblk + vb - 1) & ~(vb - 1);
-    const dim3 grid(nblk, L.dst.h, L.n * L.src.planes);
-    return vb == 16 ? launch_area_u8_colsum_t<16>(L, s, tw, grid) : launch_area_u8_colsum_t<4>(L, s, tw, grid);
+    const char* env = std::getenv("VACV_AREA_ROWS");  // output rows per workgroup
+    const int rows = std::max(1, env ? std::atoi(env) : 1);
+    const dim3 grid(nblk, (L.dst.h + rows - 1) / rows, L.n * L.src.planes);
+    return vb == 16 ? launch_area_u8_colsum_t<16>(L, s, tw, rows, grid)
+                    : launch_area_u8_colsum_t<4>(L, s, tw, rows, grid);
 }
 
 template <typename TIn>
