@@ -728,7 +728,7 @@ __global__ void __launch_bounds__(kBlock) area_fast_kernel(ResizeLaunch L) {
 // column sums, rounds and stores (adjacent bytes per lane).  Needs a dword
 // aligned source (checked on the host); bit-identical to area_fast_kernel.
 constexpr int kAreaSeg = 4096;  // source bytes per segment row (16 KiB of LDS sums)
-template <int OUT, int VB>  // VB: source bytes per thread per row (4 or 16)
+template <int OUT, int VB, int CC>  // VB: source bytes per thread per row (4 or 16); CC: channels (1..4)
 __global__ void __launch_bounds__(kBlock) area_u8_colsum_kernel(ResizeLaunch L, int tw, int rows) {
     using TOut = typename std::conditional<(OUT == kOutSame), uint8_t, float>::type;
     using TV = typename std::conditional<(VB == 16), uint4, uint32_t>::type;
@@ -739,7 +739,8 @@ __global__ void __launch_bounds__(kBlock) area_u8_colsum_kernel(ResizeLaunch L, 
     const int pidx = blockIdx.z;
     const int img = pidx / L.src.planes;
     const int plane = pidx - img * L.src.planes;
-    const int cc = L.src.cc, ax = L.area_x, ay = L.area_y;
+    constexpr int cc = CC;
+    const int ax = L.area_x, ay = L.area_y;
     const int x0 = blockIdx.x * tw;
     const int pw = min(tw, L.dst.w - x0);          // output pixels in this segment
     const int seg = pw * ax * cc;                  // source bytes per row in this segment
@@ -793,12 +794,23 @@ __global__ void __launch_bounds__(kBlock) area_u8_colsum_kernel(ResizeLaunch L, 
     }
 }
 
+template <int VB, int CC>
+hipError_t launch_area_u8_colsum_c(const ResizeLaunch& L, hipStream_t s, int tw, int rows, dim3 grid) {
+    if (L.out == kOutSame) hipLaunchKernelGGL((area_u8_colsum_kernel<kOutSame, VB, CC>), grid, dim3(kBlock), 0, s, L, tw, rows);
+    else if (L.out == kOutF32) hipLaunchKernelGGL((area_u8_colsum_kernel<kOutF32, VB, CC>), grid, dim3(kBlock), 0, s, L, tw, rows);
+    else hipLaunchKernelGGL((area_u8_colsum_kernel<kOutNorm, VB, CC>), grid, dim3(kBlock), 0, s, L, tw, rows);
+    return hipGetLastError();
+}
+
 template <int VB>
 hipError_t launch_area_u8_colsum_t(const ResizeLaunch& L, hipStream_t s, int tw, int rows, dim3 grid) {
-    if (L.out == kOutSame) hipLaunchKernelGGL((area_u8_colsum_kernel<kOutSame, VB>), grid, dim3(kBlock), 0, s, L, tw, rows);
-    else if (L.out == kOutF32) hipLaunchKernelGGL((area_u8_colsum_kernel<kOutF32, VB>), grid, dim3(kBlock), 0, s, L, tw, rows);
-    else hipLaunchKernelGGL((area_u8_colsum_kernel<kOutNorm, VB>), grid, dim3(kBlock), 0, s, L, tw, rows);
-    return hipGetLastError();
+    switch (L.src.cc) {  // NHWC c <= 4 (vacv_abi.cpp), NCHW planes have cc = 1
+        case 1: return launch_area_u8_colsum_c<VB, 1>(L, s, tw, rows, grid);
+        case 2: return launch_area_u8_colsum_c<VB, 2>(L, s, tw, rows, grid);
+        case 3: return launch_area_u8_colsum_c<VB, 3>(L, s, tw, rows, grid);
+        case 4: return launch_area_u8_colsum_c<VB, 4>(L, s, tw, rows, grid);
+        default: return hipErrorInvalidValue;
+    }
 }
 
 // vb: the source's alignment (4 or 16); segments of tw pixels start vb-aligned
