@@ -658,6 +658,60 @@ __global__ void __launch_bounds__(kBlock) nearest_kernel(ResizeLaunch L) {
     }
 }
 
+// INTER_NEAREST with the source row staged in LDS: a workgroup takes one
+// output row, reads its source row sy once as coalesced 16-byte loads (a
+// gather per pixel moves the same 128 B lines whenever the sample stride is
+// under a line, but with one load instruction per pixel per lane), then one
+// thread per output element picks from LDS and stores (adjacent elements per
+// lane).  Same index arithmetic as nearest_kernel, so bit-identical.
+constexpr int kNearestRowBytes = 64 * 1024;
+template <typename TIn, int OUT>
+__global__ void __launch_bounds__(kBlock) nearest_row_kernel(ResizeLaunch L) {
+    using TOut = typename std::conditional<(OUT == kOutSame), TIn, float>::type;
+    extern __shared__ uint4 row_lds[];
+    const int y = blockIdx.x;
+    const int pidx = blockIdx.y;
+    const int img = pidx / L.src.planes;
+    const int plane = pidx - img * L.src.planes;
+    const int cc = L.src.cc;
+    const int sy = min((int)floor((double)y * L.scale_yd), L.src.h - 1);
+    const unsigned char* sp = L.src.base + (int64_t)img * L.src.img_pitch + (int64_t)plane * L.src.plane_pitch +
+                              (int64_t)sy * L.src.row_pitch;
+    const int row_bytes = L.src.w * cc * (int)sizeof(TIn);
+    const int n16 = row_bytes >> 4;
+    for (int i = threadIdx.x; i < n16; i += kBlock) row_lds[i] = reinterpret_cast<const uint4*>(sp)[i];
+    unsigned char* lb = reinterpret_cast<unsigned char*>(row_lds);
+    for (int i = (n16 << 4) + threadIdx.x; i < row_bytes; i += kBlock) lb[i] = sp[i];
+    __syncthreads();
+    const TIn* row = reinterpret_cast<const TIn*>(lb);
+    TOut* dp = reinterpret_cast<TOut*>(const_cast<unsigned char*>(L.dst.base) + (int64_t)img * L.dst.img_pitch +
+                                       (int64_t)plane * L.dst.plane_pitch + (int64_t)y * L.dst.row_pitch);
+    const int n_el = L.dst.w * cc;
+    for (int e = threadIdx.x; e < n_el; e += kBlock) {
+        const int x = e / cc, k = e - x * cc;
+        const int sx = min((int)floor((double)x * L.scale_xd), L.src.w - 1);
+        const TIn v = row[sx * cc + k];
+        if (OUT == kOutSame) {
+            dp[e] = (TOut)v;
+        } else if (OUT == kOutF32) {
+            dp[e] = (TOut)(float)v;
+        } else {
+            const ChanNorm cn = chan_norm(L.norm, img, cc == 1 ? plane % L.norm.c_total : k);
+            dp[e] = (TOut)(std::is_same<TIn, uint8_t>::value ? normalize_u8v(cn, (int)v) : normalize_f(cn, (float)v));
+        }
+    }
+}
+
+template <typename TIn>
+hipError_t launch_nearest_row_t(const ResizeLaunch& L, hipStream_t s) {
+    const dim3 grid(L.dst.h, L.n * L.src.planes);
+    const size_t lds = ((size_t)L.src.w * L.src.cc * sizeof(TIn) + 15) & ~(size_t)15;
+    if (L.out == kOutSame) hipLaunchKernelGGL((nearest_row_kernel<TIn, kOutSame>), grid, dim3(kBlock), lds, s, L);
+    else if (L.out == kOutF32) hipLaunchKernelGGL((nearest_row_kernel<TIn, kOutF32>), grid, dim3(kBlock), lds, s, L);
+    else hipLaunchKernelGGL((nearest_row_kernel<TIn, kOutNorm>), grid, dim3(kBlock), lds, s, L);
+    return hipGetLastError();
+}
+
 template <typename TIn>
 hipError_t launch_nearest_t(const ResizeLaunch& L, hipStream_t s) {
     const dim3 grid((L.dst.w + kBlock - 1) / kBlock, L.dst.h, L.n * L.src.planes);
@@ -839,6 +893,13 @@ hipError_t launch_area_t(const ResizeLaunch& L, hipStream_t s) {
 
 hipError_t launch_resize_nearest(const ResizeLaunch& L, hipStream_t s) {
     if (L.dst.h > 65535 || (int64_t)L.n * L.src.planes > 65535) return hipErrorInvalidValue;
+    const int64_t row_bytes = (int64_t)L.src.w * L.src.cc * L.src.esize;
+    const uintptr_t bits = reinterpret_cast<uintptr_t>(L.src.base) | (uintptr_t)L.src.img_pitch |
+                           (uintptr_t)L.src.plane_pitch | (uintptr_t)L.src.row_pitch;
+    const char* env = std::getenv("VACV_NEAREST_KERNEL");  // "pixel": A/B knob
+    if ((bits & 15) == 0 && row_bytes <= kNearestRowBytes &&
+        !(env && !std::strcmp(env, "pixel")))
+        return L.src.esize == 1 ? launch_nearest_row_t<uint8_t>(L, s) : launch_nearest_row_t<float>(L, s);
     return L.src.esize == 1 ? launch_nearest_t<uint8_t>(L, s) : launch_nearest_t<float>(L, s);
 }
 
