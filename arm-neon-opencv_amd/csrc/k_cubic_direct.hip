@@ -204,8 +204,7 @@ hipError_t launch_cc(const ResizeLaunch& L, hipStream_t s) {
 }  // namespace
 
 bool cubic_direct_applies(const ResizeLaunch& L) {
-    const char* env = std::getenv("VACV_CUBIC_DIRECT");
-    if (env && env[0] == '0') return false;
+    if (tune(VACV_TUNE_CUBIC_DIRECT) == 0) return false;  // A/B: the staged kernel
     return L.kind == kCubic && L.src.esize == 1 && L.src.cc <= 3 && (L.out == kOutF32 || L.out == kOutNorm);
 }
 

@@ -729,9 +729,11 @@ hipError_t launch_nearest_t(const ResizeLaunch& L, hipStream_t s) {
 // mean of the area_x * area_y block at (x * area_x, y * area_y), summed in
 // OpenCV's order (block rows, then columns; four taps grouped per add as its
 // CV_ENABLE_UNROLLED loop does, which only matters for fp32) and scaled by
-// the fp32 1/area; u8 rounds half to even (saturate_cast = lrint on the ARM
-// build).  One thread per output pixel; a wave reads 64 * area_x * cc
-// contiguous elements per block row.
+// the fp32 1/area; u8 rounds half to even (saturate_cast = cvRound), except
+// 2x2 blocks of 1, 3 or 4 channels, which OpenCV routes through
+// ResizeAreaFastVec's fast_mode: (a + b + c + d + 2) >> 2, half up
+// (L.area_half_up).  One thread per output pixel; a wave reads 64 * area_x *
+// cc contiguous elements per block row.
 template <typename TIn, int OUT>
 __global__ void __launch_bounds__(kBlock) area_fast_kernel(ResizeLaunch L) {
     using TOut = typename std::conditional<(OUT == kOutSame), TIn, float>::type;
@@ -761,7 +763,7 @@ __global__ void __launch_bounds__(kBlock) area_fast_kernel(ResizeLaunch L) {
         for (; t < area; ++t) sum = sum + tap(t);
         const float m = __fmul_rn((float)sum, L.area_scale);
         TIn v;
-        if (std::is_same<TIn, uint8_t>::value) v = (TIn)(int)rintf(m);
+        if (std::is_same<TIn, uint8_t>::value) v = (TIn)(L.area_half_up ? ((int)sum + 2) >> 2 : (int)rintf(m));
         else v = (TIn)m;
         if (OUT == kOutSame) {
             dp[k] = (TOut)v;
@@ -835,7 +837,8 @@ __global__ void __launch_bounds__(kBlock) area_u8_colsum_kernel(ResizeLaunch L, 
         const int* cs = colsum + xl * ax * cc + k;
         int sum = 0;
         for (int q = 0; q < ax; ++q) sum += cs[q * cc];
-        const uint8_t v = (uint8_t)(int)rintf(__fmul_rn((float)sum, L.area_scale));
+        const uint8_t v = L.area_half_up ? (uint8_t)((sum + 2) >> 2)
+                                         : (uint8_t)(int)rintf(__fmul_rn((float)sum, L.area_scale));
         if (OUT == kOutSame) {
             dp[e] = v;
         } else if (OUT == kOutF32) {
@@ -873,8 +876,7 @@ hipError_t launch_area_u8_colsum(const ResizeLaunch& L, hipStream_t s, int vb) {
     const int tw_max = (kAreaSeg / per_px) & ~(vb - 1);
     const int nblk = (L.dst.w + tw_max - 1) / tw_max;
     const int tw = ((L.dst.w + nblk - 1) / nblk + vb - 1) & ~(vb - 1);
-    const char* env = std::getenv("VACV_AREA_ROWS");  // output rows per workgroup
-    const int rows = std::max(1, env ? std::atoi(env) : 1);
+    const int rows = std::max(1, tune_or(VACV_TUNE_AREA_ROWS, 1));  // output rows per workgroup
     const dim3 grid(nblk, (L.dst.h + rows - 1) / rows, L.n * L.src.planes);
     return vb == 16 ? launch_area_u8_colsum_t<16>(L, s, tw, rows, grid)
                     : launch_area_u8_colsum_t<4>(L, s, tw, rows, grid);
@@ -896,9 +898,11 @@ hipError_t launch_resize_nearest(const ResizeLaunch& L, hipStream_t s) {
     const int64_t row_bytes = (int64_t)L.src.w * L.src.cc * L.src.esize;
     const uintptr_t bits = reinterpret_cast<uintptr_t>(L.src.base) | (uintptr_t)L.src.img_pitch |
                            (uintptr_t)L.src.plane_pitch | (uintptr_t)L.src.row_pitch;
-    const char* env = std::getenv("VACV_NEAREST_KERNEL");  // "pixel": A/B knob
-    if ((bits & 15) == 0 && row_bytes <= kNearestRowBytes &&
-        !(env && !std::strcmp(env, "pixel")))
+    // the row kernel reads the whole source row: only where the samples are
+    // at most a cache line apart, so it moves no more lines than the gathers
+    // (a 4096-px fp32 row sampled 32 times would read 64 KiB for 32 pixels)
+    const bool dense_samples = L.scale_xd * L.src.cc * L.src.esize <= 128.0;
+    if ((bits & 15) == 0 && row_bytes <= kNearestRowBytes && dense_samples && tune(VACV_TUNE_NEAREST_KERNEL) != 0)
         return L.src.esize == 1 ? launch_nearest_row_t<uint8_t>(L, s) : launch_nearest_row_t<float>(L, s);
     return L.src.esize == 1 ? launch_nearest_t<uint8_t>(L, s) : launch_nearest_t<float>(L, s);
 }
@@ -911,10 +915,10 @@ hipError_t launch_resize_area(const ResizeLaunch& L, hipStream_t s) {
     if (L.src.esize == 1) {
         const uintptr_t bits = reinterpret_cast<uintptr_t>(L.src.base) | (uintptr_t)L.src.img_pitch |
                                (uintptr_t)L.src.plane_pitch | (uintptr_t)L.src.row_pitch;
-        const char* env = std::getenv("VACV_AREA_KERNEL");  // "pixel" / "dword": A/B knobs
+        const int knob = tune(VACV_TUNE_AREA_KERNEL);  // A/B: 1 per-pixel, 2 dword column sums
         const int vb = (bits & 15) == 0 && L.area_x * L.src.cc <= 256 ? 16 : (bits & 3) == 0 ? 4 : 0;
-        if (vb && L.area_x * L.src.cc <= 1024 && !(env && !std::strcmp(env, "pixel")))
-            return launch_area_u8_colsum(L, s, env && !std::strcmp(env, "dword") ? 4 : vb);
+        if (vb && L.area_x * L.src.cc <= 1024 && knob != 1)
+            return launch_area_u8_colsum(L, s, knob == 2 ? 4 : vb);
         return launch_area_t<uint8_t>(L, s);
     }
     return launch_area_t<float>(L, s);
@@ -971,8 +975,7 @@ hipError_t launch_dtype(const DtypeLaunch& L, hipStream_t s) {
 hipError_t launch_color(const ColorLaunch& L, hipStream_t s) {
     const uint32_t cpo = (uint32_t)((3LL * L.w + 3) / 4);
     const uint64_t chunks = (uint64_t)cpo * L.n * L.h;
-    const char* env = std::getenv("VACV_COLOR_CHUNKS");
-    if (L.out != kOutSame && chunks < (1ull << 32) - kBlock && env && env[0] == '1') {  // opt-in: measured slower (VALU-bound)
+    if (L.out != kOutSame && chunks < (1ull << 32) - kBlock && tune(VACV_TUNE_COLOR_CHUNKS) == 1) {  // opt-in: measured slower (VALU-bound)
         const uint32_t blocks = (uint32_t)((chunks + kBlock - 1) / kBlock);
         if (L.out == kOutF32) hipLaunchKernelGGL(color_f32_kernel<kOutF32>, dim3(blocks), dim3(kBlock), 0, s, L, cpo);
         else hipLaunchKernelGGL(color_f32_kernel<kOutNorm>, dim3(blocks), dim3(kBlock), 0, s, L, cpo);

@@ -804,8 +804,8 @@ hipError_t launch_one(ResizeLaunch L, hipStream_t s) {
         if (tiles > 0x7FFFFFFF) return hipErrorInvalidValue;
         const int64_t resident = resident_workgroups(rk, L.lds_bytes);
         if (resident <= 0) return hipErrorInvalidValue;
-        const char* env = std::getenv("VACV_RESIZE_WGS");
-        const int64_t want = env ? std::max<int64_t>(1, std::atoll(env)) : resident;
+        const int wgs = tune(VACV_TUNE_RESIZE_WGS);
+        const int64_t want = wgs > 0 ? wgs : resident;
         const int64_t blocks = std::min<int64_t>(tiles, want);
         hipLaunchKernelGGL(rk, dim3((unsigned)blocks), dim3(kBlock), L.lds_bytes, s, L);
         return hipGetLastError();
@@ -818,10 +818,10 @@ hipError_t launch_one(ResizeLaunch L, hipStream_t s) {
         // keeps its column); VACV_RESIZE_WGS overrides, for measurement
         const int64_t tasks = (int64_t)L.n * L.src.planes * L.tiles_y * L.tiles_x;
         if (tasks > 0x7FFFFFFF) return hipErrorInvalidValue;
-        const char* env = std::getenv("VACV_RESIZE_WGS");
+        const int wgs = tune(VACV_TUNE_RESIZE_WGS);
         // 3 x residency measured best (0.2326 vs 0.2351 ms at 1x on the
         // headline): queued workgroups fill in as early ones drain
-        int64_t want = env ? std::max<int64_t>(1, std::atoll(env)) : 3 * resident;
+        int64_t want = wgs > 0 ? wgs : 3 * resident;
         want = std::max<int64_t>(L.tiles_x, want / L.tiles_x * L.tiles_x);
         const int64_t blocks = std::min<int64_t>(want, tasks);
         hipLaunchKernelGGL(kernel, dim3((unsigned)blocks), dim3(kBlock), L.lds_bytes, s, L);

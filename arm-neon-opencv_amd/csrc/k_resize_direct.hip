@@ -209,9 +209,8 @@ hipError_t launch_one(const ResizeLaunch& L, hipStream_t s) {
     if (P >= 0x7FFFFFFF - kBlockPx || total > 0x7FFFFFF0LL) return hipErrorInvalidValue;
     // XCD-contiguous order only where neighbouring workgroups share source
     // rows (two-tap rows); one-tap rows stream fastest in plain address order
-    // (measured 0.222 vs 0.233 ms on the headline; VACV_DIRECT_XCD overrides)
-    const char* env = std::getenv("VACV_DIRECT_XCD");
-    const int xcd = env ? std::atoi(env) : (ONE_ROW ? 0 : 1);
+    // (measured 0.222 vs 0.233 ms on the headline; VACV_TUNE_DIRECT_XCD overrides)
+    const int xcd = tune_or(VACV_TUNE_DIRECT_XCD, ONE_ROW ? 0 : 1) ? 1 : 0;
     const int64_t blocks = xcd ? (total + 7) / 8 * 8 : total;
     hipLaunchKernelGGL((resize_direct_kernel<CC, OUT, MODE, ONE_ROW>), dim3((unsigned)blocks), dim3(64, 4), 0, s,
                        L, (int)per_plane, (int)total, xcd);

@@ -9,11 +9,10 @@
 // value (Sum S*wx*wy) >> 22.  Skipped pixels get the border value here.
 //
 // A workgroup owns a 64*kPx x 4 output tile.  Each gather instruction
-// samples an LW x (64/LW) block of output pixels: LW = 64 (one row segment
-// per instruction) by default, 16 (16 x 4 blocks, a more compact rotated
-// footprint: measured no faster) via VACV_WARP_LW.  kPx = 8 lane blocks per
+// samples one 64-pixel output row segment (16 x 4 lane blocks, a more compact
+// rotated footprint, measured no faster in round 1).  kPx = 8 lane blocks per
 // wave for byte output (10 when that pads the output width less, e.g. 1280;
-// VACV_WARP_PX overrides): more gathers in flight per wave, and the
+// VACV_TUNE_WARP_PX overrides): more gathers in flight per wave, and the
 // per-workgroup setup spread over twice the pixels (0.30 -> 0.28 -> 0.27 ms
 // at 720p rot15); 4 for fp32 output.  The tile is re-assembled in LDS and each wave writes one of its
 // rows with 16-byte stores.  Taps: one dword-aligned 8/12-byte buffer load per source row
@@ -26,19 +25,16 @@
 // gathers it saves.
 #pragma clang fp contract(off)
 
-#include <cstdlib>
-
 #include "vacv_device.hpp"
 
 namespace vacv {
 namespace {
 
 
-template <int CC, typename TIn, int OUT, int LW, int kPx>
+template <int CC, typename TIn, int OUT, int kPx>
 __global__ void __launch_bounds__(kBlock)
 warp_kernel(WarpLaunch L, int gx, int gy, int total) {
-    constexpr int LH = 64 / LW;  // rows of one lane block; the tile is 4 rows
-    static_assert(LW * LH == 64 && LH <= 4, "lane block");
+    constexpr int LW = 64, LH = 1;  // a lane block is one 64-pixel row segment; the tile is 4 rows
     using TOut = typename std::conditional<(OUT == kOutSame), TIn, float>::type;
     // u8 normalisation in registers (normalize_u8v); a per-workgroup LDS
     // table cost 3 fp64 divides per thread and a barrier (NV21 kernel: 0.58 ->
@@ -201,47 +197,38 @@ warp_kernel(WarpLaunch L, int gx, int gy, int total) {
     }
 }
 
-// lane block width (64: one row segment per gather instruction, 16: 16 x 4
-// blocks) and lane blocks per wave (8 or 4): A/B measurement knobs
-int warp_lane_width() {
-    const char* env = std::getenv("VACV_WARP_LW");
-    return (env && std::atoi(env) == 16) ? 16 : 64;
-}
 // default: 8 or 10 lane blocks per wave for byte output, whichever pads the
 // output width less (1280: 10 -> 2 tiles of 640 exactly, 0.271 ms, vs 8 ->
 // 2.5 tiles, 0.281 ms at 720p rot15; 8 vs 4: 0.283 vs 0.304), 4 for fp32
 // output (0.538 vs 0.614 ms: 8 blocks double the LDS row buffers and halve
-// the resident workgroups).  VACV_WARP_PX = 4, 5, 8 or 10 overrides.
+// the resident workgroups).  VACV_TUNE_WARP_PX = 4, 5, 8 or 10 overrides.
 int warp_blocks_per_wave(bool byte_out, int w) {
-    const char* env = std::getenv("VACV_WARP_PX");
-    if (env && (std::atoi(env) == 4 || std::atoi(env) == 5 || std::atoi(env) == 8 || std::atoi(env) == 10))
-        return std::atoi(env);
+    const int px = tune(VACV_TUNE_WARP_PX);
+    if (px == 4 || px == 5 || px == 8 || px == 10) return px;
     if (!byte_out) return 4;
     const auto pad = [w](int k) { return (w + 64 * k - 1) / (64 * k) * (64 * k) - w; };
     return pad(10) < pad(8) ? 10 : 8;
 }
 
-template <int CC, typename TIn, int OUT, int LW, int kPx>
+template <int CC, typename TIn, int OUT, int kPx>
 hipError_t launch_px(const WarpLaunch& L, hipStream_t s) {
     const int gx = (L.dst.w + 64 * kPx - 1) / (64 * kPx), gy = (L.dst.h + 3) / 4;
     const int64_t total = (int64_t)gx * gy * L.n * L.src.planes;
     if (total >= 0x7FFFFFF0LL) return hipErrorInvalidValue;
     const int64_t blocks = (total + 7) / 8 * 8;
-    hipLaunchKernelGGL((warp_kernel<CC, TIn, OUT, LW, kPx>), dim3((unsigned)blocks), dim3(64, 4), 0, s, L, gx, gy,
+    hipLaunchKernelGGL((warp_kernel<CC, TIn, OUT, kPx>), dim3((unsigned)blocks), dim3(64, 4), 0, s, L, gx, gy,
                        (int)total);
     return hipGetLastError();
 }
 
 template <int CC, typename TIn, int OUT>
 hipError_t launch_one(const WarpLaunch& L, hipStream_t s) {
-    const int bpw = warp_blocks_per_wave(OUT == kOutSame && sizeof(TIn) == 1, L.dst.w);
-    const bool wide = bpw >= 8;
-    if (warp_lane_width() == 64) {
-        if (bpw == 10) return launch_px<CC, TIn, OUT, 64, 10>(L, s);
-        if (bpw == 5) return launch_px<CC, TIn, OUT, 64, 5>(L, s);
-        return wide ? launch_px<CC, TIn, OUT, 64, 8>(L, s) : launch_px<CC, TIn, OUT, 64, 4>(L, s);
+    switch (warp_blocks_per_wave(OUT == kOutSame && sizeof(TIn) == 1, L.dst.w)) {
+        case 10: return launch_px<CC, TIn, OUT, 10>(L, s);
+        case 5: return launch_px<CC, TIn, OUT, 5>(L, s);
+        case 8: return launch_px<CC, TIn, OUT, 8>(L, s);
+        default: return launch_px<CC, TIn, OUT, 4>(L, s);
     }
-    return wide ? launch_px<CC, TIn, OUT, 16, 8>(L, s) : launch_px<CC, TIn, OUT, 16, 4>(L, s);
 }
 
 template <typename TIn, int OUT>
@@ -258,7 +245,6 @@ hipError_t launch_cc(const WarpLaunch& L, hipStream_t s) {
 }  // namespace
 
 hipError_t launch_warp(const WarpLaunch& L, hipStream_t s) {
-    if (warp_tile_applies(L)) return launch_warp_tile(L, s);
     if (L.src.esize == 1) {
         if (L.out == kOutSame) return launch_cc<uint8_t, kOutSame>(L, s);
         if (L.out == kOutF32) return launch_cc<uint8_t, kOutF32>(L, s);

@@ -121,10 +121,7 @@ bool evaluate(const ResizeLaunch& L, const std::vector<Taps>& xt, const std::vec
     return g.lds <= kLdsBudget;
 }
 
-int env_int(const char* name, int def) {
-    const char* v = std::getenv(name);
-    return v ? std::atoi(v) : def;
-}
+int knob(int key, int def) { return tune_or(key, def); }
 
 // Rows mode (resize_rows_kernel): a tile is `tile_h` whole output rows; the
 // staged rows are whole source rows (column 0 on, the kernel evaluates the
@@ -194,11 +191,11 @@ int plan_resize(ResizeLaunch& L, hipStream_t stream, int rows) {
     put(key, L.src.w); put(key, L.src.h); put(key, L.src.cc); put(key, L.src.esize);
     put(key, L.dst.w); put(key, L.dst.h); put(key, L.norm.c_total);
 
-    const int force_h = env_int("VACV_RESIZE_TILE_H", 0);
-    const int force_w = env_int("VACV_RESIZE_TILE_W", 0);
-    const int work = std::max(1, env_int("VACV_RESIZE_WORK", kWorkPerThread));
+    const int force_h = knob(VACV_TUNE_RESIZE_TILE_H, 0);
+    const int force_w = knob(VACV_TUNE_RESIZE_TILE_W, 0);
+    const int work = std::max(1, knob(VACV_TUNE_RESIZE_WORK, kWorkPerThread));
     // rows mode: ~8 KiB of output per workgroup (VACV_RESIZE_ROWS_BYTES)
-    const int rows_bytes = std::max(1, env_int("VACV_RESIZE_ROWS_BYTES", 8192));
+    const int rows_bytes = std::max(1, knob(VACV_TUNE_RESIZE_ROWS_BYTES, 8192));
     put(key, force_h); put(key, force_w); put(key, work); put(key, rows); put(key, rows_bytes);
 
     std::lock_guard<std::mutex> lk(g_mu);
@@ -391,7 +388,7 @@ int plan_resize(ResizeLaunch& L, hipStream_t stream, int rows) {
 // run a mostly idle second round.
 void set_strips(ResizeLaunch& L, int64_t resident) {
     const int64_t columns = (int64_t)L.n * L.src.planes * L.tiles_x;
-    const int64_t target = env_int("VACV_RESIZE_WGS", (int)std::max<int64_t>(1, resident));
+    const int64_t target = knob(VACV_TUNE_RESIZE_WGS, (int)std::max<int64_t>(1, resident));
     const int strips = (int)std::max<int64_t>(1, std::min<int64_t>(L.tiles_y, target / std::max<int64_t>(columns, 1)));
     L.tasks_per_strip = (L.tiles_y + strips - 1) / strips;
     L.strips = (L.tiles_y + L.tasks_per_strip - 1) / L.tasks_per_strip;

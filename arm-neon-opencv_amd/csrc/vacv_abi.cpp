@@ -291,6 +291,10 @@ int resize_impl(const vacv_image* src_d, const vacv_image* dst_d, int interpolat
         L.area_y = (int)iy;
         if ((int64_t)dst.w * L.area_x != src.w || (int64_t)dst.h * L.area_y != src.h) return VACV_ERR_UNSUPPORTED;
         L.area_scale = 1.f / (float)(L.area_x * L.area_y);
+        // OpenCV's ResizeAreaFastVec<uchar>::fast_mode: 2x2 blocks with 1, 3 or
+        // 4 interleaved channels (an NCHW plane is one) take (a+b+c+d+2)>>2
+        L.area_half_up = src.dtype == VACV_INT8 && L.area_x == 2 && L.area_y == 2 &&
+                         (L.src.cc == 1 || L.src.cc == 3 || L.src.cc == 4);
         return hip_status(launch_resize_area(L, s));
     } else {
         return VACV_ERR_UNSUPPORTED;  // resize.cpp:46-49 recurses forever for other modes
@@ -302,23 +306,20 @@ int resize_impl(const vacv_image* src_d, const vacv_image* dst_d, int interpolat
     // u8 bilinear whose output rows each weight ONE source row (downscales by
     // an integer factor >= 2, e.g. the 1080p -> 640x360 headline): the
     // per-pixel gather kernel (k_resize_direct.hip).  Elsewhere the staged
-    // kernel measured faster (1280x720: 0.63 vs 0.69 ms).  VACV_RESIZE_DIRECT
+    // kernel measured faster (1280x720: 0.63 vs 0.69 ms).  VACV_TUNE_RESIZE_DIRECT
     // = 0 never / 2 always uses the gather kernel, for A/B tests.
     // Otherwise resize_kernel with interleaved (address-ordered) tasks;
-    // VACV_RESIZE_INTERLEAVE=0 selects its strip order and VACV_RESIZE_ROWS=1
-    // the whole-row kernel.
-    const char* direct_env = std::getenv("VACV_RESIZE_DIRECT");
-    const int direct = direct_env ? std::atoi(direct_env) : 1;
+    // VACV_TUNE_RESIZE_INTERLEAVE = 0 selects its strip order and
+    // VACV_TUNE_RESIZE_ROWS = 1 the whole-row kernel.
+    const int direct = tune_or(VACV_TUNE_RESIZE_DIRECT, 1);
     if (L.kind == kLinearFixed && L.src.cc <= 4 && dst.w < (1 << 23) && dst.h < (1 << 23) &&
         (direct == 2 || (direct == 1 && resize_one_tap_rows(L))))
         return hip_status(launch_resize_direct(L, s));
     // u8 cubic (fused widen to fp32), c <= 3 interleaved: per-pixel gathers
     // (k_cubic_direct.hip); VACV_CUBIC_DIRECT=0 selects the staged kernel
     if (cubic_direct_applies(L)) return hip_status(launch_cubic_direct(L, s));
-    const char* il_env = std::getenv("VACV_RESIZE_INTERLEAVE");
-    L.interleave = !(il_env && il_env[0] == '0');
-    const char* rows_env = std::getenv("VACV_RESIZE_ROWS");
-    L.rows_mode = rows_env && rows_env[0] == '1';
+    L.interleave = tune(VACV_TUNE_RESIZE_INTERLEAVE) != 0;
+    L.rows_mode = tune(VACV_TUNE_RESIZE_ROWS) == 1;
     if (L.rows_mode) {
         st = plan_resize(L, s, 1);
         if (st == VACV_ERR_UNSUPPORTED) L.rows_mode = 0;

@@ -15,6 +15,13 @@ constexpr int kResizeMaxChunksPerLane = 1;        // fp32 resize: 4-element chun
 constexpr int kRowsMaxChunksPerLane = 2;          // resize_rows_kernel: 4-element chunks per lane per tile
 constexpr int64_t kMaxPlaneBytes = 0x7FFFFFF0LL;  // buffer-resource addressing limit of one plane
 
+// A kernel-variant knob (tuning.cpp, VACV_TUNE_*): -1 = the built-in choice.
+int tune(int key);
+inline int tune_or(int key, int def) {
+    const int v = tune(key);
+    return v < 0 ? def : v;
+}
+
 // How a batch is walked: a "plane" is what one sampler pass sees -- a whole
 // NHWC image (cc = c interleaved channels) or one NCHW channel plane (cc = 1).
 struct PlaneGeom {
@@ -97,6 +104,7 @@ struct ResizeLaunch {
     int interleave;              // resize_kernel: 1 = tasks grid-stride in address order, 0 = strips
     int area_x, area_y;          // INTER_AREA integer block (launch_resize_area)
     float area_scale;            // INTER_AREA: 1.f / (area_x * area_y)
+    int area_half_up;            // INTER_AREA u8 2x2, cn 1/3/4: (sum + 2) >> 2 (ResizeAreaFastVec fast_mode)
     ResizePlanDev plan;
     NormSpec norm;
 };
@@ -131,9 +139,6 @@ struct WarpLaunch {
     NormSpec norm;
 };
 hipError_t launch_warp(const WarpLaunch& L, hipStream_t s);
-// u8 warp with each tile's source box staged in LDS (k_warp_tile.hip)
-bool warp_tile_applies(const WarpLaunch& L);
-hipError_t launch_warp_tile(const WarpLaunch& L, hipStream_t s);
 
 struct CopyLaunch {                // crop / clone: row copies
     PlaneGeom src;                 // base already offset to the crop origin

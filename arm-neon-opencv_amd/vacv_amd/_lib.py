@@ -83,7 +83,15 @@ SIGNATURES = {
     "vacv_cvt_color_resize_normalize": ([_IMG, _IMG, _I, _I, _I, _FP, _FP, _P], _I),
     "vacv_stream_synchronize": ([_P], _I),
     "vacv_release_workspace": ([], _I),
+    "vacv_set_tuning": ([_I, _I], _I),
+    "vacv_get_tuning": ([_I], _I),
 }
+
+# kernel-variant knobs (VACV_TUNE_*, include/vacv_hip.h)
+TUNE = {"RESIZE_DIRECT": 0, "CUBIC_DIRECT": 1, "RESIZE_INTERLEAVE": 2, "RESIZE_ROWS": 3, "DIRECT_XCD": 4,
+        "WARP_PX": 5, "NEAREST_KERNEL": 6, "AREA_KERNEL": 7, "AREA_ROWS": 8, "COLOR_CHUNKS": 9,
+        "RESIZE_WGS": 10, "RESIZE_TILE_H": 11, "RESIZE_TILE_W": 12, "RESIZE_WORK": 13, "RESIZE_ROWS_BYTES": 14,
+        "WARP_KERNEL": 15, "DIRECT_ALIGN": 16}
 
 _lib = None
 
@@ -97,12 +105,11 @@ def build(quiet: bool = True) -> None:
     subprocess.run(cmd, check=True)
 
 
-def load(path: Path = None) -> ctypes.CDLL:
+def load() -> ctypes.CDLL:
     global _lib
     if _lib is not None:
         return _lib
-    if path is None:  # VACV_HIP_LIB: an alternative build of the same ABI (kernel experiments)
-        path = Path(os.environ.get("VACV_HIP_LIB", str(HIP_LIB)))
+    path = HIP_LIB
     if not path.exists():
         raise ImportError(
             f"{path} is missing: the vacv HIP library has not been built "

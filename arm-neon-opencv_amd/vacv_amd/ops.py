@@ -354,3 +354,32 @@ def mean_stddev(src: torch.Tensor, layout: int = NHWC, stream=None) -> Tuple[tor
     check("vacv_mean_stddev", L.load().vacv_mean_stddev(ctypes.byref(describe(s4, layout)), mean.data_ptr(),
                                                         std.data_ptr(), _stream(stream)))
     return mean, std
+
+
+def set_tuning(name: str, value: int) -> int:
+    """Select a kernel variant (VACV_TUNE_<name>, include/vacv_hip.h); value
+    < 0 restores the built-in choice.  Returns the previous value."""
+    key = L.TUNE[name]
+    lib = L.load()
+    old = lib.vacv_get_tuning(key)
+    check("vacv_set_tuning", lib.vacv_set_tuning(key, int(value)))
+    return old
+
+
+class tuning:
+    """Context manager: `with ops.tuning(WARP_KERNEL=0): ...` runs the block
+    with those kernel variants and restores the previous choices after."""
+
+    def __init__(self, **knobs):
+        self.knobs = knobs
+        self.old = {}
+
+    def __enter__(self):
+        for k, v in self.knobs.items():
+            self.old[k] = set_tuning(k, v)
+        return self
+
+    def __exit__(self, *exc):
+        for k, v in self.old.items():
+            set_tuning(k, v)
+        return False

@@ -19,8 +19,14 @@ Other BASELINE configs (--workload; the default is the headline above):
                 decode + resize + normalize + layout in one kernel, 256 per GPU
 The roofline covers the step's dominant kernel (HIP events around it alone).
 
-Multi-GPU: torchrun one process per GPU; images are independent, so each rank
-owns its own batch (weak scaling) and there is no data-path collective.
+Multi-GPU: one process per GPU; images are independent, so each rank owns its
+own batch (weak scaling) and there is no data-path collective (cfg5's
+statistics are the one RCCL all-reduce).  Either torchrun starts the ranks
+(WORLD_SIZE in the environment must then equal --gpus), or `bench.py --gpus N`
+with no WORLD_SIZE spawns the N rank processes itself before anything touches
+the GPU (127.0.0.1 rendezvous) and exits with the first failing rank's status.
+--dry-run exercises that launcher and the rank protocol on CPU (gloo, a CPU
+stand-in step, no measurement): the multi-rank CPU test uses it.
 Timing: barrier + synchronize around exactly --steps steps, max over ranks.
 
 Also reported: the roofline of the kernel (algorithmic bytes per launch /
@@ -62,7 +68,41 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--graph", action="store_true",
                     help="replay the step from a captured HIP graph (measured no faster than eager launches)")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="launcher / rank-protocol check on CPU: gloo, a CPU stand-in step, no GPU, no measurement")
     return ap.parse_args()
+
+
+def spawn_ranks(n: int) -> int:
+    """`bench.py --gpus N` outside torchrun: start N rank processes (RANK /
+    LOCAL_RANK / WORLD_SIZE / MASTER_* as torchrun sets them), wait for all,
+    return the first non-zero exit status.  The parent never touches the GPU
+    (no torch import), so each child owns its device from a clean process."""
+    import signal
+    import socket
+    import subprocess
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, str(Path(__file__).resolve())] + sys.argv[1:], env=env))
+    rc = 0
+    pending = list(procs)
+    while pending:
+        for p in list(pending):
+            code = p.poll()
+            if code is None:
+                continue
+            pending.remove(p)
+            if code != 0 and rc == 0:
+                rc = code if code > 0 else 128 - code
+                for q in pending:  # one rank failed: the others would wait at a barrier forever
+                    q.send_signal(signal.SIGTERM)
+        time.sleep(0.05)
+    return rc
 
 
 def ensure_built():
@@ -127,12 +167,39 @@ def cpu_case(workload: str):
     return one, imgs, W_IN * H_IN, kind, "1920x1080x3 u8 frames, resize_naive 640x360 + u8->fp32 + normalize"
 
 
+def host_cpus():
+    """(threads to use, description): the CPUs this process may actually run
+    on -- its affinity mask, capped by a cgroup-v2 `cpu.max` quota when one is
+    set (the GPU box's container shows the whole machine in nproc but grants a
+    CPU share) -- and the CPU model from /proc/cpuinfo."""
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    quota = None
+    try:
+        q, period = Path("/sys/fs/cgroup/cpu.max").read_text().split()[:2]
+        if q != "max":
+            quota = int(q) / int(period)
+    except (OSError, ValueError):
+        pass
+    threads = max(1, min(aff, int(quota + 0.999)) if quota else aff)
+    model = "unknown"
+    try:
+        for line in Path("/proc/cpuinfo").read_text().splitlines():
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    desc = f"{model}; affinity {aff} CPUs" + (f", cgroup cpu.max quota {quota:g} CPUs" if quota else ", no cgroup quota")
+    return threads, model, desc
+
+
 def cpu_baseline(budget_s: float, workload: str = "resize_normalize"):
     """The reference's own CPU path of the workload on the host, on a bounded
     sample: first on 1 thread, then batch-parallel with one image per thread
-    on up to 16 threads (the GPU box's CPU share; ctypes releases the GIL, so
-    the reference's loops run concurrently).  SURVEY.md 8(d) asks for both;
-    the multi-core figure is the reported baseline."""
+    on every CPU the process may use (host_cpus: affinity capped by the cgroup
+    quota; ctypes releases the GIL, so the reference's loops run concurrently).
+    SURVEY.md 8(d) asks for both; the multi-core figure is the reported
+    baseline.  oracle/_ref is the reference's sources built at -O3."""
     from concurrent.futures import ThreadPoolExecutor
     one, imgs, px, kind, what = cpu_case(workload)
 
@@ -152,14 +219,14 @@ def cpu_baseline(budget_s: float, workload: str = "resize_normalize"):
         return n, el
 
     n1, el1 = run(1, budget_s * 0.4)
-    threads = max(1, min(16, os.cpu_count() or 1))
+    threads, model, desc = host_cpus()
     nt, elt = run(threads, budget_s * 0.6)
     v1 = n1 * px / el1 / 1e6
     vt = nt * px / elt / 1e6
     return {"value": round(vt, 3), "unit": "Mpixels/s", "cores": threads, "kind": kind,
-            "value_1_core": round(v1, 3),
+            "value_1_core": round(v1, 3), "cpu_model": model,
             "sample": f"synthetic {what}: {nt} frames on {threads} threads (one frame per thread) in {elt:.1f} s; "
-                      f"{n1} frames on 1 thread in {el1:.1f} s"}
+                      f"{n1} frames on 1 thread in {el1:.1f} s; host: {desc}"}
 
 
 def pmc_traffic(workload: str = "resize_normalize"):
@@ -243,17 +310,68 @@ def make_workload(name: str, batch: int, dev, rank: int, world: int, ops) -> dic
             "main": lambda stream=None: ops.resize_normalize(src, W_OUT, H_OUT, MEAN, STD, out=dst, stream=stream)}
 
 
-def main():
-    args = parse()
+def dry_run(args, world: int, rank: int) -> None:
+    """The rank protocol of main() on CPU over gloo: barrier + max-over-ranks
+    timing of exactly --steps stand-in steps (a small torch CPU resize; cfg5
+    also all-reduces a (c, 2) fp64 sums tensor as its real step does).  The
+    JSON line is marked "dry_run" and carries no roofline: it measures nothing."""
     import torch
     import torch.distributed as dist
+    if world > 1:
+        dist.init_process_group("gloo")
+        world = dist.get_world_size()
+    x = torch.rand(4, 3, 108, 192)
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    def step():
+        torch.nn.functional.interpolate(x, size=(36, 64), mode="bilinear", align_corners=False)
+        if args.workload == "cubic_stats" and world > 1:
+            s = torch.ones(3, 2, dtype=torch.float64)
+            dist.all_reduce(s)
+            assert float(s[0, 0]) == world
+
+    for _ in range(args.warmup):
+        step()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    if world > 1:
+        dist.barrier()
+    t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    if rank == 0:
+        print(json.dumps({"metric": "dry run (launcher check, not a measurement)", "value": None, "unit": None,
+                          "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+                          "ms_per_step": round(float(t[0]) * 1e3 / args.steps, 4), "dry_run": True,
+                          "config": {"workload": args.workload, "parallelism": f"dp{world}"}}), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def main():
+    args = parse()
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and args.gpus > 1:
+        sys.exit(spawn_ranks(args.gpus))  # before anything touches the GPU
+    world = int(env_world or "1")
+    if world != args.gpus:
+        print(f"bench: --gpus {args.gpus} but WORLD_SIZE={world}: the rank count must equal --gpus",
+              file=sys.stderr)
+        sys.exit(2)
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.dry_run:
+        return dry_run(args, world, rank)
+
+    import torch
+    import torch.distributed as dist
     if world > 1:
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        world = dist.get_world_size()  # what RCCL agreed on, reported as n_gpus
     dev = torch.device("cuda", local if world > 1 else 0)
     torch.cuda.set_device(dev)
 

@@ -221,6 +221,35 @@ int vacv_cvt_color_resize_normalize(const vacv_image* src, const vacv_image* dst
 
 /* ---- runtime ---------------------------------------------------------- */
 
+/* Kernel-variant knobs, for A/B measurement and the parity tests that check
+ * every variant against the same oracle; normal callers never need them.
+ * Each starts from the environment variable of the same name (read once,
+ * when the library loads), else -1 = the built-in choice. */
+enum {
+    VACV_TUNE_RESIZE_DIRECT = 0,     /* u8 bilinear: 0 staged, 1 gather kernel for one-tap rows, 2 gather always */
+    VACV_TUNE_CUBIC_DIRECT = 1,      /* u8 cubic: 0 staged kernel, else the gather kernel */
+    VACV_TUNE_RESIZE_INTERLEAVE = 2, /* staged kernel: 0 strip order, else address-ordered tasks */
+    VACV_TUNE_RESIZE_ROWS = 3,       /* 1: the whole-row staged kernel */
+    VACV_TUNE_DIRECT_XCD = 4,        /* gather kernel block order: 0 plain, 1 XCD-contiguous */
+    VACV_TUNE_WARP_PX = 5,           /* warp gather kernel: lane blocks per wave (4, 5, 8, 10) */
+    VACV_TUNE_NEAREST_KERNEL = 6,    /* INTER_NEAREST: 0 per-pixel kernel, else row-staged when it applies */
+    VACV_TUNE_AREA_KERNEL = 7,       /* u8 INTER_AREA: 1 per-pixel kernel, 2 dword column sums */
+    VACV_TUNE_AREA_ROWS = 8,         /* u8 INTER_AREA column sums: output rows per workgroup */
+    VACV_TUNE_COLOR_CHUNKS = 9,      /* 1: the chunked fp32 NV21 kernel */
+    VACV_TUNE_RESIZE_WGS = 10,       /* staged kernel: workgroups launched */
+    VACV_TUNE_RESIZE_TILE_H = 11,    /* staged kernel planner: tile height */
+    VACV_TUNE_RESIZE_TILE_W = 12,    /* staged kernel planner: tile width */
+    VACV_TUNE_RESIZE_WORK = 13,      /* staged kernel planner: work per thread */
+    VACV_TUNE_RESIZE_ROWS_BYTES = 14,/* whole-row kernel planner: output bytes per workgroup */
+    VACV_TUNE_WARP_KERNEL = 15,      /* u8 warp: 0 gather kernel, 1 tile-staged kernel where it applies */
+    VACV_TUNE_DIRECT_ALIGN = 16,     /* gather kernel: 0 flat pixel order, 1 row-aligned waves */
+    VACV_TUNE_COUNT = 17
+};
+/* value < 0 restores the built-in choice.  Returns VACV_OK or INVALID_ARG. */
+int vacv_set_tuning(int key, int value);
+/* the current value (-1 = built-in), or VACV_ERR_INVALID_ARG for a bad key */
+int vacv_get_tuning(int key);
+
 /* Block until all work this library queued on `stream` has finished. */
 int vacv_stream_synchronize(void* stream);
 /* Release the per-device workspace the statistics paths cache. */

@@ -222,17 +222,26 @@ void oracle_resize_nearest(const void* src, int w_in, int h_in, int cc, int esiz
  * to cv::resize (resize.cpp:44-49); its own attempt,
  * src_deprecated/img_resize_inter_area.cpp:21-55, builds OpenCV's ofs/xofs
  * tables and stops.  OpenCV 2.4.13.4's published algorithm (imgwarp.cpp,
- * resizeAreaFast_ without a vector op, as on the ARM build), restated: with
- * ax = w_in / w_out, ay = h_in / h_out exact integers, output (x, y, k) is
- *   sum over the block rows r, columns q (taps grouped 4 per add as its
- *   CV_ENABLE_UNROLLED loop) of src(x*ax + q, y*ay + r, k), times 1.f/(ax*ay)
- *   in fp32; u8 rounds half to even (saturate_cast<uchar> = lrint).
+ * resizeAreaFast_Invoker), restated: with ax = w_in / w_out, ay = h_in / h_out
+ * exact integers, output (x, y, k) is
+ *  - u8, ax == ay == 2 and cn in {1, 3, 4}: (a + b + c + d + 2) >> 2, the
+ *    ResizeAreaFastVec<uchar>::fast_mode path (scalar loop and its SSE2/NEON
+ *    vector op alike), i.e. the 2x2 block mean rounded half UP;
+ *  - otherwise: the sum over the block rows r, columns q (taps grouped 4 per
+ *    add as its CV_ENABLE_UNROLLED loop) of src(x*ax + q, y*ay + r, k), times
+ *    1.f/(ax*ay) in fp32; u8 rounds half to even (saturate_cast<uchar> =
+ *    cvRound = lrint).  For fp32 2x2 blocks (cn 1/4) the ARM build's NEON
+ *    ResizeAreaFastVec_SIMD_32f sums (a+b)+(c+d) and multiplies by 0.25f on
+ *    its vector body; this restatement keeps the generic order there (PARITY
+ *    UNPINNED for fp32 2x2, by at most one ulp).
  * PARITY UNPINNED: no reference entry runs this path here and its tests hold
  * no area output.  esize 1 (u8, int sum) or 4 (fp32, float sum). */
 void oracle_resize_area(const void* src, int w_in, int h_in, int cc, int esize,
                         void* dst, int w_out, int h_out) {
     const int ax = w_in / w_out, ay = h_in / h_out, area = ax * ay;
     const float scale = 1.f / (float)area;
+    /* ResizeAreaFastVec<uchar>::fast_mode (scale 2x2, cn 1/3/4) */
+    const int fast22 = esize == 1 && ax == 2 && ay == 2 && (cc == 1 || cc == 3 || cc == 4);
     for (int y = 0; y < h_out; ++y)
         for (int x = 0; x < w_out; ++x)
             for (int k = 0; k < cc; ++k) {
@@ -258,7 +267,9 @@ void oracle_resize_area(const void* src, int w_in, int h_in, int cc, int esize,
                     else fsum += ((const float*)src)[i];
                 }
                 const size_t o = ((size_t)y * w_out + x) * cc + k;
-                if (esize == 1) {
+                if (esize == 1 && fast22) {
+                    ((uint8_t*)dst)[o] = (uint8_t)((isum + 2) >> 2);
+                } else if (esize == 1) {
                     const float m = (float)isum * scale;
                     ((uint8_t*)dst)[o] = (uint8_t)lrintf(m);
                 } else {

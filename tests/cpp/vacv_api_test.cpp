@@ -533,7 +533,8 @@ Result tensor_semantics_case() {
     } catch (const std::runtime_error&) {
     }
     {
-        // integer INTER_AREA (OpenCV 2.4 resizeAreaFast_): 2x2 block means
+        // integer INTER_AREA (OpenCV 2.4 resizeAreaFast_): 2x2 block means of a
+        // 3-channel image take ResizeAreaFastVec's fast_mode, rounded half up
         Tensor o;
         va_cv::resize(img, o, VSize(160, 90), 0, 0, INTER_AREA);
         const uint8_t* s = static_cast<const uint8_t*>(img.data);
@@ -543,7 +544,7 @@ Result tensor_semantics_case() {
                 for (int k = 0; k < 3; ++k) {
                     const int sum = s[((2 * y) * 320 + 2 * x) * 3 + k] + s[((2 * y) * 320 + 2 * x + 1) * 3 + k] +
                                     s[((2 * y + 1) * 320 + 2 * x) * 3 + k] + s[((2 * y + 1) * 320 + 2 * x + 1) * 3 + k];
-                    const int want_v = (int)std::nearbyint((float)sum * 0.25f);  // half to even
+                    const int want_v = (sum + 2) >> 2;  // ResizeAreaFastVec fast_mode: half up
                     if (d[(y * 160 + x) * 3 + k] != want_v) { err += "INTER_AREA value; "; y = 90; x = 160; break; }
                 }
     }

@@ -34,3 +34,38 @@ def test_workload_choices_match_parser(monkeypatch):
     for w in WORKLOADS:
         monkeypatch.setattr(sys, "argv", ["bench.py", "--workload", w])
         assert bench.parse().workload == w
+
+
+def _run_bench(args, env_extra=None, timeout=240):
+    import json
+    import os
+    import subprocess
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK",
+                                                                "MASTER_ADDR", "MASTER_PORT")}
+    env.update(env_extra or {})
+    p = subprocess.run([sys.executable, str(REPO / "bench.py")] + args, env=env, capture_output=True,
+                       text=True, timeout=timeout)
+    lines = [json.loads(l) for l in p.stdout.splitlines() if l.startswith("{")]
+    return p.returncode, lines, p.stderr
+
+
+@pytest.mark.parametrize("workload", ["resize_normalize", "cubic_stats"])
+def test_gpus_flag_spawns_ranks(workload):
+    """bench.py --gpus 2 with no torchrun environment starts two rank processes
+    itself (gloo here, via --dry-run); rank 0 alone prints the line, and the
+    rank count comes from the process group, not from the flag."""
+    rc, lines, err = _run_bench(["--gpus", "2", "--dry-run", "--steps", "3", "--warmup", "1",
+                                 "--workload", workload])
+    assert rc == 0, err
+    assert len(lines) == 1, lines
+    out = lines[0]
+    assert out["n_gpus"] == 2 and out["config"]["parallelism"] == "dp2" and out["dry_run"] is True
+    assert out["steps"] == 3 and out["warmup"] == 1
+
+
+def test_gpus_flag_must_match_world_size():
+    """Under torchrun the flag and WORLD_SIZE must agree: a mismatch fails
+    instead of reporting a 1-GPU number under an N-GPU label."""
+    rc, lines, err = _run_bench(["--gpus", "4", "--dry-run", "--steps", "1", "--warmup", "0"],
+                                {"WORLD_SIZE": "1", "RANK": "0", "LOCAL_RANK": "0"})
+    assert rc != 0 and not lines and "WORLD_SIZE" in err

@@ -71,12 +71,16 @@ SIZES = [((23, 37), 1), ((48, 64), 3), ((61, 97), 3), ((5, 7), 3), ((16, 16), 4)
 OUTS = [(20, 11), (33, 29), (111, 40), (7, 5), (2, 2), (160, 90), (1, 1), (300, 7)]
 
 
-@pytest.mark.parametrize("direct", ["1", "2"])
+@pytest.mark.parametrize("direct", [1, 2])
 @pytest.mark.parametrize("mode", [0, 1, 2])
-def test_resize_linear_u8_hwc(ops, dev, oracle, mode, direct, monkeypatch):
-    # direct "1": the default dispatch (gather kernel for one-tap-row
-    # geometries, staged kernel otherwise); "2": the gather kernel everywhere
-    monkeypatch.setenv("VACV_RESIZE_DIRECT", direct)
+def test_resize_linear_u8_hwc(ops, dev, oracle, mode, direct):
+    # direct 1: the default dispatch (gather kernel for one-tap-row
+    # geometries, staged kernel otherwise); 2: the gather kernel everywhere
+    with ops.tuning(RESIZE_DIRECT=direct):
+        _resize_linear_u8_hwc(ops, dev, oracle, mode)
+
+
+def _resize_linear_u8_hwc(ops, dev, oracle, mode):
     for i, ((h, w), c) in enumerate(SIZES):
         imgs = [synthetic_image(100 * i + k, h, w, c) for k in range(3)]
         src = to_dev(batch(imgs) if c > 1 else batch(imgs)[..., None], dev)
@@ -128,9 +132,9 @@ def test_resize_cubic(ops, dev, oracle):
             assert_same(got[k], oracle.resize_cubic(chw[k], 31, 17), "cubic chw")
 
 
-def test_cubic_direct_and_staged_agree(ops, dev, oracle, monkeypatch):
+def test_cubic_direct_and_staged_agree(ops, dev, oracle):
     """u8 cubic runs on the per-pixel gather kernel (k_cubic_direct.hip) unless
-    VACV_CUBIC_DIRECT=0 selects the staged kernel (k_resize.hip).  Both are
+    VACV_TUNE_CUBIC_DIRECT = 0 selects the staged kernel (k_resize.hip).  Both are
     the reference's arithmetic, so they agree bit for bit: BASELINE cfg5 at
     full size (2560x1440 -> 224x224, batch 6), normalized, a pitched source,
     NCHW planes and an upscale; image 0 is also checked against the oracle."""
@@ -147,13 +151,12 @@ def test_cubic_direct_and_staged_agree(ops, dev, oracle, monkeypatch):
              lambda: ops.resize(src[:1, :100, :90], 250, 333, interpolation=INTER_CUBIC),
              lambda: ops.resize(ops.change_layout(src[:2], NCHW), 97, 61, interpolation=INTER_CUBIC, layout=NCHW)]
     for i, fn in enumerate(cases):
-        monkeypatch.setenv("VACV_CUBIC_DIRECT", "1")
-        a = fn()
-        monkeypatch.setenv("VACV_CUBIC_DIRECT", "0")
-        b = fn()
+        with ops.tuning(CUBIC_DIRECT=1):
+            a = fn()
+        with ops.tuning(CUBIC_DIRECT=0):
+            b = fn()
         torch.cuda.synchronize(dev)
         assert torch.equal(a, b), f"case {i}: {(a != b).sum().item()} values differ"
-    monkeypatch.delenv("VACV_CUBIC_DIRECT")
     got = host(ops.resize(src[:1], 224, 224, interpolation=INTER_CUBIC))[0]
     assert_same(got, oracle.resize_cubic(oracle.u8_to_f32(imgs[0]), 224, 224), "cfg5 image 0 vs oracle")
     del src, big
@@ -223,9 +226,48 @@ def test_resize_nearest(ops, dev, oracle):
     assert_same(got, oracle.resize_nearest(img, 30, 20), "nearest pitched")
 
 
+def test_nearest_area_kernel_variants_agree(ops, dev, oracle):
+    """Every INTER_NEAREST / u8 INTER_AREA kernel variant gives the same bytes
+    at BASELINE's 1080p frame: nearest row-staged (default where the source is
+    16-byte aligned, its row fits 64 KiB and the sample stride is short) vs
+    the per-pixel kernel (VACV_TUNE_NEAREST_KERNEL = 0); area 16-byte column
+    sums (default) vs dword column sums (2) vs per-pixel (1); plus an fp32 row
+    past 64 KiB (5600 px x 3 ch: the per-pixel fallback) and a strong
+    horizontal downscale (wide stride: the per-pixel kernel) vs the oracle."""
+    import torch
+    from vacv_amd import INTER_AREA, INTER_NEAREST
+    imgs = np.stack([synthetic_image(750 + k, 1080, 1920, 3) for k in range(2)])
+    src = to_dev(imgs, dev)
+    for wo, ho in [(640, 360), (960, 540), (1280, 720), (3000, 1500)]:
+        a = ops.resize(src, wo, ho, interpolation=INTER_NEAREST)
+        with ops.tuning(NEAREST_KERNEL=0):
+            b = ops.resize(src, wo, ho, interpolation=INTER_NEAREST)
+        assert torch.equal(a, b), f"nearest variants differ -> {wo}x{ho}"
+        if wo <= 1920:
+            an = ops.resize_normalize(src, wo, ho, MEAN, STD, interpolation=INTER_NEAREST)
+            with ops.tuning(NEAREST_KERNEL=0):
+                bn = ops.resize_normalize(src, wo, ho, MEAN, STD, interpolation=INTER_NEAREST)
+            assert torch.equal(an, bn), f"nearest normalize variants differ -> {wo}x{ho}"
+    assert_same(host(a)[1], oracle.resize_nearest(imgs[1], 3000, 1500), "nearest upscale")
+    for wo, ho in [(640, 360), (960, 540), (480, 270)]:
+        a = ops.resize(src, wo, ho, interpolation=INTER_AREA)
+        for knob in (1, 2):
+            with ops.tuning(AREA_KERNEL=knob):
+                b = ops.resize(src, wo, ho, interpolation=INTER_AREA)
+            assert torch.equal(a, b), f"area variant {knob} differs -> {wo}x{ho}"
+        assert_same(host(a)[0], oracle.resize_area(imgs[0], wo, ho), f"area 1080p -> {wo}x{ho}")
+    wide = synthetic_image(760, 9, 5600, 3).astype(np.float32) + 0.25
+    got = host(ops.resize(to_dev(wide[None], dev), 700, 4, interpolation=INTER_NEAREST))[0]
+    assert_same(got, oracle.resize_nearest(wide, 700, 4), "nearest fp32 row > 64 KiB")
+    strided = synthetic_image(761, 40, 4096, 3).astype(np.float32)
+    got = host(ops.resize(to_dev(strided[None], dev), 32, 20, interpolation=INTER_NEAREST))[0]
+    assert_same(got, oracle.resize_nearest(strided, 32, 20), "nearest 128x horizontal downscale")
+
+
 def test_resize_area(ops, dev, oracle):
     """INTER_AREA at integer downscales (OpenCV 2.4 resizeAreaFast_, parity
-    unpinned -- see oracle/vacv_oracle.c): u8 (half-to-even rounding) and fp32
+    unpinned -- see oracle/vacv_oracle.c): u8 (half-to-even rounding; 2x2
+    blocks of 1/3/4 channels half up, ResizeAreaFastVec's fast_mode) and fp32
     (OpenCV's four-tap summation order, bit-exact), NHWC c = 1..4 and NCHW,
     block sizes 1x1 .. 7x5 incl. areas that are not a multiple of 4, the
     widen / normalize epilogues, a pitched source, and BASELINE's 1080p frame
@@ -251,6 +293,9 @@ def test_resize_area(ops, dev, oracle):
             got = host(ops.resize(to_dev(chw[None], dev), w // 3, h // 2, interpolation=INTER_AREA, layout=NCHW))[0]
             for k in range(c):
                 assert_same(got[k], oracle.resize_area(chw[k], w // 3, h // 2), "area chw")
+            got = host(ops.resize(to_dev(chw[None], dev), w // 2, h // 2, interpolation=INTER_AREA, layout=NCHW))[0]
+            for k in range(c):  # NCHW planes are 1-channel: the 2x2 fast_mode rounding
+                assert_same(got[k], oracle.resize_area(chw[k], w // 2, h // 2), "area chw 2x2")
             got = host(ops.resize_normalize(to_dev(img[None], dev), w // 2, h // 2, MEAN, STD,
                                             interpolation=INTER_AREA))[0]
             want = oracle.normalize(oracle.u8_to_f32(oracle.resize_area(img, w // 2, h // 2)), MEAN, STD)
@@ -260,6 +305,19 @@ def test_resize_area(ops, dev, oracle):
     big[0, 7:67, 3:81] = to_dev(img, dev)
     got = host(ops.resize(big[:, 7:67, 3:81], 26, 20, interpolation=INTER_AREA))[0]
     assert_same(got, oracle.resize_area(img, 26, 20), "area pitched")
+    # 2x2 ties: block sums 4k + 2 round half UP for 1/3/4 channels
+    # (ResizeAreaFastVec fast_mode) and half to even for 2 (generic path)
+    for c in (1, 2, 3, 4):
+        blk = np.zeros((2, 8, c), np.uint8)
+        for j, sm in enumerate([2, 6, 10, 14]):
+            q = [sm // 4 + (1 if t < sm % 4 else 0) for t in range(4)]
+            blk[0, 2 * j], blk[0, 2 * j + 1], blk[1, 2 * j], blk[1, 2 * j + 1] = q
+        got = host(ops.resize(to_dev(blk[None], dev), 4, 1, interpolation=INTER_AREA))[0]
+        want = [1, 2, 3, 4] if c != 2 else [0, 2, 2, 4]
+        assert got.reshape(4, c)[:, 0].tolist() == want, (c, got)
+        big = np.tile(blk, (64, 96, 1))  # the column-sum kernel (16-byte aligned rows)
+        got = host(ops.resize(to_dev(big[None], dev), 384, 64, interpolation=INTER_AREA))[0]
+        assert_same(got.reshape(64, 384, c), oracle.resize_area(big, 384, 64).reshape(64, 384, c), f"area tie c{c}")
 
 
 def test_resize_full_size_batch(ops, dev, oracle):
@@ -278,10 +336,10 @@ def test_resize_full_size_batch(ops, dev, oracle):
     assert_same(got, want, "pitched")
 
 
-def test_resize_u8_kernels_agree_and_pitched_out(ops, dev, oracle, monkeypatch):
+def test_resize_u8_kernels_agree_and_pitched_out(ops, dev, oracle):
     """u8 bilinear with one weighted source row per output row runs on the
     per-pixel gather kernel (k_resize_direct.hip), the rest on the LDS-staged
-    strip kernel; VACV_RESIZE_DIRECT=2 forces the gather kernel for every
+    strip kernel; VACV_TUNE_RESIZE_DIRECT = 2 forces the gather kernel for every
     geometry and 0 the strip kernel.  Both must give identical bytes / floats
     at full size (one-tap and two-tap geometries), and the gather kernel must
     honour a pitched (sub-window) destination in every store path: 16-byte
@@ -292,32 +350,31 @@ def test_resize_u8_kernels_agree_and_pitched_out(ops, dev, oracle, monkeypatch):
     src = to_dev(batch(imgs), dev)
     for wo, ho in [(640, 360), (1280, 720), (333, 129), (64, 1000)]:
         for mode in (0, 1, 2):
-            monkeypatch.setenv("VACV_RESIZE_DIRECT", "2")
-            a8 = ops.resize(src, wo, ho, mode=mode)
-            an = ops.resize_normalize(src, wo, ho, MEAN, STD, mode=mode)
-            monkeypatch.setenv("VACV_RESIZE_DIRECT", "0")
-            b8 = ops.resize(src, wo, ho, mode=mode)
-            bn = ops.resize_normalize(src, wo, ho, MEAN, STD, mode=mode)
-            monkeypatch.delenv("VACV_RESIZE_DIRECT")
+            with ops.tuning(RESIZE_DIRECT=2):
+                a8 = ops.resize(src, wo, ho, mode=mode)
+                an = ops.resize_normalize(src, wo, ho, MEAN, STD, mode=mode)
+            with ops.tuning(RESIZE_DIRECT=0):
+                b8 = ops.resize(src, wo, ho, mode=mode)
+                bn = ops.resize_normalize(src, wo, ho, MEAN, STD, mode=mode)
             assert torch.equal(a8, b8), f"u8 kernels differ {wo}x{ho} mode {mode}"
             assert torch.equal(an, bn), f"normalize kernels differ {wo}x{ho} mode {mode}"
     small = synthetic_image(61, 97, 151, 3)
     s = to_dev(small[None], dev)
-    monkeypatch.setenv("VACV_RESIZE_DIRECT", "2")
-    for wo, ho, dt in [(80, 50, torch.uint8), (77, 55, torch.uint8), (64, 31, torch.float32), (41, 23, torch.float32)]:
-        big = torch.zeros((1, ho + 9, wo + 24, 3), dtype=dt, device=dev)
-        view = big[:, 4:4 + ho, 8:8 + wo]
-        if dt == torch.uint8:
-            ops.resize(s, wo, ho, out=view)
-            want = oracle.resize_linear(small, wo, ho)
-        else:
-            ops.resize_normalize(s, wo, ho, MEAN, STD, out=view)
-            want = oracle.normalize(oracle.u8_to_f32(oracle.resize_linear(small, wo, ho)), MEAN, STD)
-        got = host(big)
-        assert_same(got[0, 4:4 + ho, 8:8 + wo], want, f"pitched out {wo}x{ho} {dt}")
-        rim = got.copy()
-        rim[0, 4:4 + ho, 8:8 + wo] = 0
-        assert not rim.any(), f"pitched out {wo}x{ho}: wrote outside the window"
+    with ops.tuning(RESIZE_DIRECT=2):
+        for wo, ho, dt in [(80, 50, torch.uint8), (77, 55, torch.uint8), (64, 31, torch.float32), (41, 23, torch.float32)]:
+            big = torch.zeros((1, ho + 9, wo + 24, 3), dtype=dt, device=dev)
+            view = big[:, 4:4 + ho, 8:8 + wo]
+            if dt == torch.uint8:
+                ops.resize(s, wo, ho, out=view)
+                want = oracle.resize_linear(small, wo, ho)
+            else:
+                ops.resize_normalize(s, wo, ho, MEAN, STD, out=view)
+                want = oracle.normalize(oracle.u8_to_f32(oracle.resize_linear(small, wo, ho)), MEAN, STD)
+            got = host(big)
+            assert_same(got[0, 4:4 + ho, 8:8 + wo], want, f"pitched out {wo}x{ho} {dt}")
+            rim = got.copy()
+            rim[0, 4:4 + ho, 8:8 + wo] = 0
+            assert not rim.any(), f"pitched out {wo}x{ho}: wrote outside the window"
 
 
 def test_resize_normalize(ops, dev, oracle):
@@ -421,15 +478,14 @@ def test_warp_affine_config_and_harness(ops, dev, oracle, golden):
     assert_same(got[1], want, "warp_affine_normalize")
 
 
-def test_warp_tile_and_gather_kernels_agree(ops, dev, oracle, monkeypatch):
-    """VACV_WARP_TILE=1 runs u8 warps on the LDS-staged tile kernel
-    (k_warp_tile.hip, opt-in: measured slower) when the tile's source box fits
-    its LDS budget and the source rows are 4-byte aligned; the default is the
-    per-pixel gather kernel (k_warp.hip).  VACV_WARP_LW / VACV_WARP_PX switch
-    the gather kernel's lane blocks (64 x 1 or 16 x 4; 4 or 8 per wave).
-    Identical outputs at full size for rotations,
-    flips, shears, strong down-scales (box over budget: the gather kernel),
-    fused normalisation, NCHW planes and a pitched destination."""
+def test_warp_kernels_agree(ops, dev, oracle):
+    """u8 warps run on the LDS-staged tile kernel (k_warp_staged.hip) where its
+    source footprint fits the LDS budget, else on the per-pixel gather kernel
+    (k_warp.hip); VACV_TUNE_WARP_KERNEL = 0 forces the gather kernel and
+    VACV_TUNE_WARP_PX switches its lane blocks per wave (4, 5, 8, 10).
+    Identical outputs at full size for rotations, flips, shears, strong
+    down-scales (footprint over budget: the gather kernel), fused
+    normalisation, NCHW planes and a pitched destination."""
     import torch
     from vacv_amd import NCHW
     imgs = np.stack([synthetic_image(80 + k, 720, 1280, 3) for k in range(2)])
@@ -438,46 +494,42 @@ def test_warp_tile_and_gather_kernels_agree(ops, dev, oracle, monkeypatch):
             ops.rotation_matrix(1.7, -130.0, (640, 360, 500, 300)),
             np.array([-1, 0, 1279, 0, 1, 0], np.float32),            # horizontal flip
             np.array([1.3, 0.2, 100.0, -0.1, 1.45, 50.0], np.float32),  # shear + up-scale
-            np.array([0.25, 0.0, 0.0, 0.0, 0.25, 0.0], np.float32),   # 4x down: box over budget
+            np.array([0.25, 0.0, 0.0, 0.0, 0.25, 0.0], np.float32),   # 4x down: footprint over budget
             np.array([1, 0, 0.5, 0, 1, -0.25], np.float32)]
     for m in mats:
         for wo, ho in [(1280, 720), (333, 211)]:
-            monkeypatch.setenv("VACV_WARP_TILE", "1")
-            a = ops.warp_affine(src, m, wo, ho)
-            an = ops.warp_affine_normalize(src, m, wo, ho, MEAN, STD)
-            monkeypatch.setenv("VACV_WARP_TILE", "0")
-            b = ops.warp_affine(src, m, wo, ho)
-            bn = ops.warp_affine_normalize(src, m, wo, ho, MEAN, STD)
-            assert torch.equal(a, b), f"warp kernels differ {m.tolist()} {wo}x{ho}"
-            assert torch.equal(an, bn), f"warp normalize kernels differ {m.tolist()} {wo}x{ho}"
-            for lw, px in (("16", "4"), ("16", "8"), ("64", "4")):
-                monkeypatch.setenv("VACV_WARP_LW", lw)
-                monkeypatch.setenv("VACV_WARP_PX", px)
-                assert torch.equal(ops.warp_affine(src, m, wo, ho), b), f"gather LW={lw} PX={px}"
-                assert torch.equal(ops.warp_affine_normalize(src, m, wo, ho, MEAN, STD), bn), f"gather LW={lw} PX={px} norm"
-            monkeypatch.delenv("VACV_WARP_LW")
-            monkeypatch.delenv("VACV_WARP_PX")
-            monkeypatch.delenv("VACV_WARP_TILE")
-    for c in (1, 2, 4):  # every staged pixel width, odd sizes, both kernels vs the oracle
+            with ops.tuning(WARP_KERNEL=1):
+                a = ops.warp_affine(src, m, wo, ho)
+                an = ops.warp_affine_normalize(src, m, wo, ho, MEAN, STD)
+            with ops.tuning(WARP_KERNEL=0):
+                b = ops.warp_affine(src, m, wo, ho)
+                bn = ops.warp_affine_normalize(src, m, wo, ho, MEAN, STD)
+                assert torch.equal(a, b), f"warp kernels differ {m.tolist()} {wo}x{ho}"
+                assert torch.equal(an, bn), f"warp normalize kernels differ {m.tolist()} {wo}x{ho}"
+                for px in (4, 5, 8, 10):
+                    with ops.tuning(WARP_PX=px):
+                        assert torch.equal(ops.warp_affine(src, m, wo, ho), b), f"gather PX={px}"
+                        assert torch.equal(ops.warp_affine_normalize(src, m, wo, ho, MEAN, STD), bn), \
+                            f"gather PX={px} norm"
+    for c in (1, 2, 3, 4):  # every pixel width, odd sizes, both kernels vs the oracle
         im = synthetic_image(90 + c, 97, 143, c)
         for m in mats[:2]:
-            for flag in ("1", "0"):
-                monkeypatch.setenv("VACV_WARP_TILE", flag)
-                got = host(ops.warp_affine(to_dev(im.reshape(1, 97, 143, c), dev), m, 121, 83))[0]
+            for flag in (1, 0):
+                with ops.tuning(WARP_KERNEL=flag):
+                    got = host(ops.warp_affine(to_dev(im.reshape(1, 97, 143, c), dev), m, 121, 83))[0]
                 assert_same(got.reshape(83, 121, c), oracle.warp_affine(im, m, 121, 83).reshape(83, 121, c),
-                            f"warp c={c} tile={flag}")
-    monkeypatch.setenv("VACV_WARP_TILE", "1")
+                            f"warp c={c} staged={flag}")
     chw = to_dev(np.ascontiguousarray(imgs.transpose(0, 3, 1, 2)), dev)
     got = host(ops.warp_affine(chw, mats[0], 300, 200, layout=NCHW))
     for k in range(3):
-        assert_same(got[1, k], oracle.warp_affine(np.ascontiguousarray(imgs[1, ..., k]), mats[0], 300, 200), "tile chw")
+        assert_same(got[1, k], oracle.warp_affine(np.ascontiguousarray(imgs[1, ..., k]), mats[0], 300, 200), "warp chw")
     big = torch.zeros((1, 130, 230, 3), dtype=torch.uint8, device=dev)
     view = big[:, 3:123, 5:205]
     ops.warp_affine(src[:1], mats[1], 200, 120, out=view)
     g = host(big)
-    assert_same(g[0, 3:123, 5:205], oracle.warp_affine(imgs[0], mats[1], 200, 120), "tile pitched out")
+    assert_same(g[0, 3:123, 5:205], oracle.warp_affine(imgs[0], mats[1], 200, 120), "warp pitched out")
     g[0, 3:123, 5:205] = 0
-    assert not g.any(), "tile kernel wrote outside the window"
+    assert not g.any(), "warp kernel wrote outside the window"
 
 
 # ---------------------------------------------------------------------------

@@ -186,19 +186,43 @@ def test_resize_nearest_restatement(oracle):
 def test_resize_area_restatement(oracle):
     """OpenCV 2.4 resizeAreaFast_ as restated in oracle/vacv_oracle.c (parity
     unpinned), against an independent numpy statement: u8 = rint_half_even(
-    fp32(block sum) * fp32(1/area)); fp32 = the block mean with OpenCV's
-    grouping (exact here: small-integer fp32 inputs sum exactly)."""
+    fp32(block sum) * fp32(1/area)), except 2x2 blocks with 1, 3 or 4
+    channels, which take ResizeAreaFastVec's fast_mode (sum + 2) >> 2 (half
+    up); fp32 = the block mean with OpenCV's grouping (exact here:
+    small-integer fp32 inputs sum exactly)."""
     import numpy as np
     from oracle import synthetic_image
+    for c in (1, 2, 3, 4):
+        img = synthetic_image(4 + c, 30, 42, c)
+        if c == 1:
+            img = img.reshape(30, 42)
+        for ax, ay in [(1, 1), (2, 2), (3, 2), (2, 3), (6, 5), (7, 3)]:
+            wo, ho = 42 // ax, 30 // ay
+            blk = img.reshape(ho, ay, wo, ax, c).astype(np.int64).sum(axis=(1, 3))
+            if ax == 2 and ay == 2 and c != 2:
+                want = ((blk + 2) >> 2).astype(np.uint8)
+            else:
+                want = np.rint(blk.astype(np.float32) * np.float32(1.0 / (ax * ay))).astype(np.uint8)
+            got = oracle.resize_area(img, wo, ho)
+            assert np.array_equal(got.reshape(want.shape), want), (ax, ay, c)
     img = synthetic_image(4, 30, 42, 3)
     for ax, ay in [(1, 1), (2, 2), (3, 2), (6, 5), (7, 3)]:
         wo, ho = 42 // ax, 30 // ay
         blk = img.reshape(ho, ay, wo, ax, 3).astype(np.int64).sum(axis=(1, 3))
-        want = np.rint(blk.astype(np.float32) * np.float32(1.0 / (ax * ay))).astype(np.uint8)
-        assert np.array_equal(oracle.resize_area(img, wo, ho), want), (ax, ay)
         f = img.astype(np.float32)
         wantf = blk.astype(np.float32) * np.float32(np.float32(1) / np.float32(ax * ay))
         assert np.array_equal(oracle.resize_area(f, wo, ho), wantf), (ax, ay)
     # ties round to even: a 2x1 block of (1, 2) averages 1.5 -> 2, (2, 3) -> 2
     tie = np.array([[[1], [2], [2], [3]]], np.uint8).reshape(1, 4)
     assert oracle.resize_area(tie, 2, 1).tolist() == [[2, 2]]
+    # 2x2 ties (sum = 4k + 2) round half UP for cn 1/3/4 and half to even
+    # for cn 2 (the generic path): sums 2 -> 1, 6 -> 2, 10 -> 3, 14 -> 4
+    for c in (1, 2, 3, 4):
+        sums = np.array([2, 6, 10, 14], np.int64)
+        blk = np.zeros((2, 8, c), np.uint8)
+        for j, sm in enumerate(sums):
+            q = [sm // 4 + (1 if t < sm % 4 else 0) for t in range(4)]
+            blk[0, 2 * j], blk[0, 2 * j + 1], blk[1, 2 * j], blk[1, 2 * j + 1] = q
+        got = oracle.resize_area(blk if c > 1 else blk[:, :, 0], 4, 1).reshape(4, c)[:, 0].tolist()
+        want = [1, 2, 3, 4] if c != 2 else [0, 2, 2, 4]
+        assert got == want, (c, got)
