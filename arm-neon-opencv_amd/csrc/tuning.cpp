@@ -32,7 +32,6 @@ const char* const kNames[VACV_TUNE_COUNT] = {
     "VACV_RESIZE_WORK",        // VACV_TUNE_RESIZE_WORK
     "VACV_RESIZE_ROWS_BYTES",  // VACV_TUNE_RESIZE_ROWS_BYTES
     "VACV_WARP_KERNEL",        // VACV_TUNE_WARP_KERNEL
-    "VACV_DIRECT_ALIGN",       // VACV_TUNE_DIRECT_ALIGN
 };
 
 struct Table {

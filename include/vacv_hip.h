@@ -242,8 +242,7 @@ enum {
     VACV_TUNE_RESIZE_WORK = 13,      /* staged kernel planner: work per thread */
     VACV_TUNE_RESIZE_ROWS_BYTES = 14,/* whole-row kernel planner: output bytes per workgroup */
     VACV_TUNE_WARP_KERNEL = 15,      /* u8 warp: 0 gather kernel, 1 tile-staged kernel where it applies */
-    VACV_TUNE_DIRECT_ALIGN = 16,     /* gather kernel: 0 flat pixel order, 1 row-aligned waves */
-    VACV_TUNE_COUNT = 17
+    VACV_TUNE_COUNT = 16
 };
 /* value < 0 restores the built-in choice.  Returns VACV_OK or INVALID_ARG. */
 int vacv_set_tuning(int key, int value);

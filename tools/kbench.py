@@ -22,7 +22,8 @@ def main():
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--batch", type=int, default=0)
     ap.add_argument("--sweep", default="",
-                    help="planner env knobs to sweep, e.g. 'VACV_RESIZE_WORK=2,4,8;VACV_RESIZE_TILE_H=0,4'")
+                    help="kernel-variant knobs (VACV_TUNE_*, vacv_set_tuning) to sweep, "
+                         "e.g. 'DIRECT_ALIGN=0,1;RESIZE_WORK=2,4'")
     a = ap.parse_args()
     import torch
     import vacv_amd
@@ -125,7 +126,6 @@ def main():
         cases["hwc_to_chw_640x360_u8"] = (lambda src=src: ops.change_layout(src, vacv_amd.NCHW),
                                           n * 640 * 360 * 6, n * 640 * 360)
     import itertools
-    import os
     knobs = [kv.split("=", 1) for kv in a.sweep.split(";") if kv]
     combos = list(itertools.product(*[[(k, v) for v in vals.split(",")] for k, vals in knobs])) or [()]
     for fn, _, _ in cases.values():  # clocks ramp before the first timed case
@@ -134,7 +134,7 @@ def main():
     torch.cuda.synchronize()
     for combo in combos:
         for k, v in combo:
-            os.environ[k] = v
+            ops.set_tuning(k, int(v))
         tag = " ".join(f"{k}={v}" for k, v in combo)
         run_cases(cases, a.iters, tag)
 
