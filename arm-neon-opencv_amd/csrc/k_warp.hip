@@ -25,13 +25,17 @@
 // gathers it saves.
 #pragma clang fp contract(off)
 
+#include <cmath>
+
 #include "vacv_device.hpp"
 
 namespace vacv {
 namespace {
 
 
-template <int CC, typename TIn, int OUT, int kPx>
+// EXT: border modes other than CONSTANT (a separate instance: their slow path
+// costs the CONSTANT kernel registers even when it never runs)
+template <int CC, typename TIn, int OUT, int kPx, bool EXT>
 __global__ void __launch_bounds__(kBlock)
 warp_kernel(WarpLaunch L, int gx, int gy, int total) {
     constexpr int LW = 64, LH = 1;  // a lane block is one 64-pixel row segment; the tile is 4 rows
@@ -82,6 +86,16 @@ warp_kernel(WarpLaunch L, int gx, int gy, int total) {
     const uint32_t slimit = (uint32_t)L.src.plane_bytes + srs.delta;
     const uint32_t rp32 = (rp < (1 << 24) && L.src.h < (1 << 24)) ? (uint32_t)rp : 0u;  // 24-bit row offsets
     TOut* xrow = reinterpret_cast<TOut*>(xch[ry]);
+    if (EXT && L.border_mode == kBorderTransparent && y < L.dst.h) {
+        // pixels outside the source keep dst's bytes: start from them
+        const int vb = min(64 * kPx, L.dst.w - xw) * CC * (int)sizeof(TOut);
+        const unsigned char* drow = L.dst.base + (int64_t)img * L.dst.img_pitch + (int64_t)plane * L.dst.plane_pitch +
+                                    (int64_t)y * L.dst.row_pitch + (int64_t)xw * CC * sizeof(TOut);
+        for (int e = lane; e < vb; e += 64) xch[ry][e] = drow[e];
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
 
     // pass q samples the lane block at tile columns cx0 + q*LW (+ lane % LW).
     // With LW = 64 each gather instruction reads 64 CONSECUTIVE output
@@ -100,6 +114,23 @@ warp_kernel(WarpLaunch L, int gx, int gy, int total) {
         float ax = 0.f, ay = 0.f;
         const bool ok = affine_tap(fy, L.src.h, sy, ay) && affine_tap(fx, L.src.w, sx, ax);
         if (!ok) {
+            if (EXT && L.border_mode == kBorderTransparent) continue;  // xrow holds dst's own bytes
+            if (EXT && L.border_mode != kBorderConstant) {
+                int vi[CC];
+                float vf[CC];
+                warp_border_sample<CC, TIn>(sp, rp, L.src.w, L.src.h, L.border_mode, fx, fy, vi, vf);
+#pragma unroll
+                for (int k = 0; k < CC; ++k) {
+                    if (std::is_same<TIn, uint8_t>::value) {
+                        if (OUT == kOutSame) o[k] = (TOut)vi[k];
+                        else if (OUT == kOutF32) o[k] = (TOut)(float)vi[k];
+                        else o[k] = (TOut)normalize_u8v(cn[k], vi[k]);
+                    } else {
+                        o[k] = (TOut)(OUT == kOutNorm ? normalize_value(vf[k], nmean[k], nstd[k]) : vf[k]);
+                    }
+                }
+                continue;
+            }
 #pragma unroll
             for (int k = 0; k < CC; ++k) {
                 if (OUT == kOutNorm) {
@@ -197,6 +228,164 @@ warp_kernel(WarpLaunch L, int gx, int gy, int total) {
     }
 }
 
+// u8 input, BORDER_CONSTANT: the same sampler with its gathers batched.
+// warp_kernel handles one pixel per step behind two branches (outside the
+// source / past the plane end), so a wave has two 8/12-byte gathers in flight
+// and waits on each pair before the next; here G pixels per lane compute
+// their taps first (branch-free: a pixel outside the source loads the plane's
+// first bytes and is replaced by the border value afterwards), issue all 2*G
+// gathers, and only then blend -- 2*G gathers in flight per wave.
+template <int CC, int OUT, int kPx, int G>
+__global__ void __launch_bounds__(kBlock)
+warp_u8_kernel(WarpLaunch L, int gx, int gy, int total) {
+    static_assert(kPx % G == 0, "groups");
+    using TOut = typename std::conditional<(OUT == kOutSame), uint8_t, float>::type;
+    constexpr int kRowBytes = 64 * kPx * CC * (int)sizeof(TOut);  // one wave's output row segment
+    constexpr uint32_t kTD = kTapDwords<CC, true>;                // dwords per tap row
+    __shared__ __attribute__((aligned(16))) unsigned char xch[4][kRowBytes];
+
+    const int per_xcd = (total + 7) / 8;  // XCD-aware block order (see warp_kernel)
+    const int id = (int)(blockIdx.x % 8) * per_xcd + (int)(blockIdx.x / 8);
+    if (id >= total) return;  // uniform
+    const int pidx = id / (gx * gy);
+    const int rem = id - pidx * gx * gy;
+    const int by = rem / gx, bx = rem - by * gx;
+    const int img = pidx / L.src.planes;
+    const int plane = pidx - img * L.src.planes;
+    const int lane = threadIdx.x;
+    const int xw = bx * 64 * kPx;
+    const int y = by * 4 + (int)threadIdx.y;
+    const bool row_ok = y < L.dst.h;
+
+    ChanNorm cn[CC] = {};
+    if (OUT == kOutNorm) {
+#pragma unroll
+        for (int k = 0; k < CC; ++k) cn[k] = chan_norm(L.norm, img, CC == 1 ? plane : k);
+    }
+    TOut bval[CC];
+#pragma unroll
+    for (int k = 0; k < CC; ++k)
+        bval[k] = OUT == kOutNorm ? (TOut)normalize_u8v(cn[k], (int)L.border[k]) : (TOut)L.border[k];
+
+    const unsigned char* sp = L.src.base + (int64_t)img * L.src.img_pitch + (int64_t)plane * L.src.plane_pitch;
+    const int64_t rp = L.src.row_pitch;
+    const float fy_row = L.inv[1] * (float)y;
+    const float gy_row = L.inv[4] * (float)y;
+    const Rsrc srs = make_rsrc(sp, L.src.plane_bytes);
+    const uint32_t slimit = (uint32_t)L.src.plane_bytes + srs.delta;
+    const uint32_t rp32 = (uint32_t)rp;  // plane_bytes < 2^31 (kMaxPlaneBytes)
+    TOut* xrow = reinterpret_cast<TOut*>(xch[threadIdx.y]);
+    typedef unsigned short us2v __attribute__((ext_vector_type(2)));
+
+#pragma unroll
+    for (int g = 0; g < kPx; g += G) {
+        uint32_t tp[G][2][kTD];
+        uint32_t wxp[G], wy0[G], sh[G], sh1[G];
+        bool val[G], far[G];
+        // ---- taps and gathers of G pixels (no branches) ----------------------
+#pragma unroll
+        for (int j = 0; j < G; ++j) {
+            const int x = xw + (g + j) * 64 + lane;
+            // warp_affine_naive.cpp:23-24: (m0*x + m1*y) + m2, all float
+            const float fx = L.inv[0] * (float)x + fy_row + L.inv[2];
+            const float fy = L.inv[3] * (float)x + gy_row + L.inv[5];
+            int sx = 0, sy = 0;
+            float ax = 0.f, ay = 0.f;
+            const bool ok = row_ok && x < L.dst.w && affine_tap(fy, L.src.h, sy, ay) && affine_tap(fx, L.src.w, sx, ax);
+            // SATURATE_CAST_SHORT of a value in (0, 2048]: the +0.5f branch, no clamp
+            const uint32_t w0 = (uint32_t)(int)((1.f - ay) * 2048.f + 0.5f);
+            const uint32_t x0 = (uint32_t)(int)((1.f - ax) * 2048.f + 0.5f);
+            wy0[j] = w0;
+            wxp[j] = x0 | ((2048u - x0) << 16);
+            const uint32_t o0 = ok ? __umul24((uint32_t)sy, rp32) + (uint32_t)(sx * CC) + srs.delta : srs.delta;
+            const uint32_t o1 = ok ? o0 + rp32 : srs.delta;
+            const bool inr = (o1 & ~3u) + 4u * kTD <= slimit;
+            val[j] = ok;
+            far[j] = ok && !inr;  // the plane's last pixel: bytes, below
+            sh[j] = o0 & 3u;
+            sh1[j] = o1 & 3u;  // differs from sh when the row pitch is not a multiple of 4
+            const int a0 = (int)((inr ? o0 : srs.delta) & ~3u), a1 = (int)((inr ? o1 : srs.delta) & ~3u);
+            if constexpr (kTD == 2) {
+                const auto v0 = __builtin_amdgcn_raw_buffer_load_b64(srs.r, a0, 0, 0);
+                const auto v1 = __builtin_amdgcn_raw_buffer_load_b64(srs.r, a1, 0, 0);
+                tp[j][0][0] = v0[0]; tp[j][0][1] = v0[1];
+                tp[j][1][0] = v1[0]; tp[j][1][1] = v1[1];
+            } else {
+                const auto v0 = __builtin_amdgcn_raw_buffer_load_b96(srs.r, a0, 0, 0);
+                const auto v1 = __builtin_amdgcn_raw_buffer_load_b96(srs.r, a1, 0, 0);
+#pragma unroll
+                for (uint32_t d = 0; d < kTD; ++d) { tp[j][0][d] = v0[d]; tp[j][1][d] = v1[d]; }
+            }
+            if (far[j]) {  // rare: re-read the tap bytes singly (the 12-byte load would overhang)
+                const unsigned char* r0 = sp + (int64_t)sy * rp + (int64_t)sx * CC;
+                uint32_t b[2][3] = {{0u, 0u, 0u}, {0u, 0u, 0u}};
+#pragma unroll
+                for (int e = 0; e < 2 * CC; ++e) {
+                    b[0][e >> 2] |= (uint32_t)r0[e] << (8 * (e & 3));
+                    b[1][e >> 2] |= (uint32_t)r0[rp + e] << (8 * (e & 3));
+                }
+#pragma unroll
+                for (uint32_t d = 0; d < kTD; ++d) { tp[j][0][d] = b[0][d]; tp[j][1][d] = b[1][d]; }
+                sh[j] = sh1[j] = 0u;
+            }
+        }
+        // ---- blends --------------------------------------------------------
+#pragma unroll
+        for (int j = 0; j < G; ++j) {
+            const int cxl = (g + j) * 64 + lane;
+            TOut* o = xrow + cxl * CC;
+            const uint32_t a0 = __builtin_amdgcn_alignbyte(tp[j][0][1], tp[j][0][0], sh[j]);
+            const uint32_t c0 = __builtin_amdgcn_alignbyte(tp[j][1][1], tp[j][1][0], sh1[j]);
+            uint32_t a1 = 0u, c1 = 0u;
+            if constexpr (kTD == 3) {
+                a1 = __builtin_amdgcn_alignbyte(tp[j][0][2], tp[j][0][1], sh[j]);
+                c1 = __builtin_amdgcn_alignbyte(tp[j][1][2], tp[j][1][1], sh1[j]);
+            }
+            const us2v wx = __builtin_bit_cast(us2v, wxp[j]);
+            const uint32_t wA = wy0[j], wB = 2048u - wy0[j];
+#pragma unroll
+            for (int k = 0; k < CC; ++k) {
+                // warp_affine_naive.cpp:50-54 as (tl*wx0 + tr*wx1)*wy0 +
+                // (bl*wx0 + br*wx1)*wy1 (exact int32, <= 255*2^22)
+                const uint32_t sel = (uint32_t)k | (0x0Cu << 8) | ((uint32_t)(CC + k) << 16) | (0x0Cu << 24);
+                const uint32_t top = __builtin_amdgcn_perm(a1, a0, sel);
+                const uint32_t bot = __builtin_amdgcn_perm(c1, c0, sel);
+                const uint32_t ht = __builtin_amdgcn_udot2(__builtin_bit_cast(us2v, top), wx, 0u, false);
+                const uint32_t hb = __builtin_amdgcn_udot2(__builtin_bit_cast(us2v, bot), wx, 0u, false);
+                const int v = (int)((__umul24(ht, wA) + __umul24(hb, wB)) >> 22);
+                TOut ov;
+                if (OUT == kOutSame) ov = (TOut)v;
+                else if (OUT == kOutF32) ov = (TOut)(float)v;
+                else ov = (TOut)normalize_u8v(cn[k], v);
+                o[k] = val[j] ? ov : bval[k];
+            }
+        }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+
+    // ---- the wave's row, LDS -> HBM in 16-byte chunks ---------------------
+    if (!row_ok) return;
+    const int vbytes = min(64 * kPx, L.dst.w - xw) * CC * (int)sizeof(TOut);
+    unsigned char* drow = const_cast<unsigned char*>(L.dst.base) + (int64_t)img * L.dst.img_pitch +
+                          (int64_t)plane * L.dst.plane_pitch + (int64_t)y * L.dst.row_pitch +
+                          (int64_t)xw * CC * sizeof(TOut);
+    const unsigned char* xs = xch[threadIdx.y];
+    if ((reinterpret_cast<uintptr_t>(drow) & 15) == 0) {  // uniform
+        for (int c = lane; c * 16 < vbytes; c += 64) {
+            if (c * 16 + 16 <= vbytes) {
+                __builtin_nontemporal_store(*reinterpret_cast<const u32x4*>(xs + 16 * c),
+                                            reinterpret_cast<u32x4*>(drow) + c);
+            } else {
+                for (int e = c * 16; e < vbytes; ++e) drow[e] = xs[e];
+            }
+        }
+    } else {
+        for (int e = lane; e < vbytes; e += 64) drow[e] = xs[e];
+    }
+}
+
 // default: 8 or 10 lane blocks per wave for byte output, whichever pads the
 // output width less (1280: 10 -> 2 tiles of 640 exactly, 0.271 ms, vs 8 ->
 // 2.5 tiles, 0.281 ms at 720p rot15; 8 vs 4: 0.283 vs 0.304), 4 for fp32
@@ -210,14 +399,34 @@ int warp_blocks_per_wave(bool byte_out, int w) {
     return pad(10) < pad(8) ? 10 : 8;
 }
 
+// warp_u8_kernel (2*G gathers in flight per wave) or warp_kernel (2)?  Batching
+// pays while a 64-pixel output row segment stays within a few source rows
+// (720p, scale 0.9: rotation 0 deg 0.256 -> 0.227 ms, 5 deg 0.268 -> 0.231)
+// and loses once its gathers spread over many (15 deg, 18 rows: 0.272 ->
+// 0.289; 45 deg: 0.369 -> 0.413): more lines in flight than the CU's vector
+// cache holds.  VACV_TUNE_WARP_KERNEL: 0 warp_kernel, 2 warp_u8_kernel.
+bool warp_batched(const WarpLaunch& L) {
+    const int knob = tune(VACV_TUNE_WARP_KERNEL);
+    if (knob == 0 || knob == 2) return knob == 2;
+    return 64.f * std::fabs(L.inv[3]) <= 10.f;
+}
+
 template <int CC, typename TIn, int OUT, int kPx>
 hipError_t launch_px(const WarpLaunch& L, hipStream_t s) {
     const int gx = (L.dst.w + 64 * kPx - 1) / (64 * kPx), gy = (L.dst.h + 3) / 4;
     const int64_t total = (int64_t)gx * gy * L.n * L.src.planes;
     if (total >= 0x7FFFFFF0LL) return hipErrorInvalidValue;
     const int64_t blocks = (total + 7) / 8 * 8;
-    hipLaunchKernelGGL((warp_kernel<CC, TIn, OUT, kPx>), dim3((unsigned)blocks), dim3(64, 4), 0, s, L, gx, gy,
-                       (int)total);
+    constexpr int G = kPx % 5 == 0 ? 5 : 4;
+    if (L.border_mode == kBorderConstant && std::is_same<TIn, uint8_t>::value && warp_batched(L))
+        hipLaunchKernelGGL((warp_u8_kernel<CC, OUT, kPx, G>), dim3((unsigned)blocks), dim3(64, 4), 0, s, L, gx, gy,
+                           (int)total);
+    else if (L.border_mode == kBorderConstant)
+        hipLaunchKernelGGL((warp_kernel<CC, TIn, OUT, kPx, false>), dim3((unsigned)blocks), dim3(64, 4), 0, s, L, gx,
+                           gy, (int)total);
+    else
+        hipLaunchKernelGGL((warp_kernel<CC, TIn, OUT, kPx, true>), dim3((unsigned)blocks), dim3(64, 4), 0, s, L, gx,
+                           gy, (int)total);
     return hipGetLastError();
 }
 

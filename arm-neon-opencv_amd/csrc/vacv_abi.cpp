@@ -222,8 +222,10 @@ int normalize_with(const Img& src, const Img& dst, const NormSpec& ns, hipStream
     return hip_status(launch_normalize(L, s));
 }
 
+// fx / fy > 0: cv::resize's inv_scale (the reference passes them through to
+// OpenCV for NEAREST / AREA, resize.cpp:35); 0: dsize / ssize
 int resize_impl(const vacv_image* src_d, const vacv_image* dst_d, int interpolation, int mode, int out_kind,
-                const NormSpec* ns, hipStream_t s) {
+                const NormSpec* ns, hipStream_t s, double fx = 0.0, double fy = 0.0) {
     Img src, dst;
     int st = load(src_d, src);
     if (st) return st;
@@ -269,33 +271,36 @@ int resize_impl(const vacv_image* src_d, const vacv_image* dst_d, int interpolat
         if (src.dtype == VACV_FP32 && L.out == kOutF32) L.out = kOutSame;
         const int want = L.out == kOutSame ? src.dtype : VACV_FP32;
         if (dst.dtype != want) return VACV_ERR_INVALID_ARG;
-        L.scale_xd = 1. / ((double)dst.w / src.w);  // ifx, as cv::resize computes it
-        L.scale_yd = 1. / ((double)dst.h / src.h);
+        L.scale_xd = 1. / (fx > 0 ? fx : (double)dst.w / src.w);  // ifx, as cv::resize computes it
+        L.scale_yd = 1. / (fy > 0 ? fy : (double)dst.h / src.h);
         return hip_status(launch_resize_nearest(L, s));
     } else if (interpolation == VACV_INTER_AREA) {
-        // resize.cpp:44-49 hands it to cv::resize; OpenCV 2.4 takes
-        // resizeAreaFast_ when both scales are integers to within DBL_EPSILON
-        // (imgwarp.cpp: scale = 1 / ((double)dsize / ssize), is_area_fast).
-        // Fractional downscales (its resizeArea tables) and upscales (its
-        // bilinear fallback) are not built here.
+        // resize.cpp:44-49 hands it to cv::resize; OpenCV 2.4 (imgwarp.cpp)
+        // takes resizeAreaFast_ when both scales are integers to within
+        // DBL_EPSILON, resizeArea_'s weight tables for other down-scales and
+        // its bilinear resize with area-mode taps for up-scales (k_area.hip)
         if (src.dtype != VACV_INT8 && src.dtype != VACV_FP32) return VACV_ERR_UNSUPPORTED;
         L.out = out_kind;
         if (src.dtype == VACV_FP32 && L.out == kOutF32) L.out = kOutSame;
         const int want = L.out == kOutSame ? src.dtype : VACV_FP32;
         if (dst.dtype != want) return VACV_ERR_INVALID_ARG;
-        const double sx = 1. / ((double)dst.w / src.w), sy = 1. / ((double)dst.h / src.h);
+        const double ifx = fx > 0 ? fx : (double)dst.w / src.w, ify = fy > 0 ? fy : (double)dst.h / src.h;
+        const double sx = 1. / ifx, sy = 1. / ify;
         const double ix = std::nearbyint(sx), iy = std::nearbyint(sy);
-        if (ix < 1 || iy < 1 || std::fabs(sx - ix) >= DBL_EPSILON || std::fabs(sy - iy) >= DBL_EPSILON)
-            return VACV_ERR_UNSUPPORTED;
-        L.area_x = (int)ix;
-        L.area_y = (int)iy;
-        if ((int64_t)dst.w * L.area_x != src.w || (int64_t)dst.h * L.area_y != src.h) return VACV_ERR_UNSUPPORTED;
-        L.area_scale = 1.f / (float)(L.area_x * L.area_y);
-        // OpenCV's ResizeAreaFastVec<uchar>::fast_mode: 2x2 blocks with 1, 3 or
-        // 4 interleaved channels (an NCHW plane is one) take (a+b+c+d+2)>>2
-        L.area_half_up = src.dtype == VACV_INT8 && L.area_x == 2 && L.area_y == 2 &&
-                         (L.src.cc == 1 || L.src.cc == 3 || L.src.cc == 4);
-        return hip_status(launch_resize_area(L, s));
+        if (sx >= 1 && sy >= 1 && std::fabs(sx - ix) < DBL_EPSILON && std::fabs(sy - iy) < DBL_EPSILON) {
+            L.area_x = (int)ix;
+            L.area_y = (int)iy;
+            // an fx-derived size with partial blocks (OpenCV averages those by
+            // count) is not built
+            if ((int64_t)dst.w * L.area_x != src.w || (int64_t)dst.h * L.area_y != src.h) return VACV_ERR_UNSUPPORTED;
+            L.area_scale = 1.f / (float)(L.area_x * L.area_y);
+            // OpenCV's ResizeAreaFastVec<uchar>::fast_mode: 2x2 blocks with 1, 3 or
+            // 4 interleaved channels (an NCHW plane is one) take (a+b+c+d+2)>>2
+            L.area_half_up = src.dtype == VACV_INT8 && L.area_x == 2 && L.area_y == 2 &&
+                             (L.src.cc == 1 || L.src.cc == 3 || L.src.cc == 4);
+            return hip_status(launch_resize_area(L, s));
+        }
+        return launch_resize_area_general(L, ifx, ify, s);
     } else {
         return VACV_ERR_UNSUPPORTED;  // resize.cpp:46-49 recurses forever for other modes
     }
@@ -372,8 +377,11 @@ int warp_impl(const vacv_image* src_d, const vacv_image* dst_d, const float m[6]
     if (!m) return VACV_ERR_INVALID_ARG;
     if (src.n != dst.n || src.c != dst.c || src.layout != dst.layout) return VACV_ERR_INVALID_ARG;
     if (src.dtype != VACV_INT8 && src.dtype != VACV_FP32) return VACV_ERR_UNSUPPORTED;
-    // warp_affine.cpp:114-118: anything else recurses into the OpenCV stub
-    if (flags != VACV_INTER_LINEAR || border_mode != VACV_BORDER_CONSTANT) return VACV_ERR_UNSUPPORTED;
+    // warp_affine.cpp:114-118: anything but LINEAR + CONSTANT recurses into the
+    // OpenCV stub; the other border modes are built here (vacv_semantics.hpp
+    // border_index: the naive sampler with OpenCV's borderInterpolate taps)
+    if (flags != VACV_INTER_LINEAR) return VACV_ERR_UNSUPPORTED;
+    if (border_mode < VACV_BORDER_CONSTANT || border_mode > VACV_BORDER_TRANSPARENT) return VACV_ERR_UNSUPPORTED;
     if (src.layout == VACV_NHWC && src.c > 4) return VACV_ERR_UNSUPPORTED;
     if (src.w < 2 || src.h < 2) return VACV_ERR_INVALID_ARG;
     WarpLaunch L{};
@@ -386,6 +394,8 @@ int warp_impl(const vacv_image* src_d, const vacv_image* dst_d, const float m[6]
     if (dst.dtype != want) return VACV_ERR_INVALID_ARG;
     vacv_invert_affine(m, L.inv);
     border_values(src, bv, L.border);
+    L.border_mode = border_mode;
+    if (border_mode == VACV_BORDER_TRANSPARENT && dst.data == src.data) return VACV_ERR_INVALID_ARG;  // in place
     if (ns) L.norm = *ns;
     return hip_status(launch_warp(L, s));
 }
@@ -656,6 +666,13 @@ int vacv_resize(const vacv_image* src_d, const vacv_image* dst_d, int interpolat
     return resize_impl(src_d, dst_d, interpolation, mode, kOutSame, nullptr, s);
 }
 
+int vacv_resize_scaled(const vacv_image* src, const vacv_image* dst, int interpolation, int mode, double fx,
+                       double fy, void* stream) {
+    if (!(fx > 0) || !(fy > 0)) return VACV_ERR_INVALID_ARG;
+    if (interpolation != VACV_INTER_NEAREST && interpolation != VACV_INTER_AREA) return VACV_ERR_UNSUPPORTED;
+    return resize_impl(src, dst, interpolation, mode, kOutSame, nullptr, (hipStream_t)stream, fx, fy);
+}
+
 int vacv_rotation_matrix(float scale, float rot_deg, const double aux[4], float m[6]) {
     if (!m) return VACV_ERR_INVALID_ARG;
     const double a[4] = {aux ? aux[0] : 0.0, aux ? aux[1] : 0.0, aux ? aux[2] : 0.0, aux ? aux[3] : 0.0};
@@ -820,7 +837,8 @@ int vacv_release_workspace(void) {
     }
     g_ws.clear();
     const int pst = release_plans();
-    return st ? st : pst;
+    const int ast = release_area_tables();
+    return st ? st : (pst ? pst : ast);
 }
 
 }  // extern "C"

@@ -167,6 +167,40 @@ __device__ __forceinline__ FixedTap tap_of(int d, int n_in, int n_out, float sca
     return r;
 }
 
+// A warp pixel outside the naive sampler's range under a non-CONSTANT border
+// mode (vacv_semantics.hpp border_index / border_tap): the four taps mapped
+// through the border rule, the naive sampler's weights.  u8 results in vi
+// (the >> 22 value), fp32 in vf.  sp = plane base, rp = row pitch in bytes.
+template <int CC, typename TIn>
+__device__ __forceinline__ void warp_border_sample(const unsigned char* sp, int64_t rp, int w, int h, int mode,
+                                                   float fx, float fy, int (&vi)[CC], float (&vf)[CC]) {
+    int ix, iy;
+    float ax, ay;
+    border_tap(fx, ix, ax);
+    border_tap(fy, iy, ay);
+    const int x0 = border_index(ix, w, mode) * CC, x1 = border_index(ix + 1, w, mode) * CC;
+    const TIn* r0 = reinterpret_cast<const TIn*>(sp + (int64_t)border_index(iy, h, mode) * rp);
+    const TIn* r1 = reinterpret_cast<const TIn*>(sp + (int64_t)border_index(iy + 1, h, mode) * rp);
+    if constexpr (std::is_same<TIn, uint8_t>::value) {
+        const int wy0 = (int)((1.f - ay) * 2048.f + 0.5f), wy1 = 2048 - wy0;
+        const int wx0 = (int)((1.f - ax) * 2048.f + 0.5f), wx1 = 2048 - wx0;
+#pragma unroll
+        for (int k = 0; k < CC; ++k)
+            vi[k] = ((int)r0[x0 + k] * wx0 * wy0 + (int)r1[x0 + k] * wx0 * wy1 + (int)r0[x1 + k] * wx1 * wy0 +
+                     (int)r1[x1 + k] * wx1 * wy1) >> 22;
+    } else {
+        const float ya = 1.f - ay, yb = ay, xa = 1.f - ax, xb = ax;
+#pragma unroll
+        for (int k = 0; k < CC; ++k) {  // warp_affine_naive.cpp:98-102's order: lt, lb, rt, rb
+            float v = r0[x0 + k] * xa * ya;
+            v += r1[x0 + k] * xa * yb;
+            v += r0[x1 + k] * xb * ya;
+            v += r1[x1 + k] * xb * yb;
+            vf[k] = v;
+        }
+    }
+}
+
 template <typename T>
 __device__ __forceinline__ T wave_sum(T v) {
 #pragma unroll

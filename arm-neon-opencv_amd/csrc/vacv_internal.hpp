@@ -125,6 +125,11 @@ bool resize_one_tap_rows(const ResizeLaunch& L);
 hipError_t launch_resize_nearest(const ResizeLaunch& L, hipStream_t s);
 // INTER_AREA at an integer scale (OpenCV 2.4 resizeAreaFast_): area_x/y, area_scale
 hipError_t launch_resize_area(const ResizeLaunch& L, hipStream_t s);
+// INTER_AREA at any other scale (k_area.hip): OpenCV 2.4's resizeArea_ tables
+// (down-scales) or its area-mode bilinear (up-scales); inv_x / inv_y =
+// cv::resize's inv_scale.  Returns a vacv_status.
+int launch_resize_area_general(const ResizeLaunch& L, double inv_x, double inv_y, hipStream_t s);
+int release_area_tables();
 // u8 -> fp32 cubic as per-pixel gathers (k_cubic_direct.hip); needs no plan
 bool cubic_direct_applies(const ResizeLaunch& L);
 hipError_t launch_cubic_direct(const ResizeLaunch& L, hipStream_t s);
@@ -135,6 +140,7 @@ struct WarpLaunch {
     int n;
     float inv[6];
     float border[4];
+    int border_mode;             // kBorder* (vacv_semantics.hpp)
     int out;                     // OutKind
     NormSpec norm;
 };

@@ -124,6 +124,43 @@ VACV_HD bool affine_tap(float f, int n, int& i, float& frac) {
     return true;
 }
 
+// Border modes for warp_affine beyond BORDER_CONSTANT.  The reference hands
+// every other mode to OpenCV (warp_affine.cpp:114-118 -> :48-50, recursing
+// forever without it); here they extend the reference's own naive sampler:
+// a pixel whose top-left tap is inside [0,w-2]x[0,h-2] is computed exactly as
+// for BORDER_CONSTANT, any other pixel takes its four taps at
+// floor(f) and floor(f)+1 mapped through OpenCV 2.4's borderInterpolate
+// (core: REPLICATE clamps; REFLECT fedcba|abcd|dcba; REFLECT_101 dcb|abcd|cba;
+// WRAP modulo; the reflect loops in closed form), with the same fixed-point
+// weights.  TRANSPARENT leaves such pixels untouched.  f is clamped to
+// +-1e9 first (NaN -> -1e9) so floor() stays an int.  Parity unpinned: no
+// reference entry runs these modes.
+enum : int { kBorderConstant = 0, kBorderReplicate = 1, kBorderReflect = 2, kBorderWrap = 3,
+             kBorderReflect101 = 4, kBorderTransparent = 5 };
+
+VACV_HD int border_index(int p, int len, int mode) {
+    if ((unsigned)p < (unsigned)len) return p;
+    if (mode == kBorderReplicate) return p < 0 ? 0 : len - 1;
+    if (mode == kBorderWrap) {
+        int q = p % len;
+        return q < 0 ? q + len : q;
+    }
+    // REFLECT (d = 0) / REFLECT_101 (d = 1)
+    if (len == 1) return 0;
+    const int d = mode == kBorderReflect101 ? 1 : 0;
+    const long long period = 2LL * len - 2 * d;
+    long long q = (long long)p % period;
+    if (q < 0) q += period;
+    return (int)(q < len ? q : period - 1 + d - q);
+}
+
+// floor(f) and frac of a warp coordinate outside the naive sampler's range
+VACV_HD void border_tap(float f, int& i, float& frac) {
+    const float c = fminf(fmaxf(f, -1e9f), 1e9f);
+    i = (int)floorf(c);
+    frac = c - (float)i;
+}
+
 // normalize_naive.cpp:74-90: float subtraction, double division, float result.
 VACV_HD float normalize_value(float x, float mean, float stddev) {
     float d = x - mean;

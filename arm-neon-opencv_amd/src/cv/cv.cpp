@@ -4,6 +4,7 @@
 // moves host operands across PCIe and leaves device operands in HBM.
 #include "cv.h"
 
+#include <cmath>
 #include <cstring>
 #include <vector>
 
@@ -68,8 +69,8 @@ DType resize_out_dtype(const char* fn, const Tensor& src, int interpolation) {
         return src.dtype;
     }
     if (interpolation == INTER_AREA) {
-        // resize.cpp:46-49 hands it to cv::resize; OpenCV 2.4's resizeAreaFast_
-        // (integer downscales; the C ABI rejects other scales)
+        // resize.cpp:46-49 hands it to cv::resize; OpenCV 2.4's area resize
+        // at every scale (resizeAreaFast_, resizeArea_, area-mode bilinear)
         if (src.dtype != INT8 && src.dtype != FP32) fail(fn, "INTER_AREA takes INT8 or FP32");
         return src.dtype;
     }
@@ -84,7 +85,11 @@ void check_warp_modes(const char* fn, const Tensor& src, int flags, int borderMo
     // warp_affine.cpp:114-118
     if (src.dtype != INT8 && src.dtype != FP32) fail(fn, "warp_affine takes INT8 or FP32");
     if (flags != INTER_LINEAR) fail(fn, "only INTER_LINEAR is supported");
-    if (borderMode != BORDER_CONSTANT) fail(fn, "only BORDER_CONSTANT is supported");
+    // BORDER_CONSTANT is the reference's naive path; REPLICATE, REFLECT, WRAP,
+    // REFLECT_101 and TRANSPARENT extend it (the reference hands them to
+    // OpenCV: warp_affine.cpp:114-118); BORDER_ISOLATED has no meaning here
+    if (borderMode < BORDER_CONSTANT || borderMode > BORDER_TRANSPARENT)
+        fail(fn, "unsupported border mode");
 }
 
 std::vector<float> rotation(float scale, float rot, const VScalar& aux) {
@@ -124,14 +129,25 @@ void check_yuv_code(const char* fn, int code) {
 
 }  // namespace
 
-void resize(const Tensor& src, Tensor& dst, VSize dsize, double /*fx*/, double /*fy*/, int interpolation) {
+void resize(const Tensor& src, Tensor& dst, VSize dsize, double fx, double fy, int interpolation) {
     static const char* fn = "va_cv::resize";
     const DType out = resize_out_dtype(fn, src, interpolation);
+    // INTER_NEAREST / INTER_AREA go to cv::resize in the reference, which also
+    // takes dsize = 0 with fx, fy: dsize = saturate_cast<int>(w * fx) (round
+    // half to even) and inv_scale = fx, fy.  The naive LINEAR / CUBIC paths
+    // use dsize alone (resize.cpp:77-135).
+    const bool scaled = dsize.w == 0 && dsize.h == 0 && fx > 0 && fy > 0 &&
+                        (interpolation == INTER_NEAREST || interpolation == INTER_AREA);
+    if (scaled) {
+        dsize.w = static_cast<int>(std::nearbyint(src.w * fx));
+        dsize.h = static_cast<int>(std::nearbyint(src.h * fy));
+    }
     if (dsize.w < 1 || dsize.h < 1) fail(fn, "dsize must be positive");
     Staging st(fn, src);
     const vacv_image s = st.in(src, 0);
     const vacv_image d = st.out(dst, dsize.w, dsize.h, src.c, out, src.layout, 1);
-    st.run(vacv_resize(&s, &d, interpolation, VACV_LINEAR_REFERENCE, st.stream()));
+    if (scaled) st.run(vacv_resize_scaled(&s, &d, interpolation, VACV_LINEAR_REFERENCE, fx, fy, st.stream()));
+    else st.run(vacv_resize(&s, &d, interpolation, VACV_LINEAR_REFERENCE, st.stream()));
     st.finish();
 }
 

@@ -5,7 +5,8 @@ tensors; ``dist`` adds the multi-GPU (RCCL) statistics reduction.  All
 compute happens in lib/libvacv_hip.so (hand-written gfx950 kernels).
 """
 from . import _lib
-from ._lib import (BORDER_CONSTANT, BORDER_REPLICATE, COLOR_YUV2BGR_NV12, COLOR_YUV2BGR_NV21, COLOR_YUV2RGB_NV12, COLOR_YUV2RGB_NV21,
+from ._lib import (BORDER_CONSTANT, BORDER_REFLECT, BORDER_REFLECT_101, BORDER_REPLICATE, BORDER_TRANSPARENT,
+                   BORDER_WRAP, COLOR_YUV2BGR_NV12, COLOR_YUV2BGR_NV21, COLOR_YUV2RGB_NV12, COLOR_YUV2RGB_NV21,
                    FP16, FP32, FP64, INT8, INTER_AREA, INTER_CUBIC, INTER_LINEAR, INTER_NEAREST, LINEAR_NEON, LINEAR_OPENCV,
                    LINEAR_REFERENCE, NCHW, NHWC, VacvError, build)
 

@@ -24,7 +24,7 @@ OK, ERR_INVALID_ARG, ERR_UNSUPPORTED, ERR_HIP, ERR_NO_MEMORY = 0, -1, -2, -3, -4
 FP32, FP16, INT8, FP64 = 0, 1, 2, 3
 NCHW, NHWC = 0, 1
 INTER_NEAREST, INTER_LINEAR, INTER_CUBIC, INTER_AREA = 0, 1, 2, 3
-BORDER_CONSTANT, BORDER_REPLICATE = 0, 1
+BORDER_CONSTANT, BORDER_REPLICATE, BORDER_REFLECT, BORDER_WRAP, BORDER_REFLECT_101, BORDER_TRANSPARENT = 0, 1, 2, 3, 4, 5
 COLOR_YUV2RGB_NV12, COLOR_YUV2BGR_NV12, COLOR_YUV2RGB_NV21, COLOR_YUV2BGR_NV21 = 90, 91, 92, 93
 LINEAR_REFERENCE, LINEAR_NEON, LINEAR_OPENCV = 0, 1, 2
 
@@ -67,6 +67,7 @@ SIGNATURES = {
     "vacv_change_layout": ([_IMG, _IMG, _P], _I),
     "vacv_change_dtype": ([_IMG, _IMG, _P], _I),
     "vacv_resize": ([_IMG, _IMG, _I, _I, _P], _I),
+    "vacv_resize_scaled": ([_IMG, _IMG, _I, _I, _D, _D, _P], _I),
     "vacv_warp_affine": ([_IMG, _IMG, _FP, _I, _I, _DP, _P], _I),
     "vacv_rotation_matrix": ([ctypes.c_float, ctypes.c_float, _DP, _FP], _I),
     "vacv_invert_affine": ([_FP, _FP], _I),

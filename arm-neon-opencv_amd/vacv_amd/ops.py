@@ -146,14 +146,26 @@ def change_dtype(src: torch.Tensor, dtype: torch.dtype, layout: int = NHWC, stre
 
 
 def resize(src: torch.Tensor, w: int, h: int, interpolation: int = INTER_LINEAR, mode: int = LINEAR_REFERENCE,
-           layout: int = NHWC, out=None, stream=None) -> torch.Tensor:
-    """va_cv::resize (cv.h:85-87).  INTER_CUBIC on u8 input returns fp32."""
+           layout: int = NHWC, out=None, stream=None, fx: float = 0.0, fy: float = 0.0) -> torch.Tensor:
+    """va_cv::resize (cv.h:85-87).  INTER_CUBIC on u8 input returns fp32.
+    w = h = 0 with fx, fy > 0 (INTER_NEAREST / INTER_AREA): cv::resize's
+    dsize = (round(w_in * fx), round(h_in * fy)) and inv_scale = (fx, fy)."""
     s4 = _as4d(src, layout)
     dt = torch.float32 if (interpolation == INTER_CUBIC) else src.dtype
+    scaled = w == 0 and h == 0 and fx > 0 and fy > 0
+    if scaled:  # saturate_cast<int>(double): round half to even, as Python's round
+        w_in, h_in = (s4.shape[2], s4.shape[1]) if layout == NHWC else (s4.shape[3], s4.shape[2])
+        w, h = int(round(w_in * fx)), int(round(h_in * fy))
     if out is None:
         out = _empty_like_shape(s4, layout, w, h, dt, True, src.dim())
-    check("vacv_resize", L.load().vacv_resize(ctypes.byref(describe(s4, layout)), ctypes.byref(describe(out, layout)),
-                                              interpolation, mode, _stream(stream)))
+    if scaled:
+        check("vacv_resize_scaled", L.load().vacv_resize_scaled(
+            ctypes.byref(describe(s4, layout)), ctypes.byref(describe(out, layout)), interpolation, mode,
+            float(fx), float(fy), _stream(stream)))
+    else:
+        check("vacv_resize", L.load().vacv_resize(ctypes.byref(describe(s4, layout)),
+                                                  ctypes.byref(describe(out, layout)), interpolation, mode,
+                                                  _stream(stream)))
     return _shape_back(out, src, layout)
 
 

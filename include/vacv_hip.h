@@ -50,7 +50,10 @@ enum { VACV_NCHW = 0, VACV_NHWC = 1 };
 /* va_cv::VInterMode (cv.h:27-35) */
 enum { VACV_INTER_NEAREST = 0, VACV_INTER_LINEAR = 1, VACV_INTER_CUBIC = 2, VACV_INTER_AREA = 3 };
 /* va_cv::VBorderMode (cv.h:38-48) */
-enum { VACV_BORDER_CONSTANT = 0, VACV_BORDER_REPLICATE = 1 };
+enum {
+    VACV_BORDER_CONSTANT = 0, VACV_BORDER_REPLICATE = 1, VACV_BORDER_REFLECT = 2, VACV_BORDER_WRAP = 3,
+    VACV_BORDER_REFLECT_101 = 4, VACV_BORDER_TRANSPARENT = 5
+};
 /* va_cv::InputImageFormat (cv.h:62-74) */
 enum {
     VACV_COLOR_YUV2RGB_NV12 = 90, VACV_COLOR_YUV2BGR_NV12 = 91,
@@ -113,19 +116,38 @@ int vacv_change_dtype(const vacv_image* src, const vacv_image* dst, void* stream
  *  INTER_NEAREST: INT8->INT8, FP32->FP32 with OpenCV 2.4's resizeNN
  *                semantics, which the reference delegates to cv::resize
  *                (resize.cpp:44-49): sx = min(floor(x / (w_out / w_in)), w_in - 1).
- *  INTER_AREA:   INT8->INT8, FP32->FP32 at integer downscales only (OpenCV
- *                2.4's resizeAreaFast_, also behind resize.cpp:44-49): the mean
- *                of each (w_in/w_out) x (h_in/h_out) block, u8 rounded half to
- *                even.  Other scales: VACV_ERR_UNSUPPORTED.
+ *  INTER_AREA:   INT8->INT8, FP32->FP32 (OpenCV 2.4's cv::resize, also
+ *                behind resize.cpp:44-49): integer down-scales = the mean of
+ *                each block (resizeAreaFast_; u8 rounded half to even, 2x2
+ *                blocks of 1/3/4 channels half up), other down-scales =
+ *                resizeArea_'s weight tables, up-scales = its bilinear with
+ *                area-mode taps (parity unpinned).
  * NHWC channels 1..4; NCHW any c (per plane, as resize.cpp:72-88). */
 int vacv_resize(const vacv_image* src, const vacv_image* dst, int interpolation, int mode, void* stream);
+
+/* vacv_resize with cv::resize's explicit scale factors (the reference passes
+ * fx / fy through to OpenCV, resize.cpp:35, :47): INTER_NEAREST and
+ * INTER_AREA only; dst->w/h must be the size cv::resize derives,
+ * saturate_cast<int>(w * fx) (round half to even), and the sampling uses
+ * inv_scale = fx, fy instead of dst/src. */
+int vacv_resize_scaled(const vacv_image* src, const vacv_image* dst, int interpolation, int mode, double fx,
+                       double fy, void* stream);
 
 /* WarpAffine::warp_affine (warp_affine.cpp:16-36, :111-169, cv.h:118-122).
  * m = the FORWARD 2x3 map, row-major; it is inverted on the host with the
  * reference's arithmetic and is NOT modified (the reference inverts the
- * caller's M in place).  INTER_LINEAR + BORDER_CONSTANT only; pixels whose
- * taps fall outside are written with border_value (the reference leaves
- * them untouched).  border_value may be NULL (zeros). */
+ * caller's M in place).  INTER_LINEAR only.  A pixel whose top-left tap is
+ * inside [0,w-2]x[0,h-2] is the reference's naive sampler bit for bit; the
+ * others depend on border_mode:
+ *   BORDER_CONSTANT     border_value (the reference leaves them untouched);
+ *                       border_value may be NULL (zeros)
+ *   BORDER_TRANSPARENT  left untouched (the reference's own behaviour); dst
+ *                       must not alias src
+ *   BORDER_REPLICATE, _REFLECT, _WRAP, _REFLECT_101
+ *                       the four taps at floor(f), floor(f)+1 mapped through
+ *                       OpenCV 2.4's borderInterpolate, the naive sampler's
+ *                       weights (the reference hands these modes to OpenCV,
+ *                       warp_affine.cpp:114-118; parity unpinned) */
 int vacv_warp_affine(const vacv_image* src, const vacv_image* dst, const float m[6],
                      int flags, int border_mode, const double border_value[4], void* stream);
 
@@ -241,7 +263,7 @@ enum {
     VACV_TUNE_RESIZE_TILE_W = 12,    /* staged kernel planner: tile width */
     VACV_TUNE_RESIZE_WORK = 13,      /* staged kernel planner: work per thread */
     VACV_TUNE_RESIZE_ROWS_BYTES = 14,/* whole-row kernel planner: output bytes per workgroup */
-    VACV_TUNE_WARP_KERNEL = 15,      /* u8 warp: 0 gather kernel, 1 tile-staged kernel where it applies */
+    VACV_TUNE_WARP_KERNEL = 15,      /* u8 CONSTANT warp: 0 per-pixel gathers, 2 batched gathers */
     VACV_TUNE_COUNT = 16
 };
 /* value < 0 restores the built-in choice.  Returns VACV_OK or INVALID_ARG. */

@@ -77,6 +77,8 @@ class Oracle:
             ("oracle_resize_area", [_P, _I, _I, _I, _I, _P, _I, _I], None),
             ("oracle_warp_affine_u8", [_P, _I, _I, _I, _P, _I, _I, _P], None),
             ("oracle_warp_affine_f32", [_P, _I, _I, _I, _P, _I, _I, _P], None),
+            ("oracle_resize_area_any", [_P, _I, _I, _I, _I, _P, _I, _I, ctypes.c_double, ctypes.c_double], None),
+            ("oracle_warp_affine_border", [_P, _I, _I, _I, _I, _P, _I, _I, _P, _I], None),
             ("oracle_yuv420sp_to_bgr", [_P, _P, _I, _I, _I, _I], None),
             ("oracle_bgr2nv21", [_P, _P, _I, _I], None),
             ("oracle_hwc_to_chw", [_P, _P, _I, _I, _I, _I], None),
@@ -152,6 +154,17 @@ class Oracle:
         self.lib.oracle_resize_area(_ptr(img), w, h, c, img.dtype.itemsize, _ptr(out), w_out, h_out)
         return out
 
+    def resize_area_any(self, img, w_out, h_out, inv_x=0.0, inv_y=0.0):
+        """INTER_AREA at any scale (OpenCV 2.4 cv::resize restated; parity
+        unpinned, vacv_oracle.c).  inv_x / inv_y: cv::resize's fx / fy when
+        dsize is derived from them (0: dsize / ssize)."""
+        img = np.ascontiguousarray(img)
+        w, h, c = _shape(img)
+        out = _out(h_out, w_out, c, img.dtype)
+        self.lib.oracle_resize_area_any(_ptr(img), w, h, c, img.dtype.itemsize, _ptr(out), w_out, h_out,
+                                        float(inv_x), float(inv_y))
+        return out
+
     def resize_cubic(self, img, w_out, h_out):
         img = np.ascontiguousarray(img, np.float32)
         w, h, c = _shape(img)
@@ -159,16 +172,26 @@ class Oracle:
         self.lib.oracle_resize_cubic_f32(_ptr(img), w, h, c, _ptr(out), w_out, h_out)
         return out
 
-    def warp_affine(self, img, m_forward, w_out, h_out, border=0):
+    def warp_affine(self, img, m_forward, w_out, h_out, border=0, border_mode=0, dst=None):
+        """warp_affine_naive (the inverse computed as warp_affine.cpp does).
+        border_mode 0 CONSTANT: skipped pixels = `border`; 1 REPLICATE, 2
+        REFLECT, 3 WRAP, 4 REFLECT_101: the build's extension (parity
+        unpinned, vacv_oracle.c); 5 TRANSPARENT: skipped pixels keep `dst`."""
         img = np.ascontiguousarray(img)
         w, h, c = _shape(img)
         inv = self.invert_affine(m_forward)
-        out = _out(h_out, w_out, c, img.dtype)
-        out[...] = border
+        if border_mode == 5:
+            out = np.ascontiguousarray(dst).copy()
+        else:
+            out = _out(h_out, w_out, c, img.dtype)
+            out[...] = border
         if img.dtype == np.uint8:
             self.lib.oracle_warp_affine_u8(_ptr(img), w, h, c, _ptr(out), w_out, h_out, _ptr(inv))
         else:
             self.lib.oracle_warp_affine_f32(_ptr(img), w, h, c, _ptr(out), w_out, h_out, _ptr(inv))
+        if border_mode in (1, 2, 3, 4):
+            self.lib.oracle_warp_affine_border(_ptr(img), w, h, c, img.dtype.itemsize, _ptr(out), w_out, h_out,
+                                               _ptr(inv), border_mode)
         return out
 
     # -- colour ----------------------------------------------------------------

@@ -18,6 +18,7 @@
  */
 #include "vacv_oracle.h"
 
+#include <float.h>
 #include <math.h>
 #include <stdlib.h>
 #include <string.h>
@@ -278,6 +279,171 @@ void oracle_resize_area(const void* src, int w_in, int h_in, int cc, int esize,
             }
 }
 
+/* INTER_AREA at any other scale.  The reference hands it to cv::resize
+ * (resize.cpp:44-49); OpenCV 2.4.13.4's published algorithm (imgwarp.cpp,
+ * cv::resize), restated.  inv_scale = dsize / ssize (double), scale = 1 /
+ * inv_scale:
+ *  - both scales >= 1 (a down-scale, not integral): resizeArea_ over the
+ *    computeResizeAreaTab weight tables; per output row the source rows'
+ *    horizontally weighted sums buf = sum_k S[si_k] * alpha_k (fp32, in table
+ *    order from 0) are accumulated as sum = beta_0 * buf_0, sum += beta_j *
+ *    buf_j (fp32), then saturate_cast (u8: cvRound, half to even);
+ *  - otherwise (an up-scale on either axis): the bilinear resize with the
+ *    area-mode taps sx = floor(dx * scale), fx = (float)((dx + 1) - (sx + 1)
+ *    * inv_scale), fx = fx <= 0 ? 0 : fx - floor(fx); at sx >= n - 1 the tap
+ *    is (n - 1, fx = 0).  u8: coefficients saturate_cast<short>(c * 2048)
+ *    (half even) and OpenCV's fixed-point rows, ((h0 >> 4) * b0 >> 16) +
+ *    ((h1 >> 4) * b1 >> 16) + 2 >> 2 (the VResizeLinearVec_32s8u form, the
+ *    arithmetic of this build's OPENCV bilinear mode); fp32: h = S0 * a0 +
+ *    S1 * a1 per row, out = h0 * b0 + h1 * b1.
+ * PARITY UNPINNED: no reference entry runs this path here and its tests hold
+ * no area output.  cn <= 4 (OpenCV asserts it for resizeArea_). */
+typedef struct { int di, si; float alpha; } oracle_area_tab;
+
+/* computeResizeAreaTab (imgwarp.cpp): returns the entry count */
+int oracle_area_table(int ssize, int dsize, int cn, double scale, int* di, int* si, float* alpha) {
+    int k = 0;
+    for (int dx = 0; dx < dsize; ++dx) {
+        const double fsx1 = dx * scale;
+        const double fsx2 = fsx1 + scale;
+        const double cell = scale < ssize - fsx1 ? scale : ssize - fsx1;
+        int sx1 = (int)ceil(fsx1), sx2 = (int)floor(fsx2);
+        if (sx2 > ssize - 1) sx2 = ssize - 1;
+        if (sx1 > sx2) sx1 = sx2;
+        if (sx1 - fsx1 > 1e-3) {
+            di[k] = dx * cn; si[k] = (sx1 - 1) * cn; alpha[k++] = (float)((sx1 - fsx1) / cell);
+        }
+        for (int sx = sx1; sx < sx2; ++sx) {
+            di[k] = dx * cn; si[k] = sx * cn; alpha[k++] = (float)(1.0 / cell);
+        }
+        if (fsx2 - sx2 > 1e-3) {
+            double t = fsx2 - sx2;
+            if (t > 1.) t = 1.;
+            if (t > cell) t = cell;
+            di[k] = dx * cn; si[k] = sx2 * cn; alpha[k++] = (float)(t / cell);
+        }
+    }
+    return k;
+}
+
+static void area_frac(const void* src, int w_in, int h_in, int cc, int esize, void* dst, int w_out, int h_out,
+                      double sx, double sy) {
+    int *xdi = malloc(sizeof(int) * 2 * (w_in + 2)), *xsi = malloc(sizeof(int) * 2 * (w_in + 2));
+    int *ydi = malloc(sizeof(int) * 2 * (h_in + 2)), *ysi = malloc(sizeof(int) * 2 * (h_in + 2));
+    float *xal = malloc(sizeof(float) * 2 * (w_in + 2)), *yal = malloc(sizeof(float) * 2 * (h_in + 2));
+    const int nx = oracle_area_table(w_in, w_out, cc, sx, xdi, xsi, xal);
+    const int ny = oracle_area_table(h_in, h_out, 1, sy, ydi, ysi, yal);
+    const int W = w_out * cc;
+    float* buf = malloc(sizeof(float) * W);
+    float* sum = malloc(sizeof(float) * W);
+    int prev = ydi[0];
+    for (int x = 0; x < W; ++x) sum[x] = 0.f;
+    for (int j = 0; j < ny; ++j) {
+        const float beta = yal[j];
+        const int dy = ydi[j];
+        const size_t row = (size_t)ysi[j] * w_in * cc;
+        for (int x = 0; x < W; ++x) buf[x] = 0.f;
+        for (int k = 0; k < nx; ++k)
+            for (int c = 0; c < cc; ++c) {
+                const float v = esize == 1 ? (float)((const uint8_t*)src)[row + xsi[k] + c]
+                                           : ((const float*)src)[row + xsi[k] + c];
+                buf[xdi[k] + c] = buf[xdi[k] + c] + v * xal[k];
+            }
+        if (dy != prev) {
+            for (int x = 0; x < W; ++x) {
+                const size_t o = (size_t)prev * W + x;
+                if (esize == 1) {
+                    long r = lrintf(sum[x]);
+                    ((uint8_t*)dst)[o] = (uint8_t)(r < 0 ? 0 : (r > 255 ? 255 : r));
+                } else {
+                    ((float*)dst)[o] = sum[x];
+                }
+                sum[x] = beta * buf[x];
+            }
+            prev = dy;
+        } else {
+            for (int x = 0; x < W; ++x) sum[x] = sum[x] + beta * buf[x];
+        }
+    }
+    for (int x = 0; x < W; ++x) {
+        const size_t o = (size_t)prev * W + x;
+        if (esize == 1) {
+            long r = lrintf(sum[x]);
+            ((uint8_t*)dst)[o] = (uint8_t)(r < 0 ? 0 : (r > 255 ? 255 : r));
+        } else {
+            ((float*)dst)[o] = sum[x];
+        }
+    }
+    free(xdi); free(xsi); free(ydi); free(ysi); free(xal); free(yal); free(buf); free(sum);
+}
+
+/* the area-mode bilinear taps of one axis (cv::resize, area_mode branch) */
+void oracle_area_linear_tap(int d, int n_in, double scale, double inv_scale, int* i, float* f) {
+    int sx = (int)floor(d * scale);
+    float fx = (float)((d + 1) - (sx + 1) * inv_scale);
+    fx = fx <= 0 ? 0.f : fx - (float)floor(fx);
+    if (sx >= n_in - 1) { fx = 0.f; sx = n_in - 1; }
+    *i = sx;
+    *f = fx;
+}
+
+static void area_up(const void* src, int w_in, int h_in, int cc, int esize, void* dst, int w_out, int h_out,
+                    double sx, double sy, double ix, double iy) {
+    for (int y = 0; y < h_out; ++y) {
+        int ty; float fy;
+        oracle_area_linear_tap(y, h_in, sy, iy, &ty, &fy);
+        const int ty1 = ty + 1 < h_in ? ty + 1 : h_in - 1;
+        const float b0f = 1.f - fy, b1f = fy;
+        const int b0 = (int)lrintf(b0f * 2048.f), b1 = (int)lrintf(b1f * 2048.f);
+        for (int x = 0; x < w_out; ++x) {
+            int tx; float fx;
+            oracle_area_linear_tap(x, w_in, sx, ix, &tx, &fx);
+            const int tx1 = tx + 1 < w_in ? tx + 1 : w_in - 1;
+            const float a0f = 1.f - fx, a1f = fx;
+            const int a0 = (int)lrintf(a0f * 2048.f), a1 = (int)lrintf(a1f * 2048.f);
+            for (int c = 0; c < cc; ++c) {
+                const size_t p00 = ((size_t)ty * w_in + tx) * cc + c, p01 = ((size_t)ty * w_in + tx1) * cc + c;
+                const size_t p10 = ((size_t)ty1 * w_in + tx) * cc + c, p11 = ((size_t)ty1 * w_in + tx1) * cc + c;
+                const size_t o = ((size_t)y * w_out + x) * cc + c;
+                if (esize == 1) {
+                    const uint8_t* S = (const uint8_t*)src;
+                    /* dx >= xmax (tx == w_in - 1): S[tx] * 2048, i.e. a1 = 0 */
+                    const int h0 = S[p00] * a0 + S[p01] * a1, h1 = S[p10] * a0 + S[p11] * a1;
+                    int v = ((((int16_t)(h0 >> 4)) * b0) >> 16) + ((((int16_t)(h1 >> 4)) * b1) >> 16) + 2;
+                    v >>= 2;
+                    ((uint8_t*)dst)[o] = (uint8_t)(v < 0 ? 0 : (v > 255 ? 255 : v));
+                } else {
+                    const float* S = (const float*)src;
+                    const float h0 = tx >= w_in - 1 ? S[p00] : S[p00] * a0f + S[p01] * a1f;
+                    const float h1 = tx >= w_in - 1 ? S[p10] : S[p10] * a0f + S[p11] * a1f;
+                    ((float*)dst)[o] = h0 * b0f + h1 * b1f;
+                }
+            }
+        }
+    }
+}
+
+/* INTER_AREA at any scale: the integer fast path (above), resizeArea_ or the
+ * area-mode bilinear.  inv_x / inv_y = cv::resize's inv_scale (0: dsize /
+ * ssize, the dsize given case). */
+void oracle_resize_area_any(const void* src, int w_in, int h_in, int cc, int esize, void* dst, int w_out,
+                            int h_out, double inv_x, double inv_y) {
+    if (inv_x <= 0) inv_x = (double)w_out / w_in;
+    if (inv_y <= 0) inv_y = (double)h_out / h_in;
+    const double sx = 1. / inv_x, sy = 1. / inv_y;
+    if (sx >= 1 && sy >= 1) {
+        const double rx = nearbyint(sx), ry = nearbyint(sy);
+        if (fabs(sx - rx) < DBL_EPSILON && fabs(sy - ry) < DBL_EPSILON && (int)rx * w_out == w_in &&
+            (int)ry * h_out == h_in) {
+            oracle_resize_area(src, w_in, h_in, cc, esize, dst, w_out, h_out);
+            return;
+        }
+        area_frac(src, w_in, h_in, cc, esize, dst, w_out, h_out, sx, sy);
+        return;
+    }
+    area_up(src, w_in, h_in, cc, esize, dst, w_out, h_out, sx, sy, inv_x, inv_y);
+}
+
 /* fp32 bilinear, resize_naive.cpp:70-128; value summed lt,lb,rt,rb. */
 void oracle_resize_linear_f32(const float* src, int w_in, int h_in, int cc,
                               float* dst, int w_out, int h_out) {
@@ -402,6 +568,86 @@ void oracle_warp_affine_f32(const float* src, int w_in, int h_in, int cc,
                 v += r0[cc + k] * x1 * y0;
                 v += r1[cc + k] * x1 * y1;
                 out[k] = v;
+            }
+        }
+    }
+}
+
+/* Border modes other than BORDER_CONSTANT (build extension, PARITY UNPINNED:
+ * the reference hands them to OpenCV, warp_affine.cpp:114-118 -> :48-50, and
+ * recurses forever without it).  Pixels whose top-left tap is inside
+ * [0,w-2]x[0,h-2] are exactly the naive sampler's (above); every other pixel
+ * takes its four taps at floor(f), floor(f)+1 mapped through OpenCV 2.4's
+ * borderInterpolate (core/base.hpp: REPLICATE clamps, REFLECT and
+ * REFLECT_101 mirror, WRAP is modulo; the reflect loop restated in closed
+ * form), with the naive sampler's weights: w0 = SATURATE_CAST_SHORT((1 -
+ * frac) * 2048), w1 = 2048 - w0 for u8; (1 - frac, frac) in the lt, lb, rt,
+ * rb order for fp32.  f is clamped to +-1e9 first (NaN -> -1e9).
+ * TRANSPARENT (5) and CONSTANT (0) leave those pixels to the caller.
+ * mode: 1 REPLICATE, 2 REFLECT, 3 WRAP, 4 REFLECT_101. */
+static int oracle_border_index(int p, int len, int mode) {
+    if (p >= 0 && p < len) return p;
+    if (mode == 1) return p < 0 ? 0 : len - 1;
+    if (mode == 3) {
+        int q = p % len;
+        return q < 0 ? q + len : q;
+    }
+    if (len == 1) return 0;
+    {
+        const int delta = mode == 4;
+        /* borderInterpolate's loop: p < 0 -> -p - 1 + delta; p >= len ->
+         * len - 1 - (p - len) - delta; repeat until inside.  Closed form: */
+        const long long period = 2LL * len - 2 * delta;
+        long long q = (long long)p % period;
+        if (q < 0) q += period;
+        return (int)(q < len ? q : period - 1 + delta - q);
+    }
+}
+
+static void oracle_border_tap(float f, int* i, float* frac) {
+    float c = f;
+    if (!(c >= -1e9f)) c = -1e9f; /* also NaN */
+    if (c > 1e9f) c = 1e9f;
+    *i = (int)floorf(c);
+    *frac = c - (float)*i;
+}
+
+void oracle_warp_affine_border(const void* src, int w_in, int h_in, int cc, int esize,
+                               void* dst, int w_out, int h_out, const float m[6], int mode) {
+    for (int y = 0; y < h_out; ++y) {
+        for (int x = 0; x < w_out; ++x) {
+            float fx = m[0] * (float)x + m[1] * (float)y + m[2];
+            float fy = m[3] * (float)x + m[4] * (float)y + m[5];
+            int sx, sy, ix, iy;
+            float ax, ay;
+            if (warp_tap(fy, h_in, &sy, &ay) && warp_tap(fx, w_in, &sx, &ax)) continue; /* interior */
+            if (mode < 1 || mode > 4) continue;
+            oracle_border_tap(fx, &ix, &ax);
+            oracle_border_tap(fy, &iy, &ay);
+            const int x0 = oracle_border_index(ix, w_in, mode), x1 = oracle_border_index(ix + 1, w_in, mode);
+            const int y0 = oracle_border_index(iy, h_in, mode), y1 = oracle_border_index(iy + 1, h_in, mode);
+            const size_t lt = ((size_t)y0 * w_in + x0) * cc, rt = ((size_t)y0 * w_in + x1) * cc;
+            const size_t lb = ((size_t)y1 * w_in + x0) * cc, rb = ((size_t)y1 * w_in + x1) * cc;
+            const size_t o = ((size_t)y * w_out + x) * cc;
+            if (esize == 1) {
+                const uint8_t* s = (const uint8_t*)src;
+                const int32_t wy0 = oracle_sat_short((1.f - ay) * 2048.f), wy1 = 2048 - wy0;
+                const int32_t wx0 = oracle_sat_short((1.f - ax) * 2048.f), wx1 = 2048 - wx0;
+                for (int k = 0; k < cc; ++k) {
+                    const int32_t v = s[lt + k] * wx0 * wy0 + s[lb + k] * wx0 * wy1 +
+                                      s[rt + k] * wx1 * wy0 + s[rb + k] * wx1 * wy1;
+                    ((uint8_t*)dst)[o + k] = (uint8_t)(v >> 22);
+                }
+            } else {
+                const float* s = (const float*)src;
+                const float ya = 1.f - ay, yb = ay, xa = 1.f - ax, xb = ax;
+                for (int k = 0; k < cc; ++k) {
+                    float v = s[lt + k] * xa * ya;
+                    v += s[lb + k] * xa * yb;
+                    v += s[rt + k] * xb * ya;
+                    v += s[rb + k] * xb * yb;
+                    ((float*)dst)[o + k] = v;
+                }
             }
         }
     }

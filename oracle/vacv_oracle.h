@@ -42,12 +42,22 @@ void oracle_resize_nearest(const void* src, int w_in, int h_in, int cc, int esiz
                            void* dst, int w_out, int h_out);
 void oracle_resize_area(const void* src, int w_in, int h_in, int cc, int esize,
                         void* dst, int w_out, int h_out);
+/* INTER_AREA at any scale (cv::resize of OpenCV 2.4.13.4: resizeAreaFast_,
+ * resizeArea_ or the area-mode bilinear); inv_x/inv_y <= 0: dsize / ssize */
+void oracle_resize_area_any(const void* src, int w_in, int h_in, int cc, int esize, void* dst, int w_out,
+                            int h_out, double inv_x, double inv_y);
+int oracle_area_table(int ssize, int dsize, int cn, double scale, int* di, int* si, float* alpha);
+void oracle_area_linear_tap(int d, int n_in, double scale, double inv_scale, int* i, float* f);
 void oracle_resize_cubic_f32(const float* src, int w_in, int h_in, int cc,
                              float* dst, int w_out, int h_out);
 void oracle_warp_affine_u8(const uint8_t* src, int w_in, int h_in, int cc,
                            uint8_t* dst, int w_out, int h_out, const float inv[6]);
 void oracle_warp_affine_f32(const float* src, int w_in, int h_in, int cc,
                             float* dst, int w_out, int h_out, const float inv[6]);
+/* non-CONSTANT border modes (1 REPLICATE, 2 REFLECT, 3 WRAP, 4 REFLECT_101) for
+ * the pixels the naive sampler skips; esize 1 (u8) or 4 (fp32) */
+void oracle_warp_affine_border(const void* src, int w_in, int h_in, int cc, int esize,
+                               void* dst, int w_out, int h_out, const float m[6], int mode);
 
 /* --- colour ------------------------------------------------------------ */
 void oracle_yuv420sp_to_bgr(const uint8_t* src, uint8_t* dst, int w, int h, int v_first, int rgb_out);

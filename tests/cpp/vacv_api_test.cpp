@@ -526,11 +526,16 @@ Result tensor_semantics_case() {
     va_cv::resize(img, img, VSize(320, 180));
     if (std::memcmp(img.data, want.data, want.len()) != 0) err += "aliased resize differs; ";
     // unsupported combinations fail loudly
-    try {
+    {
+        // fractional INTER_AREA (OpenCV 2.4 resizeArea_) and dsize = 0 with
+        // fx / fy (cv::resize derives the size): shapes only here, values in
+        // the Python parity tests
         Tensor o;
         va_cv::resize(img, o, VSize(7, 7), 0, 0, INTER_AREA);
-        err += "fractional INTER_AREA did not throw; ";
-    } catch (const std::runtime_error&) {
+        if (o.w != 7 || o.h != 7 || o.c != 3) err += "fractional INTER_AREA shape; ";
+        Tensor p;
+        va_cv::resize(img, p, VSize(0, 0), 0.25, 0.5, INTER_NEAREST);
+        if (p.w != 80 || p.h != 90) err += "fx/fy INTER_NEAREST shape; ";
     }
     {
         // integer INTER_AREA (OpenCV 2.4 resizeAreaFast_): 2x2 block means of a

@@ -71,12 +71,12 @@ def test_argument_validation_without_device(lib):
     assert lib.vacv_crop(ctypes.byref(good), ctypes.byref(dst), 6, 0, None) == -1      # rect outside
     assert lib.vacv_resize(ctypes.byref(good), ctypes.byref(dst), 4, 0, None) == -2    # INTER_LANCZOS4
     dst3 = VacvImage(0x2000, 1, 3, 3, 3, 2, 1, 0, 0, 0)
-    assert lib.vacv_resize(ctypes.byref(good), ctypes.byref(dst3), 3, 0, None) == -2   # INTER_AREA, 8/3
+    assert lib.vacv_resize_scaled(ctypes.byref(good), ctypes.byref(dst3), 3, 0, 0.0, 0.5, None) == -1  # fx <= 0
+    assert lib.vacv_resize_scaled(ctypes.byref(good), ctypes.byref(dst3), 1, 0, 0.5, 0.5, None) == -2  # LINEAR
     up = VacvImage(0x2000, 1, 16, 16, 3, 2, 1, 0, 0, 0)
-    assert lib.vacv_resize(ctypes.byref(good), ctypes.byref(up), 3, 0, None) == -2     # INTER_AREA upscale
     assert lib.vacv_resize(ctypes.byref(good), ctypes.byref(dst), 1, 7, None) == -1    # bad mode
     m = (ctypes.c_float * 6)(1, 0, 0, 0, 1, 0)
-    assert lib.vacv_warp_affine(ctypes.byref(good), ctypes.byref(dst), m, 1, 1, None, None) == -2  # REPLICATE
+    assert lib.vacv_warp_affine(ctypes.byref(good), ctypes.byref(dst), m, 1, 16, None, None) == -2  # BORDER_ISOLATED
     assert lib.vacv_warp_affine(ctypes.byref(good), ctypes.byref(dst), m, 2, 0, None, None) == -2  # CUBIC
     yuv = VacvImage(0x1000, 1, 7, 9, 1, 2, 1, 0, 0, 0)
     bgr = VacvImage(0x2000, 1, 7, 6, 3, 2, 1, 0, 0, 0)

@@ -320,6 +320,59 @@ def test_resize_area(ops, dev, oracle):
         assert_same(got.reshape(64, 384, c), oracle.resize_area(big, 384, 64).reshape(64, 384, c), f"area tie c{c}")
 
 
+def test_resize_area_any_scale(ops, dev, oracle):
+    """INTER_AREA at non-integer scales (OpenCV 2.4 cv::resize restated,
+    parity unpinned -- oracle/vacv_oracle.c oracle_resize_area_any):
+    resizeArea_ weight tables for down-scales, the area-mode bilinear for
+    up-scales and mixed scales; u8 and fp32, NHWC c = 1..4 and NCHW, the
+    normalize epilogue, cv::resize's fx / fy form (dsize derived, inv_scale =
+    fx), and 1080p -> 1280x720 / 800x600 at full size."""
+    from vacv_amd import INTER_AREA, NCHW
+    rng = np.random.default_rng(41)
+    for i, c in enumerate((1, 2, 3, 4)):
+        img = synthetic_image(800 + i, 60, 84, c)
+        img = img if c > 1 else img[..., None]
+        f = (img.astype(np.float32) + rng.standard_normal(img.shape).astype(np.float32)).astype(np.float32)
+        sq = (lambda a: a) if c > 1 else (lambda a: a[..., 0])
+        for wo, ho in [(33, 21), (50, 37), (83, 59), (100, 77), (30, 90), (168, 61), (84, 25)]:
+            got = host(ops.resize(to_dev(img[None], dev), wo, ho, interpolation=INTER_AREA))[0]
+            assert_same(sq(got), oracle.resize_area_any(sq(img), wo, ho), f"area u8 c{c} -> {wo}x{ho}")
+            gotf = host(ops.resize(to_dev(f[None], dev), wo, ho, interpolation=INTER_AREA))[0]
+            assert_same(sq(gotf), oracle.resize_area_any(sq(f), wo, ho), f"area f32 c{c} -> {wo}x{ho}")
+    img = synthetic_image(810, 60, 84, 3)
+    chw = np.ascontiguousarray(img.transpose(2, 0, 1))
+    got = host(ops.resize(to_dev(chw[None], dev), 37, 26, interpolation=INTER_AREA, layout=NCHW))[0]
+    for k in range(3):
+        assert_same(got[k], oracle.resize_area_any(chw[k], 37, 26), "area any chw")
+    got = host(ops.resize_normalize(to_dev(img[None], dev), 50, 37, MEAN, STD, interpolation=INTER_AREA))[0]
+    want = oracle.normalize(oracle.u8_to_f32(oracle.resize_area_any(img, 50, 37)), MEAN, STD)
+    assert_same(got, want, "area any normalize")
+    for fx, fy in [(0.3, 0.7), (2.5, 1.25), (0.5, 0.5)]:
+        got = host(ops.resize(to_dev(img[None], dev), 0, 0, interpolation=INTER_AREA, fx=fx, fy=fy))[0]
+        wo, ho = int(round(84 * fx)), int(round(60 * fy))
+        assert_same(got, oracle.resize_area_any(img, wo, ho, fx, fy), f"area fx={fx} fy={fy}")
+    big = np.stack([synthetic_image(820 + k, 1080, 1920, 3) for k in range(2)])
+    for wo, ho in [(1280, 720), (800, 600)]:
+        got = host(ops.resize(to_dev(big, dev), wo, ho, interpolation=INTER_AREA))
+        assert_same(got[1], oracle.resize_area_any(big[1], wo, ho), f"area 1080p -> {wo}x{ho}")
+
+
+def test_resize_nearest_scaled(ops, dev, oracle):
+    """cv::resize's fx / fy form for INTER_NEAREST: dsize = round(w * fx) and
+    ifx = 1 / fx (not w_in / w_out)."""
+    from vacv_amd import INTER_NEAREST
+    img = synthetic_image(830, 61, 77, 3)
+    for fx, fy in [(0.3, 0.7), (2.5, 1.25), (1.0 / 3, 0.6)]:
+        got = host(ops.resize(to_dev(img[None], dev), 0, 0, interpolation=INTER_NEAREST, fx=fx, fy=fy))[0]
+        wo, ho = int(round(77 * fx)), int(round(61 * fy))
+        want = np.empty((ho, wo, 3), np.uint8)
+        for y in range(ho):
+            sy = min(int(np.floor(y * (1.0 / fy))), 60)
+            for x in range(wo):
+                want[y, x] = img[sy, min(int(np.floor(x * (1.0 / fx))), 76)]
+        assert_same(got, want, f"nearest fx={fx} fy={fy}")
+
+
 def test_resize_full_size_batch(ops, dev, oracle):
     """BASELINE cfg2 at full size: 1920x1080 -> 640x360 / 1280x720, batch of 3,
     plus a pitched source (a sub-window of a wider buffer)."""
@@ -478,14 +531,59 @@ def test_warp_affine_config_and_harness(ops, dev, oracle, golden):
     assert_same(got[1], want, "warp_affine_normalize")
 
 
+def test_warp_border_modes(ops, dev, oracle):
+    """BORDER_REPLICATE / REFLECT / WRAP / REFLECT_101 / TRANSPARENT (the
+    reference hands them to OpenCV, warp_affine.cpp:114-118; here the naive
+    sampler with OpenCV's borderInterpolate taps, parity unpinned --
+    oracle/vacv_oracle.c): u8 and fp32, NHWC c = 1 and 3 and NCHW, the
+    batched and per-pixel kernels, maps that reach far outside the source (a
+    shrink with a large offset), the normalize epilogue; TRANSPARENT keeps
+    the destination's bytes where the sampler has no taps."""
+    import torch
+    from vacv_amd import NCHW
+    mats = [ops.rotation_matrix(0.7, 33.0, (40, 30, 50, 35)),
+            np.array([0.3, 0.05, 70.0, -0.04, 0.35, -20.0], np.float32),   # shrink + big offset: wraps often
+            np.array([-1.6, 0.1, 150.0, 0.2, 1.3, -9.5], np.float32)]       # flip + up-scale
+    for c in (1, 3):
+        img = synthetic_image(300 + c, 61, 83, c).reshape(61, 83, c)
+        f = img.astype(np.float32) * np.float32(0.75) + np.float32(0.125)
+        for m in mats:
+            for mode in (1, 2, 3, 4):
+                for knob in (2, 0):
+                    with ops.tuning(WARP_KERNEL=knob):
+                        got = host(ops.warp_affine(to_dev(img[None], dev), m, 97, 71, border_mode=mode))[0]
+                        gotf = host(ops.warp_affine(to_dev(f[None], dev), m, 97, 71, border_mode=mode))[0]
+                    want = oracle.warp_affine(img, m, 97, 71, border_mode=mode).reshape(71, 97, c)
+                    assert_same(got.reshape(71, 97, c), want, f"border {mode} u8 c{c} kernel={knob}")
+                    wantf = oracle.warp_affine(f, m, 97, 71, border_mode=mode).reshape(71, 97, c)
+                    assert_same(gotf.reshape(71, 97, c), wantf, f"border {mode} f32 c{c}")
+            prev = np.full((71, 97, c), 77, np.uint8)
+            for knob in (2, 0):
+                with ops.tuning(WARP_KERNEL=knob):
+                    out = to_dev(prev[None], dev)
+                    ops.warp_affine(to_dev(img[None], dev), m, 97, 71, border_mode=5, out=out)
+                want = oracle.warp_affine(img, m, 97, 71, border_mode=5, dst=prev.reshape(71, 97, c) if c > 1
+                                          else prev.reshape(71, 97)).reshape(71, 97, c)
+                assert_same(host(out)[0].reshape(71, 97, c), want, f"transparent c{c} kernel={knob}")
+    img = synthetic_image(310, 61, 83, 3)
+    chw = to_dev(np.ascontiguousarray(img.transpose(2, 0, 1))[None], dev)
+    got = host(ops.warp_affine(chw, mats[1], 97, 71, border_mode=4, layout=NCHW))[0]
+    for k in range(3):
+        assert_same(got[k], oracle.warp_affine(np.ascontiguousarray(img[..., k]), mats[1], 97, 71, border_mode=4),
+                    "border chw")
+    got = host(ops.warp_affine_normalize(to_dev(img[None], dev), mats[0], 97, 71, MEAN, STD, border_mode=1))[0]
+    want = oracle.normalize(oracle.u8_to_f32(oracle.warp_affine(img, mats[0], 97, 71, border_mode=1)), MEAN, STD)
+    assert_same(got, want, "border normalize")
+
+
 def test_warp_kernels_agree(ops, dev, oracle):
-    """u8 warps run on the LDS-staged tile kernel (k_warp_staged.hip) where its
-    source footprint fits the LDS budget, else on the per-pixel gather kernel
-    (k_warp.hip); VACV_TUNE_WARP_KERNEL = 0 forces the gather kernel and
-    VACV_TUNE_WARP_PX switches its lane blocks per wave (4, 5, 8, 10).
+    """u8 BORDER_CONSTANT warps run on the batched gather kernel
+    (warp_u8_kernel, k_warp.hip) where a 64-pixel output row spans few source
+    rows, else on the per-pixel kernel (warp_kernel);
+    VACV_TUNE_WARP_KERNEL = 2 / 0 forces one or the other and
+    VACV_TUNE_WARP_PX switches the lane blocks per wave (4, 5, 8, 10).
     Identical outputs at full size for rotations, flips, shears, strong
-    down-scales (footprint over budget: the gather kernel), fused
-    normalisation, NCHW planes and a pitched destination."""
+    down-scales, fused normalisation, NCHW planes and a pitched destination."""
     import torch
     from vacv_amd import NCHW
     imgs = np.stack([synthetic_image(80 + k, 720, 1280, 3) for k in range(2)])
@@ -498,7 +596,7 @@ def test_warp_kernels_agree(ops, dev, oracle):
             np.array([1, 0, 0.5, 0, 1, -0.25], np.float32)]
     for m in mats:
         for wo, ho in [(1280, 720), (333, 211)]:
-            with ops.tuning(WARP_KERNEL=1):
+            with ops.tuning(WARP_KERNEL=2):
                 a = ops.warp_affine(src, m, wo, ho)
                 an = ops.warp_affine_normalize(src, m, wo, ho, MEAN, STD)
             with ops.tuning(WARP_KERNEL=0):
@@ -514,11 +612,11 @@ def test_warp_kernels_agree(ops, dev, oracle):
     for c in (1, 2, 3, 4):  # every pixel width, odd sizes, both kernels vs the oracle
         im = synthetic_image(90 + c, 97, 143, c)
         for m in mats[:2]:
-            for flag in (1, 0):
+            for flag in (2, 0):
                 with ops.tuning(WARP_KERNEL=flag):
                     got = host(ops.warp_affine(to_dev(im.reshape(1, 97, 143, c), dev), m, 121, 83))[0]
                 assert_same(got.reshape(83, 121, c), oracle.warp_affine(im, m, 121, 83).reshape(83, 121, c),
-                            f"warp c={c} staged={flag}")
+                            f"warp c={c} kernel={flag}")
     chw = to_dev(np.ascontiguousarray(imgs.transpose(0, 3, 1, 2)), dev)
     got = host(ops.warp_affine(chw, mats[0], 300, 200, layout=NCHW))
     for k in range(3):
@@ -736,13 +834,12 @@ def test_error_statuses(ops, dev):
     with pytest.raises(V.VacvError) as e:
         ops.resize(x, 4, 4, interpolation=4)  # INTER_LANCZOS4
     assert e.value.status == V._lib.ERR_UNSUPPORTED
-    for wo, ho in [(3, 3), (16, 16), (4, 3)]:  # INTER_AREA: fractional scales, upscales
-        with pytest.raises(V.VacvError) as e:
-            ops.resize(x, wo, ho, interpolation=V.INTER_AREA)
-        assert e.value.status == V._lib.ERR_UNSUPPORTED
-    with pytest.raises(V.VacvError) as e:
-        ops.warp_affine(x, np.eye(2, 3, dtype=np.float32), 8, 8, border_mode=V.BORDER_REPLICATE)
+    with pytest.raises(V.VacvError) as e:  # BORDER_ISOLATED has no meaning for warp_affine
+        ops.warp_affine(x, np.eye(2, 3, dtype=np.float32), 8, 8, border_mode=16)
     assert e.value.status == V._lib.ERR_UNSUPPORTED
+    with pytest.raises(V.VacvError) as e:  # TRANSPARENT in place
+        ops.warp_affine(x, np.eye(2, 3, dtype=np.float32), 8, 8, border_mode=V.BORDER_TRANSPARENT, out=x)
+    assert e.value.status == V._lib.ERR_INVALID_ARG
     with pytest.raises(V.VacvError):
         ops.resize(x, 4, 4, interpolation=V.INTER_CUBIC, out=torch.zeros((1, 4, 4, 3), dtype=torch.uint8, device=dev))
     with pytest.raises(ValueError):

@@ -226,3 +226,118 @@ def test_resize_area_restatement(oracle):
         got = oracle.resize_area(blk if c > 1 else blk[:, :, 0], 4, 1).reshape(4, c)[:, 0].tolist()
         want = [1, 2, 3, 4] if c != 2 else [0, 2, 2, 4]
         assert got == want, (c, got)
+
+
+def test_warp_border_modes_restatement(oracle):
+    """The non-CONSTANT warp border modes of oracle/vacv_oracle.c (a build
+    extension, parity unpinned) against an independent numpy statement:
+    OpenCV 2.4 borderInterpolate's loops run literally, the naive sampler's
+    float coordinates and fixed-point weights."""
+    import numpy as np
+    from oracle import synthetic_image
+
+    def interp(p, n, mode):  # core/base.hpp borderInterpolate, as written
+        if 0 <= p < n:
+            return p
+        if mode == 1:
+            return 0 if p < 0 else n - 1
+        if mode == 3:
+            return p % n
+        d = 1 if mode == 4 else 0
+        if n == 1:
+            return 0
+        while not 0 <= p < n:
+            p = -p - 1 + d if p < 0 else n - 1 - (p - n) - d
+        return p
+
+    img = synthetic_image(21, 9, 13, 2)
+    m = np.array([0.8, 0.3, -4.0, -0.25, 0.9, 3.5], np.float32)
+    inv = oracle.invert_affine(m)
+    f32 = np.float32
+    for mode in (1, 2, 3, 4):
+        got = oracle.warp_affine(img, m, 20, 15, border_mode=mode)
+        for y in range(15):
+            for x in range(20):
+                fx = f32(f32(inv[0] * f32(x)) + f32(inv[1] * f32(y))) + inv[2]
+                fy = f32(f32(inv[3] * f32(x)) + f32(inv[4] * f32(y))) + inv[5]
+                ix, iy = int(np.floor(fx)), int(np.floor(fy))
+                if 0 <= ix <= 11 and 0 <= iy <= 7:
+                    continue  # the naive sampler's own pixels: pinned by the golden vectors
+                ax, ay = f32(fx - f32(ix)), f32(fy - f32(iy))
+                wx0 = int(f32(f32(f32(1) - ax) * f32(2048)) + f32(0.5))
+                wy0 = int(f32(f32(f32(1) - ay) * f32(2048)) + f32(0.5))
+                wx1, wy1 = 2048 - wx0, 2048 - wy0
+                x0, x1 = interp(ix, 13, mode), interp(ix + 1, 13, mode)
+                y0, y1 = interp(iy, 9, mode), interp(iy + 1, 9, mode)
+                for k in range(2):
+                    v = (int(img[y0, x0, k]) * wx0 * wy0 + int(img[y1, x0, k]) * wx0 * wy1 +
+                         int(img[y0, x1, k]) * wx1 * wy0 + int(img[y1, x1, k]) * wx1 * wy1) >> 22
+                    assert got[y, x, k] == v, (mode, x, y, k)
+
+
+def test_resize_area_any_restatement(oracle):
+    """OpenCV 2.4 resizeArea_ (fractional INTER_AREA down-scales) and the
+    area-mode bilinear (up-scales) as restated in oracle/vacv_oracle.c (a
+    build extension, parity unpinned), against an independent numpy
+    statement of imgwarp.cpp's computeResizeAreaTab / row loop and of the
+    area-mode tap formula with the fixed-point rows."""
+    import math
+    import numpy as np
+    from oracle import synthetic_image
+    f32 = np.float32
+
+    def tab(ssize, dsize, scale):
+        out = [[] for _ in range(dsize)]
+        for dx in range(dsize):
+            fsx1 = dx * scale
+            fsx2 = fsx1 + scale
+            cell = min(scale, ssize - fsx1)
+            sx1, sx2 = math.ceil(fsx1), math.floor(fsx2)
+            sx2 = min(sx2, ssize - 1)
+            sx1 = min(sx1, sx2)
+            if sx1 - fsx1 > 1e-3:
+                out[dx].append((sx1 - 1, f32((sx1 - fsx1) / cell)))
+            for sx in range(sx1, sx2):
+                out[dx].append((sx, f32(1.0 / cell)))
+            if fsx2 - sx2 > 1e-3:
+                out[dx].append((sx2, f32(min(min(fsx2 - sx2, 1.0), cell) / cell)))
+        return out
+
+    img = synthetic_image(31, 17, 23, 2)
+    for wo, ho in [(10, 7), (15, 11), (22, 16)]:
+        xt, yt = tab(23, wo, 23 / wo), tab(17, ho, 17 / ho)
+        got = oracle.resize_area_any(img, wo, ho)
+        for y in range(ho):
+            for x in range(wo):
+                for c in range(2):
+                    sm = None
+                    for sy, beta in yt[y]:
+                        buf = f32(0)
+                        for sx, al in xt[x]:
+                            buf = f32(buf + f32(f32(img[sy, sx, c]) * al))
+                        t = f32(beta * buf)
+                        sm = t if sm is None else f32(sm + t)
+                    assert got[y, x, c] == min(255, max(0, int(np.rint(sm)))), (wo, ho, x, y, c)
+
+    def up_tap(d, n, scale, inv):
+        sx = math.floor(d * scale)
+        fx = f32((d + 1) - (sx + 1) * inv)
+        fx = f32(0) if fx <= 0 else f32(fx - f32(math.floor(fx)))
+        if sx >= n - 1:
+            sx, fx = n - 1, f32(0)
+        return sx, min(sx + 1, n - 1), fx
+
+    for wo, ho in [(40, 30), (60, 9)]:  # up in both axes; up in x, down in y
+        got = oracle.resize_area_any(img, wo, ho)
+        ix, iy = wo / 23, ho / 17
+        for y in range(ho):
+            y0, y1, fy = up_tap(y, 17, 1 / iy, iy)
+            b0, b1 = int(np.rint(f32(f32(1) - fy) * f32(2048))), int(np.rint(fy * f32(2048)))
+            for x in range(wo):
+                x0, x1, fx = up_tap(x, 23, 1 / ix, ix)
+                a0, a1 = int(np.rint(f32(f32(1) - fx) * f32(2048))), int(np.rint(fx * f32(2048)))
+                for c in range(2):
+                    h0 = int(img[y0, x0, c]) * a0 + int(img[y0, x1, c]) * a1
+                    h1 = int(img[y1, x0, c]) * a0 + int(img[y1, x1, c]) * a1
+                    v = (((h0 >> 4) * b0) >> 16) + (((h1 >> 4) * b1) >> 16) + 2
+                    assert got[y, x, c] == min(255, max(0, v >> 2)), (wo, ho, x, y, c)

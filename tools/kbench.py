@@ -21,6 +21,7 @@ def main():
     ap.add_argument("--op", default="resize_normalize")
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--batch", type=int, default=0)
+    ap.add_argument("--only", default="", help="run only the cases whose name contains this")
     ap.add_argument("--sweep", default="",
                     help="kernel-variant knobs (VACV_TUNE_*, vacv_set_tuning) to sweep, "
                          "e.g. 'DIRECT_ALIGN=0,1;RESIZE_WORK=2,4'")
@@ -125,6 +126,8 @@ def main():
         src = frames(n, 360, 640)
         cases["hwc_to_chw_640x360_u8"] = (lambda src=src: ops.change_layout(src, vacv_amd.NCHW),
                                           n * 640 * 360 * 6, n * 640 * 360)
+    if a.only:
+        cases = {k: v for k, v in cases.items() if a.only in k}
     import itertools
     knobs = [kv.split("=", 1) for kv in a.sweep.split(";") if kv]
     combos = list(itertools.product(*[[(k, v) for v in vals.split(",")] for k, vals in knobs])) or [()]
