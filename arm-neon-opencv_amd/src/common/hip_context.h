@@ -6,6 +6,7 @@
 #include <hip/hip_runtime_api.h>
 
 #include <cstddef>
+#include <functional>
 #include <vector>
 
 #include "../../../include/vacv_hip.h"
@@ -91,6 +92,39 @@ private:
     Lease _lease;
     std::vector<Tensor> _keep;
     std::vector<Copy> _d2h;
+};
+
+/// A sequence of frames through the same operator with the PCIe copies
+/// overlapped (the batched va_cv:: entry points).  Host
+/// frames go through a ring of kRing HBM slot pairs on two streams: H2D(i)
+/// and kernel(i) in order on one, D2H(i) on the other behind the kernel's
+/// event, so the H2D of frame i+1 runs while frame i's result comes back;
+/// the host waits for a slot's previous frame before reusing it.  Device
+/// frames skip their copies.  Every operand is kept alive until finish(),
+/// which waits for both streams.
+class FramePipeline {
+public:
+    using Launch = std::function<int(const vacv_image& src, const vacv_image& dst, hipStream_t stream)>;
+    FramePipeline(const char* fn, int device);
+    ~FramePipeline();
+    FramePipeline(const FramePipeline&) = delete;
+    FramePipeline& operator=(const FramePipeline&) = delete;
+    /// queue one frame: dst is created (placement of src) as (w, h, c, dtype,
+    /// layout) and written by launch() on the compute stream
+    void frame(const Tensor& src, Tensor& dst, int w, int h, int c, DType dtype, DLayout layout,
+               const Launch& launch);
+    void finish();
+
+    static constexpr int kRing = 6;
+    struct Ctx;  // streams, events and the slot ring (hip_context.cpp)
+
+private:
+    const char* _fn;
+    int _device;
+    int _prev;
+    Ctx* _ctx;
+    long _count;
+    std::vector<Tensor> _keep;
 };
 
 }  // namespace detail

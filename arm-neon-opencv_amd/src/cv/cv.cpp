@@ -256,6 +256,105 @@ void crop(const Tensor& src, Tensor& dst, const VRect& rect) {
     st.finish();
 }
 
+// ---- batched frames (FramePipeline: overlapped PCIe staging) ---------------
+
+namespace {
+
+using detail::FramePipeline;
+
+void check_batch(const char* fn, const std::vector<Tensor>& src, std::vector<Tensor>& dst) {
+    if (src.empty()) fail(fn, "empty frame list");
+    for (const Tensor& t : src)
+        if (t.device() != src[0].device()) fail(fn, "frames live on different devices");
+    dst.resize(src.size());
+}
+
+}  // namespace
+
+void resize(const std::vector<Tensor>& src, std::vector<Tensor>& dst, VSize dsize, double fx, double fy,
+            int interpolation) {
+    static const char* fn = "va_cv::resize";
+    check_batch(fn, src, dst);
+    const DType out = resize_out_dtype(fn, src[0], interpolation);
+    if (dsize.w < 1 || dsize.h < 1) fail(fn, "dsize must be positive");
+    (void)fx;
+    (void)fy;
+    FramePipeline p(fn, detail::compute_device(src[0]));
+    for (size_t i = 0; i < src.size(); ++i)
+        p.frame(src[i], dst[i], dsize.w, dsize.h, src[i].c, out, src[i].layout,
+                [&](const vacv_image& s, const vacv_image& d, hipStream_t st) {
+                    return vacv_resize(&s, &d, interpolation, VACV_LINEAR_REFERENCE, st);
+                });
+    p.finish();
+}
+
+void resize_normalize(const std::vector<Tensor>& src, std::vector<Tensor>& dst, VSize dsize, double /*fx*/,
+                      double /*fy*/, int interpolation, const Tensor& mean, const Tensor& stddev) {
+    static const char* fn = "va_cv::resize_normalize";
+    check_batch(fn, src, dst);
+    (void)resize_out_dtype(fn, src[0], interpolation);
+    if (dsize.w < 1 || dsize.h < 1) fail(fn, "dsize must be positive");
+    const Stats stats = read_stats(fn, mean, stddev, src[0].c, true);
+    FramePipeline p(fn, detail::compute_device(src[0]));
+    for (size_t i = 0; i < src.size(); ++i)
+        p.frame(src[i], dst[i], dsize.w, dsize.h, src[i].c, FP32, src[i].layout,
+                [&](const vacv_image& s, const vacv_image& d, hipStream_t st) {
+                    return vacv_resize_normalize(&s, &d, interpolation, VACV_LINEAR_REFERENCE, stats.m(), stats.s(),
+                                                 st);
+                });
+    p.finish();
+}
+
+void warp_affine(const std::vector<Tensor>& src, std::vector<Tensor>& dst, const Tensor& M, VSize dsize, int flags,
+                 int borderMode, const VScalar& bv) {
+    static const char* fn = "va_cv::warp_affine";
+    check_batch(fn, src, dst);
+    check_warp_modes(fn, src[0], flags, borderMode);
+    if (borderMode == BORDER_TRANSPARENT) fail(fn, "BORDER_TRANSPARENT needs the per-frame call");
+    if (dsize.w < 1 || dsize.h < 1) fail(fn, "dsize must be positive");
+    const std::vector<float> m = affine_of(fn, M);
+    const double border[4] = {bv.v0, bv.v1, bv.v2, bv.v3};
+    FramePipeline p(fn, detail::compute_device(src[0]));
+    for (size_t i = 0; i < src.size(); ++i)
+        p.frame(src[i], dst[i], dsize.w, dsize.h, src[i].c, src[i].dtype, src[i].layout,
+                [&](const vacv_image& s, const vacv_image& d, hipStream_t st) {
+                    return vacv_warp_affine(&s, &d, m.data(), flags, borderMode, border, st);
+                });
+    p.finish();
+}
+
+void cvt_color(const std::vector<Tensor>& src, std::vector<Tensor>& dst, int code) {
+    static const char* fn = "va_cv::cvt_color";
+    check_batch(fn, src, dst);
+    check_yuv_code(fn, code);
+    FramePipeline p(fn, detail::compute_device(src[0]));
+    for (size_t i = 0; i < src.size(); ++i) {
+        const int h = yuv_rows(fn, src[i]);
+        p.frame(src[i], dst[i], src[i].w, h, 3, INT8, NHWC,
+                [&](const vacv_image& s, const vacv_image& d, hipStream_t st) {
+                    return vacv_cvt_color(&s, &d, code, st);
+                });
+    }
+    p.finish();
+}
+
+void cvt_color_normalize(const std::vector<Tensor>& src, std::vector<Tensor>& dst, int code, const Tensor& mean,
+                         const Tensor& stddev) {
+    static const char* fn = "va_cv::cvt_color_normalize";
+    check_batch(fn, src, dst);
+    check_yuv_code(fn, code);
+    const Stats stats = read_stats(fn, mean, stddev, 3, false);
+    FramePipeline p(fn, detail::compute_device(src[0]));
+    for (size_t i = 0; i < src.size(); ++i) {
+        const int h = yuv_rows(fn, src[i]);
+        p.frame(src[i], dst[i], src[i].w, h, 3, FP32, NHWC,
+                [&](const vacv_image& s, const vacv_image& d, hipStream_t st) {
+                    return vacv_cvt_color_normalize(&s, &d, code, stats.m(), stats.s(), st);
+                });
+    }
+    p.finish();
+}
+
 void match_template(const Tensor&, const Tensor&, Tensor&, int) {
     fail("va_cv::match_template", "not provided by the MI355X build (OpenCV-only in the reference)");
 }

@@ -86,7 +86,9 @@ enum InputImageFormat {
     COLOR_YUV2BGR_YV12 = 99
 };
 
-/// Resize to dsize (fx, fy ignored, as in resize.cpp:51-56).
+/// Resize to dsize (fx, fy ignored, as in resize.cpp:51-56, except for
+/// INTER_NEAREST / INTER_AREA with dsize = 0, which the reference hands to
+/// cv::resize: dsize = round(w * fx, h * fy), inv_scale = fx, fy).
 /// INTER_LINEAR: INT8 -> INT8 (bit-exact with resize_naive_inter_linear_u8),
 /// FP32 -> FP32.  INTER_CUBIC: FP32 -> FP32, and INT8 -> FP32 (a fused widen;
 /// the reference recurses forever on INT8 cubic).  NHWC or NCHW.
@@ -106,8 +108,10 @@ void normalize(const vision::Tensor& src, vision::Tensor& dst,
                const vision::Tensor& mean = vision::Tensor(),
                const vision::Tensor& stddev = vision::Tensor());
 
-/// Affine warp by the FORWARD 2x3 map M (3x2x1 FP32 tensor), INTER_LINEAR +
-/// BORDER_CONSTANT (warp_affine.cpp:111-169).  M is not modified.
+/// Affine warp by the FORWARD 2x3 map M (3x2x1 FP32 tensor), INTER_LINEAR
+/// (warp_affine.cpp:111-169).  M is not modified.  BORDER_CONSTANT is the
+/// reference's naive path; REPLICATE / REFLECT / WRAP / REFLECT_101 /
+/// TRANSPARENT extend it (the reference hands them to OpenCV).
 void warp_affine(const vision::Tensor& src, vision::Tensor& dst,
                  const vision::Tensor& M, VSize dsize,
                  int flags = INTER_LINEAR,
@@ -171,6 +175,26 @@ void mean_stddev(const vision::Tensor& src, vision::Tensor& mean, vision::Tensor
 
 /// cvt_color then normalize, one kernel (the BASELINE cfg3 pipeline).
 void cvt_color_normalize(const vision::Tensor& src, vision::Tensor& dst, int code,
+                         const vision::Tensor& mean = vision::Tensor(),
+                         const vision::Tensor& stddev = vision::Tensor());
+
+/// Batched frames: the operator above applied to every
+/// frame of `src` into the matching `dst` (resized to src.size()).  Host
+/// frames are staged through a ring of HBM buffers on three HIP streams, so
+/// the H2D copy of frame i+1, the kernel of frame i and the D2H copy of frame
+/// i-1 overlap -- one call per frame serialises them on one stream.  Device
+/// frames run back to back.  Returns when every dst is written.
+void resize(const std::vector<vision::Tensor>& src, std::vector<vision::Tensor>& dst, VSize dsize,
+            double fx = 0, double fy = 0, int interpolation = INTER_LINEAR);
+void resize_normalize(const std::vector<vision::Tensor>& src, std::vector<vision::Tensor>& dst, VSize dsize,
+                      double fx = 0, double fy = 0, int interpolation = INTER_LINEAR,
+                      const vision::Tensor& mean = vision::Tensor(),
+                      const vision::Tensor& stddev = vision::Tensor());
+void warp_affine(const std::vector<vision::Tensor>& src, std::vector<vision::Tensor>& dst,
+                 const vision::Tensor& M, VSize dsize, int flags = INTER_LINEAR,
+                 int borderMode = BORDER_CONSTANT, const VScalar& borderValue = VScalar());
+void cvt_color(const std::vector<vision::Tensor>& src, std::vector<vision::Tensor>& dst, int code);
+void cvt_color_normalize(const std::vector<vision::Tensor>& src, std::vector<vision::Tensor>& dst, int code,
                          const vision::Tensor& mean = vision::Tensor(),
                          const vision::Tensor& stddev = vision::Tensor());
 

@@ -424,6 +424,65 @@ Result resize_normalize_case(int wi, int hi, int wo, int ho) {  // the headline 
     return r;
 }
 
+// batched frames (FramePipeline: H2D / kernel / D2H overlapped on three
+// streams) give the same bytes as one call per frame, for host and device
+// frames and every batched operator
+Result batch_frames_case() {
+    Result r;
+    r.cosine = 1.0;
+    std::string err;
+    const Tensor base = load_image(1920, 1080);
+    const int n = 7;  // more frames than the ring has slots
+    std::vector<Tensor> src(n);
+    for (int i = 0; i < n; ++i) {
+        src[i] = base.clone();
+        unsigned char* p = static_cast<unsigned char*>(src[i].data);
+        for (size_t b = 0; b < src[i].len(); b += 97) p[b] = (unsigned char)(p[b] + 13 * i);
+    }
+    const std::vector<float> mean = {103.94f, 116.78f, 123.68f}, stdv = {57.375f, 57.12f, 58.395f};
+    const Tensor tm = floats_of(mean), ts = floats_of(stdv);
+    std::vector<Tensor> out;
+    {
+        TIME_PERF(r.vacv_ms);
+        va_cv::resize_normalize(src, out, VSize(640, 360), 0, 0, INTER_LINEAR, tm, ts);
+    }
+    {
+        TIME_PERF(r.oracle_ms);  // here: the per-frame calls
+        for (int i = 0; i < n; ++i) {
+            Tensor one;
+            va_cv::resize_normalize(src[i], one, VSize(640, 360), 0, 0, INTER_LINEAR, tm, ts);
+            if ((int)out.size() != n || out[i].len() != one.len() || std::memcmp(out[i].data, one.data, one.len()))
+                err += "batched resize_normalize differs; ";
+        }
+    }
+    std::vector<Tensor> o2;
+    va_cv::resize(src, o2, VSize(1280, 720));
+    Tensor m(3, 2, 1, FP32, NHWC);
+    const float mv[6] = {0.9f, 0.1f, -20.f, -0.1f, 0.9f, 40.f};
+    std::memcpy(m.data, mv, sizeof(mv));
+    std::vector<Tensor> o3;
+    va_cv::warp_affine(src, o3, m, VSize(1000, 600));
+    for (int i = 0; i < n; ++i) {
+        Tensor a, b;
+        va_cv::resize(src[i], a, VSize(1280, 720));
+        va_cv::warp_affine(src[i], b, m, VSize(1000, 600));
+        if (std::memcmp(o2[i].data, a.data, a.len())) err += "batched resize differs; ";
+        if (std::memcmp(o3[i].data, b.data, b.len())) err += "batched warp differs; ";
+    }
+    std::vector<Tensor> dev(n), od;
+    for (int i = 0; i < n; ++i) dev[i] = src[i].to_device(0);
+    va_cv::resize_normalize(dev, od, VSize(640, 360), 0, 0, INTER_LINEAR, tm, ts);
+    for (int i = 0; i < n; ++i) {
+        const Tensor h = od[i].to_host();
+        if (!od[i].on_device() || std::memcmp(h.data, out[i].data, h.len())) err += "device frames differ; ";
+    }
+    if (!err.empty()) {
+        r.note = err;
+        r.tol = -1;
+    }
+    return r;
+}
+
 // device placement: the same pipeline on a device-resident tensor gives the
 // same bytes as on a host tensor, and nothing leaves HBM in between
 Result device_chain_case() {
@@ -625,6 +684,7 @@ int main(int argc, char** argv) {
         // additions: the headline fused op, device placement, Tensor semantics
         {"test_resize_normalize_hwc_1920x1080_640x360", [] { return resize_normalize_case(1920, 1080, 640, 360); }},
         {"test_device_chain_1920x1080", [] { return device_chain_case(); }},
+        {"test_batch_frames_1920x1080", [] { return batch_frames_case(); }},
         {"test_tensor_semantics", [] { return tensor_semantics_case(); }},
         {"test_tensor_host_semantics", [] { return tensor_host_case(); }},
     };
