@@ -1,0 +1,422 @@
+// k_match.hip -- match_template and minMaxIdx.
+//
+// The reference's MatchTemplate::match_template / minMaxIdx call
+// cv::matchTemplate / cv::minMaxIdx (match_template.cpp:13-46; the
+// naive/NEON bodies are empty todo stubs, :48-61).  OpenCV 2.4.13.4's
+// algorithm (templmatch.cpp): R = crossCorr(image, templ) as float, then a
+// per-method normalisation in double from window sums (integral images) and
+// the template's mean / stddev.  Here:
+//  * match_corr_u8_kernel: the correlation EXACTLY (u8: v_dot4_u32_u8 over
+//    4 bytes at a time, per-template-row u32 sums into u64), one image row per
+//    wave staged in LDS, the whole template in LDS, 4 adjacent outputs per
+//    lane sharing a sliding window of source dwords (v_alignbyte picks each
+//    output's 4 bytes); fp32 input: match_corr_f32_kernel, fp64 sums;
+//  * match_box_v_kernel: column sums of h rows (S and S^2 per element);
+//  * match_finish_kernel: row sums of w columns of those -> the window's
+//    per-channel S_c and Q, then OpenCV's normalisation formula, in double,
+//    in OpenCV's operation order;
+//  * match_tstats_kernel: the template's per-channel mean / stddev (one
+//    workgroup, fixed-order tree: deterministic).
+// For u8 every sum is exact, so the result is the exact correlation rounded
+// to float followed by OpenCV's double formula (OpenCV's own DFT crossCorr
+// rounds differently: parity unpinned).
+//  * min_max_kernel + min_max_final_kernel: cv::minMaxIdx of one channel --
+//    the first (row-major) min / max of the unmasked, non-NaN elements.
+#pragma clang fp contract(off)
+
+#include <algorithm>
+
+#include "vacv_device.hpp"
+
+namespace vacv {
+namespace {
+
+constexpr int kOutPerLane = 4;
+constexpr int kTileX = 64 * kOutPerLane;  // result columns per wave
+
+// ---- correlation ------------------------------------------------------------
+
+// wave w of the workgroup: result row r = blockIdx.y * 4 + w, columns
+// [blockIdx.x * kTileX, +kTileX); lane l: columns x0 + 4l .. 4l + 3
+template <int CN>
+__global__ void __launch_bounds__(kBlock) match_corr_u8_kernel(MatchLaunch M) {
+    extern __shared__ uint32_t lds[];
+    const int w = M.tw, h = M.th;
+    const int K = w * CN, K4 = (K + 3) >> 2;          // template row bytes, dwords (zero padded)
+    constexpr int NW = (3 * CN) / 4 + 2;          // window dwords per k4 step
+    const int span4 = 64 * CN + K4 + NW + 1;      // staged image dwords per row: every lane's window
+    uint32_t* tpl = lds;                               // [h][K4]
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    uint32_t* row = lds + h * K4 + wave * span4;
+    const int img = blockIdx.z;
+    const unsigned char* ib = M.img + (int64_t)img * M.img_pitch;
+    // the template, zero padded per row, once per workgroup
+    for (int i = threadIdx.x; i < h * K4; i += kBlock) {
+        const int yy = i / K4, k4 = i - yy * K4;
+        const unsigned char* tr = M.tpl + (int64_t)yy * M.tpl_row;
+        uint32_t v = 0;
+#pragma unroll
+        for (int b = 0; b < 4; ++b)
+            if (4 * k4 + b < K) v |= (uint32_t)tr[4 * k4 + b] << (8 * b);
+        tpl[i] = v;
+    }
+    __syncthreads();
+
+    const int r = blockIdx.y * 4 + wave;
+    const int x0 = blockIdx.x * kTileX;
+    if (r >= M.rh) return;  // whole wave (no barrier below)
+    const int ebase = x0 * CN;                    // first staged byte of each image row
+    const int row_bytes = M.iw * CN;
+    uint64_t acc[kOutPerLane] = {0, 0, 0, 0};
+    for (int yy = 0; yy < h; ++yy) {
+        // stage image row r + yy, bytes [ebase, ebase + 4*span4), zero past the row
+        const unsigned char* ir = ib + (int64_t)(r + yy) * M.img_row;
+        for (int d = lane; d < span4; d += 64) {
+            const int e = ebase + 4 * d;
+            uint32_t v = 0;
+            if (e + 4 <= row_bytes && ((reinterpret_cast<uintptr_t>(ir + e) & 3) == 0)) {
+                v = *reinterpret_cast<const uint32_t*>(ir + e);
+            } else {
+#pragma unroll
+                for (int b = 0; b < 4; ++b)
+                    if (e + b < row_bytes) v |= (uint32_t)ir[e + b] << (8 * b);
+            }
+            row[d] = v;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        // lane's outputs start at byte 4*lane*CN = dword lane*CN
+        const uint32_t* rp = row + lane * CN;
+        const uint32_t* tp = tpl + yy * K4;
+        uint32_t win[NW];
+#pragma unroll
+        for (int j = 0; j < NW; ++j) win[j] = rp[j];
+        uint32_t a32[kOutPerLane] = {0, 0, 0, 0};
+        for (int k4 = 0; k4 < K4; ++k4) {
+            const uint32_t t = tp[k4];  // LDS broadcast
+#pragma unroll
+            for (int o = 0; o < kOutPerLane; ++o) {
+                const int off = o * CN;  // byte offset of output o's window
+                const uint32_t v = (off & 3) ? __builtin_amdgcn_alignbyte(win[(off >> 2) + 1], win[off >> 2], off & 3)
+                                             : win[off >> 2];
+                a32[o] = __builtin_amdgcn_udot4(v, t, a32[o], false);
+            }
+#pragma unroll
+            for (int j = 0; j < NW - 1; ++j) win[j] = win[j + 1];
+            win[NW - 1] = rp[k4 + NW];
+        }
+#pragma unroll
+        for (int o = 0; o < kOutPerLane; ++o) acc[o] += a32[o];  // a row: <= 255^2 * K < 2^32
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+    float* out = reinterpret_cast<float*>(M.res + (int64_t)img * M.res_pitch + (int64_t)r * M.res_row);
+#pragma unroll
+    for (int o = 0; o < kOutPerLane; ++o) {
+        const int x = x0 + 4 * lane + o;
+        if (x < M.rw) out[x] = (float)(double)acc[o];  // crossCorr's float result
+    }
+}
+
+template <int CN>
+__global__ void __launch_bounds__(kBlock) match_corr_f32_kernel(MatchLaunch M) {
+    extern __shared__ uint32_t lds[];
+    float* tpl = reinterpret_cast<float*>(lds);
+    const int w = M.tw, h = M.th, K = w * CN;
+    const int span = (kTileX + w - 1) * CN;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    float* row = tpl + h * K + wave * span;
+    const int img = blockIdx.z;
+    const unsigned char* ib = M.img + (int64_t)img * M.img_pitch;
+    for (int i = threadIdx.x; i < h * K; i += kBlock) {
+        const int yy = i / K, k = i - yy * K;
+        tpl[i] = reinterpret_cast<const float*>(M.tpl + (int64_t)yy * M.tpl_row)[k];
+    }
+    __syncthreads();
+    const int r = blockIdx.y * 4 + wave;
+    const int x0 = blockIdx.x * kTileX;
+    if (r >= M.rh) return;
+    const int ebase = x0 * CN, row_el = M.iw * CN;
+    double acc[kOutPerLane] = {0, 0, 0, 0};
+    for (int yy = 0; yy < h; ++yy) {
+        const float* ir = reinterpret_cast<const float*>(ib + (int64_t)(r + yy) * M.img_row);
+        for (int e = lane; e < span; e += 64) row[e] = ebase + e < row_el ? ir[ebase + e] : 0.f;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        const float* rp = row + 4 * lane * CN;
+        const float* tp = tpl + yy * K;
+        for (int k = 0; k < K; ++k) {
+            const double t = tp[k];
+#pragma unroll
+            for (int o = 0; o < kOutPerLane; ++o) acc[o] += t * (double)rp[o * CN + k];
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+    float* out = reinterpret_cast<float*>(M.res + (int64_t)img * M.res_pitch + (int64_t)r * M.res_row);
+#pragma unroll
+    for (int o = 0; o < kOutPerLane; ++o) {
+        const int x = x0 + 4 * lane + o;
+        if (x < M.rw) out[x] = (float)acc[o];
+    }
+}
+
+// ---- window statistics ------------------------------------------------------
+
+// V[r][e] = sum_{yy < h} I[r + yy][e], V2 = the same of I^2 (double; exact for u8)
+template <typename T>
+__global__ void __launch_bounds__(kBlock) match_box_v_kernel(MatchLaunch M) {
+    const int e = blockIdx.x * kBlock + threadIdx.x;
+    const int r = blockIdx.y, img = blockIdx.z;
+    const int n_el = M.iw * M.cn;
+    if (e >= n_el) return;
+    const unsigned char* ib = M.img + (int64_t)img * M.img_pitch;
+    double s = 0, q = 0;
+    for (int yy = 0; yy < M.th; ++yy) {
+        const double v = (double)reinterpret_cast<const T*>(ib + (int64_t)(r + yy) * M.img_row)[e];
+        s += v;
+        q += v * v;
+    }
+    double* vb = M.box + ((int64_t)img * M.rh + r) * n_el * 2;
+    vb[e] = s;
+    vb[n_el + e] = q;
+}
+
+// one output: S_c / Q over the window, then templmatch.cpp's formula
+__global__ void __launch_bounds__(kBlock) match_finish_kernel(MatchLaunch M) {
+    const int x = blockIdx.x * kBlock + threadIdx.x;
+    const int r = blockIdx.y, img = blockIdx.z;
+    if (x >= M.rw) return;
+    const int cn = M.cn, n_el = M.iw * cn;
+    const double* vb = M.box + ((int64_t)img * M.rh + r) * n_el * 2;
+    const double* ts = M.tstats;  // tmean[4], templNorm, templSum2, all-ones flag
+    float* out = reinterpret_cast<float*>(M.res + (int64_t)img * M.res_pitch + (int64_t)r * M.res_row) + x;
+    const int method = M.method;
+    if (ts[6] != 0.0) {  // CCOEFF_NORMED of a flat template
+        *out = 1.f;
+        return;
+    }
+    double S[4] = {0, 0, 0, 0}, Q = 0;
+    for (int xx = 0; xx < M.tw; ++xx)
+        for (int c = 0; c < cn; ++c) {
+            S[c] += vb[(x + xx) * cn + c];
+            Q += vb[n_el + (x + xx) * cn + c];
+        }
+    const int numType = (method == VACV_TM_CCORR || method == VACV_TM_CCORR_NORMED)     ? 0
+                        : (method == VACV_TM_CCOEFF || method == VACV_TM_CCOEFF_NORMED) ? 1
+                                                                                        : 2;
+    const bool isNormed = method == VACV_TM_CCORR_NORMED || method == VACV_TM_SQDIFF_NORMED ||
+                          method == VACV_TM_CCOEFF_NORMED;
+    const double invArea = M.inv_area;
+    double num = (double)*out, t;
+    double wndMean2 = 0, wndSum2 = 0;
+    if (numType == 1) {
+        for (int c = 0; c < cn; ++c) {
+            t = S[c];
+            wndMean2 += t * t;
+            num -= t * ts[c];
+        }
+        wndMean2 *= invArea;
+    }
+    if (isNormed || numType == 2) {
+        wndSum2 = Q;
+        if (numType == 2) {
+            num = wndSum2 - 2 * num + ts[5];
+            num = num > 0. ? num : 0.;
+        }
+    }
+    if (isNormed) {
+        t = sqrt(wndSum2 - wndMean2 > 0. ? wndSum2 - wndMean2 : 0.) * ts[4];
+        if (fabs(num) < t) num /= t;
+        else if (fabs(num) < t * 1.125) num = num > 0 ? 1 : -1;
+        else num = method != VACV_TM_SQDIFF_NORMED ? 0 : 1;
+    }
+    *out = (float)num;
+}
+
+// the template's mean / population stddev per channel (one workgroup per
+// image's template -- templates are shared: blockIdx.x = 0 only), then the
+// method's constants as templmatch.cpp derives them
+template <typename T>
+__global__ void __launch_bounds__(kBlock) match_tstats_kernel(MatchLaunch M) {
+    __shared__ double red[2][4][kBlock];
+    const int cn = M.cn, n = M.tw * M.th;
+    double s[4] = {0, 0, 0, 0}, q[4] = {0, 0, 0, 0};
+    for (int i = threadIdx.x; i < n; i += kBlock) {
+        const int yy = i / M.tw, xx = i - yy * M.tw;
+        const T* tr = reinterpret_cast<const T*>(M.tpl + (int64_t)yy * M.tpl_row) + xx * cn;
+        for (int c = 0; c < cn; ++c) {
+            const double v = (double)tr[c];
+            s[c] += v;
+            q[c] += v * v;
+        }
+    }
+    for (int c = 0; c < 4; ++c) {
+        red[0][c][threadIdx.x] = s[c];
+        red[1][c][threadIdx.x] = q[c];
+    }
+    __syncthreads();
+    for (int st = kBlock / 2; st > 0; st >>= 1) {
+        if ((int)threadIdx.x < st)
+            for (int c = 0; c < 4; ++c) {
+                red[0][c][threadIdx.x] += red[0][c][threadIdx.x + st];
+                red[1][c][threadIdx.x] += red[1][c][threadIdx.x + st];
+            }
+        __syncthreads();
+    }
+    if (threadIdx.x != 0) return;
+    double tm[4] = {0, 0, 0, 0}, td[4] = {0, 0, 0, 0};
+    for (int c = 0; c < cn; ++c) {  // meanStdDev: population
+        tm[c] = red[0][c][0] / n;
+        const double var = red[1][c][0] / n - tm[c] * tm[c];
+        td[c] = sqrt(var > 0 ? var : 0);
+    }
+    const int method = M.method;
+    const double invArea = M.inv_area;
+    double templNorm = 0, templSum2 = 0, ones = 0;
+    double tmean[4] = {tm[0], tm[1], tm[2], tm[3]};
+    if (method != VACV_TM_CCOEFF) {
+        templNorm = td[0] * td[0] + td[1] * td[1] + td[2] * td[2] + td[3] * td[3];
+        if (templNorm < 2.220446049250313e-16 && method == VACV_TM_CCOEFF_NORMED) ones = 1;
+        templSum2 = templNorm + tm[0] * tm[0] + tm[1] * tm[1] + tm[2] * tm[2] + tm[3] * tm[3];
+        const bool ccoeff = method == VACV_TM_CCOEFF || method == VACV_TM_CCOEFF_NORMED;
+        if (!ccoeff) {
+            tmean[0] = tmean[1] = tmean[2] = tmean[3] = 0;
+            templNorm = templSum2;
+        }
+        templSum2 /= invArea;
+        templNorm = sqrt(templNorm);
+        templNorm /= sqrt(invArea);
+    }
+    double* o = M.tstats;
+    for (int c = 0; c < 4; ++c) o[c] = tmean[c];
+    o[4] = templNorm;
+    o[5] = templSum2;
+    o[6] = ones;
+}
+
+// ---- minMaxIdx ---------------------------------------------------------------
+
+struct MinMax {
+    double mn, mx;
+    long long imn, imx;  // linear indices, -1 = none
+};
+
+__device__ __forceinline__ void mm_merge(MinMax& a, const MinMax& b) {
+    // first occurrence wins ties: the smaller index
+    if (b.imn >= 0 && (a.imn < 0 || b.mn < a.mn || (b.mn == a.mn && b.imn < a.imn))) {
+        a.mn = b.mn;
+        a.imn = b.imn;
+    }
+    if (b.imx >= 0 && (a.imx < 0 || b.mx > a.mx || (b.mx == a.mx && b.imx < a.imx))) {
+        a.mx = b.mx;
+        a.imx = b.imx;
+    }
+}
+
+template <typename T>
+__global__ void __launch_bounds__(kBlock) min_max_kernel(MinMaxLaunch L, MinMax* part) {
+    __shared__ MinMax red[kBlock];
+    const long long n = (long long)L.w * L.h;
+    MinMax m = {0, 0, -1, -1};
+    for (long long i = (long long)blockIdx.x * kBlock + threadIdx.x; i < n; i += (long long)gridDim.x * kBlock) {
+        const int y = (int)(i / L.w), x = (int)(i - (long long)y * L.w);
+        if (L.mask && !L.mask[(int64_t)y * L.mask_row + x]) continue;
+        const double v = (double)reinterpret_cast<const T*>(L.src + (int64_t)y * L.row)[x];
+        if (v != v) continue;
+        const MinMax b = {v, v, i, i};
+        mm_merge(m, b);
+    }
+    red[threadIdx.x] = m;
+    __syncthreads();
+    for (int st = kBlock / 2; st > 0; st >>= 1) {
+        if ((int)threadIdx.x < st) mm_merge(red[threadIdx.x], red[threadIdx.x + st]);
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) part[blockIdx.x] = red[0];
+}
+
+__global__ void __launch_bounds__(kBlock) min_max_final_kernel(MinMaxLaunch L, const MinMax* part, int parts) {
+    __shared__ MinMax red[kBlock];
+    MinMax m = {0, 0, -1, -1};
+    for (int i = threadIdx.x; i < parts; i += kBlock) mm_merge(m, part[i]);
+    red[threadIdx.x] = m;
+    __syncthreads();
+    for (int st = kBlock / 2; st > 0; st >>= 1) {
+        if ((int)threadIdx.x < st) mm_merge(red[threadIdx.x], red[threadIdx.x + st]);
+        __syncthreads();
+    }
+    if (threadIdx.x != 0) return;
+    const MinMax r = red[0];
+    L.out_val[0] = r.imn >= 0 ? r.mn : 0.0;
+    L.out_val[1] = r.imx >= 0 ? r.mx : 0.0;
+    L.out_idx[0] = r.imn >= 0 ? (int)(r.imn / L.w) : -1;
+    L.out_idx[1] = r.imn >= 0 ? (int)(r.imn % L.w) : -1;
+    L.out_idx[2] = r.imx >= 0 ? (int)(r.imx / L.w) : -1;
+    L.out_idx[3] = r.imx >= 0 ? (int)(r.imx % L.w) : -1;
+}
+
+}  // namespace
+size_t match_lds_bytes(int tw, int th, int cn, int esize);
+namespace {
+
+template <int CN>
+hipError_t launch_corr_cn(const MatchLaunch& M, hipStream_t s) {
+    const dim3 grid((M.rw + kTileX - 1) / kTileX, (M.rh + 3) / 4, M.n);
+    if (M.esize == 1) {
+        const size_t lds = match_lds_bytes(M.tw, M.th, CN, 1);
+        hipLaunchKernelGGL((match_corr_u8_kernel<CN>), grid, dim3(kBlock), lds, s, M);
+    } else {
+        const size_t lds = match_lds_bytes(M.tw, M.th, CN, 4);
+        hipLaunchKernelGGL((match_corr_f32_kernel<CN>), grid, dim3(kBlock), lds, s, M);
+    }
+    return hipGetLastError();
+}
+
+}  // namespace
+
+size_t match_lds_bytes(int tw, int th, int cn, int esize) {
+    if (esize == 1) {
+        const size_t K4 = ((size_t)tw * cn + 3) / 4, span4 = 64 * (size_t)cn + K4 + (3 * cn) / 4 + 2 + 1;
+        return ((size_t)th * K4 + 4 * span4) * 4;
+    }
+    return ((size_t)th * tw * cn + 4 * (size_t)(kTileX + tw - 1) * cn) * 4;
+}
+
+hipError_t launch_match_template(const MatchLaunch& M, hipStream_t s) {
+    hipError_t e;
+    switch (M.cn) {
+        case 1: e = launch_corr_cn<1>(M, s); break;
+        case 2: e = launch_corr_cn<2>(M, s); break;
+        case 3: e = launch_corr_cn<3>(M, s); break;
+        case 4: e = launch_corr_cn<4>(M, s); break;
+        default: return hipErrorInvalidValue;
+    }
+    if (e != hipSuccess || M.method == VACV_TM_CCORR) return e;
+    if (M.esize == 1) hipLaunchKernelGGL(match_tstats_kernel<uint8_t>, dim3(1), dim3(kBlock), 0, s, M);
+    else hipLaunchKernelGGL(match_tstats_kernel<float>, dim3(1), dim3(kBlock), 0, s, M);
+    const dim3 gv((M.iw * M.cn + kBlock - 1) / kBlock, M.rh, M.n);
+    if (M.esize == 1) hipLaunchKernelGGL(match_box_v_kernel<uint8_t>, gv, dim3(kBlock), 0, s, M);
+    else hipLaunchKernelGGL(match_box_v_kernel<float>, gv, dim3(kBlock), 0, s, M);
+    const dim3 gf((M.rw + kBlock - 1) / kBlock, M.rh, M.n);
+    hipLaunchKernelGGL(match_finish_kernel, gf, dim3(kBlock), 0, s, M);
+    return hipGetLastError();
+}
+
+size_t min_max_workspace_bytes() { return 1024 * sizeof(MinMax); }
+
+hipError_t launch_min_max(const MinMaxLaunch& L, void* ws, hipStream_t s) {
+    const long long n = (long long)L.w * L.h;
+    const int parts = (int)std::min<long long>(1024, std::max<long long>(1, (n + kBlock * 16 - 1) / (kBlock * 16)));
+    MinMax* part = static_cast<MinMax*>(ws);
+    if (L.esize == 1) hipLaunchKernelGGL(min_max_kernel<uint8_t>, dim3(parts), dim3(kBlock), 0, s, L, part);
+    else hipLaunchKernelGGL(min_max_kernel<float>, dim3(parts), dim3(kBlock), 0, s, L, part);
+    hipLaunchKernelGGL(min_max_final_kernel, dim3(1), dim3(kBlock), 0, s, L, part, parts);
+    return hipGetLastError();
+}
+
+}  // namespace vacv

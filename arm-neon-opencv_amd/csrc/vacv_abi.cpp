@@ -17,6 +17,7 @@
 #include <cstring>
 #include <map>
 #include <mutex>
+#include <tuple>
 #include <utility>
 
 #include "vacv_internal.hpp"
@@ -111,13 +112,13 @@ struct Workspace {
     size_t cap = 0;
 };
 std::mutex g_ws_mu;
-std::map<std::pair<int, void*>, Workspace> g_ws;
+std::map<std::tuple<int, void*, int>, Workspace> g_ws;
 
-int workspace(hipStream_t s, size_t bytes, void** out) {
+int workspace(hipStream_t s, size_t bytes, void** out, int slot = 0) {
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess) return VACV_ERR_HIP;
     std::lock_guard<std::mutex> lk(g_ws_mu);
-    Workspace& w = g_ws[{dev, (void*)s}];
+    Workspace& w = g_ws[std::make_tuple(dev, (void*)s, slot)];
     if (w.cap < bytes) {
         if (w.buf) {
             // the previous buffer may still be read by queued work
@@ -822,6 +823,88 @@ int vacv_cvt_color_resize_normalize(const vacv_image* src, const vacv_image* dst
     return fused_normalize(dst, mean, stddev, (hipStream_t)stream, yuv_resize_pass, &c);
 }
 
+int vacv_match_template(const vacv_image* img_d, const vacv_image* tpl_d, const vacv_image* res_d, int method,
+                        void* stream) {
+    Img img, tpl, res;
+    int st = load(img_d, img);
+    if (st) return st;
+    if ((st = load(tpl_d, tpl))) return st;
+    if ((st = load(res_d, res))) return st;
+    if (method < VACV_TM_SQDIFF || method > VACV_TM_CCOEFF_NORMED) return VACV_ERR_UNSUPPORTED;
+    if (img.dtype != VACV_INT8 && img.dtype != VACV_FP32) return VACV_ERR_UNSUPPORTED;
+    if (tpl.dtype != img.dtype || tpl.c != img.c || tpl.n != 1) return VACV_ERR_INVALID_ARG;
+    if (img.layout != VACV_NHWC || tpl.layout != VACV_NHWC || img.c > 4) return VACV_ERR_UNSUPPORTED;
+    // cv::matchTemplate swaps a template larger than the image (n = 1 only)
+    if (tpl.w >= img.w && tpl.h >= img.h && (tpl.w > img.w || tpl.h > img.h)) {
+        if (img.n != 1) return VACV_ERR_INVALID_ARG;
+        std::swap(img, tpl);
+    }
+    if (tpl.w > img.w || tpl.h > img.h) return VACV_ERR_INVALID_ARG;
+    const int rw = img.w - tpl.w + 1, rh = img.h - tpl.h + 1;
+    if (res.dtype != VACV_FP32 || res.c != 1 || res.w != rw || res.h != rh || res.n != img.n)
+        return VACV_ERR_INVALID_ARG;
+    if (match_lds_bytes(tpl.w, tpl.h, img.c, img.es) > 64 * 1024 || rh > 65535 * 4 || img.n > 65535)
+        return VACV_ERR_UNSUPPORTED;
+    hipStream_t s = (hipStream_t)stream;
+    MatchLaunch M{};
+    M.img = img.data;
+    M.img_pitch = img.batch;
+    M.img_row = img.row;
+    M.iw = img.w;
+    M.ih = img.h;
+    M.cn = img.c;
+    M.esize = img.es;
+    M.n = img.n;
+    M.tpl = tpl.data;
+    M.tpl_row = tpl.row;
+    M.tw = tpl.w;
+    M.th = tpl.h;
+    M.res = res.data;
+    M.res_pitch = res.batch;
+    M.res_row = res.row;
+    M.rw = rw;
+    M.rh = rh;
+    M.method = method;
+    M.inv_area = 1. / ((double)tpl.h * tpl.w);
+    if (method != VACV_TM_CCORR) {
+        const size_t box = align_up((size_t)img.n * rh * img.w * img.c * 2 * sizeof(double), 256);
+        void* ws = nullptr;
+        if ((st = workspace(s, box + 256, &ws))) return st;
+        M.box = static_cast<double*>(ws);
+        M.tstats = reinterpret_cast<double*>(static_cast<char*>(ws) + box);
+    }
+    return hip_status(launch_match_template(M, s));
+}
+
+int vacv_min_max_idx(const vacv_image* src_d, const vacv_image* mask_d, double* vals, int* idx, void* stream) {
+    Img src, mask;
+    int st = load(src_d, src);
+    if (st) return st;
+    if (!vals || !idx) return VACV_ERR_INVALID_ARG;
+    if (src.n != 1 || src.c != 1) return VACV_ERR_INVALID_ARG;  // cv::minMaxIdx: one channel
+    if (src.dtype != VACV_INT8 && src.dtype != VACV_FP32) return VACV_ERR_UNSUPPORTED;
+    MinMaxLaunch L{};
+    L.src = src.data;
+    L.row = src.row;
+    L.w = src.w;
+    L.h = src.h;
+    L.esize = src.es;
+    if (mask_d) {
+        if ((st = load(mask_d, mask))) return st;
+        if (mask.dtype != VACV_INT8 || mask.c != 1 || mask.w != src.w || mask.h != src.h) return VACV_ERR_INVALID_ARG;
+        L.mask = mask.data;
+        L.mask_row = mask.row;
+    }
+    L.out_val = vals;
+    L.out_idx = idx;
+    hipStream_t s = (hipStream_t)stream;
+    void* ws = nullptr;
+    // its own workspace key: a match_template result on the same stream may
+    // still be using the stream's main workspace
+    if ((st = workspace(s, min_max_workspace_bytes(), &ws, 1))) return st;
+    return hip_status(launch_min_max(L, ws, s));
+}
+
 int vacv_stream_synchronize(void* stream) {
     return hipStreamSynchronize((hipStream_t)stream) == hipSuccess ? VACV_OK : VACV_ERR_HIP;
 }
@@ -831,7 +914,7 @@ int vacv_release_workspace(void) {
     int st = VACV_OK;
     for (auto& kv : g_ws) {
         if (kv.second.buf) {
-            if (hipStreamSynchronize((hipStream_t)kv.first.second) != hipSuccess) st = VACV_ERR_HIP;
+            if (hipStreamSynchronize((hipStream_t)std::get<1>(kv.first)) != hipSuccess) st = VACV_ERR_HIP;
             if (hipFree(kv.second.buf) != hipSuccess) st = VACV_ERR_HIP;
         }
     }

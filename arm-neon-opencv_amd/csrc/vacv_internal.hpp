@@ -230,4 +230,35 @@ hipError_t launch_channel_sums(const SumsLaunch& L, hipStream_t s);
 hipError_t launch_stats(const double* sums, int groups, int c, double count,
                         float* mean, float* stddev, hipStream_t s);
 
+// match_template (k_match.hip): n images against one template
+struct MatchLaunch {
+    const unsigned char* img;     // image 0
+    int64_t img_pitch, img_row;   // bytes
+    int iw, ih, cn, esize, n;
+    const unsigned char* tpl;
+    int64_t tpl_row;
+    int tw, th;
+    unsigned char* res;           // FP32 result of image 0
+    int64_t res_pitch, res_row;   // bytes
+    int rw, rh;
+    int method;                   // VACV_TM_*
+    double inv_area;              // 1 / (tw * th)
+    double* box;                  // workspace: [n][rh][iw*cn][2] column sums (S, S^2)
+    double* tstats;               // workspace: template mean[4], norm, sum2, all-ones flag
+};
+size_t match_lds_bytes(int tw, int th, int cn, int esize);
+hipError_t launch_match_template(const MatchLaunch& M, hipStream_t s);
+
+struct MinMaxLaunch {             // minMaxIdx of one single-channel image
+    const unsigned char* src;
+    int64_t row;
+    int w, h, esize;
+    const unsigned char* mask;    // INT8 (w, h), non-zero = included; or null
+    int64_t mask_row;
+    double* out_val;              // device: min, max
+    int* out_idx;                 // device: min row, min col, max row, max col
+};
+size_t min_max_workspace_bytes();
+hipError_t launch_min_max(const MinMaxLaunch& L, void* ws, hipStream_t s);
+
 }  // namespace vacv

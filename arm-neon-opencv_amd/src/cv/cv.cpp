@@ -355,12 +355,49 @@ void cvt_color_normalize(const std::vector<Tensor>& src, std::vector<Tensor>& ds
     p.finish();
 }
 
-void match_template(const Tensor&, const Tensor&, Tensor&, int) {
-    fail("va_cv::match_template", "not provided by the MI355X build (OpenCV-only in the reference)");
+void match_template(const Tensor& src, const Tensor& target, Tensor& result, int method) {
+    static const char* fn = "va_cv::match_template";
+    // match_template.cpp:13-41 -> cv::matchTemplate (OpenCV 2.4 semantics,
+    // exact correlation; the C ABI swaps a larger template as OpenCV does)
+    if (src.dtype != INT8 && src.dtype != FP32) fail(fn, "match_template takes INT8 or FP32");
+    if (target.dtype != src.dtype || target.c != src.c) fail(fn, "the template must match the image's dtype and channels");
+    if (src.layout != NHWC || target.layout != NHWC) fail(fn, "match_template takes NHWC tensors");
+    const bool swap = target.w >= src.w && target.h >= src.h && (target.w > src.w || target.h > src.h);
+    const Tensor& a = swap ? target : src;
+    const Tensor& b = swap ? src : target;
+    if (b.w > a.w || b.h > a.h) fail(fn, "the template does not fit the image");
+    Staging st(fn, src);
+    const vacv_image s = st.in(a, 0);
+    const vacv_image t = st.in(b, 1);
+    const vacv_image d = st.out(result, a.w - b.w + 1, a.h - b.h + 1, 1, FP32, NHWC, 2);
+    st.run(vacv_match_template(&s, &t, &d, method, st.stream()));
+    st.finish();
 }
 
-void minMaxIdx(const Tensor&, double*, double*, int*, int*, const Tensor&) {
-    fail("va_cv::minMaxIdx", "not provided by the MI355X build (OpenCV-only in the reference)");
+void minMaxIdx(const Tensor& src, double* minVal, double* maxVal, int* minIdx, int* maxIdx, const Tensor& mask) {
+    static const char* fn = "va_cv::minMaxIdx";
+    // match_template.cpp:43-46 -> cv::minMaxIdx of a single-channel array;
+    // minIdx / maxIdx receive (row, col)
+    if (src.c != 1) fail(fn, "minMaxIdx takes a single-channel tensor");
+    Staging st(fn, src);
+    const vacv_image s = st.in(src, 0);
+    vacv_image m{};
+    const bool has_mask = !mask.empty();
+    if (has_mask) m = st.in(mask, 1);
+    Tensor out;
+    const vacv_image o = st.out(out, 48, 1, 1, INT8, NHWC, 2);  // 2 doubles + 4 ints, device scratch
+    double* vals = static_cast<double*>(o.data);
+    int* idx = reinterpret_cast<int*>(static_cast<char*>(o.data) + 16);
+    st.run(vacv_min_max_idx(&s, has_mask ? &m : nullptr, vals, idx, st.stream()));
+    double hv[2];
+    int hi[4];
+    detail::check_hip(fn, hipMemcpyAsync(hv, vals, sizeof(hv), hipMemcpyDeviceToHost, st.stream()));
+    detail::check_hip(fn, hipMemcpyAsync(hi, idx, sizeof(hi), hipMemcpyDeviceToHost, st.stream()));
+    st.finish();
+    if (minVal) *minVal = hv[0];
+    if (maxVal) *maxVal = hv[1];
+    if (minIdx) { minIdx[0] = hi[0]; minIdx[1] = hi[1]; }
+    if (maxIdx) { maxIdx[0] = hi[2]; maxIdx[1] = hi[3]; }
 }
 
 void imencode(const Tensor&, std::vector<unsigned char>&, const char*) {

@@ -158,12 +158,17 @@ void warp_affine_normalize(const vision::Tensor& src, vision::Tensor& dst,
 /// ROI copy; the rect is truncated to int (crop.cpp:127-142).
 void crop(const vision::Tensor& src, vision::Tensor& dst, const vision::VRect& rect);
 
-/// OpenCV-only in the reference (match_template.cpp); not on this build's
-/// hot path: these throw std::runtime_error.
+/// Template matching (match_template.cpp:13-41 hands it to cv::matchTemplate):
+/// OpenCV 2.4's six TM_* methods, INT8 / FP32 NHWC, c <= 4; result =
+/// (W-w+1, H-h+1, 1) FP32.  The correlation is computed exactly on the GPU.
 void match_template(const vision::Tensor& src, const vision::Tensor& target,
                     vision::Tensor& result, int method);
+/// cv::minMaxIdx of a single-channel tensor (match_template.cpp:43-46):
+/// first minimum / maximum in row-major order among mask != 0; indices are
+/// (row, col).
 void minMaxIdx(const vision::Tensor& src, double* minVal, double* maxVal,
                int* minIdx = nullptr, int* maxIdx = nullptr, const vision::Tensor& mask = vision::Tensor());
+/// OpenCV-only in the reference (imencode.cpp, a codec): throws.
 void imencode(const vision::Tensor& src, std::vector<unsigned char>& buf, const char* format);
 
 // ---- additions (not in the reference) -----------------------------------

@@ -27,6 +27,7 @@ INTER_NEAREST, INTER_LINEAR, INTER_CUBIC, INTER_AREA = 0, 1, 2, 3
 BORDER_CONSTANT, BORDER_REPLICATE, BORDER_REFLECT, BORDER_WRAP, BORDER_REFLECT_101, BORDER_TRANSPARENT = 0, 1, 2, 3, 4, 5
 COLOR_YUV2RGB_NV12, COLOR_YUV2BGR_NV12, COLOR_YUV2RGB_NV21, COLOR_YUV2BGR_NV21 = 90, 91, 92, 93
 LINEAR_REFERENCE, LINEAR_NEON, LINEAR_OPENCV = 0, 1, 2
+TM_SQDIFF, TM_SQDIFF_NORMED, TM_CCORR, TM_CCORR_NORMED, TM_CCOEFF, TM_CCOEFF_NORMED = 0, 1, 2, 3, 4, 5
 
 
 class VacvError(RuntimeError):
@@ -84,6 +85,8 @@ SIGNATURES = {
     "vacv_cvt_color_resize_normalize": ([_IMG, _IMG, _I, _I, _I, _FP, _FP, _P], _I),
     "vacv_stream_synchronize": ([_P], _I),
     "vacv_release_workspace": ([], _I),
+    "vacv_match_template": ([_IMG, _IMG, _IMG, _I, _P], _I),
+    "vacv_min_max_idx": ([_IMG, _IMG, _P, _P, _P], _I),
     "vacv_set_tuning": ([_I, _I], _I),
     "vacv_get_tuning": ([_I], _I),
 }

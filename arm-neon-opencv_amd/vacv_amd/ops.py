@@ -368,6 +368,39 @@ def mean_stddev(src: torch.Tensor, layout: int = NHWC, stream=None) -> Tuple[tor
     return mean, std
 
 
+def match_template(img: torch.Tensor, templ: torch.Tensor, method: int, out=None, stream=None) -> torch.Tensor:
+    """va_cv::match_template (cv.h:211-219): cv::matchTemplate of every image
+    (NHWC, u8 or fp32) against one template -> (n,) H-h+1 x W-w+1 fp32."""
+    i4 = _as4d(img, NHWC)
+    t4 = _as4d(templ, NHWC)
+    n, H, W, _ = i4.shape
+    _, h, w, _ = t4.shape
+    if w > W and h > H and n == 1:
+        W, H, w, h = w, h, W, H
+    if out is None:
+        out = torch.empty((n, H - h + 1, W - w + 1), dtype=torch.float32, device=img.device)
+    o4 = out.reshape(n, H - h + 1, W - w + 1, 1)  # one channel, NHWC
+    check("vacv_match_template", L.load().vacv_match_template(
+        ctypes.byref(describe(i4, NHWC)), ctypes.byref(describe(t4, NHWC)), ctypes.byref(describe(o4, NHWC)),
+        int(method), _stream(stream)))
+    return out if img.dim() == 4 else out[0]
+
+
+def min_max_idx(src: torch.Tensor, mask: Optional[torch.Tensor] = None, stream=None):
+    """va_cv::minMaxIdx (cv.h:221-231) of a 2-D single-channel tensor:
+    (min, max, (row, col) of the min, (row, col) of the max)."""
+    if src.dim() != 2:
+        raise ValueError("minMaxIdx takes a 2-D single-channel tensor")
+    vals = torch.empty(2, dtype=torch.float64, device=src.device)
+    idx = torch.empty(4, dtype=torch.int32, device=src.device)
+    md = ctypes.byref(describe(mask)) if mask is not None else None
+    check("vacv_min_max_idx", L.load().vacv_min_max_idx(ctypes.byref(describe(src)), md, vals.data_ptr(),
+                                                        idx.data_ptr(), _stream(stream)))
+    v = vals.cpu().tolist()
+    i = idx.cpu().tolist()
+    return v[0], v[1], (i[0], i[1]), (i[2], i[3])
+
+
 def set_tuning(name: str, value: int) -> int:
     """Select a kernel variant (VACV_TUNE_<name>, include/vacv_hip.h); value
     < 0 restores the built-in choice.  Returns the previous value."""

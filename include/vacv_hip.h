@@ -241,6 +241,33 @@ int vacv_cvt_color_resize(const vacv_image* src, const vacv_image* dst, int code
 int vacv_cvt_color_resize_normalize(const vacv_image* src, const vacv_image* dst, int code, int interpolation,
                                     int mode, const float* mean, const float* stddev, void* stream);
 
+/* ---- template matching ------------------------------------------------ */
+
+/* va_cv::VMatchMode (cv.h:52-59) */
+enum {
+    VACV_TM_SQDIFF = 0, VACV_TM_SQDIFF_NORMED = 1, VACV_TM_CCORR = 2, VACV_TM_CCORR_NORMED = 3,
+    VACV_TM_CCOEFF = 4, VACV_TM_CCOEFF_NORMED = 5
+};
+
+/* MatchTemplate::match_template (match_template.cpp:13-41, cv.h:211-219),
+ * which the reference hands to cv::matchTemplate: OpenCV 2.4's algorithm
+ * with the correlation computed exactly (parity unpinned).
+ * img: n images (W, H, c) NHWC INT8 or FP32, c <= 4; templ: (w, h, c), same
+ * dtype, n = 1, shared by every image; result: n x (W-w+1, H-h+1, 1) FP32.
+ * A template larger than the image in both dimensions swaps the two, as
+ * cv::matchTemplate does.  VACV_ERR_UNSUPPORTED when the template does not
+ * fit the kernel's LDS budget (about 64 KiB of template bytes). */
+int vacv_match_template(const vacv_image* img, const vacv_image* templ, const vacv_image* result, int method,
+                        void* stream);
+
+/* MatchTemplate::minMaxIdx (match_template.cpp:43-46) = cv::minMaxIdx of a
+ * single-channel 2-D array (n = 1, c = 1, INT8 or FP32): the first
+ * (row-major) minimum and maximum among the elements whose mask byte is
+ * non-zero (mask: NULL, or (w, h, 1) INT8).  DEVICE outputs: vals[2] = {min,
+ * max}, idx[4] = {min row, min col, max row, max col}; with no element 0, 0
+ * and -1s.  NaNs are never selected. */
+int vacv_min_max_idx(const vacv_image* src, const vacv_image* mask, double* vals, int* idx, void* stream);
+
 /* ---- runtime ---------------------------------------------------------- */
 
 /* Kernel-variant knobs, for A/B measurement and the parity tests that check

@@ -78,6 +78,8 @@ class Oracle:
             ("oracle_warp_affine_u8", [_P, _I, _I, _I, _P, _I, _I, _P], None),
             ("oracle_warp_affine_f32", [_P, _I, _I, _I, _P, _I, _I, _P], None),
             ("oracle_resize_area_any", [_P, _I, _I, _I, _I, _P, _I, _I, ctypes.c_double, ctypes.c_double], None),
+            ("oracle_match_template", [_P, _I, _I, _P, _I, _I, _I, _I, _I, _P], None),
+            ("oracle_min_max_idx", [_P, _I, _I, _I, _P, _P, _P], None),
             ("oracle_warp_affine_border", [_P, _I, _I, _I, _I, _P, _I, _I, _P, _I], None),
             ("oracle_yuv420sp_to_bgr", [_P, _P, _I, _I, _I, _I], None),
             ("oracle_bgr2nv21", [_P, _P, _I, _I], None),
@@ -164,6 +166,28 @@ class Oracle:
         self.lib.oracle_resize_area_any(_ptr(img), w, h, c, img.dtype.itemsize, _ptr(out), w_out, h_out,
                                         float(inv_x), float(inv_y))
         return out
+
+    def match_template(self, img, tpl, method):
+        """cv::matchTemplate restated (OpenCV 2.4 templmatch.cpp; exact
+        correlation, parity unpinned): (H - h + 1, W - w + 1) fp32."""
+        img = np.ascontiguousarray(img)
+        tpl = np.ascontiguousarray(tpl, img.dtype)
+        W, H, c = _shape(img)
+        w, h, c2 = _shape(tpl)
+        assert c == c2
+        out = np.zeros((H - h + 1, W - w + 1), np.float32)
+        self.lib.oracle_match_template(_ptr(img), W, H, _ptr(tpl), w, h, c, img.dtype.itemsize, int(method), _ptr(out))
+        return out
+
+    def min_max_idx(self, a, mask=None):
+        """cv::minMaxIdx of a 2-D array: (min, max, (row, col) of min, of max)."""
+        a = np.ascontiguousarray(a)
+        h, w = a.shape
+        mm = np.zeros(2, np.float64)
+        idx = np.zeros(4, np.int32)
+        m = None if mask is None else np.ascontiguousarray(mask, np.uint8)
+        self.lib.oracle_min_max_idx(_ptr(a), w, h, a.dtype.itemsize, None if m is None else _ptr(m), _ptr(mm), _ptr(idx))
+        return float(mm[0]), float(mm[1]), (int(idx[0]), int(idx[1])), (int(idx[2]), int(idx[3]))
 
     def resize_cubic(self, img, w_out, h_out):
         img = np.ascontiguousarray(img, np.float32)

@@ -843,3 +843,132 @@ double oracle_cosine_f64_f32(const float* a, const float* b, int64_t len) {
     }
     return dot / sqrt(n1 * n2);
 }
+
+/* ------------------------------------------------------------------------ */
+/* match_template / minMaxIdx.  The reference's MatchTemplate::match_template
+ * calls cv::matchTemplate (match_template.cpp:13-41; its naive/NEON bodies
+ * are empty todo stubs, :48-61), so the semantics are OpenCV 2.4.13.4's
+ * (templmatch.cpp, cv::matchTemplate), restated:
+ *   R = crossCorr(img, templ) stored as float (here: the exact correlation
+ *       -- integer for u8, double in row-major order for fp32 -- rounded to
+ *       float; OpenCV's DFT path rounds differently: parity unpinned);
+ *   then, in double, with the window sums S_c = sum of channel c over the
+ *   window and Q = sum of squares over the window (all channels), invArea =
+ *   1 / (w*h), the template's per-channel mean m_c and population stddev d_c:
+ *     CCOEFF*:  num -= sum_c S_c * m_c;  wndMean2 = invArea * sum_c S_c^2
+ *     SQDIFF*:  num = max(Q - 2*num + templSum2, 0), templSum2 = (sum d^2 + m^2) / invArea
+ *     *_NORMED: t = sqrt(max(Q - wndMean2, 0)) * templNorm, templNorm =
+ *               sqrt(sum d^2 (+ m^2 unless CCOEFF)) / sqrt(invArea);
+ *               num = |num| < t ? num / t : |num| < 1.125 t ? sign(num) :
+ *               (SQDIFF_NORMED ? 1 : 0)
+ *     CCOEFF_NORMED with sum d^2 < DBL_EPSILON: every R = 1.
+ * result: (W - w + 1) x (H - h + 1) fp32, one channel.  esize 1 (u8) or 4. */
+void oracle_match_template(const void* img, int W, int H, const void* tpl, int w, int h, int cn, int esize,
+                           int method, float* result) {
+    const int RW = W - w + 1, RH = H - h + 1;
+    const int n = w * h;
+    double tm[4] = {0, 0, 0, 0}, td[4] = {0, 0, 0, 0};
+#define PIX(p, i) (esize == 1 ? (double)((const uint8_t*)(p))[i] : (double)((const float*)(p))[i])
+    for (int c = 0; c < cn; ++c) {
+        double s = 0, q = 0;
+        for (int i = 0; i < n; ++i) {
+            const double v = PIX(tpl, (size_t)i * cn + c);
+            s += v;
+            q += v * v;
+        }
+        tm[c] = s / n;
+        const double var = q / n - tm[c] * tm[c];
+        td[c] = sqrt(var > 0 ? var : 0);
+    }
+    const double invArea = 1. / ((double)h * w);
+    const int numType = (method == 2 || method == 3) ? 0 : (method == 4 || method == 5) ? 1 : 2;
+    const int isNormed = method == 1 || method == 3 || method == 5;
+    double templNorm = 0, templSum2 = 0;
+    double tmean[4] = {tm[0], tm[1], tm[2], tm[3]};
+    if (method != 4) {
+        templNorm = td[0] * td[0] + td[1] * td[1] + td[2] * td[2] + td[3] * td[3];
+        if (templNorm < DBL_EPSILON && method == 5) {
+            for (int i = 0; i < RW * RH; ++i) result[i] = 1.f;
+            return;
+        }
+        templSum2 = templNorm + tm[0] * tm[0] + tm[1] * tm[1] + tm[2] * tm[2] + tm[3] * tm[3];
+        if (numType != 1) {
+            tmean[0] = tmean[1] = tmean[2] = tmean[3] = 0;
+            templNorm = templSum2;
+        }
+        templSum2 /= invArea;
+        templNorm = sqrt(templNorm);
+        templNorm /= sqrt(invArea);
+    }
+    for (int y = 0; y < RH; ++y)
+        for (int x = 0; x < RW; ++x) {
+            double corr = 0, S[4] = {0, 0, 0, 0}, Q = 0;
+            for (int yy = 0; yy < h; ++yy)
+                for (int xx = 0; xx < w; ++xx)
+                    for (int c = 0; c < cn; ++c) {
+                        const double v = PIX(img, ((size_t)(y + yy) * W + x + xx) * cn + c);
+                        corr += PIX(tpl, ((size_t)yy * w + xx) * cn + c) * v;
+                        S[c] += v;
+                        Q += v * v;
+                    }
+            double num = (double)(float)corr, t;
+            double wndMean2 = 0, wndSum2 = 0;
+            if (method == 2) {
+                result[(size_t)y * RW + x] = (float)num;
+                continue;
+            }
+            if (numType == 1) {
+                for (int c = 0; c < cn; ++c) {
+                    t = S[c];
+                    wndMean2 += t * t;
+                    num -= t * tmean[c];
+                }
+                wndMean2 *= invArea;
+            }
+            if (isNormed || numType == 2) {
+                wndSum2 = Q;
+                if (numType == 2) {
+                    num = wndSum2 - 2 * num + templSum2;
+                    num = num > 0 ? num : 0;
+                }
+            }
+            if (isNormed) {
+                t = sqrt(wndSum2 - wndMean2 > 0 ? wndSum2 - wndMean2 : 0) * templNorm;
+                if (fabs(num) < t) num /= t;
+                else if (fabs(num) < t * 1.125) num = num > 0 ? 1 : -1;
+                else num = method != 1 ? 0 : 1;
+            }
+            result[(size_t)y * RW + x] = (float)num;
+        }
+#undef PIX
+}
+
+/* cv::minMaxIdx of a single-channel array (core/stat.cpp): the first
+ * (row-major) minimum and maximum among the elements whose mask byte is
+ * non-zero (mask NULL: all); idx = (row, col).  No element: 0, 0 and -1s.
+ * NaN elements are never selected (the comparisons are false for them). */
+void oracle_min_max_idx(const void* src, int w, int h, int esize, const uint8_t* mask, double* mm, int* idx) {
+    int have = 0;
+    double mn = 0, mx = 0;
+    long imn = -1, imx = -1;
+    for (long i = 0; i < (long)w * h; ++i) {
+        if (mask && !mask[i]) continue;
+        const double v = esize == 1 ? (double)((const uint8_t*)src)[i] : (double)((const float*)src)[i];
+        if (v != v) continue;
+        if (!have) {
+            mn = mx = v;
+            imn = imx = i;
+            have = 1;
+            continue;
+        }
+        if (v < mn) { mn = v; imn = i; }
+        if (v > mx) { mx = v; imx = i; }
+    }
+    mm[0] = mn;
+    mm[1] = mx;
+    idx[0] = imn < 0 ? -1 : (int)(imn / w);
+    idx[1] = imn < 0 ? -1 : (int)(imn % w);
+    idx[2] = imx < 0 ? -1 : (int)(imx / w);
+    idx[3] = imx < 0 ? -1 : (int)(imx % w);
+}
+

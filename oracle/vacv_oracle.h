@@ -83,6 +83,13 @@ void oracle_stats_from_sums(const double* sums, double count, int cc, float* mea
 float  oracle_cosine_f32acc_u8(const uint8_t* a, const uint8_t* b, int64_t len);
 double oracle_cosine_f64_f32(const float* a, const float* b, int64_t len);
 
+/* cv::matchTemplate (OpenCV 2.4 templmatch.cpp) restated; method = TM_* */
+void oracle_match_template(const void* img, int W, int H, const void* tpl, int w, int h, int cn, int esize,
+                           int method, float* result);
+/* cv::minMaxIdx of a single-channel array: mm = {min, max}, idx = {min row,
+ * min col, max row, max col} */
+void oracle_min_max_idx(const void* src, int w, int h, int esize, const uint8_t* mask, double* mm, int* idx);
+
 #ifdef __cplusplus
 }
 #endif

@@ -531,6 +531,66 @@ def test_warp_affine_config_and_harness(ops, dev, oracle, golden):
     assert_same(got[1], want, "warp_affine_normalize")
 
 
+def test_match_template(ops, dev, oracle):
+    """match_template (match_template.cpp:13-41 -> cv::matchTemplate; OpenCV
+    2.4's six methods restated in oracle/vacv_oracle.c, parity unpinned):
+    u8 bit-exact (integer correlation, identical double formula); fp32 within
+    1e-5 (window sums in another order); c = 1, 3, 4; a batch against one
+    template; a template as large as the image; a flat template under
+    CCOEFF_NORMED (all ones); a larger template (cv::matchTemplate swaps)."""
+    import torch
+    rng = np.random.default_rng(53)
+    for c in (1, 3, 4):
+        imgs = np.stack([synthetic_image(900 + 10 * c + k, 70, 301, c).reshape(70, 301, c) for k in range(2)])
+        tpl = np.ascontiguousarray(imgs[1, 20:37, 150:173])
+        for m in range(6):
+            got = host(ops.match_template(to_dev(imgs, dev), to_dev(tpl, dev), m))
+            for k in range(2):
+                want = oracle.match_template(imgs[k], tpl, m)
+                assert_same(got[k], want, f"match u8 c{c} method {m} image {k}")
+        f = (imgs[0].astype(np.float32) * np.float32(0.5) + rng.standard_normal(imgs[0].shape).astype(np.float32))
+        tf = np.ascontiguousarray(f[5:16, 40:61])
+        for m in range(6):
+            got = host(ops.match_template(to_dev(f, dev), to_dev(tf, dev), m))
+            want = oracle.match_template(f, tf, m)
+            np.testing.assert_allclose(got, want, rtol=1e-5, atol=1e-5 * max(1.0, float(np.abs(want).max())),
+                                       err_msg=f"match f32 c{c} method {m}")
+    img = synthetic_image(950, 40, 50, 1)
+    full = host(ops.match_template(to_dev(img, dev), to_dev(img, dev), 5))
+    assert full.shape == (1, 1) and abs(float(full[0, 0]) - 1.0) < 1e-6
+    flat = np.full((5, 7), 9, np.uint8)
+    ones = host(ops.match_template(to_dev(img, dev), to_dev(flat, dev), 5))
+    assert (ones == 1.0).all()
+    small = np.ascontiguousarray(img[3:10, 4:15])
+    sw = host(ops.match_template(to_dev(small, dev), to_dev(img, dev), 0))  # swapped: img is the template
+    assert_same(sw, oracle.match_template(img, small, 0), "match swapped")
+    # minMaxIdx on a match result finds the template's position
+    got = ops.match_template(to_dev(img, dev), to_dev(small, dev), 0)
+    mn, mx, imn, imx = ops.min_max_idx(got)
+    want = oracle.min_max_idx(host(got))
+    assert (mn, mx, imn, imx) == want and imn == (3, 4), ((mn, mx, imn, imx), want)
+
+
+def test_min_max_idx(ops, dev, oracle):
+    """minMaxIdx (match_template.cpp:43-46 -> cv::minMaxIdx): first min / max
+    in row-major order, masks, ties, NaNs skipped, u8 and fp32, an all-masked
+    input (0, 0, -1s), sizes past one workgroup's share."""
+    rng = np.random.default_rng(59)
+    for h, w in [(1, 1), (7, 13), (333, 517), (1080, 1920)]:
+        a = rng.standard_normal((h, w)).astype(np.float32)
+        if h * w > 4:
+            a[h // 2, w // 3] = np.nan
+            a.flat[h * w - 1] = a.min()  # a later tie of the minimum
+        assert ops.min_max_idx(to_dev(a, dev)) == oracle.min_max_idx(a), (h, w)
+        u = rng.integers(0, 256, (h, w), dtype=np.uint8)
+        assert ops.min_max_idx(to_dev(u, dev)) == oracle.min_max_idx(u), (h, w, "u8")
+        m = (rng.random((h, w)) < 0.3).astype(np.uint8)
+        assert ops.min_max_idx(to_dev(u, dev), to_dev(m, dev)) == oracle.min_max_idx(u, m), (h, w, "mask")
+    z = np.zeros((5, 6), np.uint8)
+    assert ops.min_max_idx(to_dev(z, dev)) == (0.0, 0.0, (0, 0), (0, 0))
+    assert ops.min_max_idx(to_dev(z, dev), to_dev(z, dev)) == (0.0, 0.0, (-1, -1), (-1, -1))
+
+
 def test_warp_border_modes(ops, dev, oracle):
     """BORDER_REPLICATE / REFLECT / WRAP / REFLECT_101 / TRANSPARENT (the
     reference hands them to OpenCV, warp_affine.cpp:114-118; here the naive

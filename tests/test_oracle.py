@@ -341,3 +341,49 @@ def test_resize_area_any_restatement(oracle):
                     h1 = int(img[y1, x0, c]) * a0 + int(img[y1, x1, c]) * a1
                     v = (((h0 >> 4) * b0) >> 16) + (((h1 >> 4) * b1) >> 16) + 2
                     assert got[y, x, c] == min(255, max(0, v >> 2)), (wo, ho, x, y, c)
+
+
+def test_match_template_restatement(oracle):
+    """oracle_match_template (cv::matchTemplate restated, parity unpinned)
+    against an independent numpy statement of templmatch.cpp's formulas."""
+    import numpy as np
+    from oracle import synthetic_image
+    img = synthetic_image(61, 20, 26, 3).astype(np.float64)
+    tpl = img[4:11, 6:15].copy()
+    h, w, cn = tpl.shape
+    H, W = img.shape[:2]
+    inv_area = 1.0 / (h * w)
+    tm = tpl.reshape(-1, cn).mean(0)
+    td = np.sqrt(np.maximum((tpl.reshape(-1, cn) ** 2).mean(0) - tm * tm, 0))
+    for method in range(6):
+        got = oracle.match_template(img.astype(np.uint8), tpl.astype(np.uint8), method)
+        want = np.zeros((H - h + 1, W - w + 1))
+        norm = float((td ** 2).sum())
+        sum2 = norm + float((tm ** 2).sum())
+        tmean = tm if method in (4, 5) else np.zeros(cn)
+        if method not in (4, 5):
+            norm = sum2
+        tsum2 = sum2 / inv_area
+        tnorm = np.sqrt(norm) / np.sqrt(inv_area)
+        for y in range(H - h + 1):
+            for x in range(W - w + 1):
+                win = img[y:y + h, x:x + w]
+                num = float(np.float32((win * tpl).sum()))
+                if method == 2:
+                    want[y, x] = num
+                    continue
+                S = win.reshape(-1, cn).sum(0)
+                Q = float((win ** 2).sum())
+                m2 = 0.0
+                if method in (4, 5):
+                    for c in range(cn):
+                        m2 += S[c] * S[c]
+                        num -= S[c] * tmean[c]
+                    m2 *= inv_area
+                if method in (0, 1):
+                    num = max(Q - 2 * num + tsum2, 0.0)
+                if method in (1, 3, 5):
+                    t = np.sqrt(max(Q - m2, 0.0)) * tnorm
+                    num = num / t if abs(num) < t else (np.sign(num) if abs(num) < t * 1.125 else (1 if method == 1 else 0))
+                want[y, x] = num
+        np.testing.assert_allclose(got, want.astype(np.float32), rtol=2e-6, atol=1e-6, err_msg=str(method))
