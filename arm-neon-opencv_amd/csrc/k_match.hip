@@ -11,10 +11,11 @@
 //    wave staged in LDS, the whole template in LDS, 4 adjacent outputs per
 //    lane sharing a sliding window of source dwords (v_alignbyte picks each
 //    output's 4 bytes); fp32 input: match_corr_f32_kernel, fp64 sums;
-//  * match_box_v_kernel: column sums of h rows (S and S^2 per element);
-//  * match_finish_kernel: row sums of w columns of those -> the window's
-//    per-channel S_c and Q, then OpenCV's normalisation formula, in double,
-//    in OpenCV's operation order;
+//  * match_integral_rows_kernel / _cols_kernel: OpenCV's double integral
+//    images (sum, sqsum) in its summation order;
+//  * match_finish_kernel: the window's per-channel S_c and Q as their 4-term
+//    differences, then OpenCV's normalisation formula, in double, in OpenCV's
+//    operation order;
 //  * match_tstats_kernel: the template's per-channel mean / stddev (one
 //    workgroup, fixed-order tree: deterministic).
 // For u8 every sum is exact, so the result is the exact correlation rounded
@@ -165,34 +166,71 @@ __global__ void __launch_bounds__(kBlock) match_corr_f32_kernel(MatchLaunch M) {
     }
 }
 
-// ---- window statistics ------------------------------------------------------
+// ---- window statistics: OpenCV's integral images -----------------------------
+// cv::integral(img, sum, sqsum, CV_64F) as templmatch.cpp builds them, in its
+// order: per channel a running row sum s (s += v left to right), then
+// sum[y+1][x+1] = sum[y][x+1] + s (sqsum likewise with (double)v * v).  The
+// window sums are then its 4-term differences, so S_c and Q are OpenCV's own
+// double values (exact for u8).  Layout per image: [H+1][(W+1)*cn] for sum,
+// then the same for sqsum; row 0 and column 0 are zero.
 
-// V[r][e] = sum_{yy < h} I[r + yy][e], V2 = the same of I^2 (double; exact for u8)
+// pass 1: the running row sums of row y, channel c, into integral row y+1
 template <typename T>
-__global__ void __launch_bounds__(kBlock) match_box_v_kernel(MatchLaunch M) {
-    const int e = blockIdx.x * kBlock + threadIdx.x;
-    const int r = blockIdx.y, img = blockIdx.z;
-    const int n_el = M.iw * M.cn;
-    if (e >= n_el) return;
-    const unsigned char* ib = M.img + (int64_t)img * M.img_pitch;
+__global__ void __launch_bounds__(kBlock) match_integral_rows_kernel(MatchLaunch M) {
+    const int cn = M.cn;
+    const int t = blockIdx.x * kBlock + threadIdx.x;  // y * cn + c
+    const int img = blockIdx.y;
+    if (t >= M.ih * cn) return;
+    const int y = t / cn, c = t - y * cn;
+    const int64_t step = (int64_t)(M.iw + 1) * cn;
+    double* sum = M.box + (int64_t)img * 2 * (M.ih + 1) * step;
+    double* sq = sum + (int64_t)(M.ih + 1) * step;
+    const T* src = reinterpret_cast<const T*>(M.img + (int64_t)img * M.img_pitch + (int64_t)y * M.img_row);
     double s = 0, q = 0;
-    for (int yy = 0; yy < M.th; ++yy) {
-        const double v = (double)reinterpret_cast<const T*>(ib + (int64_t)(r + yy) * M.img_row)[e];
+    sum[(int64_t)(y + 1) * step + c] = 0;
+    sq[(int64_t)(y + 1) * step + c] = 0;
+    for (int x = 0; x < M.iw; ++x) {
+        const double v = (double)src[x * cn + c];
         s += v;
         q += v * v;
+        sum[(int64_t)(y + 1) * step + (x + 1) * cn + c] = s;
+        sq[(int64_t)(y + 1) * step + (x + 1) * cn + c] = q;
     }
-    double* vb = M.box + ((int64_t)img * M.rh + r) * n_el * 2;
-    vb[e] = s;
-    vb[n_el + e] = q;
+    if (y == 0) {  // row 0 is zero
+        for (int x = 0; x <= M.iw; ++x) {
+            sum[x * cn + c] = 0;
+            sq[x * cn + c] = 0;
+        }
+    }
 }
 
-// one output: S_c / Q over the window, then templmatch.cpp's formula
+// pass 2: sum[y+1][e] = sum[y][e] + rowsum, down each column, in place
+__global__ void __launch_bounds__(kBlock) match_integral_cols_kernel(MatchLaunch M) {
+    const int64_t step = (int64_t)(M.iw + 1) * M.cn;
+    const int e = blockIdx.x * kBlock + threadIdx.x;
+    const int img = blockIdx.y;
+    if (e >= step) return;
+    double* sum = M.box + (int64_t)img * 2 * (M.ih + 1) * step;
+    double* sq = sum + (int64_t)(M.ih + 1) * step;
+    double a = 0, b = 0;
+    for (int y = 1; y <= M.ih; ++y) {
+        a = a + sum[(int64_t)y * step + e];
+        b = b + sq[(int64_t)y * step + e];
+        sum[(int64_t)y * step + e] = a;
+        sq[(int64_t)y * step + e] = b;
+    }
+}
+
+// one output: S_c / Q from the integral images (templmatch.cpp's p0 - p1 -
+// p2 + p3), then its normalisation formula, in its operation order
 __global__ void __launch_bounds__(kBlock) match_finish_kernel(MatchLaunch M) {
     const int x = blockIdx.x * kBlock + threadIdx.x;
     const int r = blockIdx.y, img = blockIdx.z;
     if (x >= M.rw) return;
-    const int cn = M.cn, n_el = M.iw * cn;
-    const double* vb = M.box + ((int64_t)img * M.rh + r) * n_el * 2;
+    const int cn = M.cn;
+    const int64_t step = (int64_t)(M.iw + 1) * cn;
+    const double* sum = M.box + (int64_t)img * 2 * (M.ih + 1) * step;
+    const double* sq = sum + (int64_t)(M.ih + 1) * step;
     const double* ts = M.tstats;  // tmean[4], templNorm, templSum2, all-ones flag
     float* out = reinterpret_cast<float*>(M.res + (int64_t)img * M.res_pitch + (int64_t)r * M.res_row) + x;
     const int method = M.method;
@@ -200,12 +238,8 @@ __global__ void __launch_bounds__(kBlock) match_finish_kernel(MatchLaunch M) {
         *out = 1.f;
         return;
     }
-    double S[4] = {0, 0, 0, 0}, Q = 0;
-    for (int xx = 0; xx < M.tw; ++xx)
-        for (int c = 0; c < cn; ++c) {
-            S[c] += vb[(x + xx) * cn + c];
-            Q += vb[n_el + (x + xx) * cn + c];
-        }
+    const int64_t i0 = (int64_t)r * step + (int64_t)x * cn;
+    const int64_t dw = (int64_t)M.tw * cn, dh = (int64_t)M.th * step;
     const int numType = (method == VACV_TM_CCORR || method == VACV_TM_CCORR_NORMED)     ? 0
                         : (method == VACV_TM_CCOEFF || method == VACV_TM_CCOEFF_NORMED) ? 1
                                                                                         : 2;
@@ -216,14 +250,17 @@ __global__ void __launch_bounds__(kBlock) match_finish_kernel(MatchLaunch M) {
     double wndMean2 = 0, wndSum2 = 0;
     if (numType == 1) {
         for (int c = 0; c < cn; ++c) {
-            t = S[c];
+            t = sum[i0 + c] - sum[i0 + dw + c] - sum[i0 + dh + c] + sum[i0 + dh + dw + c];
             wndMean2 += t * t;
             num -= t * ts[c];
         }
         wndMean2 *= invArea;
     }
     if (isNormed || numType == 2) {
-        wndSum2 = Q;
+        for (int c = 0; c < cn; ++c) {
+            t = sq[i0 + c] - sq[i0 + dw + c] - sq[i0 + dh + c] + sq[i0 + dh + dw + c];
+            wndSum2 += t;
+        }
         if (numType == 2) {
             num = wndSum2 - 2 * num + ts[5];
             num = num > 0. ? num : 0.;
@@ -399,9 +436,11 @@ hipError_t launch_match_template(const MatchLaunch& M, hipStream_t s) {
     if (e != hipSuccess || M.method == VACV_TM_CCORR) return e;
     if (M.esize == 1) hipLaunchKernelGGL(match_tstats_kernel<uint8_t>, dim3(1), dim3(kBlock), 0, s, M);
     else hipLaunchKernelGGL(match_tstats_kernel<float>, dim3(1), dim3(kBlock), 0, s, M);
-    const dim3 gv((M.iw * M.cn + kBlock - 1) / kBlock, M.rh, M.n);
-    if (M.esize == 1) hipLaunchKernelGGL(match_box_v_kernel<uint8_t>, gv, dim3(kBlock), 0, s, M);
-    else hipLaunchKernelGGL(match_box_v_kernel<float>, gv, dim3(kBlock), 0, s, M);
+    const dim3 gr((M.ih * M.cn + kBlock - 1) / kBlock, M.n);
+    if (M.esize == 1) hipLaunchKernelGGL(match_integral_rows_kernel<uint8_t>, gr, dim3(kBlock), 0, s, M);
+    else hipLaunchKernelGGL(match_integral_rows_kernel<float>, gr, dim3(kBlock), 0, s, M);
+    const dim3 gc(((M.iw + 1) * M.cn + kBlock - 1) / kBlock, M.n);
+    hipLaunchKernelGGL(match_integral_cols_kernel, gc, dim3(kBlock), 0, s, M);
     const dim3 gf((M.rw + kBlock - 1) / kBlock, M.rh, M.n);
     hipLaunchKernelGGL(match_finish_kernel, gf, dim3(kBlock), 0, s, M);
     return hipGetLastError();

@@ -867,7 +867,7 @@ int vacv_match_template(const vacv_image* img_d, const vacv_image* tpl_d, const 
     M.method = method;
     M.inv_area = 1. / ((double)tpl.h * tpl.w);
     if (method != VACV_TM_CCORR) {
-        const size_t box = align_up((size_t)img.n * rh * img.w * img.c * 2 * sizeof(double), 256);
+        const size_t box = align_up((size_t)img.n * 2 * (img.h + 1) * (img.w + 1) * img.c * sizeof(double), 256);
         void* ws = nullptr;
         if ((st = workspace(s, box + 256, &ws))) return st;
         M.box = static_cast<double*>(ws);

@@ -243,7 +243,7 @@ struct MatchLaunch {
     int rw, rh;
     int method;                   // VACV_TM_*
     double inv_area;              // 1 / (tw * th)
-    double* box;                  // workspace: [n][rh][iw*cn][2] column sums (S, S^2)
+    double* box;                  // workspace: [n][2][ih+1][(iw+1)*cn] integral images (sum, sqsum)
     double* tstats;               // workspace: template mean[4], norm, sum2, all-ones flag
 };
 size_t match_lds_bytes(int tw, int th, int cn, int esize);

@@ -853,7 +853,10 @@ double oracle_cosine_f64_f32(const float* a, const float* b, int64_t len) {
  *       -- integer for u8, double in row-major order for fp32 -- rounded to
  *       float; OpenCV's DFT path rounds differently: parity unpinned);
  *   then, in double, with the window sums S_c = sum of channel c over the
- *   window and Q = sum of squares over the window (all channels), invArea =
+ *   window and Q = sum of squares over the window (all channels) -- taken as
+ *   OpenCV takes them, 4-term differences of cv::integral's double sum /
+ *   sqsum images built in its order (templmatch.cpp's p0 - p1 - p2 + p3) --
+ *   invArea =
  *   1 / (w*h), the template's per-channel mean m_c and population stddev d_c:
  *     CCOEFF*:  num -= sum_c S_c * m_c;  wndMean2 = invArea * sum_c S_c^2
  *     SQDIFF*:  num = max(Q - 2*num + templSum2, 0), templSum2 = (sum d^2 + m^2) / invArea
@@ -900,6 +903,22 @@ void oracle_match_template(const void* img, int W, int H, const void* tpl, int w
         templNorm = sqrt(templNorm);
         templNorm /= sqrt(invArea);
     }
+    /* cv::integral(img, sum, sqsum, CV_64F) in its order: a running row sum
+     * per channel, added to the integral row above (imgproc/sumpixels.cpp) */
+    const size_t step = (size_t)(W + 1) * cn;
+    double* isum = (double*)calloc((size_t)(H + 1) * step, sizeof(double));
+    double* isq = (double*)calloc((size_t)(H + 1) * step, sizeof(double));
+    for (int y = 0; y < H; ++y)
+        for (int c = 0; c < cn; ++c) {
+            double s = 0, q = 0;
+            for (int x = 0; x < W; ++x) {
+                const double v = PIX(img, ((size_t)y * W + x) * cn + c);
+                s += v;
+                q += v * v;
+                isum[(y + 1) * step + (x + 1) * cn + c] = isum[y * step + (x + 1) * cn + c] + s;
+                isq[(y + 1) * step + (x + 1) * cn + c] = isq[y * step + (x + 1) * cn + c] + q;
+            }
+        }
     for (int y = 0; y < RH; ++y)
         for (int x = 0; x < RW; ++x) {
             double corr = 0, S[4] = {0, 0, 0, 0}, Q = 0;
@@ -908,9 +927,13 @@ void oracle_match_template(const void* img, int W, int H, const void* tpl, int w
                     for (int c = 0; c < cn; ++c) {
                         const double v = PIX(img, ((size_t)(y + yy) * W + x + xx) * cn + c);
                         corr += PIX(tpl, ((size_t)yy * w + xx) * cn + c) * v;
-                        S[c] += v;
-                        Q += v * v;
                     }
+            /* the window sums as templmatch.cpp takes them: p0 - p1 - p2 + p3 */
+            const size_t i0 = y * step + (size_t)x * cn, dw = (size_t)w * cn, dh = (size_t)h * step;
+            for (int c = 0; c < cn; ++c) {
+                S[c] = isum[i0 + c] - isum[i0 + dw + c] - isum[i0 + dh + c] + isum[i0 + dh + dw + c];
+                Q += isq[i0 + c] - isq[i0 + dw + c] - isq[i0 + dh + c] + isq[i0 + dh + dw + c];
+            }
             double num = (double)(float)corr, t;
             double wndMean2 = 0, wndSum2 = 0;
             if (method == 2) {
@@ -940,6 +963,8 @@ void oracle_match_template(const void* img, int W, int H, const void* tpl, int w
             }
             result[(size_t)y * RW + x] = (float)num;
         }
+    free(isum);
+    free(isq);
 #undef PIX
 }
 

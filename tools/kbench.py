@@ -115,6 +115,19 @@ def main():
         o = torch.empty((n, 224, 224, 3), dtype=torch.float32, device=dev)
         cases["cubic_1440p_224_u8_f32"] = (lambda src=src, o=o: ops.resize(src, 224, 224, interpolation=vacv_amd.INTER_CUBIC, out=o),
                                            n * resize_bytes(2560, 1440, 3, 224, 224, 1, 4, cubic=True), n * 2560 * 1440)
+    if a.op in ("match", "all"):
+        # correlation MACs: (W-w+1)(H-h+1) * w*h*c; bytes: image + result
+        n = a.batch or 8
+        src = frames(n, 720, 1280)
+        tpl = frames(1, 64, 64)[0]
+        o = torch.empty((n, 720 - 63, 1280 - 63), dtype=torch.float32, device=dev)
+        for m, name in ((2, "ccorr"), (5, "ccoeff_normed")):
+            cases[f"match_720p_64x64_{name}"] = (lambda src=src, tpl=tpl, o=o, m=m: ops.match_template(src, tpl, m, out=o),
+                                                 n * (1280 * 720 * 3 + 657 * 1217 * 4), n * 1280 * 720)
+        # GMAC/s of the correlation, for its compute roofline (v_dot4_u32_u8)
+        macs = n * 657 * 1217 * 64 * 64 * 3
+        cases["match_720p_64x64_ccorr_macs"] = (lambda src=src, tpl=tpl, o=o: ops.match_template(src, tpl, 2, out=o),
+                                                macs, n * 1280 * 720)
     if a.op in ("dtype", "all", "calib"):
         n = a.batch or 64
         src = frames(n, 1080, 1920)
