@@ -386,6 +386,255 @@ warp_u8_kernel(WarpLaunch L, int gx, int gy, int total) {
     }
 }
 
+// u8 input, BORDER_CONSTANT, staged through LDS.  Measured (tools/gathercal,
+// PMC): the gather kernels above are bound by the vector cache's per-quad tag
+// lookups -- ~1.8 cycles per (4-lane group x cache line) access, 19-33 of them
+// per 64-lane gather instruction -- not by bytes or ALU.  Here a workgroup
+// owns a kTW x kTH output tile, loads the source rectangle its taps can reach
+// with coalesced 16-byte loads (one access per 4 lanes), and takes the taps
+// from LDS.  The rectangle comes from the tile's corners: the reference's
+// coordinate ((m0*x + m1*y) + m2 in float) is monotone in x and in y
+// separately, so its extremes over the tile are at corners.  A pixel whose
+// taps fall outside the staged rectangle anyway (the host's size cap) takes
+// them from memory, so the result never depends on the staging.
+// Thread layout: 16 lanes per output row, 4 consecutive pixels per lane (one
+// 4*CC-byte store), 16 rows per pass, kTH / 16 passes.
+constexpr int kTileW = 64, kTileH = 32;
+constexpr size_t kWarpTileLds = 32 * 1024;  // per workgroup: 5 resident per CU at the cap
+
+template <int CC, int OUT>
+__global__ void __launch_bounds__(kBlock)
+warp_tile_kernel(WarpLaunch L, int gx, int gy, int total, int max_rows, int max_chunks, int dst_al) {
+    using TOut = typename std::conditional<(OUT == kOutSame), uint8_t, float>::type;
+    extern __shared__ __attribute__((aligned(16))) unsigned char box[];
+    const int per_xcd = (total + 7) / 8;  // XCD-aware block order (see warp_kernel)
+    const int id = (int)(blockIdx.x % 8) * per_xcd + (int)(blockIdx.x / 8);
+    if (id >= total) return;  // uniform
+    const int pidx = id / (gx * gy);
+    const int rem = id - pidx * gx * gy;
+    const int by = rem / gx, bx = rem - by * gx;
+    const int img = pidx / L.src.planes;
+    const int plane = pidx - img * L.src.planes;
+    const int tid = threadIdx.x;
+    const int tx0 = bx * kTileW, ty0 = by * kTileH;
+    const int txe = min(tx0 + kTileW, L.dst.w) - 1, tye = min(ty0 + kTileH, L.dst.h) - 1;
+
+    // ---- the source rectangle of the tile's taps ---------------------------
+    const float* M = L.inv;
+    const float c0x = M[0] * (float)tx0, c1x = M[0] * (float)txe;
+    const float c0y = M[1] * (float)ty0, c1y = M[1] * (float)tye;
+    const float d0x = M[3] * (float)tx0, d1x = M[3] * (float)txe;
+    const float d0y = M[4] * (float)ty0, d1y = M[4] * (float)tye;
+    const float fxa = (c0x + c0y) + M[2], fxb = (c1x + c0y) + M[2], fxc = (c0x + c1y) + M[2], fxd = (c1x + c1y) + M[2];
+    const float fya = (d0x + d0y) + M[5], fyb = (d1x + d0y) + M[5], fyc = (d0x + d1y) + M[5], fyd = (d1x + d1y) + M[5];
+    const float fx_lo = fminf(fminf(fxa, fxb), fminf(fxc, fxd)), fx_hi = fmaxf(fmaxf(fxa, fxb), fmaxf(fxc, fxd));
+    const float fy_lo = fminf(fminf(fya, fyb), fminf(fyc, fyd)), fy_hi = fmaxf(fmaxf(fya, fyb), fmaxf(fyc, fyd));
+    const int sw = L.src.w, shh = L.src.h;
+    // clamp in float first: the corners may be far outside (or NaN)
+    const int x0 = (int)floorf(fminf(fmaxf(fx_lo, 0.f), (float)(sw - 1)));
+    const int x1 = min((int)floorf(fminf(fmaxf(fx_hi, 0.f), (float)(sw - 1))) + 1, sw - 1);
+    const int y0 = (int)floorf(fminf(fmaxf(fy_lo, 0.f), (float)(shh - 1)));
+    const int y1 = min((int)floorf(fminf(fmaxf(fy_hi, 0.f), (float)(shh - 1))) + 1, shh - 1);
+    const unsigned char* sp = L.src.base + (int64_t)img * L.src.img_pitch + (int64_t)plane * L.src.plane_pitch;
+    const uint32_t rp = (uint32_t)L.src.row_pitch;       // host: plane_bytes < 2^31
+    const Rsrc srs = make_rsrc(sp, L.src.plane_bytes);
+    // staged row r = source row y0 + r from the 16-byte chunk holding its
+    // pixel x0 on; that pixel sits at byte dx_r of the LDS row.  dx_r is the
+    // same for every row when the row pitch is a multiple of 16 (rpm == 0).
+    const uint32_t off0 = (uint32_t)y0 * rp + (uint32_t)(x0 * CC) + srs.delta;  // from the 16-aligned base
+    const uint32_t dxb = off0 & 15u, rpm = rp & 15u;
+    const int chunks = min((int)((rpm ? 15u : dxb) + (uint32_t)(x1 - x0 + 1) * CC + 15u) >> 4, max_chunks);
+    const int rows = min(y1 - y0 + 1, max_rows);
+    const int stride = chunks * 16;
+    const int bw_px = (chunks * 16 - (rpm ? 15 : (int)dxb)) / CC;  // pixels every staged row holds from x0
+
+    {
+        const int wave = tid >> 6, lane = tid & 63;
+        // a buffer load that crosses the end of the resource returns zeros
+        // whole: the chunk holding the plane's last bytes is read bytewise
+        const uint32_t lim = (uint32_t)L.src.plane_bytes + srs.delta;
+        for (int r = wave; r < rows; r += kBlock / 64) {
+            const uint32_t ro = (off0 + (uint32_t)r * rp) & ~15u;
+            for (int c = lane; c < chunks; c += 64) {
+                const uint32_t o = ro + 16u * (uint32_t)c;
+                uint4 v;
+                if (o + 16u <= lim) {
+                    v = load16(srs, o);
+                } else {
+                    uint32_t d[4] = {0u, 0u, 0u, 0u};
+                    for (uint32_t e = 0; e < 16u && o + e < lim; ++e)
+                        d[e >> 2] |= (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(srs.r, (int)(o + e), 0, 0) << (8 * (e & 3));
+                    v = make_uint4(d[0], d[1], d[2], d[3]);
+                }
+                *reinterpret_cast<uint4*>(box + r * stride + 16 * c) = v;
+            }
+        }
+    }
+    __syncthreads();
+
+    ChanNorm cn[CC] = {};
+    if (OUT == kOutNorm) {
+#pragma unroll
+        for (int k = 0; k < CC; ++k) cn[k] = chan_norm(L.norm, img, CC == 1 ? plane : k);
+    }
+    TOut bval[CC];
+#pragma unroll
+    for (int k = 0; k < CC; ++k)
+        bval[k] = OUT == kOutNorm ? (TOut)normalize_u8v(cn[k], (int)L.border[k]) : (TOut)L.border[k];
+
+    const int xl = (tid & 15) * 4;       // the lane's 4 pixels: tile columns xl .. xl + 3
+    const int yl = tid >> 4;             // tile row of pass 0
+    float ax_m[4], ay_m[4];
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+        ax_m[p] = M[0] * (float)(tx0 + xl + p);
+        ay_m[p] = M[3] * (float)(tx0 + xl + p);
+    }
+    unsigned char* dbase = const_cast<unsigned char*>(L.dst.base) + (int64_t)img * L.dst.img_pitch +
+                           (int64_t)plane * L.dst.plane_pitch;
+    typedef unsigned short us2v __attribute__((ext_vector_type(2)));
+    constexpr uint32_t kTD = kTapDwords<CC, true>;
+
+#pragma unroll
+    for (int pass = 0; pass < kTileH / 16; ++pass) {
+        const int y = ty0 + yl + 16 * pass;
+        if (y >= L.dst.h) break;
+        const float by_ = M[1] * (float)y, dy_ = M[4] * (float)y;
+        TOut res[4][CC];
+#pragma unroll
+        for (int p = 0; p < 4; ++p) {
+            const float fx = (ax_m[p] + by_) + M[2];
+            const float fy = (ay_m[p] + dy_) + M[5];
+            const bool ok = fx >= 0.f && fx < (float)(sw - 1) && fy >= 0.f && fy < (float)(shh - 1);
+            if (!ok) {
+#pragma unroll
+                for (int k = 0; k < CC; ++k) res[p][k] = bval[k];
+                continue;
+            }
+            const int sx = (int)fx, sy = (int)fy;  // floor: fx, fy >= 0
+            const float ax = fx - (float)sx, ay = fy - (float)sy;
+            // SATURATE_CAST_SHORT of a value in (0, 2048]: the +0.5f branch, no clamp
+            const uint32_t wy0 = (uint32_t)(int)((1.f - ay) * 2048.f + 0.5f);
+            const uint32_t wx0 = (uint32_t)(int)((1.f - ax) * 2048.f + 0.5f);
+            const us2v wx = __builtin_bit_cast(us2v, wx0 | ((2048u - wx0) << 16));
+            const uint32_t lx = (uint32_t)(sx - x0), ly = (uint32_t)(sy - y0);
+            uint32_t t0[kTD], t1[kTD];
+            uint32_t sh;
+            uint32_t sh1;
+            if (lx + 2u <= (uint32_t)bw_px && ly + 2u <= (uint32_t)rows) {
+                uint32_t a0, a1;
+                if (rpm == 0u) {  // uniform
+                    a0 = ly * (uint32_t)stride + lx * CC + dxb;
+                    a1 = a0 + (uint32_t)stride;
+                } else {
+                    const uint32_t d0 = (dxb + __umul24(ly, rpm)) & 15u;
+                    a0 = ly * (uint32_t)stride + lx * CC + d0;
+                    a1 = (ly + 1u) * (uint32_t)stride + lx * CC + ((d0 + rpm) & 15u);
+                }
+                const uint32_t* b0 = reinterpret_cast<const uint32_t*>(box + (a0 & ~3u));
+                const uint32_t* b1 = reinterpret_cast<const uint32_t*>(box + (a1 & ~3u));
+#pragma unroll
+                for (uint32_t d = 0; d < kTD; ++d) { t0[d] = b0[d]; t1[d] = b1[d]; }
+                sh = a0 & 3u;
+                sh1 = a1 & 3u;
+            } else {  // outside the staged rectangle: the taps from memory
+                const unsigned char* r0 = sp + (int64_t)sy * rp + (int64_t)sx * CC;
+                uint32_t b[2][3] = {{0u, 0u, 0u}, {0u, 0u, 0u}};
+#pragma unroll
+                for (int e = 0; e < 2 * CC; ++e) {
+                    b[0][e >> 2] |= (uint32_t)r0[e] << (8 * (e & 3));
+                    b[1][e >> 2] |= (uint32_t)r0[rp + e] << (8 * (e & 3));
+                }
+#pragma unroll
+                for (uint32_t d = 0; d < kTD; ++d) { t0[d] = b[0][d]; t1[d] = b[1][d]; }
+                sh = sh1 = 0u;
+            }
+            const uint32_t a0 = __builtin_amdgcn_alignbyte(t0[1], t0[0], sh);
+            const uint32_t c0 = __builtin_amdgcn_alignbyte(t1[1], t1[0], sh1);
+            uint32_t a1 = 0u, c1 = 0u;
+            if constexpr (kTD == 3) {
+                a1 = __builtin_amdgcn_alignbyte(t0[2], t0[1], sh);
+                c1 = __builtin_amdgcn_alignbyte(t1[2], t1[1], sh1);
+            }
+            const uint32_t wA = wy0, wB = 2048u - wy0;
+#pragma unroll
+            for (int k = 0; k < CC; ++k) {
+                // warp_affine_naive.cpp:50-54 as (tl*wx0 + tr*wx1)*wy0 +
+                // (bl*wx0 + br*wx1)*wy1 (exact int32, <= 255*2^22)
+                const uint32_t sel = (uint32_t)k | (0x0Cu << 8) | ((uint32_t)(CC + k) << 16) | (0x0Cu << 24);
+                const uint32_t top = __builtin_amdgcn_perm(a1, a0, sel);
+                const uint32_t bot = __builtin_amdgcn_perm(c1, c0, sel);
+                const uint32_t ht = __builtin_amdgcn_udot2(__builtin_bit_cast(us2v, top), wx, 0u, false);
+                const uint32_t hb = __builtin_amdgcn_udot2(__builtin_bit_cast(us2v, bot), wx, 0u, false);
+                const int v = (int)((__umul24(ht, wA) + __umul24(hb, wB)) >> 22);
+                if (OUT == kOutSame) res[p][k] = (TOut)v;
+                else if (OUT == kOutF32) res[p][k] = (TOut)(float)v;
+                else res[p][k] = (TOut)normalize_u8v(cn[k], v);
+            }
+        }
+        // ---- the lane's 4 pixels: one 4*CC-element store ---------------------
+        const int x = tx0 + xl;
+        if (x >= L.dst.w) continue;
+        TOut* o = reinterpret_cast<TOut*>(dbase + (int64_t)y * L.dst.row_pitch) + (int64_t)x * CC;
+        if (x + 4 <= L.dst.w && dst_al) {
+            if constexpr (OUT == kOutSame) {
+                uint32_t wd[CC];
+#pragma unroll
+                for (int d = 0; d < CC; ++d) {
+                    uint32_t v = 0;
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) v |= (uint32_t)res[(4 * d + e) / CC][(4 * d + e) % CC] << (8 * e);
+                    wd[d] = v;
+                }
+                if constexpr (CC == 1) {
+                    __builtin_nontemporal_store(wd[0], reinterpret_cast<uint32_t*>(o));
+                } else if constexpr (CC == 2) {
+                    typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+                    __builtin_nontemporal_store(u32x2{wd[0], wd[1]}, reinterpret_cast<u32x2*>(o));
+                } else if constexpr (CC == 3) {
+                    typedef unsigned int u32x3 __attribute__((ext_vector_type(3)));
+                    __builtin_nontemporal_store(u32x3{wd[0], wd[1], wd[2]}, reinterpret_cast<u32x3*>(o));
+                } else {
+                    __builtin_nontemporal_store(u32x4{wd[0], wd[1], wd[2], wd[3]}, reinterpret_cast<u32x4*>(o));
+                }
+            } else {
+#pragma unroll
+                for (int q = 0; q < CC; ++q) {  // 4*CC floats as CC 16-byte stores
+                    typedef float f32x4 __attribute__((ext_vector_type(4)));
+                    f32x4 v;
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) v[e] = res[(4 * q + e) / CC][(4 * q + e) % CC];
+                    __builtin_nontemporal_store(v, reinterpret_cast<f32x4*>(o) + q);
+                }
+            }
+        } else {
+            for (int p = 0; p < L.dst.w - x; ++p)
+#pragma unroll
+                for (int k = 0; k < CC; ++k) o[p * CC + k] = res[p][k];
+        }
+    }
+}
+
+// The staged kernel's LDS rectangle for this matrix (rows, 16-byte chunks per
+// row), or false when it does not apply: strided / misaligned planes, or a
+// rectangle over the LDS budget (strong down-scales).
+bool warp_tile_plan(const WarpLaunch& L, int& max_rows, int& max_chunks, int& dst_al) {
+    if (L.src.esize != 1 || L.border_mode != kBorderConstant) return false;
+    const int cc = L.src.cc;
+    // the lane's 4-pixel store needs its natural alignment; else byte stores
+    const int64_t out_align = L.out == kOutSame ? (cc == 3 ? 4 : 4 * cc) : 16;
+    dst_al = !(L.dst.row_pitch % out_align || L.dst.img_pitch % out_align || L.dst.plane_pitch % out_align ||
+               reinterpret_cast<uintptr_t>(L.dst.base) % out_align);
+    for (int i = 0; i < 6; ++i)
+        if (!std::isfinite(L.inv[i])) return false;
+    // corner-to-corner spans (+ floor, the second tap, float slack)
+    const double bw = std::fabs(L.inv[0]) * (kTileW - 1) + std::fabs(L.inv[1]) * (kTileH - 1) + 4.0;
+    const double bh = std::fabs(L.inv[3]) * (kTileW - 1) + std::fabs(L.inv[4]) * (kTileH - 1) + 4.0;
+    max_rows = (int)std::ceil(bh);
+    max_chunks = (int)std::ceil((15.0 + bw * cc) / 16.0);
+    return (size_t)max_rows * max_chunks * 16 <= kWarpTileLds;
+}
+
 // default: 8 or 10 lane blocks per wave for byte output, whichever pads the
 // output width less (1280: 10 -> 2 tiles of 640 exactly, 0.271 ms, vs 8 ->
 // 2.5 tiles, 0.281 ms at 720p rot15; 8 vs 4: 0.283 vs 0.304), 4 for fp32
@@ -405,10 +654,10 @@ int warp_blocks_per_wave(bool byte_out, int w) {
 // and loses once its gathers spread over many (15 deg, 18 rows: 0.272 ->
 // 0.289; 45 deg: 0.369 -> 0.413): more lines in flight than the CU's vector
 // cache holds.  VACV_TUNE_WARP_KERNEL: 0 warp_kernel, 2 warp_u8_kernel.
-bool warp_batched(const WarpLaunch& L) {
+int warp_batched(const WarpLaunch& L) {
     const int knob = tune(VACV_TUNE_WARP_KERNEL);
-    if (knob == 0 || knob == 2) return knob == 2;
-    return 64.f * std::fabs(L.inv[3]) <= 10.f;
+    if (knob == 0 || knob == 2) return knob;
+    return 64.f * std::fabs(L.inv[3]) <= 10.f ? 2 : 0;
 }
 
 template <int CC, typename TIn, int OUT, int kPx>
@@ -418,7 +667,7 @@ hipError_t launch_px(const WarpLaunch& L, hipStream_t s) {
     if (total >= 0x7FFFFFF0LL) return hipErrorInvalidValue;
     const int64_t blocks = (total + 7) / 8 * 8;
     constexpr int G = kPx % 5 == 0 ? 5 : 4;
-    if (L.border_mode == kBorderConstant && std::is_same<TIn, uint8_t>::value && warp_batched(L))
+    if (L.border_mode == kBorderConstant && std::is_same<TIn, uint8_t>::value && warp_batched(L) == 2)
         hipLaunchKernelGGL((warp_u8_kernel<CC, OUT, kPx, G>), dim3((unsigned)blocks), dim3(64, 4), 0, s, L, gx, gy,
                            (int)total);
     else if (L.border_mode == kBorderConstant)
@@ -432,6 +681,20 @@ hipError_t launch_px(const WarpLaunch& L, hipStream_t s) {
 
 template <int CC, typename TIn, int OUT>
 hipError_t launch_one(const WarpLaunch& L, hipStream_t s) {
+    int max_rows = 0, max_chunks = 0, dst_al = 0;
+    const int knob = tune(VACV_TUNE_WARP_KERNEL);
+    if constexpr (std::is_same<TIn, uint8_t>::value) {
+      if (knob == 3 && warp_tile_plan(L, max_rows, max_chunks, dst_al)) {
+        const int gx = (L.dst.w + kTileW - 1) / kTileW, gy = (L.dst.h + kTileH - 1) / kTileH;
+        const int64_t total = (int64_t)gx * gy * L.n * L.src.planes;
+        if (total >= 0x7FFFFFF0LL) return hipErrorInvalidValue;
+        const int64_t blocks = (total + 7) / 8 * 8;
+        const size_t lds = (size_t)max_rows * max_chunks * 16 + 16;  // + the last tap dword's overhang
+        hipLaunchKernelGGL((warp_tile_kernel<CC, OUT>), dim3((unsigned)blocks), dim3(kBlock), lds, s, L, gx, gy,
+                           (int)total, max_rows, max_chunks, dst_al);
+        return hipGetLastError();
+      }
+    }
     switch (warp_blocks_per_wave(OUT == kOutSame && sizeof(TIn) == 1, L.dst.w)) {
         case 10: return launch_px<CC, TIn, OUT, 10>(L, s);
         case 5: return launch_px<CC, TIn, OUT, 5>(L, s);

@@ -290,7 +290,7 @@ enum {
     VACV_TUNE_RESIZE_TILE_W = 12,    /* staged kernel planner: tile width */
     VACV_TUNE_RESIZE_WORK = 13,      /* staged kernel planner: work per thread */
     VACV_TUNE_RESIZE_ROWS_BYTES = 14,/* whole-row kernel planner: output bytes per workgroup */
-    VACV_TUNE_WARP_KERNEL = 15,      /* u8 CONSTANT warp: 0 per-pixel gathers, 2 batched gathers */
+    VACV_TUNE_WARP_KERNEL = 15,      /* u8 CONSTANT warp: 0 per-pixel gathers, 2 batched gathers, 3 LDS-staged tiles */
     VACV_TUNE_COUNT = 16
 };
 /* value < 0 restores the built-in choice.  Returns VACV_OK or INVALID_ARG. */

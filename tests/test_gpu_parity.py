@@ -637,11 +637,12 @@ def test_warp_border_modes(ops, dev, oracle):
 
 
 def test_warp_kernels_agree(ops, dev, oracle):
-    """u8 BORDER_CONSTANT warps run on the batched gather kernel
-    (warp_u8_kernel, k_warp.hip) where a 64-pixel output row spans few source
-    rows, else on the per-pixel kernel (warp_kernel);
-    VACV_TUNE_WARP_KERNEL = 2 / 0 forces one or the other and
-    VACV_TUNE_WARP_PX switches the lane blocks per wave (4, 5, 8, 10).
+    """u8 BORDER_CONSTANT warps run on the LDS-staged tile kernel
+    (warp_tile_kernel, k_warp.hip) unless its source rectangle is over the LDS
+    budget; then on the batched gather kernel (warp_u8_kernel) where a
+    64-pixel output row spans few source rows, else on the per-pixel kernel
+    (warp_kernel).  VACV_TUNE_WARP_KERNEL = 3 / 2 / 0 forces one of them and
+    VACV_TUNE_WARP_PX switches the gather kernels' lane blocks per wave.
     Identical outputs at full size for rotations, flips, shears, strong
     down-scales, fused normalisation, NCHW planes and a pitched destination."""
     import torch
@@ -659,11 +660,16 @@ def test_warp_kernels_agree(ops, dev, oracle):
             with ops.tuning(WARP_KERNEL=2):
                 a = ops.warp_affine(src, m, wo, ho)
                 an = ops.warp_affine_normalize(src, m, wo, ho, MEAN, STD)
+            with ops.tuning(WARP_KERNEL=3):
+                t = ops.warp_affine(src, m, wo, ho)
+                tn = ops.warp_affine_normalize(src, m, wo, ho, MEAN, STD)
             with ops.tuning(WARP_KERNEL=0):
                 b = ops.warp_affine(src, m, wo, ho)
                 bn = ops.warp_affine_normalize(src, m, wo, ho, MEAN, STD)
                 assert torch.equal(a, b), f"warp kernels differ {m.tolist()} {wo}x{ho}"
                 assert torch.equal(an, bn), f"warp normalize kernels differ {m.tolist()} {wo}x{ho}"
+                assert torch.equal(t, b), f"staged warp differs {m.tolist()} {wo}x{ho}"
+                assert torch.equal(tn, bn), f"staged warp normalize differs {m.tolist()} {wo}x{ho}"
                 for px in (4, 5, 8, 10):
                     with ops.tuning(WARP_PX=px):
                         assert torch.equal(ops.warp_affine(src, m, wo, ho), b), f"gather PX={px}"
@@ -671,12 +677,13 @@ def test_warp_kernels_agree(ops, dev, oracle):
                             f"gather PX={px} norm"
     for c in (1, 2, 3, 4):  # every pixel width, odd sizes, both kernels vs the oracle
         im = synthetic_image(90 + c, 97, 143, c)
-        for m in mats[:2]:
-            for flag in (2, 0):
-                with ops.tuning(WARP_KERNEL=flag):
-                    got = host(ops.warp_affine(to_dev(im.reshape(1, 97, 143, c), dev), m, 121, 83))[0]
-                assert_same(got.reshape(83, 121, c), oracle.warp_affine(im, m, 121, 83).reshape(83, 121, c),
-                            f"warp c={c} kernel={flag}")
+        for m in mats[:2] + mats[3:4]:
+            for wo in (121, 128):  # byte stores / the aligned 4-pixel stores, partial tiles
+                want = oracle.warp_affine(im, m, wo, 83).reshape(83, wo, c)
+                for flag in (3, 2, 0):
+                    with ops.tuning(WARP_KERNEL=flag):
+                        got = host(ops.warp_affine(to_dev(im.reshape(1, 97, 143, c), dev), m, wo, 83))[0]
+                    assert_same(got.reshape(83, wo, c), want, f"warp c={c} {wo} kernel={flag}")
     chw = to_dev(np.ascontiguousarray(imgs.transpose(0, 3, 1, 2)), dev)
     got = host(ops.warp_affine(chw, mats[0], 300, 200, layout=NCHW))
     for k in range(3):
