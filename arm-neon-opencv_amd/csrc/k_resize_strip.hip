@@ -1,0 +1,299 @@
+// k_resize_strip.hip -- u8 bilinear resize (all three fixed-point modes, u8 /
+// fp32 / normalised-fp32 out) for geometries whose output rows weight TWO
+// source rows (e.g. 1080p -> 1280x720), as column strips walking down an image.
+//
+// Reference arithmetic: the same as resize_direct_kernel (k_resize_direct.hip):
+// fixed_tap() taps (resize_naive.cpp:19-45 / resize_neon.cpp:17-78) and
+// blend_fixed<MODE> (resize_naive.cpp:61-64 / resize_neon.cpp:103-167).
+//
+// Why.  A source row of a two-tap geometry feeds ~1.33 output rows; the staged
+// and gather kernels compute those output rows in different workgroups, often
+// on different XCDs, so the row is fetched into L2 more than once and every
+// workgroup pays its own latency.  Here a workgroup owns a 64-column output
+// strip of one plane and walks down its rows, keeping the source rows in an
+// LDS ring: every source byte of the strip leaves HBM once.
+//  * Batches of BR = 16 output rows (32: VACV_TUNE_RESIZE_STRIP = 2, measured
+//    slower); the source rows a batch adds to the ring are loaded with
+//    coalesced 16-byte loads into registers while the previous batch is being
+//    blended (one barrier per batch).
+//  * Lane l takes output column ox0 + l: its horizontal taps and its byte
+//    offset in a ring row are computed once; a row's vertical taps are
+//    wave-uniform.  Per pixel: two (CC <= 2) or three dword LDS reads per tap
+//    row, v_alignbyte, the packed-u16 dot products of resize_direct_kernel.
+//  * u8 output: the lane quads' bytes are packed (DPP) into 4*CC-byte stores;
+//    fp32: CC floats per lane, lane-contiguous.
+#pragma clang fp contract(off)
+
+#include <algorithm>
+#include <cmath>
+
+#include "vacv_device.hpp"
+
+namespace vacv {
+namespace {
+
+constexpr int kStripW = 64;       // output columns per workgroup (one per lane)
+constexpr int kFetchIters = 4;    // 16-byte chunks per thread and batch
+constexpr int kMaxLds = 64 * 1024;
+
+template <int CC, int OUT, int MODE, int BR>
+__global__ void __launch_bounds__(kBlock)
+resize_strip_kernel(ResizeLaunch L, int strips_x, int groups, int rows_per_group, int ring, int stride, int dst_al) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int id = blockIdx.x;
+    const int per_plane = strips_x * groups;
+    const int pidx = id / per_plane;
+    const int rem = id - pidx * per_plane;
+    const int grp = rem / strips_x, sxi = rem - grp * strips_x;
+    const int img = pidx / L.src.planes, plane = pidx - img * L.src.planes;
+    const int W = L.dst.w, H = L.dst.h;
+    const int oy_begin = grp * rows_per_group, oy_end = min(oy_begin + rows_per_group, H);
+    const int ox0 = sxi * kStripW, ox = ox0 + lane;
+
+    const unsigned char* sp = L.src.base + (int64_t)img * L.src.img_pitch + (int64_t)plane * L.src.plane_pitch;
+    const Rsrc srs = make_rsrc(sp, L.src.plane_bytes);
+    const uint32_t lim = (uint32_t)L.src.plane_bytes + srs.delta;
+    const uint32_t rp = (uint32_t)L.src.row_pitch;  // % 16 == 0 (host)
+
+    // ---- the strip's source columns and the lane's taps -----------------------
+    const FixedTap tx = tap_of<MODE>(min(ox, W - 1), L.src.w, W, L.scale_xf, L.scale_xd);
+    const int xs0 = tap_of<MODE>(ox0, L.src.w, W, L.scale_xf, L.scale_xd).i;  // uniform
+    const int xs1 = tap_of<MODE>(min(ox0 + kStripW, W) - 1, L.src.w, W, L.scale_xf, L.scale_xd).i + 1;
+    const uint32_t col0 = (uint32_t)(xs0 * CC) + srs.delta;  // strip's first byte within a row (from base16)
+    const uint32_t dxb = col0 & 15u;                          // ... within its chunk (every row: rp % 16 == 0)
+    const int chunks = (int)((dxb + (uint32_t)(xs1 - xs0 + 1) * CC + 15u) >> 4);
+    const uint32_t lo = (uint32_t)((tx.i - xs0) * CC) + dxb;  // the lane's taps in a ring row
+    const uint32_t lo4 = lo & ~3u, sh = lo & 3u;
+    const us2 wx = __builtin_bit_cast(us2, (uint32_t)tx.w0 | ((uint32_t)tx.w1 << 16));
+
+    ChanNorm cn[CC] = {};
+    if (OUT == kOutNorm) {
+#pragma unroll
+        for (int k = 0; k < CC; ++k) cn[k] = chan_norm(L.norm, img, CC == 1 ? plane % L.norm.c_total : k);
+    }
+    unsigned char* dp = const_cast<unsigned char*>(L.dst.base) + (int64_t)img * L.dst.img_pitch +
+                        (int64_t)plane * L.dst.plane_pitch;
+    const Rsrc drs = make_rsrc(dp, L.dst.plane_bytes);  // 32-bit store offsets
+    const int qx = ox0 + (lane & ~3);
+    const bool quad_full = qx + 4 <= W && dst_al;
+    constexpr int kTD = (int)kTapDwords<CC, true>;
+
+    // ---- ring fill: source rows (next_row .. hi] --------------------------------
+    uint4 pre[kFetchIters];
+    uint32_t dst_off[kFetchIters];
+    auto fetch = [&](int r_first, int r_last) {
+        const int n = max(r_last - r_first + 1, 0) * chunks;
+        const uint32_t magic = (uint32_t)((0x100000000ull + (uint64_t)chunks - 1) / (uint64_t)chunks);
+#pragma unroll
+        for (int u = 0; u < kFetchIters; ++u) {
+            const int i = u * kBlock + tid;
+            dst_off[u] = 0xFFFFFFFFu;
+            if (i < n) {
+                const uint32_t rr = chunks == 1 ? (uint32_t)i : __umulhi((uint32_t)i, magic);  // i / chunks
+                const uint32_t c = (uint32_t)i - rr * (uint32_t)chunks;
+                const uint32_t r = (uint32_t)r_first + rr;
+                const uint32_t o = ((r * rp + col0) & ~15u) + 16u * c;
+                if (o + 16u <= lim) {
+                    pre[u] = load16(srs, o);
+                } else {  // the plane's last chunk: a straddling 16-byte load reads as zeros
+                    uint32_t d[4] = {0u, 0u, 0u, 0u};
+#pragma unroll 1
+                    for (uint32_t e = 0; e < 16u; ++e)
+                        if (o + e < lim)
+                            d[e >> 2] |= (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(srs.r, (int)(o + e), 0, 0) << (8 * (e & 3));
+                    pre[u] = make_uint4(d[0], d[1], d[2], d[3]);
+                }
+                dst_off[u] = (r & (uint32_t)(ring - 1)) * (uint32_t)stride + 16u * c;
+            }
+        }
+    };
+    auto park = [&]() {
+#pragma unroll
+        for (int u = 0; u < kFetchIters; ++u)
+            if (dst_off[u] != 0xFFFFFFFFu) *reinterpret_cast<uint4*>(lds + dst_off[u]) = pre[u];
+    };
+    auto rows_of = [&](int b, int& lo_row, int& hi_row) {  // source rows batch b reads
+        const int y0 = oy_begin + b * BR, y1 = min(y0 + BR, oy_end) - 1;
+        lo_row = tap_of<MODE>(y0, L.src.h, H, L.scale_yf, L.scale_yd).i;
+        hi_row = tap_of<MODE>(y1, L.src.h, H, L.scale_yf, L.scale_yd).i + 1;  // <= h - 1 (linear_tap)
+    };
+
+    const int batches = (oy_end - oy_begin + BR - 1) / BR;
+    if (batches <= 0) return;  // uniform
+    int lo_row, hi_row;
+    rows_of(0, lo_row, hi_row);
+    fetch(lo_row, hi_row);
+    int loaded = hi_row;
+    for (int b = 0; b < batches; ++b) {
+        park();
+        __syncthreads();
+        if (b + 1 < batches) {  // the next batch's new rows, in flight while this one blends
+            int l1, h1;
+            rows_of(b + 1, l1, h1);
+            fetch(max(l1, loaded + 1), h1);
+            loaded = max(loaded, h1);
+        }
+        // ---- blend: wave w takes rows w, w + 4, ... of the batch, 4 at a time ---
+#pragma unroll
+        for (int g = 0; g < BR / 16; ++g) {
+        uint32_t t0[4][3], t1[4][3];
+        uint32_t wyv[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int oy = min(oy_begin + b * BR + 16 * g + wave + 4 * j, H - 1);
+            const FixedTap ty = tap_of<MODE>(oy, L.src.h, H, L.scale_yf, L.scale_yd);  // wave-uniform
+            wyv[j] = (uint32_t)ty.w0 | ((uint32_t)ty.w1 << 16);
+            const uint32_t ra = ((uint32_t)ty.i & (uint32_t)(ring - 1)) * (uint32_t)stride;
+            const uint32_t rb = ((uint32_t)(ty.i + 1) & (uint32_t)(ring - 1)) * (uint32_t)stride;
+            const uint32_t* pa = reinterpret_cast<const uint32_t*>(lds + ra + lo4);
+            const uint32_t* pb = reinterpret_cast<const uint32_t*>(lds + rb + lo4);
+#pragma unroll
+            for (int d = 0; d < kTD; ++d) { t0[j][d] = pa[d]; t1[j][d] = pb[d]; }
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int oy = oy_begin + b * BR + 16 * g + wave + 4 * j;
+            const uint32_t a0 = __builtin_amdgcn_alignbyte(t0[j][1], t0[j][0], sh);
+            const uint32_t c0 = __builtin_amdgcn_alignbyte(t1[j][1], t1[j][0], sh);
+            uint32_t a1 = 0u, c1 = 0u;
+            if constexpr (kTD == 3) {
+                a1 = __builtin_amdgcn_alignbyte(t0[j][2], t0[j][1], sh);
+                c1 = __builtin_amdgcn_alignbyte(t1[j][2], t1[j][1], sh);
+            }
+            const uint32_t wA = wyv[j] & 0xFFFFu, wB = wyv[j] >> 16;
+            int v[CC];
+#pragma unroll
+            for (int k = 0; k < CC; ++k) {
+                const uint32_t sel = (uint32_t)k | (0x0Cu << 8) | ((uint32_t)(CC + k) << 16) | (0x0Cu << 24);
+                v[k] = blend_fixed<MODE>(__builtin_amdgcn_perm(a1, a0, sel), __builtin_amdgcn_perm(c1, c0, sel), wx, wA, wB);
+            }
+            if (oy >= oy_end) continue;  // wave-uniform
+            const uint32_t row_off = (uint32_t)oy * (uint32_t)L.dst.row_pitch + drs.delta;
+            if constexpr (OUT == kOutSame) {
+                uint32_t own = 0;
+#pragma unroll
+                for (int k = 0; k < CC; ++k) own |= (uint32_t)v[k] << (8 * k);
+                const uint32_t word = quad_pack<CC>(own, lane & 3);
+                if (quad_full) {
+                    if ((lane & 3) < CC)
+                        __builtin_amdgcn_raw_buffer_store_b32(word, drs.r, (int)(row_off + (uint32_t)(qx * CC + 4 * (lane & 3))),
+                                                              0, VACV_STORE_AUX);
+                } else if (ox < W) {
+#pragma unroll
+                    for (int k = 0; k < CC; ++k)
+                        __builtin_amdgcn_raw_buffer_store_b8((unsigned char)v[k], drs.r, (int)(row_off + (uint32_t)(ox * CC + k)), 0,
+                                                             VACV_STORE_AUX);
+                }
+            } else if (ox < W) {
+                float f[CC];
+#pragma unroll
+                for (int k = 0; k < CC; ++k) f[k] = OUT == kOutF32 ? (float)v[k] : normalize_u8v(cn[k], v[k]);
+                const int off = (int)(row_off + (uint32_t)(ox * CC * 4));
+                if constexpr (CC == 1) {
+                    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, f[0]), drs.r, off, 0, VACV_STORE_AUX);
+                } else if constexpr (CC == 2) {
+                    typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+                    __builtin_amdgcn_raw_buffer_store_b64(u32x2{__builtin_bit_cast(uint32_t, f[0]), __builtin_bit_cast(uint32_t, f[1])},
+                                                          drs.r, off, 0, VACV_STORE_AUX);
+                } else if constexpr (CC == 3) {
+                    typedef unsigned int u32x3 __attribute__((ext_vector_type(3)));
+                    __builtin_amdgcn_raw_buffer_store_b96(u32x3{__builtin_bit_cast(uint32_t, f[0]), __builtin_bit_cast(uint32_t, f[1]),
+                                                                __builtin_bit_cast(uint32_t, f[2])},
+                                                          drs.r, off, 0, VACV_STORE_AUX);
+                } else {
+                    __builtin_amdgcn_raw_buffer_store_b128(u32x4{__builtin_bit_cast(uint32_t, f[0]), __builtin_bit_cast(uint32_t, f[1]),
+                                                                 __builtin_bit_cast(uint32_t, f[2]), __builtin_bit_cast(uint32_t, f[3])},
+                                                           drs.r, off, 0, VACV_STORE_AUX);
+                }
+            }
+        }
+        }
+    }
+}
+
+struct StripPlan {
+    int strips_x, groups, rows_per_group, ring, stride, lds, br;
+};
+
+// The ring (a power of two holding two batches' source rows) and the row
+// stride (a strip's source bytes plus the worst chunk offset), or false when
+// the strip kernel does not apply.
+bool strip_plan(const ResizeLaunch& L, StripPlan& p) {
+    if (L.kind != kLinearFixed || L.src.esize != 1 || L.src.cc < 1 || L.src.cc > 4) return false;
+    if (L.src.row_pitch % 16) return false;
+    if (L.dst.w >= (1 << 23) || L.dst.h >= (1 << 23)) return false;
+    const int cc = L.src.cc;
+    const double sx = L.scale_xd, sy = L.scale_yd;
+    const int span = (int)std::ceil((kStripW - 1) * sx) + 3;  // source columns of a strip, + taps and slack
+    const int chunks = (15 + span * cc + 15) / 16;
+    p.br = tune_or(VACV_TUNE_RESIZE_STRIP, 1) == 2 ? 32 : 16;
+    const int batch_rows = (int)std::ceil(p.br * sy) + 3;  // source rows one batch can add
+    if ((int64_t)batch_rows * chunks > (int64_t)kFetchIters * kBlock) return false;
+    int ring = 1;
+    while (ring < 2 * batch_rows + 2) ring <<= 1;
+    p.stride = chunks * 16;
+    p.ring = ring;
+    p.lds = ring * p.stride + 16;  // + the last tap dword's overhang
+    if (p.lds > kMaxLds) return false;
+    p.strips_x = (L.dst.w + kStripW - 1) / kStripW;
+    // enough workgroups for the chip: split the rows when the strips are few
+    const int64_t strips = (int64_t)p.strips_x * L.n * L.src.planes;
+    p.groups = 1;
+    while (strips * p.groups < 2048 && L.dst.h / (p.groups * 2) >= 4 * p.br) p.groups *= 2;
+    p.rows_per_group = (L.dst.h + p.groups - 1) / p.groups;
+    return strips * p.groups < 0x7FFFFFF0LL;
+}
+
+template <int CC, int OUT, int MODE>
+hipError_t launch_one(const ResizeLaunch& L, const StripPlan& p, hipStream_t s) {
+    const int64_t blocks = (int64_t)p.strips_x * p.groups * L.n * L.src.planes;
+    const int64_t out_align = OUT == kOutSame ? 4 : 4;
+    const int dst_al = !(L.dst.row_pitch % out_align || L.dst.img_pitch % out_align || L.dst.plane_pitch % out_align ||
+                         reinterpret_cast<uintptr_t>(L.dst.base) % out_align);
+    if (p.br == 32)
+        hipLaunchKernelGGL((resize_strip_kernel<CC, OUT, MODE, 32>), dim3((unsigned)blocks), dim3(kBlock), p.lds, s, L,
+                           p.strips_x, p.groups, p.rows_per_group, p.ring, p.stride, dst_al);
+    else
+        hipLaunchKernelGGL((resize_strip_kernel<CC, OUT, MODE, 16>), dim3((unsigned)blocks), dim3(kBlock), p.lds, s, L,
+                           p.strips_x, p.groups, p.rows_per_group, p.ring, p.stride, dst_al);
+    return hipGetLastError();
+}
+
+template <int OUT, int MODE>
+hipError_t launch_cc(const ResizeLaunch& L, const StripPlan& p, hipStream_t s) {
+    switch (L.src.cc) {
+        case 1: return launch_one<1, OUT, MODE>(L, p, s);
+        case 2: return launch_one<2, OUT, MODE>(L, p, s);
+        case 3: return launch_one<3, OUT, MODE>(L, p, s);
+        case 4: return launch_one<4, OUT, MODE>(L, p, s);
+        default: return hipErrorInvalidValue;
+    }
+}
+
+template <int OUT>
+hipError_t launch_mode(const ResizeLaunch& L, const StripPlan& p, hipStream_t s) {
+    switch (L.mode) {
+        case VACV_LINEAR_REFERENCE: return launch_cc<OUT, VACV_LINEAR_REFERENCE>(L, p, s);
+        case VACV_LINEAR_NEON: return launch_cc<OUT, VACV_LINEAR_NEON>(L, p, s);
+        case VACV_LINEAR_OPENCV: return launch_cc<OUT, VACV_LINEAR_OPENCV>(L, p, s);
+        default: return hipErrorInvalidValue;
+    }
+}
+
+}  // namespace
+
+bool resize_strip_applies(const ResizeLaunch& L) {
+    StripPlan p;
+    return strip_plan(L, p);
+}
+
+hipError_t launch_resize_strip(const ResizeLaunch& L, hipStream_t s) {
+    StripPlan p;
+    if (!strip_plan(L, p)) return hipErrorInvalidValue;
+    if (L.out == kOutSame) return launch_mode<kOutSame>(L, p, s);
+    if (L.out == kOutF32) return launch_mode<kOutF32>(L, p, s);
+    return launch_mode<kOutNorm>(L, p, s);
+}
+
+}  // namespace vacv

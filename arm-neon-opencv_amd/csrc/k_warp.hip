@@ -26,6 +26,8 @@
 #pragma clang fp contract(off)
 
 #include <cmath>
+#include <map>
+#include <mutex>
 
 #include "vacv_device.hpp"
 
@@ -390,36 +392,32 @@ warp_u8_kernel(WarpLaunch L, int gx, int gy, int total) {
 // PMC): the gather kernels above are bound by the vector cache's per-quad tag
 // lookups -- ~1.8 cycles per (4-lane group x cache line) access, 19-33 of them
 // per 64-lane gather instruction -- not by bytes or ALU.  Here a workgroup
-// owns a kTW x kTH output tile, loads the source rectangle its taps can reach
-// with coalesced 16-byte loads (one access per 4 lanes), and takes the taps
-// from LDS.  The rectangle comes from the tile's corners: the reference's
-// coordinate ((m0*x + m1*y) + m2 in float) is monotone in x and in y
-// separately, so its extremes over the tile are at corners.  A pixel whose
-// taps fall outside the staged rectangle anyway (the host's size cap) takes
-// them from memory, so the result never depends on the staging.
-// Thread layout: 16 lanes per output row, 4 consecutive pixels per lane (one
-// 4*CC-byte store), 16 rows per pass, kTH / 16 passes.
+// walks kTileW x kTileH output tiles; for each it loads the source rectangle
+// the tile's taps can reach with coalesced 16-byte loads (one access per 4
+// lanes) into LDS and takes the taps from there.
+//  * The rectangle comes from the tile's corners (warp_rect_kernel, once per
+//    launch): the reference's coordinate ((m0*x + m1*y) + m2 in float) is
+//    monotone in x and in y separately, so its extremes over the tile are at
+//    corners, and every in-source pixel's taps lie inside.
+//  * Persistent workgroups, two LDS buffers: tile i+1's loads are in flight
+//    (in registers) while tile i is sampled; one barrier per tile.
+//  * Wave w samples tile rows w, w + 4, ...; lane l takes column l, so a tap
+//    read covers 64 consecutive output pixels (few LDS bank conflicts).  Byte
+//    results are packed across each lane quad (DPP) into 4*CC-byte stores.
+//  * A 16-byte load that crosses the end of the plane returns zeros: pixels
+//    whose taps reach the plane's last partial chunk, and tiles whose
+//    rectangle exceeds the LDS budget, take their taps from memory instead.
 constexpr int kTileW = 64, kTileH = 32;
-constexpr size_t kWarpTileLds = 32 * 1024;  // per workgroup: 5 resident per CU at the cap
+constexpr int kStageIters = 3;                        // 16-byte chunks per thread and tile
+constexpr int kWarpBoxBytes = kStageIters * kBlock * 16;  // per LDS buffer (12 KiB)
 
-template <int CC, int OUT>
-__global__ void __launch_bounds__(kBlock)
-warp_tile_kernel(WarpLaunch L, int gx, int gy, int total, int max_rows, int max_chunks, int dst_al) {
-    using TOut = typename std::conditional<(OUT == kOutSame), uint8_t, float>::type;
-    extern __shared__ __attribute__((aligned(16))) unsigned char box[];
-    const int per_xcd = (total + 7) / 8;  // XCD-aware block order (see warp_kernel)
-    const int id = (int)(blockIdx.x % 8) * per_xcd + (int)(blockIdx.x / 8);
-    if (id >= total) return;  // uniform
-    const int pidx = id / (gx * gy);
-    const int rem = id - pidx * gx * gy;
-    const int by = rem / gx, bx = rem - by * gx;
-    const int img = pidx / L.src.planes;
-    const int plane = pidx - img * L.src.planes;
-    const int tid = threadIdx.x;
+// per tile of one plane: the source rectangle [x0, x1] x [y0, y1] its taps can reach
+__global__ void warp_rect_kernel(WarpLaunch L, int gx, int gy, int4* rects) {
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= gx * gy) return;
+    const int by = t / gx, bx = t - by * gx;
     const int tx0 = bx * kTileW, ty0 = by * kTileH;
     const int txe = min(tx0 + kTileW, L.dst.w) - 1, tye = min(ty0 + kTileH, L.dst.h) - 1;
-
-    // ---- the source rectangle of the tile's taps ---------------------------
     const float* M = L.inv;
     const float c0x = M[0] * (float)tx0, c1x = M[0] * (float)txe;
     const float c0y = M[1] * (float)ty0, c1y = M[1] * (float)tye;
@@ -431,208 +429,324 @@ warp_tile_kernel(WarpLaunch L, int gx, int gy, int total, int max_rows, int max_
     const float fy_lo = fminf(fminf(fya, fyb), fminf(fyc, fyd)), fy_hi = fmaxf(fmaxf(fya, fyb), fmaxf(fyc, fyd));
     const int sw = L.src.w, shh = L.src.h;
     // clamp in float first: the corners may be far outside (or NaN)
-    const int x0 = (int)floorf(fminf(fmaxf(fx_lo, 0.f), (float)(sw - 1)));
-    const int x1 = min((int)floorf(fminf(fmaxf(fx_hi, 0.f), (float)(sw - 1))) + 1, sw - 1);
-    const int y0 = (int)floorf(fminf(fmaxf(fy_lo, 0.f), (float)(shh - 1)));
-    const int y1 = min((int)floorf(fminf(fmaxf(fy_hi, 0.f), (float)(shh - 1))) + 1, shh - 1);
-    const unsigned char* sp = L.src.base + (int64_t)img * L.src.img_pitch + (int64_t)plane * L.src.plane_pitch;
-    const uint32_t rp = (uint32_t)L.src.row_pitch;       // host: plane_bytes < 2^31
-    const Rsrc srs = make_rsrc(sp, L.src.plane_bytes);
-    // staged row r = source row y0 + r from the 16-byte chunk holding its
-    // pixel x0 on; that pixel sits at byte dx_r of the LDS row.  dx_r is the
-    // same for every row when the row pitch is a multiple of 16 (rpm == 0).
-    const uint32_t off0 = (uint32_t)y0 * rp + (uint32_t)(x0 * CC) + srs.delta;  // from the 16-aligned base
-    const uint32_t dxb = off0 & 15u, rpm = rp & 15u;
-    const int chunks = min((int)((rpm ? 15u : dxb) + (uint32_t)(x1 - x0 + 1) * CC + 15u) >> 4, max_chunks);
-    const int rows = min(y1 - y0 + 1, max_rows);
-    const int stride = chunks * 16;
-    const int bw_px = (chunks * 16 - (rpm ? 15 : (int)dxb)) / CC;  // pixels every staged row holds from x0
+    int4 r;
+    r.x = (int)floorf(fminf(fmaxf(fx_lo, 0.f), (float)(sw - 1)));
+    r.z = min((int)floorf(fminf(fmaxf(fx_hi, 0.f), (float)(sw - 1))) + 1, sw - 1);
+    r.y = (int)floorf(fminf(fmaxf(fy_lo, 0.f), (float)(shh - 1)));
+    r.w = min((int)floorf(fminf(fmaxf(fy_hi, 0.f), (float)(shh - 1))) + 1, shh - 1);
+    rects[t] = r;
+}
 
-    {
-        const int wave = tid >> 6, lane = tid & 63;
-        // a buffer load that crosses the end of the resource returns zeros
-        // whole: the chunk holding the plane's last bytes is read bytewise
-        const uint32_t lim = (uint32_t)L.src.plane_bytes + srs.delta;
-        for (int r = wave; r < rows; r += kBlock / 64) {
-            const uint32_t ro = (off0 + (uint32_t)r * rp) & ~15u;
-            for (int c = lane; c < chunks; c += 64) {
-                const uint32_t o = ro + 16u * (uint32_t)c;
-                uint4 v;
-                if (o + 16u <= lim) {
-                    v = load16(srs, o);
-                } else {
-                    uint32_t d[4] = {0u, 0u, 0u, 0u};
-                    for (uint32_t e = 0; e < 16u && o + e < lim; ++e)
-                        d[e >> 2] |= (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(srs.r, (int)(o + e), 0, 0) << (8 * (e & 3));
-                    v = make_uint4(d[0], d[1], d[2], d[3]);
-                }
-                *reinterpret_cast<uint4*>(box + r * stride + 16 * c) = v;
-            }
-        }
+// the taps of one pixel from memory, bytewise (the staged kernel's rare
+// fallback: the plane's last bytes, or a tile over the LDS budget)
+template <int CC>
+__device__ __forceinline__ void taps_from_memory(const unsigned char* sp, uint32_t rp, int sx, int sy, uint32_t (&t0)[3],
+                                                 uint32_t (&t1)[3]) {
+    const unsigned char* r0 = sp + (int64_t)sy * rp + (int64_t)sx * CC;
+#pragma unroll
+    for (int d = 0; d < 3; ++d) t0[d] = t1[d] = 0u;
+#pragma unroll
+    for (int e = 0; e < 2 * CC; ++e) {
+        t0[e >> 2] |= (uint32_t)r0[e] << (8 * (e & 3));
+        t1[e >> 2] |= (uint32_t)r0[rp + e] << (8 * (e & 3));
     }
-    __syncthreads();
+}
 
-    ChanNorm cn[CC] = {};
-    if (OUT == kOutNorm) {
-#pragma unroll
-        for (int k = 0; k < CC; ++k) cn[k] = chan_norm(L.norm, img, CC == 1 ? plane : k);
-    }
-    TOut bval[CC];
-#pragma unroll
-    for (int k = 0; k < CC; ++k)
-        bval[k] = OUT == kOutNorm ? (TOut)normalize_u8v(cn[k], (int)L.border[k]) : (TOut)L.border[k];
+// A tile's staging plan (wave-uniform integers).
+struct TileBox {
+    int x0, y0;
+    uint32_t off0;     // byte of (x0, y0) from the 16-aligned plane base
+    int chunks, rows;  // 16-byte chunks per staged row, staged rows
+    int stride;        // LDS bytes per staged row
+    uint32_t dxb;      // (x0, y0)'s byte within its chunk
+    uint32_t bw_lim;   // lx <= bw_lim: both taps staged
+    int ly_max;        // ly <= ly_max: rows ly, ly + 1 staged and whole (may be < 0)
+    bool staged;       // the rectangle fits the LDS buffer
+    bool tail;         // some tap row may reach the plane's last partial chunk
+};
 
-    const int xl = (tid & 15) * 4;       // the lane's 4 pixels: tile columns xl .. xl + 3
-    const int yl = tid >> 4;             // tile row of pass 0
-    float ax_m[4], ay_m[4];
-#pragma unroll
-    for (int p = 0; p < 4; ++p) {
-        ax_m[p] = M[0] * (float)(tx0 + xl + p);
-        ay_m[p] = M[3] * (float)(tx0 + xl + p);
-    }
-    unsigned char* dbase = const_cast<unsigned char*>(L.dst.base) + (int64_t)img * L.dst.img_pitch +
-                           (int64_t)plane * L.dst.plane_pitch;
+template <int CC, bool RA>
+__device__ __forceinline__ TileBox tile_box(const int4 r, uint32_t rp, uint32_t delta, uint32_t lim16) {
+    TileBox b;
+    b.x0 = r.x;
+    b.y0 = r.y;
+    b.off0 = (uint32_t)r.y * rp + (uint32_t)(r.x * CC) + delta;
+    b.dxb = b.off0 & 15u;
+    const uint32_t dmax = RA ? b.dxb : 15u;
+    b.chunks = (int)((dmax + (uint32_t)(r.z - r.x + 1) * CC + 15u) >> 4);
+    b.rows = r.w - r.y + 1;
+    b.stride = b.chunks * 16;
+    b.staged = b.rows * b.chunks <= kStageIters * kBlock;
+    b.bw_lim = (uint32_t)max((b.stride - (int)dmax) / CC - 2, 0);
+    const int sy_safe = (int)((lim16 - delta) / rp) - 2;  // sy <= sy_safe: rows sy, sy + 1 whole
+    b.tail = r.w + 1 > sy_safe + 2 || !b.staged;
+    b.ly_max = min(b.rows - 2, sy_safe - r.y);
+    return b;
+}
+
+// RA: the source row pitch is a multiple of 16, so every staged row starts at
+// the same byte offset within its first chunk.
+template <int CC, int OUT, bool RA>
+__global__ void __launch_bounds__(kBlock)
+warp_tile_kernel(WarpLaunch L, int gx, int gy, int total, const int4* __restrict__ rects, int dst_al) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    // XCD-aware tile order: workgroup b runs on XCD b % 8 and walks that
+    // XCD's contiguous range of tiles, interleaved with its XCD siblings
+    const int per_xcd = (total + 7) / 8;
+    const int xcd = (int)(blockIdx.x % 8), wg_on_xcd = (int)(blockIdx.x / 8), wgs_per_xcd = (int)(gridDim.x / 8);
+    const int t_begin = xcd * per_xcd, t_end = min(t_begin + per_xcd, total);
+    const int tiles_per_plane = gx * gy;
+    const uint32_t rp = (uint32_t)L.src.row_pitch;  // host: plane_bytes < 2^31
+    const float* M = L.inv;
+    const float wlim = (float)(L.src.w - 1), hlim = (float)(L.src.h - 1);
     typedef unsigned short us2v __attribute__((ext_vector_type(2)));
-    constexpr uint32_t kTD = kTapDwords<CC, true>;
+    constexpr int kTD = (int)kTapDwords<CC, true>;
+
+    auto plane_of = [&](int t, int& img, int& plane, int& tile) {
+        const int pidx = t / tiles_per_plane;
+        tile = t - pidx * tiles_per_plane;
+        img = pidx / L.src.planes;
+        plane = pidx - img * L.src.planes;
+    };
+    auto plane_ptr = [&](int img, int plane) {
+        return L.src.base + (int64_t)img * L.src.img_pitch + (int64_t)plane * L.src.plane_pitch;
+    };
+
+    // ---- prefetch of a tile's chunks into registers ------------------------
+    uint4 pre[kStageIters];
+    auto fetch = [&](int t) {
+        int img, plane, tile;
+        plane_of(t, img, plane, tile);
+        const Rsrc srs = make_rsrc(plane_ptr(img, plane), L.src.plane_bytes);
+        const uint32_t lim16 = ((uint32_t)L.src.plane_bytes + srs.delta) & ~15u;
+        const TileBox b = tile_box<CC, RA>(rects[tile], rp, srs.delta, lim16);
+        const int n = b.staged ? b.rows * b.chunks : 0;
+        const uint32_t magic = (uint32_t)((0x100000000ull + (uint64_t)b.chunks - 1) / (uint64_t)b.chunks);
+#pragma unroll
+        for (int u = 0; u < kStageIters; ++u) {
+            const int i = min(u * kBlock + tid, max(n - 1, 0));
+            const uint32_t r = b.chunks == 1 ? (uint32_t)i : __umulhi((uint32_t)i, magic);  // i / chunks, exact (i < 2^12)
+            const uint32_t c = (uint32_t)i - r * (uint32_t)b.chunks;
+            pre[u] = load16(srs, ((b.off0 + r * rp) & ~15u) + 16u * c);
+        }
+    };
+    auto park = [&](int t, unsigned char* box) {
+        int img, plane, tile;
+        plane_of(t, img, plane, tile);
+        const uint32_t delta = (uint32_t)reinterpret_cast<uintptr_t>(plane_ptr(img, plane)) & 15u;
+        const uint32_t lim16 = ((uint32_t)L.src.plane_bytes + delta) & ~15u;
+        const TileBox b = tile_box<CC, RA>(rects[tile], rp, delta, lim16);
+        const int n = b.staged ? b.rows * b.chunks : 0;
+#pragma unroll
+        for (int u = 0; u < kStageIters; ++u) {
+            const int i = u * kBlock + tid;
+            if (i < n) *reinterpret_cast<uint4*>(box + 16 * i) = pre[u];  // row-major chunks: byte r*stride + 16c
+        }
+    };
+
+    int t = t_begin + wg_on_xcd;
+    if (t >= t_end) return;  // uniform
+    fetch(t);
+    for (int buf = 0; t < t_end; t += wgs_per_xcd, buf ^= 1) {
+        unsigned char* box = lds + buf * kWarpBoxBytes;
+        park(t, box);
+        __syncthreads();
+        const int tn = t + wgs_per_xcd;
+        if (tn < t_end) fetch(tn);  // in flight while this tile is sampled
+
+        int img, plane, tile;
+        plane_of(t, img, plane, tile);
+        const unsigned char* sp = plane_ptr(img, plane);
+        const uint32_t delta = (uint32_t)reinterpret_cast<uintptr_t>(sp) & 15u;
+        const uint32_t lim16 = ((uint32_t)L.src.plane_bytes + delta) & ~15u;
+        const TileBox b = tile_box<CC, RA>(rects[tile], rp, delta, lim16);
+        const uint32_t rpm = rp & 15u;
+        const int by = tile / gx, bx = tile - by * gx;
+        const int x = bx * kTileW + lane;
+        const float axm = M[0] * (float)x, aym = M[3] * (float)x;
+
+        ChanNorm cn[CC] = {};
+        if (OUT == kOutNorm) {
+#pragma unroll
+            for (int k = 0; k < CC; ++k) cn[k] = chan_norm(L.norm, img, CC == 1 ? plane : k);
+        }
+        unsigned char* drow0 = const_cast<unsigned char*>(L.dst.base) + (int64_t)img * L.dst.img_pitch +
+                               (int64_t)plane * L.dst.plane_pitch;
+        const Rsrc drs = make_rsrc(drow0, L.dst.plane_bytes);  // 32-bit store offsets
+        const int qx = bx * kTileW + (lane & ~3);  // the lane quad's first column
+        const bool quad_full = qx + 4 <= L.dst.w && dst_al;
 
 #pragma unroll
-    for (int pass = 0; pass < kTileH / 16; ++pass) {
-        const int y = ty0 + yl + 16 * pass;
-        if (y >= L.dst.h) break;
-        const float by_ = M[1] * (float)y, dy_ = M[4] * (float)y;
-        TOut res[4][CC];
+        for (int g = 0; g < kTileH / 16; ++g) {
+            // ---- 4 rows per lane: taps, weights, LDS reads (branch-free) -----
+            uint32_t t0[4][3], t1[4][3], sh0[4], sh1[4], wxp[4], wy0[4];
+            int sxv[4], syv[4];
+            bool okv[4], fbv[4];
 #pragma unroll
-        for (int p = 0; p < 4; ++p) {
-            const float fx = (ax_m[p] + by_) + M[2];
-            const float fy = (ay_m[p] + dy_) + M[5];
-            const bool ok = fx >= 0.f && fx < (float)(sw - 1) && fy >= 0.f && fy < (float)(shh - 1);
-            if (!ok) {
-#pragma unroll
-                for (int k = 0; k < CC; ++k) res[p][k] = bval[k];
-                continue;
-            }
-            const int sx = (int)fx, sy = (int)fy;  // floor: fx, fy >= 0
-            const float ax = fx - (float)sx, ay = fy - (float)sy;
-            // SATURATE_CAST_SHORT of a value in (0, 2048]: the +0.5f branch, no clamp
-            const uint32_t wy0 = (uint32_t)(int)((1.f - ay) * 2048.f + 0.5f);
-            const uint32_t wx0 = (uint32_t)(int)((1.f - ax) * 2048.f + 0.5f);
-            const us2v wx = __builtin_bit_cast(us2v, wx0 | ((2048u - wx0) << 16));
-            const uint32_t lx = (uint32_t)(sx - x0), ly = (uint32_t)(sy - y0);
-            uint32_t t0[kTD], t1[kTD];
-            uint32_t sh;
-            uint32_t sh1;
-            if (lx + 2u <= (uint32_t)bw_px && ly + 2u <= (uint32_t)rows) {
+            for (int j = 0; j < 4; ++j) {
+                const int y = by * kTileH + wave + 4 * (4 * g + j);
+                const float fx = (axm + M[1] * (float)y) + M[2];
+                const float fy = (aym + M[4] * (float)y) + M[5];
+                // bitwise: no short-circuit branches
+                const bool ok = (fx >= 0.f) & (fx < wlim) & (fy >= 0.f) & (fy < hlim);
+                const int sx = (int)fx, sy = (int)fy;  // floor where ok (fx, fy >= 0)
+                const float ax = fx - (float)sx, ay = fy - (float)sy;
+                // SATURATE_CAST_SHORT of a value in (0, 2048]: the +0.5f branch, no clamp
+                const uint32_t w0 = (uint32_t)(int)((1.f - ay) * 2048.f + 0.5f);
+                const uint32_t v0 = (uint32_t)(int)((1.f - ax) * 2048.f + 0.5f);
+                wy0[j] = w0;
+                wxp[j] = v0 | ((2048u - v0) << 16);
+                okv[j] = ok;
+                sxv[j] = sx;
+                syv[j] = sy;
+                // clamped into the staged rectangle: a no-op for every
+                // in-source pixel of a staged, tail-free tile
+                const uint32_t lx = min((uint32_t)(sx - b.x0), b.bw_lim);
+                const uint32_t lyr = (uint32_t)(sy - b.y0);
+                const uint32_t ly = min(lyr, (uint32_t)max(b.ly_max, 0));
+                fbv[j] = b.tail & ok & (!b.staged | ((int)lyr > b.ly_max));
                 uint32_t a0, a1;
-                if (rpm == 0u) {  // uniform
-                    a0 = ly * (uint32_t)stride + lx * CC + dxb;
-                    a1 = a0 + (uint32_t)stride;
+                if constexpr (RA) {
+                    a0 = __umul24(ly, (uint32_t)b.stride) + __umul24(lx, (uint32_t)CC) + b.dxb;
+                    a1 = a0 + (uint32_t)b.stride;
                 } else {
-                    const uint32_t d0 = (dxb + __umul24(ly, rpm)) & 15u;
-                    a0 = ly * (uint32_t)stride + lx * CC + d0;
-                    a1 = (ly + 1u) * (uint32_t)stride + lx * CC + ((d0 + rpm) & 15u);
+                    const uint32_t d0 = (b.dxb + __umul24(ly, rpm)) & 15u;
+                    a0 = __umul24(ly, (uint32_t)b.stride) + __umul24(lx, (uint32_t)CC) + d0;
+                    a1 = a0 + (uint32_t)b.stride - d0 + ((d0 + rpm) & 15u);
                 }
                 const uint32_t* b0 = reinterpret_cast<const uint32_t*>(box + (a0 & ~3u));
                 const uint32_t* b1 = reinterpret_cast<const uint32_t*>(box + (a1 & ~3u));
 #pragma unroll
-                for (uint32_t d = 0; d < kTD; ++d) { t0[d] = b0[d]; t1[d] = b1[d]; }
-                sh = a0 & 3u;
-                sh1 = a1 & 3u;
-            } else {  // outside the staged rectangle: the taps from memory
-                const unsigned char* r0 = sp + (int64_t)sy * rp + (int64_t)sx * CC;
-                uint32_t b[2][3] = {{0u, 0u, 0u}, {0u, 0u, 0u}};
+                for (int d = 0; d < kTD; ++d) { t0[j][d] = b0[d]; t1[j][d] = b1[d]; }
+                sh0[j] = a0 & 3u;
+                sh1[j] = a1 & 3u;
+            }
+            if (b.tail) {  // uniform; rare: taps from memory (selected, so the LDS reads stay unconditional)
 #pragma unroll
-                for (int e = 0; e < 2 * CC; ++e) {
-                    b[0][e >> 2] |= (uint32_t)r0[e] << (8 * (e & 3));
-                    b[1][e >> 2] |= (uint32_t)r0[rp + e] << (8 * (e & 3));
+                for (int j = 0; j < 4; ++j) {
+                    uint32_t m0[3] = {0u, 0u, 0u}, m1[3] = {0u, 0u, 0u};
+                    if (fbv[j]) taps_from_memory<CC>(sp, rp, sxv[j], syv[j], m0, m1);
+#pragma unroll
+                    for (int d = 0; d < 3; ++d) {
+                        t0[j][d] = fbv[j] ? m0[d] : t0[j][d];
+                        t1[j][d] = fbv[j] ? m1[d] : t1[j][d];
+                    }
+                    sh0[j] = fbv[j] ? 0u : sh0[j];
+                    sh1[j] = fbv[j] ? 0u : sh1[j];
                 }
-#pragma unroll
-                for (uint32_t d = 0; d < kTD; ++d) { t0[d] = b[0][d]; t1[d] = b[1][d]; }
-                sh = sh1 = 0u;
             }
-            const uint32_t a0 = __builtin_amdgcn_alignbyte(t0[1], t0[0], sh);
-            const uint32_t c0 = __builtin_amdgcn_alignbyte(t1[1], t1[0], sh1);
-            uint32_t a1 = 0u, c1 = 0u;
-            if constexpr (kTD == 3) {
-                a1 = __builtin_amdgcn_alignbyte(t0[2], t0[1], sh);
-                c1 = __builtin_amdgcn_alignbyte(t1[2], t1[1], sh1);
-            }
-            const uint32_t wA = wy0, wB = 2048u - wy0;
+            // ---- blends and stores -----------------------------------------
 #pragma unroll
-            for (int k = 0; k < CC; ++k) {
-                // warp_affine_naive.cpp:50-54 as (tl*wx0 + tr*wx1)*wy0 +
-                // (bl*wx0 + br*wx1)*wy1 (exact int32, <= 255*2^22)
-                const uint32_t sel = (uint32_t)k | (0x0Cu << 8) | ((uint32_t)(CC + k) << 16) | (0x0Cu << 24);
-                const uint32_t top = __builtin_amdgcn_perm(a1, a0, sel);
-                const uint32_t bot = __builtin_amdgcn_perm(c1, c0, sel);
-                const uint32_t ht = __builtin_amdgcn_udot2(__builtin_bit_cast(us2v, top), wx, 0u, false);
-                const uint32_t hb = __builtin_amdgcn_udot2(__builtin_bit_cast(us2v, bot), wx, 0u, false);
-                const int v = (int)((__umul24(ht, wA) + __umul24(hb, wB)) >> 22);
-                if (OUT == kOutSame) res[p][k] = (TOut)v;
-                else if (OUT == kOutF32) res[p][k] = (TOut)(float)v;
-                else res[p][k] = (TOut)normalize_u8v(cn[k], v);
-            }
-        }
-        // ---- the lane's 4 pixels: one 4*CC-element store ---------------------
-        const int x = tx0 + xl;
-        if (x >= L.dst.w) continue;
-        TOut* o = reinterpret_cast<TOut*>(dbase + (int64_t)y * L.dst.row_pitch) + (int64_t)x * CC;
-        if (x + 4 <= L.dst.w && dst_al) {
-            if constexpr (OUT == kOutSame) {
-                uint32_t wd[CC];
-#pragma unroll
-                for (int d = 0; d < CC; ++d) {
-                    uint32_t v = 0;
-#pragma unroll
-                    for (int e = 0; e < 4; ++e) v |= (uint32_t)res[(4 * d + e) / CC][(4 * d + e) % CC] << (8 * e);
-                    wd[d] = v;
+            for (int j = 0; j < 4; ++j) {
+                const int y = by * kTileH + wave + 4 * (4 * g + j);
+                const uint32_t a0 = __builtin_amdgcn_alignbyte(t0[j][1], t0[j][0], sh0[j]);
+                const uint32_t c0 = __builtin_amdgcn_alignbyte(t1[j][1], t1[j][0], sh1[j]);
+                uint32_t a1 = 0u, c1 = 0u;
+                if constexpr (kTD == 3) {
+                    a1 = __builtin_amdgcn_alignbyte(t0[j][2], t0[j][1], sh0[j]);
+                    c1 = __builtin_amdgcn_alignbyte(t1[j][2], t1[j][1], sh1[j]);
                 }
-                if constexpr (CC == 1) {
-                    __builtin_nontemporal_store(wd[0], reinterpret_cast<uint32_t*>(o));
-                } else if constexpr (CC == 2) {
-                    typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
-                    __builtin_nontemporal_store(u32x2{wd[0], wd[1]}, reinterpret_cast<u32x2*>(o));
-                } else if constexpr (CC == 3) {
-                    typedef unsigned int u32x3 __attribute__((ext_vector_type(3)));
-                    __builtin_nontemporal_store(u32x3{wd[0], wd[1], wd[2]}, reinterpret_cast<u32x3*>(o));
+                const us2v wx = __builtin_bit_cast(us2v, wxp[j]);
+                // weights x4: the sum's bits 24..31 are the result (<= 255 * 2^24 < 2^32)
+                const uint32_t wA = 4u * wy0[j], wB = 8192u - 4u * wy0[j];
+                uint32_t vv[CC];
+#pragma unroll
+                for (int k = 0; k < CC; ++k) {
+                    // warp_affine_naive.cpp:50-54 as (tl*wx0 + tr*wx1)*wy0 +
+                    // (bl*wx0 + br*wx1)*wy1 (exact integers), >> 22
+                    const uint32_t sel = (uint32_t)k | (0x0Cu << 8) | ((uint32_t)(CC + k) << 16) | (0x0Cu << 24);
+                    const uint32_t top = __builtin_amdgcn_perm(a1, a0, sel);
+                    const uint32_t bot = __builtin_amdgcn_perm(c1, c0, sel);
+                    const uint32_t ht = __builtin_amdgcn_udot2(__builtin_bit_cast(us2v, top), wx, 0u, false);
+                    const uint32_t hb = __builtin_amdgcn_udot2(__builtin_bit_cast(us2v, bot), wx, 0u, false);
+                    vv[k] = __umul24(ht, wA) + __umul24(hb, wB);
+                }
+                if (y >= L.dst.h) continue;
+                unsigned char* drow = drow0 + (int64_t)y * L.dst.row_pitch;
+                if constexpr (OUT == kOutSame) {
+                    // the pixel's bytes (bits 24..31 of each channel sum), border outside
+                    uint32_t own = 0;
+#pragma unroll
+                    for (int k = 0; k < CC; ++k) {
+                        const uint32_t byte = okv[j] ? (vv[k] >> 24) : (uint32_t)(int)L.border[k];
+                        own |= byte << (8 * k);
+                    }
+                    const uint32_t word = quad_pack<CC>(own, lane & 3);
+                    if (quad_full) {
+                        if ((lane & 3) < CC)
+                            __builtin_amdgcn_raw_buffer_store_b32(
+                                word, drs.r, (int)((uint32_t)y * (uint32_t)L.dst.row_pitch + (uint32_t)(qx * CC + 4 * (lane & 3)) + drs.delta),
+                                0, VACV_STORE_AUX);
+                    } else if (x < L.dst.w) {
+#pragma unroll
+                        for (int k = 0; k < CC; ++k) drow[(int64_t)x * CC + k] = (unsigned char)(own >> (8 * k));
+                    }
                 } else {
-                    __builtin_nontemporal_store(u32x4{wd[0], wd[1], wd[2], wd[3]}, reinterpret_cast<u32x4*>(o));
-                }
-            } else {
+                    if (x < L.dst.w) {
+                        float* o = reinterpret_cast<float*>(drow) + (int64_t)x * CC;
 #pragma unroll
-                for (int q = 0; q < CC; ++q) {  // 4*CC floats as CC 16-byte stores
-                    typedef float f32x4 __attribute__((ext_vector_type(4)));
-                    f32x4 v;
-#pragma unroll
-                    for (int e = 0; e < 4; ++e) v[e] = res[(4 * q + e) / CC][(4 * q + e) % CC];
-                    __builtin_nontemporal_store(v, reinterpret_cast<f32x4*>(o) + q);
+                        for (int k = 0; k < CC; ++k) {
+                            const int v = okv[j] ? (int)(vv[k] >> 24) : (int)L.border[k];
+                            o[k] = OUT == kOutF32 ? (float)v : normalize_u8v(cn[k], v);
+                        }
+                    }
                 }
             }
-        } else {
-            for (int p = 0; p < L.dst.w - x; ++p)
-#pragma unroll
-                for (int k = 0; k < CC; ++k) o[p * CC + k] = res[p][k];
         }
     }
 }
 
-// The staged kernel's LDS rectangle for this matrix (rows, 16-byte chunks per
-// row), or false when it does not apply: strided / misaligned planes, or a
-// rectangle over the LDS budget (strong down-scales).
-bool warp_tile_plan(const WarpLaunch& L, int& max_rows, int& max_chunks, int& dst_al) {
+// The staged kernel applies to u8 BORDER_CONSTANT warps whose tile rectangle
+// fits one LDS buffer (kStageIters * kBlock chunks); the bound is the corner
+// spans plus floor, the second tap and float slack.  dst_al: the lane quads'
+// 4*CC-byte stores are dword-aligned (else bytewise).
+bool warp_tile_plan(const WarpLaunch& L, int& dst_al) {
     if (L.src.esize != 1 || L.border_mode != kBorderConstant) return false;
     const int cc = L.src.cc;
-    // the lane's 4-pixel store needs its natural alignment; else byte stores
-    const int64_t out_align = L.out == kOutSame ? (cc == 3 ? 4 : 4 * cc) : 16;
-    dst_al = !(L.dst.row_pitch % out_align || L.dst.img_pitch % out_align || L.dst.plane_pitch % out_align ||
-               reinterpret_cast<uintptr_t>(L.dst.base) % out_align);
+    dst_al = !(L.dst.row_pitch % 4 || L.dst.img_pitch % 4 || L.dst.plane_pitch % 4 ||
+               reinterpret_cast<uintptr_t>(L.dst.base) % 4);
     for (int i = 0; i < 6; ++i)
         if (!std::isfinite(L.inv[i])) return false;
-    // corner-to-corner spans (+ floor, the second tap, float slack)
     const double bw = std::fabs(L.inv[0]) * (kTileW - 1) + std::fabs(L.inv[1]) * (kTileH - 1) + 4.0;
     const double bh = std::fabs(L.inv[3]) * (kTileW - 1) + std::fabs(L.inv[4]) * (kTileH - 1) + 4.0;
-    max_rows = (int)std::ceil(bh);
-    max_chunks = (int)std::ceil((15.0 + bw * cc) / 16.0);
-    return (size_t)max_rows * max_chunks * 16 <= kWarpTileLds;
+    const double chunks = std::ceil((15.0 + bw * cc) / 16.0) + 1.0;
+    return std::ceil(bh) * chunks <= kStageIters * kBlock;
+}
+
+template <typename K>
+int64_t warp_resident(K kernel, size_t lds) {
+    static std::mutex mu;
+    static std::map<std::pair<const void*, int>, int64_t> cache;  // (kernel, device) -> workgroups
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return 0;
+    std::lock_guard<std::mutex> lk(mu);
+    const auto key = std::make_pair(reinterpret_cast<const void*>(kernel), dev);
+    auto it = cache.find(key);
+    if (it != cache.end()) return it->second;
+    int per_cu = 0, cus = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, kBlock, lds) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+        return 0;
+    const int64_t r = (int64_t)std::max(per_cu, 1) * std::max(cus, 1);
+    cache.emplace(key, r);
+    return r;
+}
+
+template <int CC, int OUT, bool RA>
+hipError_t launch_tiles(const WarpLaunch& L, int dst_al, int4* rects, hipStream_t s) {
+    const int gx = (L.dst.w + kTileW - 1) / kTileW, gy = (L.dst.h + kTileH - 1) / kTileH;
+    const int64_t total = (int64_t)gx * gy * L.n * L.src.planes;
+    if (total >= 0x7FFFFFF0LL) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(warp_rect_kernel, dim3((gx * gy + 255) / 256), dim3(256), 0, s, L, gx, gy, rects);
+    const size_t lds = 2 * (size_t)kWarpBoxBytes + 16;  // + the last tap dword's overhang
+    auto kern = warp_tile_kernel<CC, OUT, RA>;
+    int64_t grid = warp_resident(kern, lds);
+    if (grid <= 0) grid = 256 * 4;
+    grid = std::min<int64_t>(grid, (total + 7) / 8 * 8);
+    grid = std::max<int64_t>(grid / 8 * 8, 8);
+    hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(kBlock), lds, s, L, gx, gy, (int)total, rects, dst_al);
+    return hipGetLastError();
 }
 
 // default: 8 or 10 lane blocks per wave for byte output, whichever pads the
@@ -681,19 +795,14 @@ hipError_t launch_px(const WarpLaunch& L, hipStream_t s) {
 
 template <int CC, typename TIn, int OUT>
 hipError_t launch_one(const WarpLaunch& L, hipStream_t s) {
-    int max_rows = 0, max_chunks = 0, dst_al = 0;
+    int dst_al = 0;
     const int knob = tune(VACV_TUNE_WARP_KERNEL);
     if constexpr (std::is_same<TIn, uint8_t>::value) {
-      if (knob == 3 && warp_tile_plan(L, max_rows, max_chunks, dst_al)) {
-        const int gx = (L.dst.w + kTileW - 1) / kTileW, gy = (L.dst.h + kTileH - 1) / kTileH;
-        const int64_t total = (int64_t)gx * gy * L.n * L.src.planes;
-        if (total >= 0x7FFFFFF0LL) return hipErrorInvalidValue;
-        const int64_t blocks = (total + 7) / 8 * 8;
-        const size_t lds = (size_t)max_rows * max_chunks * 16 + 16;  // + the last tap dword's overhang
-        hipLaunchKernelGGL((warp_tile_kernel<CC, OUT>), dim3((unsigned)blocks), dim3(kBlock), lds, s, L, gx, gy,
-                           (int)total, max_rows, max_chunks, dst_al);
-        return hipGetLastError();
-      }
+        if (knob == 3 && L.tile_rects && warp_tile_plan(L, dst_al)) {
+            int4* rects = static_cast<int4*>(L.tile_rects);
+            return L.src.row_pitch % 16 == 0 ? launch_tiles<CC, OUT, true>(L, dst_al, rects, s)
+                                             : launch_tiles<CC, OUT, false>(L, dst_al, rects, s);
+        }
     }
     switch (warp_blocks_per_wave(OUT == kOutSame && sizeof(TIn) == 1, L.dst.w)) {
         case 10: return launch_px<CC, TIn, OUT, 10>(L, s);
@@ -715,6 +824,11 @@ hipError_t launch_cc(const WarpLaunch& L, hipStream_t s) {
 }
 
 }  // namespace
+
+size_t warp_workspace_bytes(const WarpLaunch& L) {
+    const int gx = (L.dst.w + kTileW - 1) / kTileW, gy = (L.dst.h + kTileH - 1) / kTileH;
+    return (size_t)gx * gy * sizeof(int4);
+}
 
 hipError_t launch_warp(const WarpLaunch& L, hipStream_t s) {
     if (L.src.esize == 1) {

@@ -32,6 +32,7 @@ const char* const kNames[VACV_TUNE_COUNT] = {
     "VACV_RESIZE_WORK",        // VACV_TUNE_RESIZE_WORK
     "VACV_RESIZE_ROWS_BYTES",  // VACV_TUNE_RESIZE_ROWS_BYTES
     "VACV_WARP_KERNEL",        // VACV_TUNE_WARP_KERNEL
+    "VACV_RESIZE_STRIP",       // VACV_TUNE_RESIZE_STRIP
 };
 
 struct Table {

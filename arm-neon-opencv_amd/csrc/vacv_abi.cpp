@@ -321,6 +321,12 @@ int resize_impl(const vacv_image* src_d, const vacv_image* dst_d, int interpolat
     if (L.kind == kLinearFixed && L.src.cc <= 4 && dst.w < (1 << 23) && dst.h < (1 << 23) &&
         (direct == 2 || (direct == 1 && resize_one_tap_rows(L))))
         return hip_status(launch_resize_direct(L, s));
+    // the other u8 bilinear geometries (two weighted rows per output row):
+    // column strips with an LDS ring of source rows (k_resize_strip.hip;
+    // 1080p -> 1280x720: 0.59 vs 0.62 ms staged); VACV_TUNE_RESIZE_STRIP = 0
+    // selects the staged kernel below, 2 the strip kernel's 32-row batches
+    if (L.kind == kLinearFixed && tune_or(VACV_TUNE_RESIZE_STRIP, 1) >= 1 && resize_strip_applies(L))
+        return hip_status(launch_resize_strip(L, s));
     // u8 cubic (fused widen to fp32), c <= 3 interleaved: per-pixel gathers
     // (k_cubic_direct.hip); VACV_CUBIC_DIRECT=0 selects the staged kernel
     if (cubic_direct_applies(L)) return hip_status(launch_cubic_direct(L, s));
@@ -398,6 +404,11 @@ int warp_impl(const vacv_image* src_d, const vacv_image* dst_d, const float m[6]
     L.border_mode = border_mode;
     if (border_mode == VACV_BORDER_TRANSPARENT && dst.data == src.data) return VACV_ERR_INVALID_ARG;  // in place
     if (ns) L.norm = *ns;
+    if (src.dtype == VACV_INT8 && border_mode == VACV_BORDER_CONSTANT) {  // the LDS-staged kernel's tile table
+        void* ws = nullptr;
+        if ((st = workspace(s, warp_workspace_bytes(L), &ws, 2))) return st;
+        L.tile_rects = ws;
+    }
     return hip_status(launch_warp(L, s));
 }
 

@@ -201,6 +201,26 @@ __device__ __forceinline__ void warp_border_sample(const unsigned char* sp, int6
     }
 }
 
+// quad-pack a pixel's CC bytes (low bytes of `own`) with its quad neighbours'
+// into the quad's 4*CC output bytes: lane k < CC of the quad returns dword k
+template <int CC>
+__device__ __forceinline__ uint32_t quad_pack(uint32_t own, int k) {
+    if constexpr (CC == 4) {
+        return own;
+    } else if constexpr (CC == 3) {
+        const uint32_t nxt = (uint32_t)__builtin_amdgcn_mov_dpp((int)own, 0xF9, 0xF, 0xF, false);  // [1,2,3,3]
+        const uint32_t sel = k == 0 ? 0x04020100u : k == 1 ? 0x05040201u : 0x06050402u;
+        return __builtin_amdgcn_perm(nxt, own, sel);
+    } else if constexpr (CC == 2) {
+        const uint32_t a = (uint32_t)__builtin_amdgcn_mov_dpp((int)own, 0x08, 0xF, 0xF, false);  // [0,2,.,.]
+        const uint32_t b = (uint32_t)__builtin_amdgcn_mov_dpp((int)own, 0x0D, 0xF, 0xF, false);  // [1,3,.,.]
+        return (a & 0xFFFFu) | (b << 16);
+    } else {
+        const uint32_t t = own | ((uint32_t)__builtin_amdgcn_mov_dpp((int)own, 0xF9, 0xF, 0xF, false) << 8);
+        return (t & 0xFFFFu) | ((uint32_t)__builtin_amdgcn_mov_dpp((int)t, 0xFE, 0xF, 0xF, false) << 16);
+    }
+}
+
 template <typename T>
 __device__ __forceinline__ T wave_sum(T v) {
 #pragma unroll

@@ -121,6 +121,10 @@ hipError_t launch_resize(const ResizeLaunch& L, hipStream_t s);
 // resize_one_tap_rows: no output row of L has two weighted source rows.
 hipError_t launch_resize_direct(const ResizeLaunch& L, hipStream_t s);
 bool resize_one_tap_rows(const ResizeLaunch& L);
+// u8 bilinear as column strips walking down the image with an LDS ring of
+// source rows (k_resize_strip.hip): two-tap geometries
+bool resize_strip_applies(const ResizeLaunch& L);
+hipError_t launch_resize_strip(const ResizeLaunch& L, hipStream_t s);
 // INTER_NEAREST (OpenCV 2.4 resizeNN): scale_xd / scale_yd carry ifx / ify
 hipError_t launch_resize_nearest(const ResizeLaunch& L, hipStream_t s);
 // INTER_AREA at an integer scale (OpenCV 2.4 resizeAreaFast_): area_x/y, area_scale
@@ -143,7 +147,9 @@ struct WarpLaunch {
     int border_mode;             // kBorder* (vacv_semantics.hpp)
     int out;                     // OutKind
     NormSpec norm;
+    void* tile_rects;            // workspace of warp_workspace_bytes() for the LDS-staged kernel, or null
 };
+size_t warp_workspace_bytes(const WarpLaunch& L);
 hipError_t launch_warp(const WarpLaunch& L, hipStream_t s);
 
 struct CopyLaunch {                // crop / clone: row copies

@@ -71,12 +71,13 @@ SIZES = [((23, 37), 1), ((48, 64), 3), ((61, 97), 3), ((5, 7), 3), ((16, 16), 4)
 OUTS = [(20, 11), (33, 29), (111, 40), (7, 5), (2, 2), (160, 90), (1, 1), (300, 7)]
 
 
-@pytest.mark.parametrize("direct", [1, 2])
+@pytest.mark.parametrize("direct", [1, 2, 3])
 @pytest.mark.parametrize("mode", [0, 1, 2])
 def test_resize_linear_u8_hwc(ops, dev, oracle, mode, direct):
     # direct 1: the default dispatch (gather kernel for one-tap-row
-    # geometries, staged kernel otherwise); 2: the gather kernel everywhere
-    with ops.tuning(RESIZE_DIRECT=direct):
+    # geometries, staged kernel otherwise); 2: the gather kernel everywhere;
+    # 3: the column-strip kernel for two-tap geometries it applies to
+    with ops.tuning(RESIZE_DIRECT=min(direct, 2), RESIZE_STRIP=1 if direct == 3 else 0):
         _resize_linear_u8_hwc(ops, dev, oracle, mode)
 
 
@@ -428,6 +429,58 @@ def test_resize_u8_kernels_agree_and_pitched_out(ops, dev, oracle):
             rim = got.copy()
             rim[0, 4:4 + ho, 8:8 + wo] = 0
             assert not rim.any(), f"pitched out {wo}x{ho}: wrote outside the window"
+
+
+def test_resize_strip_kernel(ops, dev, oracle):
+    """Two-tap u8 bilinear on the column-strip kernel (k_resize_strip.hip,
+    VACV_TUNE_RESIZE_STRIP = 1; it needs a source row pitch that is a multiple
+    of 16): bit-exact against the oracle for every mode and channel count,
+    down- and up-scales, odd output widths (partial lane quads, byte stores);
+    at full size identical to the staged kernel for u8 / fp32 / normalised
+    output, NCHW planes and a pitched destination."""
+    import torch
+    from vacv_amd import NCHW
+    cases = [((48, 64), 3), ((16, 16), 4), ((144, 176), 3), ((61, 96), 1), ((40, 32), 2), ((97, 160), 3)]
+    for i, ((h, w), c) in enumerate(cases):
+        imgs = [synthetic_image(300 + 10 * i + k, h, w, c).reshape(h, w, c) for k in range(2)]
+        src = to_dev(np.stack(imgs), dev)
+        for wo, ho in OUTS + [(w * 2 // 3, h * 2 // 3), (w + 5, h * 3), (w - 3, h - 1)]:
+            for mode in (0, 1, 2):
+                wants = [oracle.resize_linear(imgs[k] if c > 1 else imgs[k][..., 0], wo, ho, mode=mode) for k in range(2)]
+                for sv in (1, 2):  # 16- and 32-row batches
+                    with ops.tuning(RESIZE_STRIP=sv):
+                        out = host(ops.resize(src, wo, ho, mode=mode))
+                    for k in range(2):
+                        assert_same(out[k].reshape(wants[k].shape), wants[k], f"strip{sv} {h}x{w}x{c}->{ho}x{wo} mode {mode}")
+    big = [synthetic_image(330 + k, 1080, 1920, 3) for k in range(2)]
+    src = to_dev(np.stack(big), dev)
+    chw = to_dev(np.ascontiguousarray(np.stack(big).transpose(0, 3, 1, 2)), dev)
+    for wo, ho in [(1280, 720), (1000, 999), (333, 129)]:
+        for mode in (0, 1, 2):
+            res = {}
+            for strip in (1, 2, 0):
+                with ops.tuning(RESIZE_STRIP=strip):
+                    res[strip] = (ops.resize(src, wo, ho, mode=mode),
+                                  ops.resize_normalize(src, wo, ho, MEAN, STD, mode=mode),
+                                  ops.resize(chw, wo, ho, mode=mode, layout=NCHW))
+            for sv in (1, 2):
+                for a, b in zip(res[sv], res[0]):
+                    assert torch.equal(a, b), f"strip{sv} vs staged {wo}x{ho} mode {mode}"
+    s1 = to_dev(big[0][None, :200, :320].copy(), dev)
+    for wo, ho, dt in [(211, 150, torch.uint8), (200, 151, torch.uint8), (150, 140, torch.float32)]:
+        buf = torch.zeros((1, ho + 9, wo + 23, 3), dtype=dt, device=dev)
+        view = buf[:, 4:4 + ho, 7:7 + wo]
+        with ops.tuning(RESIZE_STRIP=1):
+            if dt == torch.uint8:
+                ops.resize(s1, wo, ho, out=view)
+                want = oracle.resize_linear(big[0][:200, :320].copy(), wo, ho)
+            else:
+                ops.resize_normalize(s1, wo, ho, MEAN, STD, out=view)
+                want = oracle.normalize(oracle.u8_to_f32(oracle.resize_linear(big[0][:200, :320].copy(), wo, ho)), MEAN, STD)
+        got = host(buf)
+        assert_same(got[0, 4:4 + ho, 7:7 + wo], want, f"strip pitched out {wo}x{ho} {dt}")
+        got[0, 4:4 + ho, 7:7 + wo] = 0
+        assert not got.any(), f"strip pitched out {wo}x{ho}: wrote outside the window"
 
 
 def test_resize_normalize(ops, dev, oracle):
