@@ -9,14 +9,15 @@
 // Why.  A source row of a two-tap geometry feeds ~1.33 output rows; the staged
 // and gather kernels compute those output rows in different workgroups, often
 // on different XCDs, so the row is fetched into L2 more than once and every
-// workgroup pays its own latency.  Here a workgroup owns a 64-column output
+// workgroup pays its own latency.  Here a workgroup owns an SW-column output
 // strip of one plane and walks down its rows, keeping the source rows in an
 // LDS ring: every source byte of the strip leaves HBM once.
-//  * Batches of BR = 16 output rows (32: VACV_TUNE_RESIZE_STRIP = 2, measured
-//    slower); the source rows a batch adds to the ring are loaded with
+//  * The ring holds the source rows of two batches (slot = row mod ring).
+//  * Batches of BR output rows; the source rows a batch adds to the ring are
+//    loaded with
 //    coalesced 16-byte loads into registers while the previous batch is being
 //    blended (one barrier per batch).
-//  * Lane l takes output column ox0 + l: its horizontal taps and its byte
+//  * Lane l takes output columns ox0 + l + 64q: its horizontal taps and its byte
 //    offset in a ring row are computed once; a row's vertical taps are
 //    wave-uniform.  Per pixel: two (CC <= 2) or three dword LDS reads per tap
 //    row, v_alignbyte, the packed-u16 dot products of resize_direct_kernel.
@@ -32,16 +33,60 @@
 namespace vacv {
 namespace {
 
-constexpr int kStripW = 64;       // output columns per workgroup (one per lane)
-constexpr int kFetchIters = 4;    // 16-byte chunks per thread and batch
+constexpr int kFetchIters = 3;    // 16-byte chunks per thread and batch
 constexpr int kMaxLds = 64 * 1024;
 
-template <int CC, int OUT, int MODE, int BR>
-__global__ void __launch_bounds__(kBlock)
-resize_strip_kernel(ResizeLaunch L, int strips_x, int groups, int rows_per_group, int ring, int stride, int dst_al) {
+// one output pixel (lane-quad packed for u8) at row byte offset row_off
+template <int CC, int OUT>
+__device__ __forceinline__ void store_pixel(const int (&v)[CC], const ChanNorm (&cn)[CC], const Rsrc& drs, uint32_t row_off,
+                                            int ox, int qx, int W, bool quad_full, int lane) {
+    if constexpr (OUT == kOutSame) {
+        uint32_t own = 0;
+#pragma unroll
+        for (int k = 0; k < CC; ++k) own |= (uint32_t)v[k] << (8 * k);
+        const uint32_t word = quad_pack<CC>(own, lane & 3);
+        if (quad_full) {
+            if ((lane & 3) < CC)
+                __builtin_amdgcn_raw_buffer_store_b32(word, drs.r, (int)(row_off + (uint32_t)(qx * CC + 4 * (lane & 3))), 0,
+                                                      VACV_STORE_AUX);
+        } else if (ox < W) {
+#pragma unroll
+            for (int k = 0; k < CC; ++k)
+                __builtin_amdgcn_raw_buffer_store_b8((unsigned char)v[k], drs.r, (int)(row_off + (uint32_t)(ox * CC + k)), 0,
+                                                     VACV_STORE_AUX);
+        }
+    } else if (ox < W) {
+        uint32_t f[CC];
+#pragma unroll
+        for (int k = 0; k < CC; ++k)
+            f[k] = __builtin_bit_cast(uint32_t, OUT == kOutF32 ? (float)v[k] : normalize_u8v(cn[k], v[k]));
+        const int off = (int)(row_off + (uint32_t)(ox * CC * 4));
+        if constexpr (CC == 1) {
+            __builtin_amdgcn_raw_buffer_store_b32(f[0], drs.r, off, 0, VACV_STORE_AUX);
+        } else if constexpr (CC == 2) {
+            typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+            __builtin_amdgcn_raw_buffer_store_b64(u32x2{f[0], f[1]}, drs.r, off, 0, VACV_STORE_AUX);
+        } else if constexpr (CC == 3) {
+            typedef unsigned int u32x3 __attribute__((ext_vector_type(3)));
+            __builtin_amdgcn_raw_buffer_store_b96(u32x3{f[0], f[1], f[2]}, drs.r, off, 0, VACV_STORE_AUX);
+        } else {
+            __builtin_amdgcn_raw_buffer_store_b128(u32x4{f[0], f[1], f[2], f[3]}, drs.r, off, 0, VACV_STORE_AUX);
+        }
+    }
+}
+
+// SW output columns per workgroup (SW / 64 per lane), BR output rows per batch
+template <int CC, int OUT, int MODE, int SW, int BR>
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(OUT == kOutSame ? 8 : 6)))
+resize_strip_kernel(ResizeLaunch L, int strips_x, int groups, int rows_per_group, int ring, int stride, int dst_al,
+                    int total) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int id = blockIdx.x;
+    // XCD-contiguous order: neighbouring strips share the 128-byte lines at
+    // their edges; on one XCD those come from one L2
+    const int per_xcd = (total + 7) / 8;
+    const int id = (int)(blockIdx.x % 8) * per_xcd + (int)(blockIdx.x / 8);
+    if (id >= total) return;  // uniform
     const int per_plane = strips_x * groups;
     const int pidx = id / per_plane;
     const int rem = id - pidx * per_plane;
@@ -49,7 +94,8 @@ resize_strip_kernel(ResizeLaunch L, int strips_x, int groups, int rows_per_group
     const int img = pidx / L.src.planes, plane = pidx - img * L.src.planes;
     const int W = L.dst.w, H = L.dst.h;
     const int oy_begin = grp * rows_per_group, oy_end = min(oy_begin + rows_per_group, H);
-    const int ox0 = sxi * kStripW, ox = ox0 + lane;
+    constexpr int PXL = SW / 64;
+    const int ox0 = sxi * SW;
 
     const unsigned char* sp = L.src.base + (int64_t)img * L.src.img_pitch + (int64_t)plane * L.src.plane_pitch;
     const Rsrc srs = make_rsrc(sp, L.src.plane_bytes);
@@ -57,15 +103,22 @@ resize_strip_kernel(ResizeLaunch L, int strips_x, int groups, int rows_per_group
     const uint32_t rp = (uint32_t)L.src.row_pitch;  // % 16 == 0 (host)
 
     // ---- the strip's source columns and the lane's taps -----------------------
-    const FixedTap tx = tap_of<MODE>(min(ox, W - 1), L.src.w, W, L.scale_xf, L.scale_xd);
     const int xs0 = tap_of<MODE>(ox0, L.src.w, W, L.scale_xf, L.scale_xd).i;  // uniform
-    const int xs1 = tap_of<MODE>(min(ox0 + kStripW, W) - 1, L.src.w, W, L.scale_xf, L.scale_xd).i + 1;
+    const int xs1 = tap_of<MODE>(min(ox0 + SW, W) - 1, L.src.w, W, L.scale_xf, L.scale_xd).i + 1;
     const uint32_t col0 = (uint32_t)(xs0 * CC) + srs.delta;  // strip's first byte within a row (from base16)
     const uint32_t dxb = col0 & 15u;                          // ... within its chunk (every row: rp % 16 == 0)
     const int chunks = (int)((dxb + (uint32_t)(xs1 - xs0 + 1) * CC + 15u) >> 4);
-    const uint32_t lo = (uint32_t)((tx.i - xs0) * CC) + dxb;  // the lane's taps in a ring row
-    const uint32_t lo4 = lo & ~3u, sh = lo & 3u;
-    const us2 wx = __builtin_bit_cast(us2, (uint32_t)tx.w0 | ((uint32_t)tx.w1 << 16));
+    int oxv[PXL];
+    uint32_t lo4[PXL], sh[PXL], wxv[PXL];  // the lane's taps in a ring row, its horizontal weights
+#pragma unroll
+    for (int q = 0; q < PXL; ++q) {
+        oxv[q] = ox0 + 64 * q + lane;
+        const FixedTap tx = tap_of<MODE>(min(oxv[q], W - 1), L.src.w, W, L.scale_xf, L.scale_xd);
+        const uint32_t lo = (uint32_t)((tx.i - xs0) * CC) + dxb;
+        lo4[q] = lo & ~3u;
+        sh[q] = lo & 3u;
+        wxv[q] = (uint32_t)tx.w0 | ((uint32_t)tx.w1 << 16);
+    }
 
     ChanNorm cn[CC] = {};
     if (OUT == kOutNorm) {
@@ -75,23 +128,33 @@ resize_strip_kernel(ResizeLaunch L, int strips_x, int groups, int rows_per_group
     unsigned char* dp = const_cast<unsigned char*>(L.dst.base) + (int64_t)img * L.dst.img_pitch +
                         (int64_t)plane * L.dst.plane_pitch;
     const Rsrc drs = make_rsrc(dp, L.dst.plane_bytes);  // 32-bit store offsets
-    const int qx = ox0 + (lane & ~3);
-    const bool quad_full = qx + 4 <= W && dst_al;
     constexpr int kTD = (int)kTapDwords<CC, true>;
 
     // ---- ring fill: source rows (next_row .. hi] --------------------------------
-    uint4 pre[kFetchIters];
-    uint32_t dst_off[kFetchIters];
-    auto fetch = [&](int r_first, int r_last) {
-        const int n = max(r_last - r_first + 1, 0) * chunks;
+    // ring slot of source row r: r mod ring (exact: r < 2^16, ring < 2^8)
+    const uint32_t rmagic = (uint32_t)((0x100000000ull + (uint64_t)ring - 1) / (uint64_t)ring);
+    auto slot = [&](uint32_t r) { return r - (uint32_t)ring * __umulhi(r, rmagic); };
+    // chunk u*kBlock + tid of a fill is (row rcu[u] >> 16, chunk rcu[u] & 0xFFFF)
+    // of the rows being added, whatever the fill: the division happens once
+    uint32_t rcu[kFetchIters];
+    {
         const uint32_t magic = (uint32_t)((0x100000000ull + (uint64_t)chunks - 1) / (uint64_t)chunks);
 #pragma unroll
         for (int u = 0; u < kFetchIters; ++u) {
-            const int i = u * kBlock + tid;
+            const uint32_t i = (uint32_t)(u * kBlock + tid);
+            const uint32_t rr = chunks == 1 ? i : __umulhi(i, magic);  // i / chunks, exact (i < 2^12)
+            rcu[u] = (rr << 16) | (i - rr * (uint32_t)chunks);
+        }
+    }
+    uint4 pre[kFetchIters];
+    uint32_t dst_off[kFetchIters];
+    auto fetch = [&](int r_first, int r_last) {
+        const uint32_t nrows = (uint32_t)max(r_last - r_first + 1, 0);
+#pragma unroll
+        for (int u = 0; u < kFetchIters; ++u) {
+            const uint32_t rr = rcu[u] >> 16, c = rcu[u] & 0xFFFFu;
             dst_off[u] = 0xFFFFFFFFu;
-            if (i < n) {
-                const uint32_t rr = chunks == 1 ? (uint32_t)i : __umulhi((uint32_t)i, magic);  // i / chunks
-                const uint32_t c = (uint32_t)i - rr * (uint32_t)chunks;
+            if (rr < nrows) {
                 const uint32_t r = (uint32_t)r_first + rr;
                 const uint32_t o = ((r * rp + col0) & ~15u) + 16u * c;
                 if (o + 16u <= lim) {
@@ -104,7 +167,7 @@ resize_strip_kernel(ResizeLaunch L, int strips_x, int groups, int rows_per_group
                             d[e >> 2] |= (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(srs.r, (int)(o + e), 0, 0) << (8 * (e & 3));
                     pre[u] = make_uint4(d[0], d[1], d[2], d[3]);
                 }
-                dst_off[u] = (r & (uint32_t)(ring - 1)) * (uint32_t)stride + 16u * c;
+                dst_off[u] = slot(r) * (uint32_t)stride + 16u * c;
             }
         }
     };
@@ -134,86 +197,60 @@ resize_strip_kernel(ResizeLaunch L, int strips_x, int groups, int rows_per_group
             fetch(max(l1, loaded + 1), h1);
             loaded = max(loaded, h1);
         }
-        // ---- blend: wave w takes rows w, w + 4, ... of the batch, 4 at a time ---
+        // ---- blend: wave w takes rows w, w + 4, ... of the batch, 2 at a time ---
 #pragma unroll
-        for (int g = 0; g < BR / 16; ++g) {
-        uint32_t t0[4][3], t1[4][3];
-        uint32_t wyv[4];
+        for (int g = 0; g < BR / 8; ++g) {
+            uint32_t wyv[2], ra[2], rb[2];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const int oy = min(oy_begin + b * BR + 16 * g + wave + 4 * j, H - 1);
-            const FixedTap ty = tap_of<MODE>(oy, L.src.h, H, L.scale_yf, L.scale_yd);  // wave-uniform
-            wyv[j] = (uint32_t)ty.w0 | ((uint32_t)ty.w1 << 16);
-            const uint32_t ra = ((uint32_t)ty.i & (uint32_t)(ring - 1)) * (uint32_t)stride;
-            const uint32_t rb = ((uint32_t)(ty.i + 1) & (uint32_t)(ring - 1)) * (uint32_t)stride;
-            const uint32_t* pa = reinterpret_cast<const uint32_t*>(lds + ra + lo4);
-            const uint32_t* pb = reinterpret_cast<const uint32_t*>(lds + rb + lo4);
-#pragma unroll
-            for (int d = 0; d < kTD; ++d) { t0[j][d] = pa[d]; t1[j][d] = pb[d]; }
-        }
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const int oy = oy_begin + b * BR + 16 * g + wave + 4 * j;
-            const uint32_t a0 = __builtin_amdgcn_alignbyte(t0[j][1], t0[j][0], sh);
-            const uint32_t c0 = __builtin_amdgcn_alignbyte(t1[j][1], t1[j][0], sh);
-            uint32_t a1 = 0u, c1 = 0u;
-            if constexpr (kTD == 3) {
-                a1 = __builtin_amdgcn_alignbyte(t0[j][2], t0[j][1], sh);
-                c1 = __builtin_amdgcn_alignbyte(t1[j][2], t1[j][1], sh);
+            for (int j = 0; j < 2; ++j) {
+                const int oy = min(oy_begin + b * BR + 8 * g + wave + 4 * j, H - 1);
+                const FixedTap ty = tap_of<MODE>(oy, L.src.h, H, L.scale_yf, L.scale_yd);  // wave-uniform
+                wyv[j] = (uint32_t)ty.w0 | ((uint32_t)ty.w1 << 16);
+                ra[j] = slot((uint32_t)ty.i) * (uint32_t)stride;
+                rb[j] = slot((uint32_t)ty.i + 1u) * (uint32_t)stride;
             }
-            const uint32_t wA = wyv[j] & 0xFFFFu, wB = wyv[j] >> 16;
-            int v[CC];
 #pragma unroll
-            for (int k = 0; k < CC; ++k) {
-                const uint32_t sel = (uint32_t)k | (0x0Cu << 8) | ((uint32_t)(CC + k) << 16) | (0x0Cu << 24);
-                v[k] = blend_fixed<MODE>(__builtin_amdgcn_perm(a1, a0, sel), __builtin_amdgcn_perm(c1, c0, sel), wx, wA, wB);
-            }
-            if (oy >= oy_end) continue;  // wave-uniform
-            const uint32_t row_off = (uint32_t)oy * (uint32_t)L.dst.row_pitch + drs.delta;
-            if constexpr (OUT == kOutSame) {
-                uint32_t own = 0;
+            for (int q = 0; q < PXL; ++q) {
+                uint32_t t0[2][3], t1[2][3];
 #pragma unroll
-                for (int k = 0; k < CC; ++k) own |= (uint32_t)v[k] << (8 * k);
-                const uint32_t word = quad_pack<CC>(own, lane & 3);
-                if (quad_full) {
-                    if ((lane & 3) < CC)
-                        __builtin_amdgcn_raw_buffer_store_b32(word, drs.r, (int)(row_off + (uint32_t)(qx * CC + 4 * (lane & 3))),
-                                                              0, VACV_STORE_AUX);
-                } else if (ox < W) {
+                for (int j = 0; j < 2; ++j) {
+                    const uint32_t* pa = reinterpret_cast<const uint32_t*>(lds + ra[j] + lo4[q]);
+                    const uint32_t* pb = reinterpret_cast<const uint32_t*>(lds + rb[j] + lo4[q]);
 #pragma unroll
-                    for (int k = 0; k < CC; ++k)
-                        __builtin_amdgcn_raw_buffer_store_b8((unsigned char)v[k], drs.r, (int)(row_off + (uint32_t)(ox * CC + k)), 0,
-                                                             VACV_STORE_AUX);
+                    for (int d = 0; d < kTD; ++d) { t0[j][d] = pa[d]; t1[j][d] = pb[d]; }
                 }
-            } else if (ox < W) {
-                float f[CC];
+                const int ox = oxv[q];
+                const int qx = ox0 + 64 * q + (lane & ~3);
+                const bool quad_full = qx + 4 <= W && dst_al;
+                const us2 wx = __builtin_bit_cast(us2, wxv[q]);
 #pragma unroll
-                for (int k = 0; k < CC; ++k) f[k] = OUT == kOutF32 ? (float)v[k] : normalize_u8v(cn[k], v[k]);
-                const int off = (int)(row_off + (uint32_t)(ox * CC * 4));
-                if constexpr (CC == 1) {
-                    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, f[0]), drs.r, off, 0, VACV_STORE_AUX);
-                } else if constexpr (CC == 2) {
-                    typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
-                    __builtin_amdgcn_raw_buffer_store_b64(u32x2{__builtin_bit_cast(uint32_t, f[0]), __builtin_bit_cast(uint32_t, f[1])},
-                                                          drs.r, off, 0, VACV_STORE_AUX);
-                } else if constexpr (CC == 3) {
-                    typedef unsigned int u32x3 __attribute__((ext_vector_type(3)));
-                    __builtin_amdgcn_raw_buffer_store_b96(u32x3{__builtin_bit_cast(uint32_t, f[0]), __builtin_bit_cast(uint32_t, f[1]),
-                                                                __builtin_bit_cast(uint32_t, f[2])},
-                                                          drs.r, off, 0, VACV_STORE_AUX);
-                } else {
-                    __builtin_amdgcn_raw_buffer_store_b128(u32x4{__builtin_bit_cast(uint32_t, f[0]), __builtin_bit_cast(uint32_t, f[1]),
-                                                                 __builtin_bit_cast(uint32_t, f[2]), __builtin_bit_cast(uint32_t, f[3])},
-                                                           drs.r, off, 0, VACV_STORE_AUX);
+                for (int j = 0; j < 2; ++j) {
+                    const int oy = oy_begin + b * BR + 8 * g + wave + 4 * j;
+                    const uint32_t a0 = __builtin_amdgcn_alignbyte(t0[j][1], t0[j][0], sh[q]);
+                    const uint32_t c0 = __builtin_amdgcn_alignbyte(t1[j][1], t1[j][0], sh[q]);
+                    uint32_t a1 = 0u, c1 = 0u;
+                    if constexpr (kTD == 3) {
+                        a1 = __builtin_amdgcn_alignbyte(t0[j][2], t0[j][1], sh[q]);
+                        c1 = __builtin_amdgcn_alignbyte(t1[j][2], t1[j][1], sh[q]);
+                    }
+                    const uint32_t wA = wyv[j] & 0xFFFFu, wB = wyv[j] >> 16;
+                    int v[CC];
+#pragma unroll
+                    for (int k = 0; k < CC; ++k) {
+                        const uint32_t sel = (uint32_t)k | (0x0Cu << 8) | ((uint32_t)(CC + k) << 16) | (0x0Cu << 24);
+                        v[k] = blend_fixed<MODE>(__builtin_amdgcn_perm(a1, a0, sel), __builtin_amdgcn_perm(c1, c0, sel), wx, wA, wB);
+                    }
+                    if (oy >= oy_end) continue;  // wave-uniform
+                    const uint32_t row_off = (uint32_t)oy * (uint32_t)L.dst.row_pitch + drs.delta;
+                    store_pixel<CC, OUT>(v, cn, drs, row_off, ox, qx, W, quad_full, lane);
                 }
             }
-        }
         }
     }
 }
 
 struct StripPlan {
-    int strips_x, groups, rows_per_group, ring, stride, lds, br;
+    int strips_x, groups, rows_per_group, ring, stride, lds, sw, br;
 };
 
 // The ring (a power of two holding two batches' source rows) and the row
@@ -225,18 +262,21 @@ bool strip_plan(const ResizeLaunch& L, StripPlan& p) {
     if (L.dst.w >= (1 << 23) || L.dst.h >= (1 << 23)) return false;
     const int cc = L.src.cc;
     const double sx = L.scale_xd, sy = L.scale_yd;
-    const int span = (int)std::ceil((kStripW - 1) * sx) + 3;  // source columns of a strip, + taps and slack
+    // 1: 64-column strips, 16-row batches; 2: 128 columns, 8 rows (measured: RESIZE_STRIP sweep)
+    const bool wide = tune_or(VACV_TUNE_RESIZE_STRIP, 1) == 2;
+    p.sw = wide ? 128 : 64;
+    p.br = wide ? 8 : 16;
+    const int span = (int)std::ceil((p.sw - 1) * sx) + 3;  // source columns of a strip, + taps and slack
     const int chunks = (15 + span * cc + 15) / 16;
-    p.br = tune_or(VACV_TUNE_RESIZE_STRIP, 1) == 2 ? 32 : 16;
     const int batch_rows = (int)std::ceil(p.br * sy) + 3;  // source rows one batch can add
     if ((int64_t)batch_rows * chunks > (int64_t)kFetchIters * kBlock) return false;
-    int ring = 1;
-    while (ring < 2 * batch_rows + 2) ring <<= 1;
+    const int ring = 2 * batch_rows + 2;  // rows of two batches (any size: the slot is r mod ring)
+    if (ring >= 256 || L.src.h >= (1 << 16)) return false;
     p.stride = chunks * 16;
     p.ring = ring;
     p.lds = ring * p.stride + 16;  // + the last tap dword's overhang
     if (p.lds > kMaxLds) return false;
-    p.strips_x = (L.dst.w + kStripW - 1) / kStripW;
+    p.strips_x = (L.dst.w + p.sw - 1) / p.sw;
     // enough workgroups for the chip: split the rows when the strips are few
     const int64_t strips = (int64_t)p.strips_x * L.n * L.src.planes;
     p.groups = 1;
@@ -247,16 +287,17 @@ bool strip_plan(const ResizeLaunch& L, StripPlan& p) {
 
 template <int CC, int OUT, int MODE>
 hipError_t launch_one(const ResizeLaunch& L, const StripPlan& p, hipStream_t s) {
-    const int64_t blocks = (int64_t)p.strips_x * p.groups * L.n * L.src.planes;
+    const int64_t total = (int64_t)p.strips_x * p.groups * L.n * L.src.planes;
+    const int64_t blocks = (total + 7) / 8 * 8;
     const int64_t out_align = OUT == kOutSame ? 4 : 4;
     const int dst_al = !(L.dst.row_pitch % out_align || L.dst.img_pitch % out_align || L.dst.plane_pitch % out_align ||
                          reinterpret_cast<uintptr_t>(L.dst.base) % out_align);
-    if (p.br == 32)
-        hipLaunchKernelGGL((resize_strip_kernel<CC, OUT, MODE, 32>), dim3((unsigned)blocks), dim3(kBlock), p.lds, s, L,
-                           p.strips_x, p.groups, p.rows_per_group, p.ring, p.stride, dst_al);
+    if (p.sw == 128)
+        hipLaunchKernelGGL((resize_strip_kernel<CC, OUT, MODE, 128, 8>), dim3((unsigned)blocks), dim3(kBlock), p.lds, s, L,
+                           p.strips_x, p.groups, p.rows_per_group, p.ring, p.stride, dst_al, (int)total);
     else
-        hipLaunchKernelGGL((resize_strip_kernel<CC, OUT, MODE, 16>), dim3((unsigned)blocks), dim3(kBlock), p.lds, s, L,
-                           p.strips_x, p.groups, p.rows_per_group, p.ring, p.stride, dst_al);
+        hipLaunchKernelGGL((resize_strip_kernel<CC, OUT, MODE, 64, 16>), dim3((unsigned)blocks), dim3(kBlock), p.lds, s, L,
+                           p.strips_x, p.groups, p.rows_per_group, p.ring, p.stride, dst_al, (int)total);
     return hipGetLastError();
 }
 

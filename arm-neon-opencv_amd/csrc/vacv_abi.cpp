@@ -323,8 +323,8 @@ int resize_impl(const vacv_image* src_d, const vacv_image* dst_d, int interpolat
         return hip_status(launch_resize_direct(L, s));
     // the other u8 bilinear geometries (two weighted rows per output row):
     // column strips with an LDS ring of source rows (k_resize_strip.hip;
-    // 1080p -> 1280x720: 0.59 vs 0.62 ms staged); VACV_TUNE_RESIZE_STRIP = 0
-    // selects the staged kernel below, 2 the strip kernel's 32-row batches
+    // 1080p -> 1280x720: 0.565 vs 0.62 ms staged); VACV_TUNE_RESIZE_STRIP = 0
+    // selects the staged kernel below, 2 the strip kernel's 128-column strips
     if (L.kind == kLinearFixed && tune_or(VACV_TUNE_RESIZE_STRIP, 1) >= 1 && resize_strip_applies(L))
         return hip_status(launch_resize_strip(L, s));
     // u8 cubic (fused widen to fp32), c <= 3 interleaved: per-pixel gathers

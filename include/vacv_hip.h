@@ -291,7 +291,7 @@ enum {
     VACV_TUNE_RESIZE_WORK = 13,      /* staged kernel planner: work per thread */
     VACV_TUNE_RESIZE_ROWS_BYTES = 14,/* whole-row kernel planner: output bytes per workgroup */
     VACV_TUNE_WARP_KERNEL = 15,      /* u8 CONSTANT warp: 0 per-pixel gathers, 2 batched gathers, 3 LDS-staged tiles */
-    VACV_TUNE_RESIZE_STRIP = 16,     /* two-tap u8 bilinear: 1 / 2 column strips with an LDS row ring (16 / 32-row batches), 0 staged kernel */
+    VACV_TUNE_RESIZE_STRIP = 16,     /* two-tap u8 bilinear: column strips with an LDS row ring, 1: 64 columns x 16-row batches, 2: 128 x 8; 0 staged kernel */
     VACV_TUNE_COUNT = 17
 };
 /* value < 0 restores the built-in choice.  Returns VACV_OK or INVALID_ARG. */

@@ -447,7 +447,7 @@ def test_resize_strip_kernel(ops, dev, oracle):
         for wo, ho in OUTS + [(w * 2 // 3, h * 2 // 3), (w + 5, h * 3), (w - 3, h - 1)]:
             for mode in (0, 1, 2):
                 wants = [oracle.resize_linear(imgs[k] if c > 1 else imgs[k][..., 0], wo, ho, mode=mode) for k in range(2)]
-                for sv in (1, 2):  # 16- and 32-row batches
+                for sv in (1, 2):  # 64- and 128-column strips
                     with ops.tuning(RESIZE_STRIP=sv):
                         out = host(ops.resize(src, wo, ho, mode=mode))
                     for k in range(2):

@@ -21,7 +21,6 @@
         }                                                                                  \
     } while (0)
 
-constexpr int kPitch = 3840;  // 1280 x 3 bytes
 constexpr int kIters = 256;
 constexpr int kUnroll = 8;
 
@@ -30,47 +29,49 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* p, uint32_t b
 }
 
 template <int W>
-__global__ __launch_bounds__(256) void gpat(const unsigned char* buf, uint32_t ws, int R, int step, unsigned* sink) {
+__global__ __launch_bounds__(256) void gpat(const unsigned char* buf, uint32_t ws, int R, int step, int pitch, unsigned* sink) {
     const auto r = rsrc(buf, ws + 64);
     const int lane = threadIdx.x & 63;
     const int wave = (int)blockIdx.x * 4 + (threadIdx.x >> 6);
     const int per = 64 / R;
-    const uint32_t lo = (uint32_t)((lane / per) * kPitch + (lane % per) * step) & ~3u;
-    // each wave starts somewhere else in the working set and walks it
-    const uint32_t span = ws - (uint32_t)(R * kPitch + per * step + 16);
-    uint32_t base = ((uint32_t)wave * 40961u * 4u) % span;
+    // per-lane offset fixed; the wave's base moves in the scalar soffset, so
+    // the loop costs no vector ALU per load
+    const uint32_t lo = (uint32_t)((lane / per) * pitch + (lane % per) * step) & ~3u;
+    const uint32_t span = (ws - (uint32_t)(R * pitch + per * step + 16) - 8u * 1556u) & ~1023u;  // multiple of 1 KiB
+    uint32_t base = __builtin_amdgcn_readfirstlane(((uint32_t)wave * 40960u) % span);
     unsigned acc = 0;
     for (int it = 0; it < kIters; it += kUnroll) {
 #pragma unroll
         for (int u = 0; u < kUnroll; ++u) {
-            const uint32_t o = ((base + (uint32_t)u * 389u * 4u) % span & ~3u) + lo;
+            const uint32_t so = base + (uint32_t)u * 1556u;  // < span + 8 * 1556
             if constexpr (W == 1) {
-                acc ^= (unsigned)__builtin_amdgcn_raw_buffer_load_b32(r, (int)o, 0, 0);
+                acc ^= (unsigned)__builtin_amdgcn_raw_buffer_load_b32(r, (int)lo, (int)so, 0);
             } else if constexpr (W == 2) {
-                const auto v = __builtin_amdgcn_raw_buffer_load_b64(r, (int)o, 0, 0);
+                const auto v = __builtin_amdgcn_raw_buffer_load_b64(r, (int)lo, (int)so, 0);
                 acc ^= v[0] ^ v[1];
             } else if constexpr (W == 3) {
-                const auto v = __builtin_amdgcn_raw_buffer_load_b96(r, (int)o, 0, 0);
+                const auto v = __builtin_amdgcn_raw_buffer_load_b96(r, (int)lo, (int)so, 0);
                 acc ^= v[0] ^ v[1] ^ v[2];
             } else {
-                const auto v = __builtin_amdgcn_raw_buffer_load_b128(r, (int)o, 0, 0);
+                const auto v = __builtin_amdgcn_raw_buffer_load_b128(r, (int)lo, (int)so, 0);
                 acc ^= v[0] ^ v[1] ^ v[2] ^ v[3];
             }
         }
-        base = (base + 8u * 389u * 4u) % span;
+        base += 8u * 1556u;
+        base = base >= span ? base - span : base;
     }
     if (acc == 0x9E3779B9u) sink[wave] = acc;
 }
 
 template <int W>
-double run(const unsigned char* buf, uint32_t ws, int R, int step, unsigned* sink, int blocks) {
+double run(const unsigned char* buf, uint32_t ws, int R, int step, int pitch, unsigned* sink, int blocks) {
     hipEvent_t a, b;
     CHECK(hipEventCreate(&a));
     CHECK(hipEventCreate(&b));
-    hipLaunchKernelGGL(gpat<W>, dim3(blocks), dim3(256), 0, 0, buf, ws, R, step, sink);
+    hipLaunchKernelGGL(gpat<W>, dim3(blocks), dim3(256), 0, 0, buf, ws, R, step, pitch, sink);
     CHECK(hipEventRecord(a));
     constexpr int kReps = 5;
-    for (int i = 0; i < kReps; ++i) hipLaunchKernelGGL(gpat<W>, dim3(blocks), dim3(256), 0, 0, buf, ws, R, step, sink);
+    for (int i = 0; i < kReps; ++i) hipLaunchKernelGGL(gpat<W>, dim3(blocks), dim3(256), 0, 0, buf, ws, R, step, pitch, sink);
     CHECK(hipEventRecord(b));
     CHECK(hipEventSynchronize(b));
     float ms = 0;
@@ -89,18 +90,22 @@ int main(int argc, char** argv) {
     CHECK(hipMalloc(&buf, big + 4096));
     CHECK(hipMemset(buf, 7, big + 4096));
     CHECK(hipMalloc(&sink, blocks * 4 * sizeof(unsigned)));
-    const uint32_t wss[] = {24u << 10, 2u << 20};
+    // (working set, row pitch): L1-resident rows 256 B apart; L2-resident 1280x3 rows
+    const uint32_t wss[] = {32u << 10, 2u << 20};
+    const int pitches[] = {256, 3840};
     const int Rs[] = {1, 2, 4, 8, 16, 32, 64};
-    for (uint32_t ws : wss) {
-        for (int step : {6, 8}) {
+    for (int wi = 0; wi < 2; ++wi) {
+        const uint32_t ws = wss[wi];
+        const int pitch = pitches[wi];
+        for (int step : {3, 6, 12}) {
             for (int R : Rs) {
-                const double c1 = run<1>(buf, ws, R, step, sink, blocks);
-                const double c2 = run<2>(buf, ws, R, step, sink, blocks);
-                const double c3 = run<3>(buf, ws, R, step, sink, blocks);
-                const double c4 = run<4>(buf, ws, R, step, sink, blocks);
-                std::printf("{\"ws_bytes\": %u, \"step\": %d, \"rows\": %d, \"cyc_b32\": %.2f, \"cyc_b64\": %.2f, "
+                const double c1 = run<1>(buf, ws, R, step, pitch, sink, blocks);
+                const double c2 = run<2>(buf, ws, R, step, pitch, sink, blocks);
+                const double c3 = run<3>(buf, ws, R, step, pitch, sink, blocks);
+                const double c4 = run<4>(buf, ws, R, step, pitch, sink, blocks);
+                std::printf("{\"ws_bytes\": %u, \"pitch\": %d, \"step\": %d, \"rows\": %d, \"cyc_b32\": %.2f, \"cyc_b64\": %.2f, "
                             "\"cyc_b96\": %.2f, \"cyc_b128\": %.2f}\n",
-                            ws, step, R, c1, c2, c3, c4);
+                            ws, pitch, step, R, c1, c2, c3, c4);
                 std::fflush(stdout);
             }
         }
