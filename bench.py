@@ -448,7 +448,8 @@ def main():
 
     out = None
     if rank == 0:
-        cpu = None if args.no_cpu_baseline else cpu_baseline(args.cpu_seconds, args.workload)
+        # the host-CPU leg runs at N = 1 only (the multi-GPU lines time the GPUs)
+        cpu = None if (args.no_cpu_baseline or world > 1) else cpu_baseline(args.cpu_seconds, args.workload)
         out = {
             "metric": "Mpixels/sec per op (resize/warp/normalize) at 1080p; achieved HBM GB/s vs peak",
             "value": round(value, 2),
