@@ -702,6 +702,113 @@ __global__ void __launch_bounds__(kBlock) nearest_row_kernel(ResizeLaunch L) {
     }
 }
 
+// INTER_NEAREST, one output row per WAVE (four per workgroup, no barrier):
+// the wave stages its source row sy in its own LDS slice with 16-byte loads,
+// then each lane takes 4 consecutive output pixels -- the index arithmetic of
+// nearest_row_kernel, CC a compile-time constant -- and writes them with one
+// 4*CC-element store (u8: dwords; fp32: 16-byte stores).  nearest_row_kernel
+// stored one element per lane per instruction (byte stores for u8).
+template <typename TIn, int OUT, int CC>
+__global__ void __launch_bounds__(kBlock) nearest_wave_kernel(ResizeLaunch L, int row_slice) {
+    using TOut = typename std::conditional<(OUT == kOutSame), TIn, float>::type;
+    extern __shared__ uint4 row_lds[];
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int y = blockIdx.x * 4 + wave;
+    if (y >= L.dst.h) return;  // whole wave; no workgroup barrier below
+    const int pidx = blockIdx.y;
+    const int img = pidx / L.src.planes;
+    const int plane = pidx - img * L.src.planes;
+    const int sy = min((int)floor((double)y * L.scale_yd), L.src.h - 1);
+    const unsigned char* sp = L.src.base + (int64_t)img * L.src.img_pitch + (int64_t)plane * L.src.plane_pitch +
+                              (int64_t)sy * L.src.row_pitch;
+    const int row_bytes = L.src.w * CC * (int)sizeof(TIn);
+    uint4* slice = row_lds + wave * (row_slice >> 4);
+    const int n16 = row_bytes >> 4;
+    for (int i = lane; i < n16; i += 64) {
+        const u32x4 t = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(sp) + i);
+        slice[i] = make_uint4(t[0], t[1], t[2], t[3]);
+    }
+    unsigned char* lb = reinterpret_cast<unsigned char*>(slice);
+    for (int i = (n16 << 4) + lane; i < row_bytes; i += 64) lb[i] = sp[i];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const TIn* row = reinterpret_cast<const TIn*>(lb);
+
+    ChanNorm cn[CC] = {};
+    if (OUT == kOutNorm) {
+#pragma unroll
+        for (int k = 0; k < CC; ++k) cn[k] = chan_norm(L.norm, img, CC == 1 ? plane % L.norm.c_total : k);
+    }
+    unsigned char* dp = const_cast<unsigned char*>(L.dst.base) + (int64_t)img * L.dst.img_pitch +
+                        (int64_t)plane * L.dst.plane_pitch + (int64_t)y * L.dst.row_pitch;
+    // vector stores need the output row aligned to the store width
+    constexpr int kStore = OUT == kOutSame ? (int)sizeof(TIn) * 4 * CC : 16;
+    const bool vec = (reinterpret_cast<uintptr_t>(dp) & ((OUT == kOutSame && sizeof(TIn) == 1) ? 3 : 15)) == 0;
+    for (int x0 = 4 * lane; x0 < L.dst.w; x0 += 256) {
+        TOut v[4 * CC];
+#pragma unroll
+        for (int p = 0; p < 4; ++p) {
+            const int x = min(x0 + p, L.dst.w - 1);
+            const int sx = min((int)floor((double)x * L.scale_xd), L.src.w - 1);
+#pragma unroll
+            for (int k = 0; k < CC; ++k) {
+                const TIn t = row[sx * CC + k];
+                if (OUT == kOutSame) v[p * CC + k] = (TOut)t;
+                else if (OUT == kOutF32) v[p * CC + k] = (TOut)(float)t;
+                else v[p * CC + k] = (TOut)(std::is_same<TIn, uint8_t>::value ? normalize_u8v(cn[k], (int)t)
+                                                                              : normalize_f(cn[k], (float)t));
+            }
+        }
+        TOut* o = reinterpret_cast<TOut*>(dp) + (int64_t)x0 * CC;
+        if (vec && x0 + 4 <= L.dst.w) {
+            if constexpr (OUT == kOutSame && sizeof(TIn) == 1) {
+#pragma unroll
+                for (int d = 0; d < CC; ++d) {
+                    const uint32_t w = (uint32_t)v[4 * d] | ((uint32_t)v[4 * d + 1] << 8) | ((uint32_t)v[4 * d + 2] << 16) |
+                                       ((uint32_t)v[4 * d + 3] << 24);
+                    __builtin_nontemporal_store(w, reinterpret_cast<uint32_t*>(o) + d);
+                }
+            } else {
+#pragma unroll
+                for (int q = 0; q < CC; ++q) {
+                    u32x4 w;
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) w[e] = __builtin_bit_cast(uint32_t, v[4 * q + e]);
+                    __builtin_nontemporal_store(w, reinterpret_cast<u32x4*>(o) + q);
+                }
+            }
+        } else {
+            for (int p = 0; p < 4 && x0 + p < L.dst.w; ++p)
+#pragma unroll
+                for (int k = 0; k < CC; ++k) o[p * CC + k] = v[p * CC + k];
+        }
+    }
+    (void)kStore;
+}
+
+template <typename TIn, int OUT>
+hipError_t launch_nearest_wave_cc(const ResizeLaunch& L, hipStream_t s) {
+    const int row_slice = (int)(((size_t)L.src.w * L.src.cc * sizeof(TIn) + 15) & ~(size_t)15);
+    const dim3 grid((L.dst.h + 3) / 4, L.n * L.src.planes);
+    const size_t lds = 4 * (size_t)row_slice;
+    switch (L.src.cc) {
+        case 1: hipLaunchKernelGGL((nearest_wave_kernel<TIn, OUT, 1>), grid, dim3(kBlock), lds, s, L, row_slice); break;
+        case 2: hipLaunchKernelGGL((nearest_wave_kernel<TIn, OUT, 2>), grid, dim3(kBlock), lds, s, L, row_slice); break;
+        case 3: hipLaunchKernelGGL((nearest_wave_kernel<TIn, OUT, 3>), grid, dim3(kBlock), lds, s, L, row_slice); break;
+        case 4: hipLaunchKernelGGL((nearest_wave_kernel<TIn, OUT, 4>), grid, dim3(kBlock), lds, s, L, row_slice); break;
+        default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+template <typename TIn>
+hipError_t launch_nearest_wave_t(const ResizeLaunch& L, hipStream_t s) {
+    if (L.out == kOutSame) return launch_nearest_wave_cc<TIn, kOutSame>(L, s);
+    if (L.out == kOutF32) return launch_nearest_wave_cc<TIn, kOutF32>(L, s);
+    return launch_nearest_wave_cc<TIn, kOutNorm>(L, s);
+}
+
 template <typename TIn>
 hipError_t launch_nearest_row_t(const ResizeLaunch& L, hipStream_t s) {
     const dim3 grid(L.dst.h, L.n * L.src.planes);
@@ -902,7 +1009,10 @@ hipError_t launch_resize_nearest(const ResizeLaunch& L, hipStream_t s) {
     // at most a cache line apart, so it moves no more lines than the gathers
     // (a 4096-px fp32 row sampled 32 times would read 64 KiB for 32 pixels)
     const bool dense_samples = L.scale_xd * L.src.cc * L.src.esize <= 128.0;
-    if ((bits & 15) == 0 && row_bytes <= kNearestRowBytes && dense_samples && tune(VACV_TUNE_NEAREST_KERNEL) != 0)
+    const int knob = tune(VACV_TUNE_NEAREST_KERNEL);  // 0 per-pixel, 1 row per workgroup, else row per wave
+    if ((bits & 15) == 0 && row_bytes <= kNearestRowBytes / 4 && dense_samples && L.src.cc <= 4 && knob != 0 && knob != 1)
+        return L.src.esize == 1 ? launch_nearest_wave_t<uint8_t>(L, s) : launch_nearest_wave_t<float>(L, s);
+    if ((bits & 15) == 0 && row_bytes <= kNearestRowBytes && dense_samples && knob != 0)
         return L.src.esize == 1 ? launch_nearest_row_t<uint8_t>(L, s) : launch_nearest_row_t<float>(L, s);
     return L.src.esize == 1 ? launch_nearest_t<uint8_t>(L, s) : launch_nearest_t<float>(L, s);
 }

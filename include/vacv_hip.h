@@ -281,7 +281,7 @@ enum {
     VACV_TUNE_RESIZE_ROWS = 3,       /* 1: the whole-row staged kernel */
     VACV_TUNE_DIRECT_XCD = 4,        /* gather kernel block order: 0 plain, 1 XCD-contiguous */
     VACV_TUNE_WARP_PX = 5,           /* warp gather kernel: lane blocks per wave (4, 5, 8, 10) */
-    VACV_TUNE_NEAREST_KERNEL = 6,    /* INTER_NEAREST: 0 per-pixel kernel, else row-staged when it applies */
+    VACV_TUNE_NEAREST_KERNEL = 6,    /* INTER_NEAREST: 0 per-pixel kernel, 1 row per workgroup, else row per wave (when they apply) */
     VACV_TUNE_AREA_KERNEL = 7,       /* u8 INTER_AREA: 1 per-pixel kernel, 2 dword column sums */
     VACV_TUNE_AREA_ROWS = 8,         /* u8 INTER_AREA column sums: output rows per workgroup */
     VACV_TUNE_COLOR_CHUNKS = 9,      /* 1: the chunked fp32 NV21 kernel */

@@ -229,9 +229,10 @@ def test_resize_nearest(ops, dev, oracle):
 
 def test_nearest_area_kernel_variants_agree(ops, dev, oracle):
     """Every INTER_NEAREST / u8 INTER_AREA kernel variant gives the same bytes
-    at BASELINE's 1080p frame: nearest row-staged (default where the source is
-    16-byte aligned, its row fits 64 KiB and the sample stride is short) vs
-    the per-pixel kernel (VACV_TUNE_NEAREST_KERNEL = 0); area 16-byte column
+    at BASELINE's 1080p frame: nearest row-staged per wave (default where the
+    source is 16-byte aligned, its row fits 16 KiB and the sample stride is
+    short) vs row-staged per workgroup (VACV_TUNE_NEAREST_KERNEL = 1) vs the
+    per-pixel kernel (0); area 16-byte column
     sums (default) vs dword column sums (2) vs per-pixel (1); plus an fp32 row
     past 64 KiB (5600 px x 3 ch: the per-pixel fallback) and a strong
     horizontal downscale (wide stride: the per-pixel kernel) vs the oracle."""
@@ -241,14 +242,16 @@ def test_nearest_area_kernel_variants_agree(ops, dev, oracle):
     src = to_dev(imgs, dev)
     for wo, ho in [(640, 360), (960, 540), (1280, 720), (3000, 1500)]:
         a = ops.resize(src, wo, ho, interpolation=INTER_NEAREST)
-        with ops.tuning(NEAREST_KERNEL=0):
-            b = ops.resize(src, wo, ho, interpolation=INTER_NEAREST)
-        assert torch.equal(a, b), f"nearest variants differ -> {wo}x{ho}"
+        for knob in (1, 0):  # row per workgroup, per-pixel (default: row per wave)
+            with ops.tuning(NEAREST_KERNEL=knob):
+                b = ops.resize(src, wo, ho, interpolation=INTER_NEAREST)
+            assert torch.equal(a, b), f"nearest variant {knob} differs -> {wo}x{ho}"
         if wo <= 1920:
             an = ops.resize_normalize(src, wo, ho, MEAN, STD, interpolation=INTER_NEAREST)
-            with ops.tuning(NEAREST_KERNEL=0):
-                bn = ops.resize_normalize(src, wo, ho, MEAN, STD, interpolation=INTER_NEAREST)
-            assert torch.equal(an, bn), f"nearest normalize variants differ -> {wo}x{ho}"
+            for knob in (1, 0):
+                with ops.tuning(NEAREST_KERNEL=knob):
+                    bn = ops.resize_normalize(src, wo, ho, MEAN, STD, interpolation=INTER_NEAREST)
+                assert torch.equal(an, bn), f"nearest normalize variant {knob} differs -> {wo}x{ho}"
     assert_same(host(a)[1], oracle.resize_nearest(imgs[1], 3000, 1500), "nearest upscale")
     for wo, ho in [(640, 360), (960, 540), (480, 270)]:
         a = ops.resize(src, wo, ho, interpolation=INTER_AREA)
