@@ -891,14 +891,20 @@ __global__ void __launch_bounds__(kBlock) area_fast_kernel(ResizeLaunch L) {
 // column sums, rounds and stores (adjacent bytes per lane).  Needs a dword
 // aligned source (checked on the host); bit-identical to area_fast_kernel.
 constexpr int kAreaSeg = 4096;  // source bytes per segment row (16 KiB of LDS sums)
+// u8 INTER_AREA at integer scales: column sums.  A workgroup takes R = 2
+// output rows of one segment (tw output pixels): every thread issues the
+// loads of its 16-byte (VB) column chunk for all R * ay source rows first --
+// twice the bytes in flight of one row at a time, which is what bounded the
+// one-row version (measured 0.42 / 0.55 ms at 3x3 / 2x2) -- sums them per
+// output row into u16 column sums in LDS (<= 255 * ay), then one thread per
+// output element adds its ax column sums.  Integer sums do not depend on
+// their order, so the result is resizeAreaFast_'s.
 template <int OUT, int VB, int CC>  // VB: source bytes per thread per row (4 or 16); CC: channels (1..4)
 __global__ void __launch_bounds__(kBlock) area_u8_colsum_kernel(ResizeLaunch L, int tw, int rows) {
     using TOut = typename std::conditional<(OUT == kOutSame), uint8_t, float>::type;
     using TV = typename std::conditional<(VB == 16), uint4, uint32_t>::type;
-    __shared__ int colsum[kAreaSeg];
-    const int y_end = min(L.dst.h, (int)(blockIdx.y + 1) * rows);
-    for (int y = blockIdx.y * rows; y < y_end; ++y) {
-    if (y != (int)blockIdx.y * rows) __syncthreads();  // colsum of the previous row is consumed
+    constexpr int R = 2;  // output rows per pass
+    __shared__ __attribute__((aligned(16))) unsigned short colsum[R][kAreaSeg];
     const int pidx = blockIdx.z;
     const int img = pidx / L.src.planes;
     const int plane = pidx - img * L.src.planes;
@@ -909,52 +915,85 @@ __global__ void __launch_bounds__(kBlock) area_u8_colsum_kernel(ResizeLaunch L, 
     const int seg = pw * ax * cc;                  // source bytes per row in this segment
     const int row_bytes = L.src.w * cc;
     const int b0 = x0 * ax * cc;                   // multiple of VB (host picks tw)
-    const unsigned char* row0 = L.src.base + (int64_t)img * L.src.img_pitch + (int64_t)plane * L.src.plane_pitch +
-                                (int64_t)y * ay * L.src.row_pitch + b0;
-    for (int j = threadIdx.x; j * VB < seg; j += kBlock) {
-        int acc[VB];
+    const unsigned char* pbase = L.src.base + (int64_t)img * L.src.img_pitch + (int64_t)plane * L.src.plane_pitch + b0;
+    const int y_end = min(L.dst.h, (int)(blockIdx.y + 1) * rows);
+    for (int yp = blockIdx.y * rows; yp < y_end; yp += R) {
+        if (yp != (int)blockIdx.y * rows) __syncthreads();  // the previous pass's sums are consumed
+        const int nr = min(R, y_end - yp);
+        for (int j = threadIdx.x; j * VB < seg; j += kBlock) {
+            // packed u16 column sums: even / odd bytes of each dword in two
+            // 16-bit lanes (<= 255 * ay < 2^16: no carry crosses a lane)
+            constexpr int ND = VB / 4;
+            uint32_t ev[R][ND], od[R][ND];
 #pragma unroll
-        for (int i = 0; i < VB; ++i) acc[i] = 0;
-        if (b0 + (j + 1) * VB <= row_bytes) {
-            for (int r = 0; r < ay; ++r) {
-                const TV t = *reinterpret_cast<const TV*>(row0 + (int64_t)r * L.src.row_pitch + j * VB);
-                const uint32_t* w = reinterpret_cast<const uint32_t*>(&t);
+            for (int q = 0; q < R; ++q)
 #pragma unroll
-                for (int i = 0; i < VB; ++i) acc[i] += (w[i >> 2] >> (8 * (i & 3))) & 0xff;
+                for (int d = 0; d < ND; ++d) ev[q][d] = od[q][d] = 0u;
+            if (b0 + (j + 1) * VB <= row_bytes) {
+                for (int r = 0; r < ay; ++r) {
+                    TV t[R];
+#pragma unroll
+                    for (int q = 0; q < R; ++q)  // both output rows' loads in flight
+                        if (q < nr)
+                            t[q] = *reinterpret_cast<const TV*>(pbase + (int64_t)((yp + q) * ay + r) * L.src.row_pitch + j * VB);
+#pragma unroll
+                    for (int q = 0; q < R; ++q) {
+                        if (q >= nr) continue;
+                        const uint32_t* w = reinterpret_cast<const uint32_t*>(&t[q]);
+#pragma unroll
+                        for (int d = 0; d < ND; ++d) {
+                            ev[q][d] += w[d] & 0x00FF00FFu;
+                            od[q][d] += (w[d] >> 8) & 0x00FF00FFu;
+                        }
+                    }
+                }
+            } else {  // the row's last partial chunk
+                const int lim = row_bytes - (b0 + j * VB);
+                for (int q = 0; q < nr; ++q)
+                    for (int r = 0; r < ay; ++r) {
+                        const unsigned char* p = pbase + (int64_t)((yp + q) * ay + r) * L.src.row_pitch + j * VB;
+#pragma unroll
+                        for (int i = 0; i < VB; ++i)
+                            if (i < lim) {
+                                const uint32_t v = (uint32_t)p[i] << (16 * ((i >> 1) & 1));
+                                if (i & 1) od[q][i >> 2] += v;
+                                else ev[q][i >> 2] += v;
+                            }
+                    }
             }
-        } else {  // the row's last partial chunk
-            const int lim = row_bytes - (b0 + j * VB);
-            for (int r = 0; r < ay; ++r) {
-                const unsigned char* p = row0 + (int64_t)r * L.src.row_pitch + j * VB;
 #pragma unroll
-                for (int i = 0; i < VB; ++i)
-                    if (i < lim) acc[i] += p[i];
+            for (int q = 0; q < R; ++q)
+#pragma unroll
+                for (int d = 0; d < ND; ++d) {
+                    // bytes 4d .. 4d+3 -> u16 sums {ev.lo, od.lo, ev.hi, od.hi}
+                    uint32_t* cw = reinterpret_cast<uint32_t*>(&colsum[q][j * VB + 4 * d]);
+                    cw[0] = __builtin_amdgcn_perm(od[q][d], ev[q][d], 0x05040100u);
+                    cw[1] = __builtin_amdgcn_perm(od[q][d], ev[q][d], 0x07060302u);
+                }
+        }
+        __syncthreads();
+        for (int q = 0; q < nr; ++q) {
+            const int y = yp + q;
+            TOut* dp = reinterpret_cast<TOut*>(const_cast<unsigned char*>(L.dst.base) + (int64_t)img * L.dst.img_pitch +
+                                               (int64_t)plane * L.dst.plane_pitch + (int64_t)y * L.dst.row_pitch) +
+                       (int64_t)x0 * cc;
+            for (int e = threadIdx.x; e < pw * cc; e += kBlock) {
+                const int xl = e / cc, k = e - xl * cc;
+                const unsigned short* cs = colsum[q] + xl * ax * cc + k;
+                int sum = 0;
+                for (int a = 0; a < ax; ++a) sum += cs[a * cc];
+                const uint8_t v = L.area_half_up ? (uint8_t)((sum + 2) >> 2)
+                                                 : (uint8_t)(int)rintf(__fmul_rn((float)sum, L.area_scale));
+                if (OUT == kOutSame) {
+                    dp[e] = v;
+                } else if (OUT == kOutF32) {
+                    dp[e] = (float)v;
+                } else {
+                    const ChanNorm cn = chan_norm(L.norm, img, cc == 1 ? plane % L.norm.c_total : k);
+                    dp[e] = normalize_u8v(cn, (int)v);
+                }
             }
         }
-#pragma unroll
-        for (int i = 0; i < VB; i += 4)
-            *reinterpret_cast<int4*>(&colsum[j * VB + i]) = make_int4(acc[i], acc[i + 1], acc[i + 2], acc[i + 3]);
-    }
-    __syncthreads();
-    TOut* dp = reinterpret_cast<TOut*>(const_cast<unsigned char*>(L.dst.base) + (int64_t)img * L.dst.img_pitch +
-                                       (int64_t)plane * L.dst.plane_pitch + (int64_t)y * L.dst.row_pitch) +
-               (int64_t)x0 * cc;
-    for (int e = threadIdx.x; e < pw * cc; e += kBlock) {
-        const int xl = e / cc, k = e - xl * cc;
-        const int* cs = colsum + xl * ax * cc + k;
-        int sum = 0;
-        for (int q = 0; q < ax; ++q) sum += cs[q * cc];
-        const uint8_t v = L.area_half_up ? (uint8_t)((sum + 2) >> 2)
-                                         : (uint8_t)(int)rintf(__fmul_rn((float)sum, L.area_scale));
-        if (OUT == kOutSame) {
-            dp[e] = v;
-        } else if (OUT == kOutF32) {
-            dp[e] = (float)v;
-        } else {
-            const ChanNorm cn = chan_norm(L.norm, img, cc == 1 ? plane % L.norm.c_total : k);
-            dp[e] = normalize_u8v(cn, (int)v);
-        }
-    }
     }
 }
 
@@ -983,7 +1022,7 @@ hipError_t launch_area_u8_colsum(const ResizeLaunch& L, hipStream_t s, int vb) {
     const int tw_max = (kAreaSeg / per_px) & ~(vb - 1);
     const int nblk = (L.dst.w + tw_max - 1) / tw_max;
     const int tw = ((L.dst.w + nblk - 1) / nblk + vb - 1) & ~(vb - 1);
-    const int rows = std::max(1, tune_or(VACV_TUNE_AREA_ROWS, 1));  // output rows per workgroup
+    const int rows = std::max(1, tune_or(VACV_TUNE_AREA_ROWS, 4));  // output rows per workgroup (2 per pass; 4: 0.51 vs 0.53 ms at 2x2)
     const dim3 grid(nblk, (L.dst.h + rows - 1) / rows, L.n * L.src.planes);
     return vb == 16 ? launch_area_u8_colsum_t<16>(L, s, tw, rows, grid)
                     : launch_area_u8_colsum_t<4>(L, s, tw, rows, grid);
@@ -1027,7 +1066,7 @@ hipError_t launch_resize_area(const ResizeLaunch& L, hipStream_t s) {
                                (uintptr_t)L.src.plane_pitch | (uintptr_t)L.src.row_pitch;
         const int knob = tune(VACV_TUNE_AREA_KERNEL);  // A/B: 1 per-pixel, 2 dword column sums
         const int vb = (bits & 15) == 0 && L.area_x * L.src.cc <= 256 ? 16 : (bits & 3) == 0 ? 4 : 0;
-        if (vb && L.area_x * L.src.cc <= 1024 && knob != 1)
+        if (vb && L.area_x * L.src.cc <= 1024 && L.area_y <= 257 && knob != 1)  // u16 column sums: 255 * ay < 2^16
             return launch_area_u8_colsum(L, s, knob == 2 ? 4 : vb);
         return launch_area_t<uint8_t>(L, s);
     }
