@@ -401,9 +401,145 @@ __global__ void __launch_bounds__(kBlock) min_max_final_kernel(MinMaxLaunch L, c
 size_t match_lds_bytes(int tw, int th, int cn, int esize);
 namespace {
 
+// ---- u8 correlation on the matrix cores ------------------------------------
+// For template row yy the correlation of an output tile is a GEMM: with
+// a' = image - 128 (i8) and the template split into nibbles b = 16*b_hi +
+// b_lo (both in [0, 15], i8), D[r][x] = sum_k a'(r + yy, cn*x + k) * b(yy, k)
+// = sum_kappa A[r][kappa] * B[kappa][x] where A is the image block (rows r,
+// columns cn*x0 + kappa) and B the Toeplitz matrix B[kappa][x] = b(yy,
+// kappa - cn*x) (0 outside [0, K)).  Then sum a*b = 16*D_hi + D_lo + 128*T, T
+// = the template's byte sum -- exact in int32 (|16*D_hi| <= 2^31 / 2 for
+// K*h <= 2^20 / 2).  v_mfma_i32_32x32x32_i8, a wave owns 32 x 32 outputs; B
+// depends only on (yy, kappa - cn*x), so its fragments are built once per
+// launch (match_bfrag_kernel) and read from L2 by every wave.
+typedef int v4i __attribute__((ext_vector_type(4)));
+typedef int v16i __attribute__((ext_vector_type(16)));
+
+// bf[((part * th + yy) * KB + kb) * 64 + lane]: lane (j = lane & 31, h =
+// lane >> 5) element e is B[kappa = 32 kb + 16 h + e][j] of nibble part
+__global__ void match_bfrag_kernel(MatchLaunch M, int KB, uint4* bf, int* tsum) {
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    const int K = M.tw * M.cn;
+    if (blockIdx.x == 0) {  // the template's byte sum (one workgroup, fixed order)
+        __shared__ int part_sum[256];
+        int acc = 0;
+        for (int i = threadIdx.x; i < K * M.th; i += blockDim.x) {
+            const int yy = i / K, k = i - yy * K;
+            acc += M.tpl[(int64_t)yy * M.tpl_row + k];
+        }
+        part_sum[threadIdx.x] = acc;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            int sum = 0;
+            for (int i = 0; i < (int)blockDim.x; ++i) sum += part_sum[i];
+            *tsum = sum;
+        }
+    }
+    if (t >= 2 * M.th * KB * 64) return;
+    const int lane = t & 63;
+    int rest = t >> 6;
+    const int kb = rest % KB;
+    rest /= KB;
+    const int yy = rest % M.th, part = rest / M.th;
+    const int j = lane & 31, h = lane >> 5;
+    const unsigned char* trow = M.tpl + (int64_t)yy * M.tpl_row;
+    uint32_t d[4] = {0u, 0u, 0u, 0u};
+    for (int e = 0; e < 16; ++e) {
+        const int tt = kb * 32 + 16 * h + e - M.cn * j;
+        uint32_t v = 0u;
+        if (tt >= 0 && tt < K) {
+            const uint32_t b = trow[tt];
+            v = part == 0 ? (b >> 4) : (b & 15u);
+        }
+        d[e >> 2] |= v << (8 * (e & 3));
+    }
+    bf[t] = make_uint4(d[0], d[1], d[2], d[3]);
+}
+
+// workgroup: 64 output rows x 64 output columns of one image; wave w: rows
+// 32 (w & 1) .., columns 32 (w >> 1) ..; the image block (rows r0 .. r0 + 63
+// + th - 1, bytes cn*x0 .. + stride) staged in LDS as i8 (XOR 0x80)
+template <int CN>
+__global__ void __launch_bounds__(kBlock) match_corr_mfma_kernel(MatchLaunch M, int KB, int stride,
+                                                                 const uint4* __restrict__ bf, const int* tsum) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char blk[];
+    const int x0 = blockIdx.x * 64, r0 = blockIdx.y * 64, img = blockIdx.z;
+    const int rows = 63 + M.th;
+    const int chunks = stride >> 4;
+    {
+        const unsigned char* base = M.img + (int64_t)img * M.img_pitch;
+        // the image's readable bytes from row r0 on: loads past them read 0
+        const int64_t avail = (int64_t)(M.ih - r0) * M.img_row;
+        const Rsrc rs = make_rsrc(base + (int64_t)r0 * M.img_row, avail - (M.img_row - (int64_t)M.iw * CN));
+        const uint32_t magic = (uint32_t)((0x100000000ull + (uint64_t)chunks - 1) / (uint64_t)chunks);
+        for (int i = threadIdx.x; i < rows * chunks; i += kBlock) {
+            const uint32_t rr = chunks == 1 ? (uint32_t)i : __umulhi((uint32_t)i, magic);
+            const uint32_t c = (uint32_t)i - rr * (uint32_t)chunks;
+            uint4 v = make_uint4(0u, 0u, 0u, 0u);
+            if ((int)rr + r0 < M.ih) {
+                const uint32_t o = rr * (uint32_t)M.img_row + (uint32_t)(CN * x0) + 16u * c + rs.delta;
+                const uint32_t lim = (uint32_t)(avail - (M.img_row - (int64_t)M.iw * CN)) + rs.delta;
+                if (o + 16u <= lim) {
+                    v = load16(rs, o);
+                } else {  // straddles the image's end: a 16-byte load would read as zeros
+                    uint32_t d[4] = {0u, 0u, 0u, 0u};
+#pragma unroll 1
+                    for (uint32_t e = 0; e < 16u; ++e)
+                        if (o + e < lim)
+                            d[e >> 2] |= (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(rs.r, (int)(o + e), 0, 0) << (8 * (e & 3));
+                    v = make_uint4(d[0], d[1], d[2], d[3]);
+                }
+            }
+            v.x ^= 0x80808080u; v.y ^= 0x80808080u; v.z ^= 0x80808080u; v.w ^= 0x80808080u;
+            *reinterpret_cast<uint4*>(blk + (int)rr * stride + 16 * (int)c) = v;
+        }
+    }
+    __syncthreads();
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int mi = wave & 1, ni = wave >> 1;
+    const int i = lane & 31, h = lane >> 5;
+    const unsigned char* abase = blk + (mi * 32 + i) * stride + ni * CN * 32 + 16 * h;
+    const int per_part = M.th * KB * 64;
+    v16i acc_hi = {}, acc_lo = {};
+    for (int yy = 0; yy < M.th; ++yy) {
+        const unsigned char* arow = abase + yy * stride;
+        const uint4* bh = bf + (int64_t)yy * KB * 64 + lane;
+        const uint4* bl = bh + per_part;
+        for (int kb = 0; kb < KB; ++kb) {
+            const v4i a = *reinterpret_cast<const v4i*>(arow + 32 * kb);
+            const uint4 vh = bh[kb * 64], vl = bl[kb * 64];
+            const v4i b_hi = {(int)vh.x, (int)vh.y, (int)vh.z, (int)vh.w};
+            const v4i b_lo = {(int)vl.x, (int)vl.y, (int)vl.z, (int)vl.w};
+            acc_hi = __builtin_amdgcn_mfma_i32_32x32x32_i8(a, b_hi, acc_hi, 0, 0, 0);
+            acc_lo = __builtin_amdgcn_mfma_i32_32x32x32_i8(a, b_lo, acc_lo, 0, 0, 0);
+        }
+    }
+    const int t128 = 128 * *tsum;
+    const int x = x0 + ni * 32 + i;
+    if (x >= M.rw) return;
+#pragma unroll
+    for (int reg = 0; reg < 16; ++reg) {
+        const int r = r0 + mi * 32 + (reg & 3) + 8 * (reg >> 2) + 4 * h;
+        if (r >= M.rh) continue;
+        const int d = 16 * acc_hi[reg] + acc_lo[reg] + t128;
+        reinterpret_cast<float*>(M.res + (int64_t)img * M.res_pitch + (int64_t)r * M.res_row)[x] = (float)d;
+    }
+}
+
 template <int CN>
 hipError_t launch_corr_cn(const MatchLaunch& M, hipStream_t s) {
     const dim3 grid((M.rw + kTileX - 1) / kTileX, (M.rh + 3) / 4, M.n);
+    int KB = 0, stride = 0;
+    if (M.esize == 1 && M.bfrag && match_mfma_plan(M.tw, M.th, CN, KB, stride)) {
+        uint4* bf = static_cast<uint4*>(M.bfrag);
+        int* tsum = reinterpret_cast<int*>(bf + 2 * (size_t)M.th * KB * 64);
+        const int nfrag = 2 * M.th * KB * 64;
+        hipLaunchKernelGGL(match_bfrag_kernel, dim3((nfrag + kBlock - 1) / kBlock), dim3(kBlock), 0, s, M, KB, bf, tsum);
+        const dim3 g((M.rw + 63) / 64, (M.rh + 63) / 64, M.n);
+        const size_t lds = (size_t)(63 + M.th) * stride;
+        hipLaunchKernelGGL((match_corr_mfma_kernel<CN>), g, dim3(kBlock), lds, s, M, KB, stride, bf, tsum);
+        return hipGetLastError();
+    }
     if (M.esize == 1) {
         const size_t lds = match_lds_bytes(M.tw, M.th, CN, 1);
         hipLaunchKernelGGL((match_corr_u8_kernel<CN>), grid, dim3(kBlock), lds, s, M);
@@ -415,6 +551,22 @@ hipError_t launch_corr_cn(const MatchLaunch& M, hipStream_t s) {
 }
 
 }  // namespace
+
+// The MFMA path's K blocks per template row and LDS row stride, or false when
+// its image block does not fit 64 KiB or the int32 sums could overflow.
+bool match_mfma_plan(int tw, int th, int cn, int& KB, int& stride) {
+    if (tune(VACV_TUNE_MATCH_KERNEL) == 0) return false;
+    const int K = tw * cn;
+    KB = (cn * 31 + K + 31) / 32;
+    stride = (cn * 32 + KB * 32 + 15) / 16 * 16;
+    return (size_t)(63 + th) * stride <= 64 * 1024 && (int64_t)K * th <= (1 << 19);
+}
+
+size_t match_bfrag_bytes(int tw, int th, int cn) {
+    int KB = 0, stride = 0;
+    if (!match_mfma_plan(tw, th, cn, KB, stride)) return 0;
+    return 2 * (size_t)th * KB * 64 * 16 + 256;
+}
 
 size_t match_lds_bytes(int tw, int th, int cn, int esize) {
     if (esize == 1) {

@@ -33,6 +33,7 @@ const char* const kNames[VACV_TUNE_COUNT] = {
     "VACV_RESIZE_ROWS_BYTES",  // VACV_TUNE_RESIZE_ROWS_BYTES
     "VACV_WARP_KERNEL",        // VACV_TUNE_WARP_KERNEL
     "VACV_RESIZE_STRIP",       // VACV_TUNE_RESIZE_STRIP
+    "VACV_MATCH_KERNEL",       // VACV_TUNE_MATCH_KERNEL
 };
 
 struct Table {

@@ -877,6 +877,14 @@ int vacv_match_template(const vacv_image* img_d, const vacv_image* tpl_d, const 
     M.rh = rh;
     M.method = method;
     M.inv_area = 1. / ((double)tpl.h * tpl.w);
+    if (img.dtype == VACV_INT8) {  // the matrix-core correlation's B fragments
+        const size_t bytes = match_bfrag_bytes(tpl.w, tpl.h, img.c);
+        if (bytes) {
+            void* ws = nullptr;
+            if ((st = workspace(s, bytes, &ws, 3))) return st;
+            M.bfrag = ws;
+        }
+    }
     if (method != VACV_TM_CCORR) {
         const size_t box = align_up((size_t)img.n * 2 * (img.h + 1) * (img.w + 1) * img.c * sizeof(double), 256);
         void* ws = nullptr;

@@ -251,8 +251,11 @@ struct MatchLaunch {
     double inv_area;              // 1 / (tw * th)
     double* box;                  // workspace: [n][2][ih+1][(iw+1)*cn] integral images (sum, sqsum)
     double* tstats;               // workspace: template mean[4], norm, sum2, all-ones flag
+    void* bfrag;                  // workspace of match_bfrag_bytes() (u8 MFMA correlation), or null
 };
 size_t match_lds_bytes(int tw, int th, int cn, int esize);
+bool match_mfma_plan(int tw, int th, int cn, int& KB, int& stride);
+size_t match_bfrag_bytes(int tw, int th, int cn);
 hipError_t launch_match_template(const MatchLaunch& M, hipStream_t s);
 
 struct MinMaxLaunch {             // minMaxIdx of one single-channel image

@@ -620,6 +620,21 @@ def test_match_template(ops, dev, oracle):
     small = np.ascontiguousarray(img[3:10, 4:15])
     sw = host(ops.match_template(to_dev(small, dev), to_dev(img, dev), 0))  # swapped: img is the template
     assert_same(sw, oracle.match_template(img, small, 0), "match swapped")
+    # the u8 correlation on the matrix cores (default where its image block
+    # fits) and on the v_dot4 kernel (VACV_TUNE_MATCH_KERNEL = 0): identical,
+    # at a size with several output tiles, partial tiles and every method
+    big = np.stack([synthetic_image(960 + k, 203, 301, 3).reshape(203, 301, 3) for k in range(3)])
+    btpl = np.ascontiguousarray(big[1, 50:97, 100:141])
+    for m in range(6):
+        a = host(ops.match_template(to_dev(big, dev), to_dev(btpl, dev), m))
+        with ops.tuning(MATCH_KERNEL=0):
+            b = host(ops.match_template(to_dev(big, dev), to_dev(btpl, dev), m))
+        assert_same(a, b, f"match mfma vs dot4 method {m}")
+    for c in (1, 4):  # other channel counts through the matrix cores, against the oracle
+        im = synthetic_image(970 + c, 90, 150, c).reshape(90, 150, c)
+        tp = np.ascontiguousarray(im[10:43, 20:77])
+        got = host(ops.match_template(to_dev(im[None], dev), to_dev(tp, dev), 2))
+        assert_same(got[0], oracle.match_template(im, tp, 2), f"match mfma c{c}")
     # minMaxIdx on a match result finds the template's position
     got = ops.match_template(to_dev(img, dev), to_dev(small, dev), 0)
     mn, mx, imn, imx = ops.min_max_idx(got)
