@@ -798,6 +798,8 @@ hipError_t launch_one(const WarpLaunch& L, hipStream_t s) {
     int dst_al = 0;
     const int knob = tune(VACV_TUNE_WARP_KERNEL);
     if constexpr (std::is_same<TIn, uint8_t>::value) {
+        WarpFramesPlan P;
+        if (warp_frames_plan(L, P)) return launch_warp_frames(L, P, s);
         if (knob == 3 && L.tile_rects && warp_tile_plan(L, dst_al)) {
             int4* rects = static_cast<int4*>(L.tile_rects);
             return L.src.row_pitch % 16 == 0 ? launch_tiles<CC, OUT, true>(L, dst_al, rects, s)

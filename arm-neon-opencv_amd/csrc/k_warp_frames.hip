@@ -1,0 +1,620 @@
+// k_warp_frames.hip -- u8 affine bilinear warp, BORDER_CONSTANT, 3 or 4
+// interleaved channels: the source staged through LDS, the per-pixel geometry
+// computed once for many frames.
+//
+// Reference: WarpAffineNaive::warp_affine_naive_hwc_u8 (warp_affine_naive.cpp:
+// 9-58) driven by WarpAffine::warp_affine_naive (warp_affine.cpp:111-169).
+// Per output pixel: f = (m0*x + m1*y) + m2 in float; floor; skip when the
+// top-left tap is outside [0,w-2]x[0,h-2]; weights SAT((1-f)*2048) and
+// 2048-that; value (Sum S*wx*wy) >> 22.  Skipped pixels get the border value.
+//
+// Why this shape.  The gather kernels of k_warp.hip are
+// bound by the vector cache's tag lookups (one per lane quad and cache line of
+// every gather instruction), and the earlier LDS-staged tile kernel by its
+// per-pixel arithmetic: coordinates, weights and LDS addresses (~90 VALU per
+// pixel).  But one launch warps a whole batch with ONE matrix, so all of that
+// arithmetic is the same for every frame.  Here a workgroup owns a 64 x TH
+// output tile of kf consecutive frames:
+//  1. once: each lane computes its NP pixels' taps -- the LDS address of the
+//     top-left tap, packed u16 x-weights, 4x the y-weight -- and the workgroup
+//     reduces them to the source box the tile's taps reach;
+//  2. per frame: the box is staged into LDS with coalesced dword loads (4
+//     pixels = 12 bytes per lane for 3 channels, re-spread to one dword per
+//     pixel so every tap pair is two aligned dwords), one frame ahead in
+//     registers, two LDS buffers, one barrier per frame; each pixel then reads
+//     its two tap pairs (2 x ds_read2_b32) and blends: ~24 VALU per pixel and
+//     frame instead of ~90.
+// Pixels outside the source point at a border pattern kept in each LDS
+// buffer, with weights (2048, 0) x (2048, 0), so they come out as the border
+// value with no select.  A tile whose box exceeds the planned LDS buffer
+// (never for the planned geometry; the plan's bound is conservative) takes its
+// taps from memory bytewise.
+#pragma clang fp contract(off)
+
+#include <climits>
+#include <cstring>
+#include <cmath>
+#include <map>
+#include <mutex>
+
+#include "vacv_device.hpp"
+
+namespace vacv {
+namespace {
+
+constexpr int kFrTileW = 64;   // output columns per tile (one per lane)
+constexpr int kFrMaxIt = 6;    // staging groups (4 pixels) per thread and frame, at most
+
+template <int CC>
+__device__ __forceinline__ uint32_t pack_bytes(const unsigned char* p) {
+    uint32_t v = 0;
+#pragma unroll
+    for (int k = 0; k < CC; ++k) v |= (uint32_t)p[k] << (8 * k);
+    return v;
+}
+
+// The taps of pixel (x, y) from memory, bytewise, or the border pattern
+// outside the source: the rare path of a tile whose box exceeds the LDS plan.
+template <int CC>
+__device__ __forceinline__ void direct_taps(const WarpLaunch& L, const unsigned char* sp, int x, int y, uint32_t& tl,
+                                         uint32_t& tr, uint32_t& bl, uint32_t& br) {
+    const float* M = L.inv;
+    const float fx = (M[0] * (float)x + M[1] * (float)y) + M[2];
+    const float fy = (M[3] * (float)x + M[4] * (float)y) + M[5];
+    if ((x < L.dst.w) & (fx >= 0.f) & (fx < (float)(L.src.w - 1)) & (fy >= 0.f) & (fy < (float)(L.src.h - 1))) {
+        const unsigned char* r0 = sp + (int64_t)(int)fy * L.src.row_pitch + (int64_t)(int)fx * CC;
+        tl = pack_bytes<CC>(r0);
+        tr = pack_bytes<CC>(r0 + CC);
+        bl = pack_bytes<CC>(r0 + L.src.row_pitch);
+        br = pack_bytes<CC>(r0 + L.src.row_pitch + CC);
+    } else {
+        uint32_t bp = 0;
+#pragma unroll
+        for (int k = 0; k < CC; ++k) bp |= (uint32_t)(int)L.border[k] << (8 * k);
+        tl = tr = bl = br = bp;
+    }
+}
+
+// L: launch block; gx, gy: tiles per frame; kf: frames per workgroup; S: LDS
+// bytes per staged row; rows_max: staged rows per buffer; buf: bytes per LDS
+// buffer ((rows_max + 2) * S: the rows, then the border pattern, two pixels
+// at rows_max * S and at (rows_max + 1) * S); dst_al: the destination allows dword
+// (u8 out) stores.
+template <int CC, int OUT, int NP>
+__global__ void __launch_bounds__(kBlock)
+warp_frames_kernel(WarpLaunch L, int gx, int gy, int kf, int S, int rows_max, int buf, int dst_al) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+    constexpr int TH = 4 * NP;
+    constexpr int kLd = CC == 3 ? 3 : 4;  // dwords loaded per 4-pixel group
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: keeps rows and bases scalar
+    int* red = reinterpret_cast<int*>(lds + 2 * buf);  // 4 waves x 4 ints
+
+    // XCD-aware order: workgroup b runs on XCD b % 8 and each XCD walks a
+    // contiguous range of (frame group, tile) items, so neighbouring tiles of
+    // the same frames -- whose boxes share edge rows -- meet in one L2
+    const int tiles = gx * gy;
+    const int total = tiles * ((L.n + kf - 1) / kf);
+    const int per_xcd = (total + 7) / 8;
+    const int id = (int)(blockIdx.x % 8) * per_xcd + (int)(blockIdx.x / 8);
+    if (id >= total) return;  // uniform
+    const int fg = id / tiles, tile = id - fg * tiles;
+    const int by = tile / gx, bx = tile - by * gx;
+    const int f0 = fg * kf, f1 = min(f0 + kf, L.n);
+    const float* M = L.inv;
+    const float wlim = (float)(L.src.w - 1), hlim = (float)(L.src.h - 1);
+    const int x = bx * kFrTileW + lane;
+    const int yw = by * TH + wave * NP;  // this wave's first output row
+    const uint32_t rp = (uint32_t)L.src.row_pitch;
+
+    // ---- 1. per-pixel taps, once for every frame ---------------------------
+    const float axm = M[0] * (float)x, aym = M[3] * (float)x;
+    int sxv[NP], syv[NP];
+    uint32_t wxp[NP], wa4[NP], okm = 0;
+    int xmin = INT_MAX, xmax = INT_MIN, ymin = INT_MAX, ymax = INT_MIN;
+#pragma unroll
+    for (int j = 0; j < NP; ++j) {
+        const int y = yw + j;
+        // warp_affine_naive.cpp:23-24: (m0*x + m1*y) + m2, all float
+        const float fx = (axm + M[1] * (float)y) + M[2];
+        const float fy = (aym + M[4] * (float)y) + M[5];
+        // warp_affine_naive.cpp:26-39: floor(f) in [0, n-2] <=> 0 <= f < n-1
+        const bool ok = (x < L.dst.w) & (y < L.dst.h) & (fx >= 0.f) & (fx < wlim) & (fy >= 0.f) & (fy < hlim);
+        const int sx = ok ? (int)fx : 0, sy = ok ? (int)fy : 0;  // floor where ok
+        const float ax = fx - (float)sx, ay = fy - (float)sy;
+        // SATURATE_CAST_SHORT of a value in (0, 2048]: the +0.5f branch, no clamp
+        const uint32_t w0 = (uint32_t)(int)((1.f - ay) * 2048.f + 0.5f);
+        const uint32_t v0 = (uint32_t)(int)((1.f - ax) * 2048.f + 0.5f);
+        sxv[j] = sx;
+        syv[j] = sy;
+        // outside the source: the border pattern with weights (2048,0) x (2048,0)
+        wxp[j] = ok ? (v0 | ((2048u - v0) << 16)) : 2048u;
+        wa4[j] = ok ? 4u * w0 : 8192u;  // x4: the sum's bits 24..31 are the result
+        okm |= (uint32_t)ok << j;
+        if (ok) {
+            xmin = min(xmin, sx);
+            xmax = max(xmax, sx);
+            ymin = min(ymin, sy);
+            ymax = max(ymax, sy);
+        }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        xmin = min(xmin, __shfl_xor(xmin, o, 64));
+        xmax = max(xmax, __shfl_xor(xmax, o, 64));
+        ymin = min(ymin, __shfl_xor(ymin, o, 64));
+        ymax = max(ymax, __shfl_xor(ymax, o, 64));
+    }
+    if (lane == 0) {
+        red[4 * wave + 0] = xmin;
+        red[4 * wave + 1] = xmax;
+        red[4 * wave + 2] = ymin;
+        red[4 * wave + 3] = ymax;
+    }
+    // the border pattern (one pixel per dword) at rows_max and rows_max + 1 of both buffers
+    if (tid < 8) {
+        uint32_t bp = 0;
+#pragma unroll
+        for (int k = 0; k < CC; ++k) bp |= (uint32_t)(int)L.border[k] << (8 * k);
+        const int b = tid >> 2, r = (tid >> 1) & 1, d = tid & 1;
+        *reinterpret_cast<uint32_t*>(lds + b * buf + (rows_max + r) * S + 4 * d) = bp;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+        xmin = min(xmin, red[4 * w + 0]);
+        xmax = max(xmax, red[4 * w + 1]);
+        ymin = min(ymin, red[4 * w + 2]);
+        ymax = max(ymax, red[4 * w + 3]);
+    }
+    // uniform (the compiler cannot tell: LDS loads), so everything derived
+    // from the box -- staged, the staging shape, the frame loop -- stays scalar
+    xmin = __builtin_amdgcn_readfirstlane(xmin);
+    xmax = __builtin_amdgcn_readfirstlane(xmax);
+    ymin = __builtin_amdgcn_readfirstlane(ymin);
+    ymax = __builtin_amdgcn_readfirstlane(ymax);
+    const bool any = xmax >= 0;
+    const int bx0 = any ? (xmin & ~3) : 0;              // first staged column (4-aligned)
+    const int G = any ? (xmax + 2 - bx0 + 3) >> 2 : 0;  // 4-pixel groups per staged row: columns .. xmax + 1
+    const int R = any ? ymax + 2 - ymin : 0;            // staged rows ymin .. ymax + 1
+    // staging shape: one wave instruction loads kr = 64 / G whole staged rows
+    // (lane l: row l / G, group l % G), a step of the workgroup 4 kr rows
+    const int kr = (G > 0 && G <= 64) ? 64 / G : 0;
+    const int its = kr > 0 ? (R + 4 * kr - 1) / (4 * kr) : 0;
+    const bool staged = kr > 0 && 16 * G <= S && R <= rows_max && its <= kFrMaxIt;  // uniform
+    const uint32_t border_ra = (uint32_t)(rows_max * S);
+    uint32_t ra[NP];
+#pragma unroll
+    for (int j = 0; j < NP; ++j)
+        ra[j] = ((okm >> j) & 1u) ? (uint32_t)((syv[j] - ymin) * S + (sxv[j] - bx0) * 4) : border_ra;
+
+    // Row spans.  The box's rows near its top and bottom need only part of
+    // its width (a rotated tile's source footprint is a parallelogram: ~0.6
+    // of its bounding box at 15 degrees).  Thread t < R clips the
+    // parallelogram of the tile's corners to the band of source rows whose
+    // pixels tap row ymin + t (fy in [r - 1, r + 1), widened by 0.05 px for
+    // the float rounding of the reference's coordinates) and records the
+    // 4-pixel groups it needs, columns floor(x) .. floor(x) + 1.  The table
+    // lives in LDS buffer 1 until the first frame is parked there.
+    uint32_t* spans = reinterpret_cast<uint32_t*>(lds + buf);
+    if (staged && tid < R) {
+        const float X0 = (float)(bx * kFrTileW), X1 = (float)(min(bx * kFrTileW + kFrTileW, L.dst.w) - 1);
+        const float Y0 = (float)(by * TH), Y1 = (float)(min(by * TH + TH, L.dst.h) - 1);
+        float cx[4], cy[4];
+        const float px[4] = {X0, X1, X1, X0}, py[4] = {Y0, Y0, Y1, Y1};
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            cx[i] = (M[0] * px[i] + M[1] * py[i]) + M[2];
+            cy[i] = (M[3] * px[i] + M[4] * py[i]) + M[5];
+        }
+        const float r = (float)(ymin + tid), ya = r - 1.05f, yb = r + 1.05f;
+        float lo = 3.0e38f, hi = -3.0e38f;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int i2 = (i + 1) & 3;
+            if (cy[i] >= ya && cy[i] <= yb) { lo = fminf(lo, cx[i]); hi = fmaxf(hi, cx[i]); }
+#pragma unroll
+            for (int e = 0; e < 2; ++e) {
+                const float yl = e ? yb : ya;
+                if ((cy[i] - yl) * (cy[i2] - yl) < 0.f) {
+                    const float xc = cx[i] + (yl - cy[i]) / (cy[i2] - cy[i]) * (cx[i2] - cx[i]);
+                    lo = fminf(lo, xc);
+                    hi = fmaxf(hi, xc);
+                }
+            }
+        }
+        uint32_t sp = 1u;  // empty: glo = 1 > ghi = 0
+        if (lo <= hi) {
+            const int clo = (int)floorf(fmaxf(lo - 0.05f, -1.0e9f)) - bx0;
+            const int chi = (int)floorf(fminf(hi + 0.05f, 1.0e9f)) + 1 - bx0;
+            if (chi >= 0 && clo <= 4 * G - 1) {
+                const int glo = max(clo, 0) >> 2, ghi = min(chi >> 2, G - 1);
+                sp = (uint32_t)glo | ((uint32_t)ghi << 16);
+            }
+        }
+        spans[tid] = sp;
+    }
+    __syncthreads();
+
+    // this lane's staging offsets, frame-independent; step u adds 4 kr rows.
+    // vm: steps with a group this lane stages (inside its row's span; the
+    // others load out of range -- zeros, no memory traffic -- and are not
+    // parked).  tailm: steps whose group reaches past the plane's last byte
+    // (a partly out-of-range load returns zeros): re-read bytewise when parked.
+    const int rl = kr > 0 ? lane / G : 0, cl = lane - rl * G;
+    const int r0 = wave * kr + rl;
+    const int nu = (staged && rl < kr && r0 < R) ? (R - r0 + 4 * kr - 1) / (4 * kr) : 0;
+    const uint32_t g0 = (uint32_t)(ymin + r0) * rp + (uint32_t)((bx0 + 4 * cl) * CC);
+    const uint32_t l0 = (uint32_t)(r0 * S + 16 * cl);
+    const uint32_t gstep = 4u * (uint32_t)kr * rp, lstep = 4u * (uint32_t)(kr * S);
+    uint32_t tailm = 0, vm = 0;
+#pragma unroll
+    for (int u = 0; u < kFrMaxIt; ++u) {
+        if (u < nu) {
+            const uint32_t sp = spans[r0 + 4 * kr * u];
+            if ((int)(sp & 0xFFFFu) <= cl && cl <= (int)(sp >> 16)) {
+                vm |= 1u << u;
+                if ((int64_t)(g0 + u * gstep) + 4 * CC > L.src.plane_bytes) tailm |= 1u << u;
+            }
+        }
+    }
+
+    uint32_t pre[kFrMaxIt][kLd];
+    // branch-free: every step issues, idle lanes (and every lane when !live)
+    // out of range, so the loaded registers need no phi -- a conditional fetch
+    // made the compiler copy them out right after the loads, i.e. wait for them
+    auto fetch = [&](int f, bool live) {
+        const Rsrc rs = make_rsrc(L.src.base + (int64_t)f * L.src.img_pitch, L.src.plane_bytes);
+        const int lim = live ? nu : 0;
+#pragma unroll
+        for (int u = 0; u < kFrMaxIt; ++u) {
+            const int off = (u < lim && ((vm >> u) & 1u)) ? (int)(g0 + u * gstep + rs.delta) : (int)0x80000000;
+            if constexpr (CC == 3) {
+                const auto v = __builtin_amdgcn_raw_buffer_load_b96(rs.r, off, 0, VACV_LOAD_AUX);
+                pre[u][0] = v[0]; pre[u][1] = v[1]; pre[u][2] = v[2];
+            } else {
+                const auto v = __builtin_amdgcn_raw_buffer_load_b128(rs.r, off, 0, VACV_LOAD_AUX);
+                pre[u][0] = v[0]; pre[u][1] = v[1]; pre[u][2] = v[2]; pre[u][3] = v[3];
+            }
+        }
+    };
+    // 4 pixels x CC bytes -> one pixel per dword (byte 3 unused for CC = 3)
+    auto spread = [&](const uint32_t (&d)[kLd]) {
+        u32x4 q;
+        if constexpr (CC == 3) {
+            q[0] = d[0];
+            q[1] = __builtin_amdgcn_perm(d[1], d[0], 0x0C050403u);
+            q[2] = __builtin_amdgcn_perm(d[2], d[1], 0x0C040302u);
+            q[3] = d[2] >> 8;
+        } else {
+            q[0] = d[0]; q[1] = d[1]; q[2] = d[2]; q[3] = d[3];
+        }
+        return q;
+    };
+    auto park = [&](int f, uint32_t boff) {
+#pragma unroll
+        for (int u = 0; u < kFrMaxIt; ++u)
+            if ((vm >> u) & 1u) *reinterpret_cast<u32x4*>(lds + boff + l0 + u * lstep) = spread(pre[u]);
+        if (tailm) {  // rare: the plane's last group, bytewise
+            const Rsrc rs = make_rsrc(L.src.base + (int64_t)f * L.src.img_pitch, L.src.plane_bytes);
+#pragma unroll
+            for (int u = 0; u < kFrMaxIt; ++u) {
+                if ((tailm >> u) & 1u) {
+                    const int off = (int)(g0 + u * gstep + rs.delta);
+                    uint32_t d[kLd];
+#pragma unroll
+                    for (int q = 0; q < kLd; ++q) {
+                        uint32_t w = 0;
+#pragma unroll
+                        for (int e = 0; e < 4; ++e)
+                            w |= (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(rs.r, off + 4 * q + e, 0, 0) << (8 * e);
+                        d[q] = w;
+                    }
+                    *reinterpret_cast<u32x4*>(lds + boff + l0 + u * lstep) = spread(d);
+                }
+            }
+        }
+    };
+
+    const uint32_t dpitch = (uint32_t)L.dst.row_pitch;
+    const int qx = bx * kFrTileW + (lane & ~3);  // the lane quad's first column
+    // uniform: every pixel of the tile is inside the output (and, for byte
+    // output, every lane quad's 4*CC bytes are dword-aligned): the
+    // branch-free store path
+    const bool tile_full = bx * kFrTileW + kFrTileW <= L.dst.w && by * TH + TH <= L.dst.h &&
+                           (OUT != kOutSame || dst_al);
+    constexpr uint32_t kOob = 0x80000000u;  // a buffer offset past any plane: the access is dropped
+
+    // blend pixel j of frame f from its taps and store it; FULL: tile_full
+    auto emit = [&](auto full_c, int fv, int j, uint32_t tl, uint32_t tr, uint32_t bl, uint32_t br) {
+        constexpr bool FULL = decltype(full_c)::value;
+        // uniform, and said so: with it in VGPRs the compiler wrapped every
+        // store in a waterfall loop over the buffer resource
+        const int f = __builtin_amdgcn_readfirstlane(fv);
+        const int y = yw + j;
+        const bool inside = FULL || (x < L.dst.w && y < L.dst.h);
+        unsigned char* dbase = const_cast<unsigned char*>(L.dst.base) + (int64_t)f * L.dst.img_pitch;
+        const Rsrc drs = make_rsrc(dbase, L.dst.plane_bytes);
+        const us2 wx = __builtin_bit_cast(us2, wxp[j]);
+        const uint32_t wA = wa4[j], wB = 8192u - wa4[j];
+        uint32_t vv[CC];
+#pragma unroll
+        for (int k = 0; k < CC; ++k) {
+            // warp_affine_naive.cpp:50-54 as (tl*wx0 + tr*wx1)*wy0 + (bl*wx0 +
+            // br*wx1)*wy1: exact integers (<= 255 * 2^22), here x4 so that
+            // bits 24..31 are the >> 22 result
+            const uint32_t sel = (uint32_t)k | (0x0Cu << 8) | ((uint32_t)(4 + k) << 16) | (0x0Cu << 24);
+            const uint32_t top = __builtin_amdgcn_perm(tr, tl, sel);
+            const uint32_t bot = __builtin_amdgcn_perm(br, bl, sel);
+            const uint32_t ht = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, top), wx, 0u, false);
+            const uint32_t hb = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, bot), wx, 0u, false);
+            vv[k] = __umul24(ht, wA) + __umul24(hb, wB);
+        }
+        const uint32_t drow = (uint32_t)y * dpitch + drs.delta;
+        if constexpr (OUT == kOutSame) {
+            uint32_t own;
+            if constexpr (CC == 3) {
+                own = __builtin_amdgcn_perm(vv[2], __builtin_amdgcn_perm(vv[1], vv[0], 0x0C0C0703u), 0x0C070100u);
+            } else {
+                own = __builtin_amdgcn_perm(__builtin_amdgcn_perm(vv[3], vv[2], 0x0C0C0703u),
+                                            __builtin_amdgcn_perm(vv[1], vv[0], 0x0C0C0703u), 0x05040100u);
+            }
+            const uint32_t word = quad_pack<CC>(own, lane & 3);  // every lane takes part (DPP)
+            if constexpr (FULL) {
+                const uint32_t off = (lane & 3) < CC ? drow + (uint32_t)(qx * CC + 4 * (lane & 3)) : kOob;
+                __builtin_amdgcn_raw_buffer_store_b32(word, drs.r, (int)off, 0, VACV_STORE_AUX);
+            } else if (inside) {  // the edges, or a byte-aligned destination
+                unsigned char* o = dbase + (int64_t)y * L.dst.row_pitch + (int64_t)x * CC;
+#pragma unroll
+                for (int k = 0; k < CC; ++k) o[k] = (unsigned char)(own >> (8 * k));
+            }
+        } else {
+            u32x4 o;
+#pragma unroll
+            for (int k = 0; k < CC; ++k) {
+                const int v = (int)(vv[k] >> 24);
+                float fv;
+                if (OUT == kOutF32) {
+                    fv = (float)v;
+                } else {
+                    const ChanNorm cn = chan_norm(L.norm, f, k);
+                    fv = normalize_u8v(cn, v);
+                }
+                o[k] = __builtin_bit_cast(uint32_t, fv);
+            }
+            const int off = (int)(inside ? drow + (uint32_t)(x * CC * 4) : kOob);
+            if constexpr (CC == 3) {
+                typedef unsigned int u32x3 __attribute__((ext_vector_type(3)));
+                const u32x3 o3 = {o[0], o[1], o[2]};
+                __builtin_amdgcn_raw_buffer_store_b96(o3, drs.r, off, 0, VACV_STORE_AUX);
+            } else {
+                __builtin_amdgcn_raw_buffer_store_b128(o, drs.r, off, 0, VACV_STORE_AUX);
+            }
+        }
+    };
+
+    using full_t = std::integral_constant<bool, true>;
+    using edge_t = std::integral_constant<bool, false>;
+    if (!staged) {  // uniform, rare: the box is over the LDS plan -- taps from memory
+        for (int f = f0; f < f1; ++f) {
+            const unsigned char* sp = L.src.base + (int64_t)f * L.src.img_pitch;
+            for (int j = 0; j < NP; ++j) {
+                uint32_t tl, tr, bl, br;
+                direct_taps<CC>(L, sp, x, yw + j, tl, tr, bl, br);
+                emit(edge_t(), f, j, tl, tr, bl, br);
+            }
+        }
+        return;
+    }
+    // all NP pixels' LDS reads first, then the blends and stores
+    // (in groups of 4 pixels: all of a lane's 8 pixels' taps at once cost
+    // 139 VGPRs, 3 waves per SIMD)
+    auto sample = [&](auto full_c, int f, uint32_t boff) {
+        constexpr int kGrp = NP < 4 ? NP : 4;
+#pragma unroll
+        for (int j0 = 0; j0 < NP; j0 += kGrp) {
+            uint32_t tp[kGrp][4];
+#pragma unroll
+            for (int j = 0; j < kGrp; ++j) {
+                const uint32_t* t = reinterpret_cast<const uint32_t*>(lds + boff + ra[j0 + j]);
+                const uint32_t* b = reinterpret_cast<const uint32_t*>(lds + boff + ra[j0 + j] + S);
+                tp[j][0] = t[0]; tp[j][1] = t[1]; tp[j][2] = b[0]; tp[j][3] = b[1];
+            }
+#pragma unroll
+            for (int j = 0; j < kGrp; ++j) emit(full_c, f, j0 + j, tp[j][0], tp[j][1], tp[j][2], tp[j][3]);
+        }
+    };
+    fetch(f0, true);
+    for (int f = f0; f < f1; ++f) {
+        const uint32_t boff = (uint32_t)(((f - f0) & 1) * buf);
+        park(f, boff);
+        __syncthreads();  // the box of frame f is in LDS; frame f - 1's reads of the other buffer are done
+        fetch(min(f + 1, f1 - 1), f + 1 < f1);  // in flight while frame f is sampled
+        if (tile_full) sample(full_t(), f, boff);
+        else sample(edge_t(), f, boff);
+    }
+}
+
+template <typename K>
+int64_t frames_resident(K kernel, size_t lds) {
+    static std::mutex mu;
+    static std::map<std::pair<const void*, size_t>, int64_t> cache;  // (kernel, lds) -> workgroups, device 0 shape
+    std::lock_guard<std::mutex> lk(mu);
+    const auto key = std::make_pair(reinterpret_cast<const void*>(kernel), lds);
+    auto it = cache.find(key);
+    if (it != cache.end()) return it->second;
+    int per_cu = 0, cus = 0, dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, kBlock, lds) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+        return 0;
+    const int64_t r = (int64_t)std::max(per_cu, 1) * std::max(cus, 1);
+    cache.emplace(key, r);
+    return r;
+}
+
+template <int CC, int OUT, int NP>
+hipError_t launch_frames(const WarpLaunch& L, const WarpFramesPlan& P, hipStream_t s) {
+    constexpr int TH = 4 * NP;
+    const int gx = (L.dst.w + kFrTileW - 1) / kFrTileW, gy = (L.dst.h + TH - 1) / TH;
+    auto kern = warp_frames_kernel<CC, OUT, NP>;
+    int kf = P.kf;
+    if (kf <= 0) {
+        // at most 8 frames per workgroup (720p rot15: 4 / 8 / 16 frames 0.225 /
+        // 0.200 / 0.210 ms), fewer when that leaves < ~3 rounds of residency
+        const int64_t res = std::max<int64_t>(frames_resident(kern, (size_t)P.lds), 256);
+        const int64_t tiles = (int64_t)gx * gy;
+        kf = (int)std::max<int64_t>(1, std::min<int64_t>(8, tiles * L.n / (3 * res)));
+    }
+    const int64_t total = (int64_t)gx * gy * ((L.n + kf - 1) / kf);
+    if (total >= 0x7FFFFFF0LL) return hipErrorInvalidValue;
+    const int64_t blocks = (total + 7) / 8 * 8;
+    hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(kBlock), (size_t)P.lds, s, L, gx, gy, kf, P.S, P.rows_max,
+                       P.buf, P.dst_al);
+    return hipGetLastError();
+}
+
+template <int CC, int OUT>
+hipError_t launch_frames_np(const WarpLaunch& L, const WarpFramesPlan& P, hipStream_t s) {
+    return P.th == 16 ? launch_frames<CC, OUT, 4>(L, P, s) : launch_frames<CC, OUT, 8>(L, P, s);
+}
+
+template <int OUT>
+hipError_t launch_frames_cc(const WarpLaunch& L, const WarpFramesPlan& P, hipStream_t s) {
+    return L.src.cc == 3 ? launch_frames_np<3, OUT>(L, P, s) : launch_frames_np<4, OUT>(L, P, s);
+}
+
+}  // namespace
+
+// The LDS row stride (bytes, a multiple of 16, >= 16 G) with the fewest LDS
+// bank conflicts for the tap reads.  A wave's 64 lanes read the taps of 64
+// consecutive output pixels of one row; rotated, they fall on several staged
+// rows, and the stride decides whether those rows' dwords land on distinct
+// banks (ds_read_b32: bank = dword mod 32 within each half-wave; distinct
+// dwords on one bank serialise).  Counted on a few sample rows of the output
+// for the 8 strides 16 G .. 16 G + 112; ties go to the smaller stride.
+int frames_stride(const WarpLaunch& L, int G) {
+    const float* M = L.inv;
+    int best_s = 16 * G;
+    long best_cost = -1;
+    for (int k = 0; k < 8; ++k) {
+        const int S = 16 * (G + k), sd = S / 4;
+        long cost = 0;
+        for (int yi = 1; yi <= 3; ++yi) {
+            const int y = L.dst.h * yi / 4;
+            for (int xi = 0; xi < 3; ++xi) {
+                const int x0 = std::max(0, std::min(L.dst.w - 64, (L.dst.w - 64) * xi / 2));
+                for (int half = 0; half < 2; ++half) {
+                    for (int d = 0; d < 2; ++d) {  // the tap pair's two dwords
+                        long a[32];
+                        for (int l = 0; l < 32; ++l) {
+                            const int x = x0 + 32 * half + l;
+                            const float fx = (M[0] * (float)x + M[1] * (float)y) + M[2];
+                            const float fy = (M[3] * (float)x + M[4] * (float)y) + M[5];
+                            a[l] = -1 - d;  // outside: the shared border pattern
+                            if (fx >= 0.f && fx < (float)(L.src.w - 1) && fy >= 0.f && fy < (float)(L.src.h - 1))
+                                a[l] = (long)(int)fy * sd + (int)fx + d;
+                        }
+                        int worst = 1;
+                        for (int l = 0; l < 32; ++l) {  // distinct dwords on lane l's bank
+                            int n = 0;
+                            for (int m = 0; m < 32; ++m) {
+                                if ((((a[m] - a[l]) % 32) + 32) % 32 != 0) continue;
+                                bool first = true;
+                                for (int q = 0; q < m; ++q) first = first && a[q] != a[m];
+                                n += first;
+                            }
+                            worst = std::max(worst, n);
+                        }
+                        cost += worst;
+                    }
+                }
+            }
+        }
+        if (best_cost < 0 || cost < best_cost) {
+            best_cost = cost;
+            best_s = S;
+        }
+    }
+    return best_s;
+}
+
+// The LDS layout of one geometry (pointer-independent): tile rows, stride,
+// rows per buffer.  The bound is the tile's coordinate span (|m0|*63 +
+// |m1|*(TH-1) columns, |m3|*63 + |m4|*(TH-1) rows) plus floor, the second
+// tap, 4-alignment and slack; the kernel re-checks the real box and reads
+// memory if it is larger.
+bool frames_layout_th(const WarpLaunch& L, WarpFramesPlan& P, int th) {
+    P.th = th;
+    const double sx = std::fabs(L.inv[0]) * (kFrTileW - 1) + std::fabs(L.inv[1]) * (P.th - 1);
+    const double sy = std::fabs(L.inv[3]) * (kFrTileW - 1) + std::fabs(L.inv[4]) * (P.th - 1);
+    const int W = (int)std::ceil(sx * (1 + 1e-5) + 1e-3) + 6;  // + floor spread, right tap, 4-alignment
+    const int G = (W + 3) / 4;
+    P.rows_max = (int)std::ceil(sy * (1 + 1e-5) + 1e-3) + 3;
+    if (G > 64 || (P.rows_max + 4 * (64 / G) - 1) / (4 * (64 / G)) > kFrMaxIt) return false;
+    P.S = frames_stride(L, G);
+    P.buf = ((P.rows_max + 2) * P.S + 15) / 16 * 16;
+    P.lds = 2 * P.buf + 64;
+    return P.lds <= 64 * 1024;
+}
+
+// 32-row tiles (measured faster: 0.200 vs 0.222 ms at 720p rot15) unless
+// their box is over the staging budget (e.g. 45 degrees), then 16
+bool frames_layout(const WarpLaunch& L, WarpFramesPlan& P) {
+    const int th_knob = tune(VACV_TUNE_WARP_TILE_H);
+    if (th_knob == 16 || th_knob == 32) return frames_layout_th(L, P, th_knob);
+    return frames_layout_th(L, P, 32) || frames_layout_th(L, P, 16);
+}
+
+// Host plan: does the frames kernel apply, and with which LDS layout?
+// Layouts are cached per geometry (the stride search costs ~0.1 ms of host
+// time); the alignment checks are per call.
+bool warp_frames_plan(const WarpLaunch& L, WarpFramesPlan& P) {
+    const int knob = tune(VACV_TUNE_WARP_KERNEL);
+    if (knob >= 0 && knob != 4) return false;
+    if (L.src.esize != 1 || L.border_mode != kBorderConstant || L.src.planes != 1) return false;
+    if (L.src.cc != 3 && L.src.cc != 4) return false;
+    if (L.src.plane_bytes > kMaxPlaneBytes || L.dst.plane_bytes > kMaxPlaneBytes) return false;
+    const auto al4 = [](const PlaneGeom& g) {
+        return !(g.row_pitch % 4 || g.img_pitch % 4 || reinterpret_cast<uintptr_t>(g.base) % 4);
+    };
+    if (!al4(L.src)) return false;
+    if (L.out != kOutSame && !al4(L.dst)) return false;  // float stores
+    for (int i = 0; i < 6; ++i)
+        if (!std::isfinite(L.inv[i])) return false;
+    struct Key {
+        float inv[6];
+        int sw, sh, dw, dh, th;
+        bool operator<(const Key& o) const { return std::memcmp(this, &o, sizeof(Key)) < 0; }
+    };
+    Key k;
+    std::memset(&k, 0, sizeof(k));
+    std::memcpy(k.inv, L.inv, sizeof(k.inv));
+    k.sw = L.src.w; k.sh = L.src.h; k.dw = L.dst.w; k.dh = L.dst.h; k.th = tune(VACV_TUNE_WARP_TILE_H);
+    static std::mutex mu;
+    static std::map<Key, std::pair<bool, WarpFramesPlan>> cache;
+    bool ok;
+    {
+        std::lock_guard<std::mutex> lk(mu);
+        auto it = cache.find(k);
+        if (it == cache.end()) {
+            WarpFramesPlan Q{};
+            const bool r = frames_layout(L, Q);
+            if (cache.size() > 256) cache.clear();
+            it = cache.emplace(k, std::make_pair(r, Q)).first;
+        }
+        ok = it->second.first;
+        P = it->second.second;
+    }
+    P.dst_al = al4(L.dst) ? 1 : 0;
+    P.kf = tune(VACV_TUNE_WARP_FRAMES);
+    return ok;
+}
+
+hipError_t launch_warp_frames(const WarpLaunch& L, const WarpFramesPlan& P, hipStream_t s) {
+    if (L.out == kOutSame) return launch_frames_cc<kOutSame>(L, P, s);
+    if (L.out == kOutF32) return launch_frames_cc<kOutF32>(L, P, s);
+    return launch_frames_cc<kOutNorm>(L, P, s);
+}
+
+}  // namespace vacv

@@ -34,6 +34,8 @@ const char* const kNames[VACV_TUNE_COUNT] = {
     "VACV_WARP_KERNEL",        // VACV_TUNE_WARP_KERNEL
     "VACV_RESIZE_STRIP",       // VACV_TUNE_RESIZE_STRIP
     "VACV_MATCH_KERNEL",       // VACV_TUNE_MATCH_KERNEL
+    "VACV_WARP_FRAMES",        // VACV_TUNE_WARP_FRAMES
+    "VACV_WARP_TILE_H",        // VACV_TUNE_WARP_TILE_H
 };
 
 struct Table {

@@ -151,6 +151,19 @@ struct WarpLaunch {
 };
 size_t warp_workspace_bytes(const WarpLaunch& L);
 hipError_t launch_warp(const WarpLaunch& L, hipStream_t s);
+// u8 CONSTANT warp of 3/4-channel NHWC batches with the source staged in LDS
+// and the geometry shared by kf frames per workgroup (k_warp_frames.hip)
+struct WarpFramesPlan {
+    int th;                      // tile rows (16 or 32; 64 columns)
+    int S;                       // LDS bytes per staged source row (one dword per pixel)
+    int rows_max;                // staged rows per LDS buffer
+    int buf;                     // bytes per LDS buffer (rows + border pattern)
+    int lds;                     // dynamic LDS per workgroup
+    int kf;                      // frames per workgroup (<= 0: chosen at launch)
+    int dst_al;                  // destination dword-aligned (u8 quad stores)
+};
+bool warp_frames_plan(const WarpLaunch& L, WarpFramesPlan& P);
+hipError_t launch_warp_frames(const WarpLaunch& L, const WarpFramesPlan& P, hipStream_t s);
 
 struct CopyLaunch {                // crop / clone: row copies
     PlaneGeom src;                 // base already offset to the crop origin

@@ -95,7 +95,8 @@ SIGNATURES = {
 TUNE = {"RESIZE_DIRECT": 0, "CUBIC_DIRECT": 1, "RESIZE_INTERLEAVE": 2, "RESIZE_ROWS": 3, "DIRECT_XCD": 4,
         "WARP_PX": 5, "NEAREST_KERNEL": 6, "AREA_KERNEL": 7, "AREA_ROWS": 8, "COLOR_CHUNKS": 9,
         "RESIZE_WGS": 10, "RESIZE_TILE_H": 11, "RESIZE_TILE_W": 12, "RESIZE_WORK": 13, "RESIZE_ROWS_BYTES": 14,
-        "WARP_KERNEL": 15, "RESIZE_STRIP": 16, "MATCH_KERNEL": 17}
+        "WARP_KERNEL": 15, "RESIZE_STRIP": 16, "MATCH_KERNEL": 17,
+        "WARP_FRAMES": 18, "WARP_TILE_H": 19}
 
 _lib = None
 

@@ -707,6 +707,61 @@ def test_warp_border_modes(ops, dev, oracle):
     assert_same(got, want, "border normalize")
 
 
+def test_warp_frames_kernel(ops, dev, oracle):
+    """The LDS-staged frames kernel (k_warp_frames.hip: per-pixel taps computed
+    once for kf frames, the source box staged per frame) is the default for u8
+    BORDER_CONSTANT warps of 3/4-channel NHWC batches.  Against the per-pixel
+    gather kernel (VACV_TUNE_WARP_KERNEL = 0) at full size over frames per
+    workgroup 1, 2, 3, 16 and tile heights 16 / 32 (odd batch: a partial last
+    frame group), u8 / fp32 / normalised outputs, a non-zero border value and a
+    pitched destination; against the oracle at odd sizes where the source box
+    reaches the plane's last bytes (the bytewise tail path)."""
+    import torch
+    n = 7
+    imgs = np.stack([synthetic_image(500 + k, 720, 1280, 3) for k in range(n)])
+    src = to_dev(imgs, dev)
+    mats = [ops.rotation_matrix(0.9, 15.0, (640, 360, 640, 360)),
+            ops.rotation_matrix(0.9, 45.0, (640, 360, 640, 360)),
+            ops.rotation_matrix(1.2, -100.0, (640, 360, 600, 350)),
+            np.array([1, 0, -0.5, 0, 1, -0.5], np.float32)]
+    for m in mats:
+        with ops.tuning(WARP_KERNEL=0):
+            want = ops.warp_affine(src, m, 1280, 720, border_value=(7, 200, 31, 0))
+            wantn = ops.warp_affine_normalize(src, m, 1280, 720, MEAN, STD)
+        for th in (16, 32):
+            for kf in (1, 2, 3, 16):
+                with ops.tuning(WARP_KERNEL=4, WARP_FRAMES=kf, WARP_TILE_H=th):
+                    got = ops.warp_affine(src, m, 1280, 720, border_value=(7, 200, 31, 0))
+                    assert torch.equal(got, want), f"frames kernel {m.tolist()} th={th} kf={kf}"
+            with ops.tuning(WARP_KERNEL=4, WARP_TILE_H=th):
+                assert torch.equal(ops.warp_affine_normalize(src, m, 1280, 720, MEAN, STD), wantn), \
+                    f"frames kernel normalize {m.tolist()} th={th}"
+    # pitched destination (dword-aligned quads and bytewise columns)
+    for x0 in (4, 5):
+        big = torch.zeros((n, 130, 230, 3), dtype=torch.uint8, device=dev)
+        view = big[:, 3:123, x0:x0 + 200]
+        ops.warp_affine(src, mats[2], 200, 120, out=view)
+        g = host(big)
+        for k in (0, n - 1):
+            assert_same(g[k, 3:123, x0:x0 + 200], oracle.warp_affine(imgs[k], mats[2], 200, 120), f"pitched {x0}")
+        g[:, 3:123, x0:x0 + 200] = 0
+        assert not g.any(), "frames kernel wrote outside the window"
+    for c in (3, 4):  # odd sizes: the source box reaches the plane's last group
+        ims = np.stack([synthetic_image(600 + 7 * c + k, 97, 143, c) for k in range(3)])
+        mu = MEAN if c == 3 else np.append(MEAN, np.float32(1.0)).astype(np.float32)
+        sd = STD if c == 3 else np.append(STD, np.float32(2.0)).astype(np.float32)
+        for m in mats:
+            for wo, ho in ((143, 97), (121, 83)):
+                with ops.tuning(WARP_KERNEL=4, WARP_FRAMES=2):
+                    got = host(ops.warp_affine(to_dev(ims, dev), m, wo, ho))
+                    gotf = host(ops.warp_affine_normalize(to_dev(ims, dev), m, wo, ho, mu, sd))
+                for k in range(3):
+                    want = oracle.warp_affine(ims[k], m, wo, ho).reshape(ho, wo, c)
+                    assert_same(got[k].reshape(ho, wo, c), want, f"frames c={c} {wo}x{ho} {m.tolist()}")
+                    wantf = oracle.normalize(oracle.u8_to_f32(want), mu, sd)
+                    assert_same(gotf[k].reshape(ho, wo, c), wantf.reshape(ho, wo, c), f"frames norm c={c}")
+
+
 def test_warp_kernels_agree(ops, dev, oracle):
     """u8 BORDER_CONSTANT warps run on the LDS-staged tile kernel
     (warp_tile_kernel, k_warp.hip) unless its source rectangle is over the LDS
