@@ -19,10 +19,11 @@
 // (load_taps, vacv_device.hpp), packed
 // u16 dot products for the fixed-point sum.  Blocks are ordered so each XCD
 // walks a contiguous range (its L2 keeps the shared source rows).
-// Measured alternative, kept out: staging each tile's source bounding box in
-// LDS (coalesced 16-B loads) ran 1.2-1.9x slower at 1280x720 rot15 -- the
-// box overlap between tiles and the per-tile barrier cost more than the
-// gathers it saves.
+// These gather kernels serve fp32 sources, the non-CONSTANT border modes,
+// 1/2-channel and NCHW u8 planes, and geometries whose source box is over
+// the LDS plan of the u8 frames kernel (k_warp_frames.hip), which takes the
+// rest: it stages the source in LDS and computes the taps once for 8 frames
+// (DESIGN.md 3.3).
 #pragma clang fp contract(off)
 
 #include <cmath>
@@ -388,367 +389,6 @@ warp_u8_kernel(WarpLaunch L, int gx, int gy, int total) {
     }
 }
 
-// u8 input, BORDER_CONSTANT, staged through LDS.  Measured (tools/gathercal,
-// PMC): the gather kernels above are bound by the vector cache's per-quad tag
-// lookups -- ~1.8 cycles per (4-lane group x cache line) access, 19-33 of them
-// per 64-lane gather instruction -- not by bytes or ALU.  Here a workgroup
-// walks kTileW x kTileH output tiles; for each it loads the source rectangle
-// the tile's taps can reach with coalesced 16-byte loads (one access per 4
-// lanes) into LDS and takes the taps from there.
-//  * The rectangle comes from the tile's corners (warp_rect_kernel, once per
-//    launch): the reference's coordinate ((m0*x + m1*y) + m2 in float) is
-//    monotone in x and in y separately, so its extremes over the tile are at
-//    corners, and every in-source pixel's taps lie inside.
-//  * Persistent workgroups, two LDS buffers: tile i+1's loads are in flight
-//    (in registers) while tile i is sampled; one barrier per tile.
-//  * Wave w samples tile rows w, w + 4, ...; lane l takes column l, so a tap
-//    read covers 64 consecutive output pixels (few LDS bank conflicts).  Byte
-//    results are packed across each lane quad (DPP) into 4*CC-byte stores.
-//  * A 16-byte load that crosses the end of the plane returns zeros: pixels
-//    whose taps reach the plane's last partial chunk, and tiles whose
-//    rectangle exceeds the LDS budget, take their taps from memory instead.
-constexpr int kTileW = 64, kTileH = 32;
-constexpr int kStageIters = 3;                        // 16-byte chunks per thread and tile
-constexpr int kWarpBoxBytes = kStageIters * kBlock * 16;  // per LDS buffer (12 KiB)
-
-// per tile of one plane: the source rectangle [x0, x1] x [y0, y1] its taps can reach
-__global__ void warp_rect_kernel(WarpLaunch L, int gx, int gy, int4* rects) {
-    const int t = blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= gx * gy) return;
-    const int by = t / gx, bx = t - by * gx;
-    const int tx0 = bx * kTileW, ty0 = by * kTileH;
-    const int txe = min(tx0 + kTileW, L.dst.w) - 1, tye = min(ty0 + kTileH, L.dst.h) - 1;
-    const float* M = L.inv;
-    const float c0x = M[0] * (float)tx0, c1x = M[0] * (float)txe;
-    const float c0y = M[1] * (float)ty0, c1y = M[1] * (float)tye;
-    const float d0x = M[3] * (float)tx0, d1x = M[3] * (float)txe;
-    const float d0y = M[4] * (float)ty0, d1y = M[4] * (float)tye;
-    const float fxa = (c0x + c0y) + M[2], fxb = (c1x + c0y) + M[2], fxc = (c0x + c1y) + M[2], fxd = (c1x + c1y) + M[2];
-    const float fya = (d0x + d0y) + M[5], fyb = (d1x + d0y) + M[5], fyc = (d0x + d1y) + M[5], fyd = (d1x + d1y) + M[5];
-    const float fx_lo = fminf(fminf(fxa, fxb), fminf(fxc, fxd)), fx_hi = fmaxf(fmaxf(fxa, fxb), fmaxf(fxc, fxd));
-    const float fy_lo = fminf(fminf(fya, fyb), fminf(fyc, fyd)), fy_hi = fmaxf(fmaxf(fya, fyb), fmaxf(fyc, fyd));
-    const int sw = L.src.w, shh = L.src.h;
-    // clamp in float first: the corners may be far outside (or NaN)
-    int4 r;
-    r.x = (int)floorf(fminf(fmaxf(fx_lo, 0.f), (float)(sw - 1)));
-    r.z = min((int)floorf(fminf(fmaxf(fx_hi, 0.f), (float)(sw - 1))) + 1, sw - 1);
-    r.y = (int)floorf(fminf(fmaxf(fy_lo, 0.f), (float)(shh - 1)));
-    r.w = min((int)floorf(fminf(fmaxf(fy_hi, 0.f), (float)(shh - 1))) + 1, shh - 1);
-    rects[t] = r;
-}
-
-// the taps of one pixel from memory, bytewise (the staged kernel's rare
-// fallback: the plane's last bytes, or a tile over the LDS budget)
-template <int CC>
-__device__ __forceinline__ void taps_from_memory(const unsigned char* sp, uint32_t rp, int sx, int sy, uint32_t (&t0)[3],
-                                                 uint32_t (&t1)[3]) {
-    const unsigned char* r0 = sp + (int64_t)sy * rp + (int64_t)sx * CC;
-#pragma unroll
-    for (int d = 0; d < 3; ++d) t0[d] = t1[d] = 0u;
-#pragma unroll
-    for (int e = 0; e < 2 * CC; ++e) {
-        t0[e >> 2] |= (uint32_t)r0[e] << (8 * (e & 3));
-        t1[e >> 2] |= (uint32_t)r0[rp + e] << (8 * (e & 3));
-    }
-}
-
-// A tile's staging plan (wave-uniform integers).
-struct TileBox {
-    int x0, y0;
-    uint32_t off0;     // byte of (x0, y0) from the 16-aligned plane base
-    int chunks, rows;  // 16-byte chunks per staged row, staged rows
-    int stride;        // LDS bytes per staged row
-    uint32_t dxb;      // (x0, y0)'s byte within its chunk
-    uint32_t bw_lim;   // lx <= bw_lim: both taps staged
-    int ly_max;        // ly <= ly_max: rows ly, ly + 1 staged and whole (may be < 0)
-    bool staged;       // the rectangle fits the LDS buffer
-    bool tail;         // some tap row may reach the plane's last partial chunk
-};
-
-template <int CC, bool RA>
-__device__ __forceinline__ TileBox tile_box(const int4 r, uint32_t rp, uint32_t delta, uint32_t lim16) {
-    TileBox b;
-    b.x0 = r.x;
-    b.y0 = r.y;
-    b.off0 = (uint32_t)r.y * rp + (uint32_t)(r.x * CC) + delta;
-    b.dxb = b.off0 & 15u;
-    const uint32_t dmax = RA ? b.dxb : 15u;
-    b.chunks = (int)((dmax + (uint32_t)(r.z - r.x + 1) * CC + 15u) >> 4);
-    b.rows = r.w - r.y + 1;
-    b.stride = b.chunks * 16;
-    b.staged = b.rows * b.chunks <= kStageIters * kBlock;
-    b.bw_lim = (uint32_t)max((b.stride - (int)dmax) / CC - 2, 0);
-    const int sy_safe = (int)((lim16 - delta) / rp) - 2;  // sy <= sy_safe: rows sy, sy + 1 whole
-    b.tail = r.w + 1 > sy_safe + 2 || !b.staged;
-    b.ly_max = min(b.rows - 2, sy_safe - r.y);
-    return b;
-}
-
-// RA: the source row pitch is a multiple of 16, so every staged row starts at
-// the same byte offset within its first chunk.
-template <int CC, int OUT, bool RA>
-__global__ void __launch_bounds__(kBlock)
-warp_tile_kernel(WarpLaunch L, int gx, int gy, int total, const int4* __restrict__ rects, int dst_al) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    // XCD-aware tile order: workgroup b runs on XCD b % 8 and walks that
-    // XCD's contiguous range of tiles, interleaved with its XCD siblings
-    const int per_xcd = (total + 7) / 8;
-    const int xcd = (int)(blockIdx.x % 8), wg_on_xcd = (int)(blockIdx.x / 8), wgs_per_xcd = (int)(gridDim.x / 8);
-    const int t_begin = xcd * per_xcd, t_end = min(t_begin + per_xcd, total);
-    const int tiles_per_plane = gx * gy;
-    const uint32_t rp = (uint32_t)L.src.row_pitch;  // host: plane_bytes < 2^31
-    const float* M = L.inv;
-    const float wlim = (float)(L.src.w - 1), hlim = (float)(L.src.h - 1);
-    typedef unsigned short us2v __attribute__((ext_vector_type(2)));
-    constexpr int kTD = (int)kTapDwords<CC, true>;
-
-    auto plane_of = [&](int t, int& img, int& plane, int& tile) {
-        const int pidx = t / tiles_per_plane;
-        tile = t - pidx * tiles_per_plane;
-        img = pidx / L.src.planes;
-        plane = pidx - img * L.src.planes;
-    };
-    auto plane_ptr = [&](int img, int plane) {
-        return L.src.base + (int64_t)img * L.src.img_pitch + (int64_t)plane * L.src.plane_pitch;
-    };
-
-    // ---- prefetch of a tile's chunks into registers ------------------------
-    uint4 pre[kStageIters];
-    auto fetch = [&](int t) {
-        int img, plane, tile;
-        plane_of(t, img, plane, tile);
-        const Rsrc srs = make_rsrc(plane_ptr(img, plane), L.src.plane_bytes);
-        const uint32_t lim16 = ((uint32_t)L.src.plane_bytes + srs.delta) & ~15u;
-        const TileBox b = tile_box<CC, RA>(rects[tile], rp, srs.delta, lim16);
-        const int n = b.staged ? b.rows * b.chunks : 0;
-        const uint32_t magic = (uint32_t)((0x100000000ull + (uint64_t)b.chunks - 1) / (uint64_t)b.chunks);
-#pragma unroll
-        for (int u = 0; u < kStageIters; ++u) {
-            const int i = min(u * kBlock + tid, max(n - 1, 0));
-            const uint32_t r = b.chunks == 1 ? (uint32_t)i : __umulhi((uint32_t)i, magic);  // i / chunks, exact (i < 2^12)
-            const uint32_t c = (uint32_t)i - r * (uint32_t)b.chunks;
-            pre[u] = load16(srs, ((b.off0 + r * rp) & ~15u) + 16u * c);
-        }
-    };
-    auto park = [&](int t, unsigned char* box) {
-        int img, plane, tile;
-        plane_of(t, img, plane, tile);
-        const uint32_t delta = (uint32_t)reinterpret_cast<uintptr_t>(plane_ptr(img, plane)) & 15u;
-        const uint32_t lim16 = ((uint32_t)L.src.plane_bytes + delta) & ~15u;
-        const TileBox b = tile_box<CC, RA>(rects[tile], rp, delta, lim16);
-        const int n = b.staged ? b.rows * b.chunks : 0;
-#pragma unroll
-        for (int u = 0; u < kStageIters; ++u) {
-            const int i = u * kBlock + tid;
-            if (i < n) *reinterpret_cast<uint4*>(box + 16 * i) = pre[u];  // row-major chunks: byte r*stride + 16c
-        }
-    };
-
-    int t = t_begin + wg_on_xcd;
-    if (t >= t_end) return;  // uniform
-    fetch(t);
-    for (int buf = 0; t < t_end; t += wgs_per_xcd, buf ^= 1) {
-        unsigned char* box = lds + buf * kWarpBoxBytes;
-        park(t, box);
-        __syncthreads();
-        const int tn = t + wgs_per_xcd;
-        if (tn < t_end) fetch(tn);  // in flight while this tile is sampled
-
-        int img, plane, tile;
-        plane_of(t, img, plane, tile);
-        const unsigned char* sp = plane_ptr(img, plane);
-        const uint32_t delta = (uint32_t)reinterpret_cast<uintptr_t>(sp) & 15u;
-        const uint32_t lim16 = ((uint32_t)L.src.plane_bytes + delta) & ~15u;
-        const TileBox b = tile_box<CC, RA>(rects[tile], rp, delta, lim16);
-        const uint32_t rpm = rp & 15u;
-        const int by = tile / gx, bx = tile - by * gx;
-        const int x = bx * kTileW + lane;
-        const float axm = M[0] * (float)x, aym = M[3] * (float)x;
-
-        ChanNorm cn[CC] = {};
-        if (OUT == kOutNorm) {
-#pragma unroll
-            for (int k = 0; k < CC; ++k) cn[k] = chan_norm(L.norm, img, CC == 1 ? plane : k);
-        }
-        unsigned char* drow0 = const_cast<unsigned char*>(L.dst.base) + (int64_t)img * L.dst.img_pitch +
-                               (int64_t)plane * L.dst.plane_pitch;
-        const Rsrc drs = make_rsrc(drow0, L.dst.plane_bytes);  // 32-bit store offsets
-        const int qx = bx * kTileW + (lane & ~3);  // the lane quad's first column
-        const bool quad_full = qx + 4 <= L.dst.w && dst_al;
-
-#pragma unroll
-        for (int g = 0; g < kTileH / 16; ++g) {
-            // ---- 4 rows per lane: taps, weights, LDS reads (branch-free) -----
-            uint32_t t0[4][3], t1[4][3], sh0[4], sh1[4], wxp[4], wy0[4];
-            int sxv[4], syv[4];
-            bool okv[4], fbv[4];
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const int y = by * kTileH + wave + 4 * (4 * g + j);
-                const float fx = (axm + M[1] * (float)y) + M[2];
-                const float fy = (aym + M[4] * (float)y) + M[5];
-                // bitwise: no short-circuit branches
-                const bool ok = (fx >= 0.f) & (fx < wlim) & (fy >= 0.f) & (fy < hlim);
-                const int sx = (int)fx, sy = (int)fy;  // floor where ok (fx, fy >= 0)
-                const float ax = fx - (float)sx, ay = fy - (float)sy;
-                // SATURATE_CAST_SHORT of a value in (0, 2048]: the +0.5f branch, no clamp
-                const uint32_t w0 = (uint32_t)(int)((1.f - ay) * 2048.f + 0.5f);
-                const uint32_t v0 = (uint32_t)(int)((1.f - ax) * 2048.f + 0.5f);
-                wy0[j] = w0;
-                wxp[j] = v0 | ((2048u - v0) << 16);
-                okv[j] = ok;
-                sxv[j] = sx;
-                syv[j] = sy;
-                // clamped into the staged rectangle: a no-op for every
-                // in-source pixel of a staged, tail-free tile
-                const uint32_t lx = min((uint32_t)(sx - b.x0), b.bw_lim);
-                const uint32_t lyr = (uint32_t)(sy - b.y0);
-                const uint32_t ly = min(lyr, (uint32_t)max(b.ly_max, 0));
-                fbv[j] = b.tail & ok & (!b.staged | ((int)lyr > b.ly_max));
-                uint32_t a0, a1;
-                if constexpr (RA) {
-                    a0 = __umul24(ly, (uint32_t)b.stride) + __umul24(lx, (uint32_t)CC) + b.dxb;
-                    a1 = a0 + (uint32_t)b.stride;
-                } else {
-                    const uint32_t d0 = (b.dxb + __umul24(ly, rpm)) & 15u;
-                    a0 = __umul24(ly, (uint32_t)b.stride) + __umul24(lx, (uint32_t)CC) + d0;
-                    a1 = a0 + (uint32_t)b.stride - d0 + ((d0 + rpm) & 15u);
-                }
-                const uint32_t* b0 = reinterpret_cast<const uint32_t*>(box + (a0 & ~3u));
-                const uint32_t* b1 = reinterpret_cast<const uint32_t*>(box + (a1 & ~3u));
-#pragma unroll
-                for (int d = 0; d < kTD; ++d) { t0[j][d] = b0[d]; t1[j][d] = b1[d]; }
-                sh0[j] = a0 & 3u;
-                sh1[j] = a1 & 3u;
-            }
-            if (b.tail) {  // uniform; rare: taps from memory (selected, so the LDS reads stay unconditional)
-#pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    uint32_t m0[3] = {0u, 0u, 0u}, m1[3] = {0u, 0u, 0u};
-                    if (fbv[j]) taps_from_memory<CC>(sp, rp, sxv[j], syv[j], m0, m1);
-#pragma unroll
-                    for (int d = 0; d < 3; ++d) {
-                        t0[j][d] = fbv[j] ? m0[d] : t0[j][d];
-                        t1[j][d] = fbv[j] ? m1[d] : t1[j][d];
-                    }
-                    sh0[j] = fbv[j] ? 0u : sh0[j];
-                    sh1[j] = fbv[j] ? 0u : sh1[j];
-                }
-            }
-            // ---- blends and stores -----------------------------------------
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const int y = by * kTileH + wave + 4 * (4 * g + j);
-                const uint32_t a0 = __builtin_amdgcn_alignbyte(t0[j][1], t0[j][0], sh0[j]);
-                const uint32_t c0 = __builtin_amdgcn_alignbyte(t1[j][1], t1[j][0], sh1[j]);
-                uint32_t a1 = 0u, c1 = 0u;
-                if constexpr (kTD == 3) {
-                    a1 = __builtin_amdgcn_alignbyte(t0[j][2], t0[j][1], sh0[j]);
-                    c1 = __builtin_amdgcn_alignbyte(t1[j][2], t1[j][1], sh1[j]);
-                }
-                const us2v wx = __builtin_bit_cast(us2v, wxp[j]);
-                // weights x4: the sum's bits 24..31 are the result (<= 255 * 2^24 < 2^32)
-                const uint32_t wA = 4u * wy0[j], wB = 8192u - 4u * wy0[j];
-                uint32_t vv[CC];
-#pragma unroll
-                for (int k = 0; k < CC; ++k) {
-                    // warp_affine_naive.cpp:50-54 as (tl*wx0 + tr*wx1)*wy0 +
-                    // (bl*wx0 + br*wx1)*wy1 (exact integers), >> 22
-                    const uint32_t sel = (uint32_t)k | (0x0Cu << 8) | ((uint32_t)(CC + k) << 16) | (0x0Cu << 24);
-                    const uint32_t top = __builtin_amdgcn_perm(a1, a0, sel);
-                    const uint32_t bot = __builtin_amdgcn_perm(c1, c0, sel);
-                    const uint32_t ht = __builtin_amdgcn_udot2(__builtin_bit_cast(us2v, top), wx, 0u, false);
-                    const uint32_t hb = __builtin_amdgcn_udot2(__builtin_bit_cast(us2v, bot), wx, 0u, false);
-                    vv[k] = __umul24(ht, wA) + __umul24(hb, wB);
-                }
-                if (y >= L.dst.h) continue;
-                unsigned char* drow = drow0 + (int64_t)y * L.dst.row_pitch;
-                if constexpr (OUT == kOutSame) {
-                    // the pixel's bytes (bits 24..31 of each channel sum), border outside
-                    uint32_t own = 0;
-#pragma unroll
-                    for (int k = 0; k < CC; ++k) {
-                        const uint32_t byte = okv[j] ? (vv[k] >> 24) : (uint32_t)(int)L.border[k];
-                        own |= byte << (8 * k);
-                    }
-                    const uint32_t word = quad_pack<CC>(own, lane & 3);
-                    if (quad_full) {
-                        if ((lane & 3) < CC)
-                            __builtin_amdgcn_raw_buffer_store_b32(
-                                word, drs.r, (int)((uint32_t)y * (uint32_t)L.dst.row_pitch + (uint32_t)(qx * CC + 4 * (lane & 3)) + drs.delta),
-                                0, VACV_STORE_AUX);
-                    } else if (x < L.dst.w) {
-#pragma unroll
-                        for (int k = 0; k < CC; ++k) drow[(int64_t)x * CC + k] = (unsigned char)(own >> (8 * k));
-                    }
-                } else {
-                    if (x < L.dst.w) {
-                        float* o = reinterpret_cast<float*>(drow) + (int64_t)x * CC;
-#pragma unroll
-                        for (int k = 0; k < CC; ++k) {
-                            const int v = okv[j] ? (int)(vv[k] >> 24) : (int)L.border[k];
-                            o[k] = OUT == kOutF32 ? (float)v : normalize_u8v(cn[k], v);
-                        }
-                    }
-                }
-            }
-        }
-    }
-}
-
-// The staged kernel applies to u8 BORDER_CONSTANT warps whose tile rectangle
-// fits one LDS buffer (kStageIters * kBlock chunks); the bound is the corner
-// spans plus floor, the second tap and float slack.  dst_al: the lane quads'
-// 4*CC-byte stores are dword-aligned (else bytewise).
-bool warp_tile_plan(const WarpLaunch& L, int& dst_al) {
-    if (L.src.esize != 1 || L.border_mode != kBorderConstant) return false;
-    const int cc = L.src.cc;
-    dst_al = !(L.dst.row_pitch % 4 || L.dst.img_pitch % 4 || L.dst.plane_pitch % 4 ||
-               reinterpret_cast<uintptr_t>(L.dst.base) % 4);
-    for (int i = 0; i < 6; ++i)
-        if (!std::isfinite(L.inv[i])) return false;
-    const double bw = std::fabs(L.inv[0]) * (kTileW - 1) + std::fabs(L.inv[1]) * (kTileH - 1) + 4.0;
-    const double bh = std::fabs(L.inv[3]) * (kTileW - 1) + std::fabs(L.inv[4]) * (kTileH - 1) + 4.0;
-    const double chunks = std::ceil((15.0 + bw * cc) / 16.0) + 1.0;
-    return std::ceil(bh) * chunks <= kStageIters * kBlock;
-}
-
-template <typename K>
-int64_t warp_resident(K kernel, size_t lds) {
-    static std::mutex mu;
-    static std::map<std::pair<const void*, int>, int64_t> cache;  // (kernel, device) -> workgroups
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess) return 0;
-    std::lock_guard<std::mutex> lk(mu);
-    const auto key = std::make_pair(reinterpret_cast<const void*>(kernel), dev);
-    auto it = cache.find(key);
-    if (it != cache.end()) return it->second;
-    int per_cu = 0, cus = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, kBlock, lds) != hipSuccess ||
-        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-        return 0;
-    const int64_t r = (int64_t)std::max(per_cu, 1) * std::max(cus, 1);
-    cache.emplace(key, r);
-    return r;
-}
-
-template <int CC, int OUT, bool RA>
-hipError_t launch_tiles(const WarpLaunch& L, int dst_al, int4* rects, hipStream_t s) {
-    const int gx = (L.dst.w + kTileW - 1) / kTileW, gy = (L.dst.h + kTileH - 1) / kTileH;
-    const int64_t total = (int64_t)gx * gy * L.n * L.src.planes;
-    if (total >= 0x7FFFFFF0LL) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(warp_rect_kernel, dim3((gx * gy + 255) / 256), dim3(256), 0, s, L, gx, gy, rects);
-    const size_t lds = 2 * (size_t)kWarpBoxBytes + 16;  // + the last tap dword's overhang
-    auto kern = warp_tile_kernel<CC, OUT, RA>;
-    int64_t grid = warp_resident(kern, lds);
-    if (grid <= 0) grid = 256 * 4;
-    grid = std::min<int64_t>(grid, (total + 7) / 8 * 8);
-    grid = std::max<int64_t>(grid / 8 * 8, 8);
-    hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(kBlock), lds, s, L, gx, gy, (int)total, rects, dst_al);
-    return hipGetLastError();
-}
-
 // default: 8 or 10 lane blocks per wave for byte output, whichever pads the
 // output width less (1280: 10 -> 2 tiles of 640 exactly, 0.271 ms, vs 8 ->
 // 2.5 tiles, 0.281 ms at 720p rot15; 8 vs 4: 0.283 vs 0.304), 4 for fp32
@@ -795,16 +435,11 @@ hipError_t launch_px(const WarpLaunch& L, hipStream_t s) {
 
 template <int CC, typename TIn, int OUT>
 hipError_t launch_one(const WarpLaunch& L, hipStream_t s) {
-    int dst_al = 0;
-    const int knob = tune(VACV_TUNE_WARP_KERNEL);
     if constexpr (std::is_same<TIn, uint8_t>::value) {
+        // u8 CONSTANT, 3/4-channel NHWC: the LDS-staged frames kernel
+        // (k_warp_frames.hip), unless its box plan does not fit
         WarpFramesPlan P;
         if (warp_frames_plan(L, P)) return launch_warp_frames(L, P, s);
-        if (knob == 3 && L.tile_rects && warp_tile_plan(L, dst_al)) {
-            int4* rects = static_cast<int4*>(L.tile_rects);
-            return L.src.row_pitch % 16 == 0 ? launch_tiles<CC, OUT, true>(L, dst_al, rects, s)
-                                             : launch_tiles<CC, OUT, false>(L, dst_al, rects, s);
-        }
     }
     switch (warp_blocks_per_wave(OUT == kOutSame && sizeof(TIn) == 1, L.dst.w)) {
         case 10: return launch_px<CC, TIn, OUT, 10>(L, s);
@@ -826,11 +461,6 @@ hipError_t launch_cc(const WarpLaunch& L, hipStream_t s) {
 }
 
 }  // namespace
-
-size_t warp_workspace_bytes(const WarpLaunch& L) {
-    const int gx = (L.dst.w + kTileW - 1) / kTileW, gy = (L.dst.h + kTileH - 1) / kTileH;
-    return (size_t)gx * gy * sizeof(int4);
-}
 
 hipError_t launch_warp(const WarpLaunch& L, hipStream_t s) {
     if (L.src.esize == 1) {

@@ -404,11 +404,6 @@ int warp_impl(const vacv_image* src_d, const vacv_image* dst_d, const float m[6]
     L.border_mode = border_mode;
     if (border_mode == VACV_BORDER_TRANSPARENT && dst.data == src.data) return VACV_ERR_INVALID_ARG;  // in place
     if (ns) L.norm = *ns;
-    if (src.dtype == VACV_INT8 && border_mode == VACV_BORDER_CONSTANT) {  // the LDS-staged kernel's tile table
-        void* ws = nullptr;
-        if ((st = workspace(s, warp_workspace_bytes(L), &ws, 2))) return st;
-        L.tile_rects = ws;
-    }
     return hip_status(launch_warp(L, s));
 }
 

@@ -147,9 +147,7 @@ struct WarpLaunch {
     int border_mode;             // kBorder* (vacv_semantics.hpp)
     int out;                     // OutKind
     NormSpec norm;
-    void* tile_rects;            // workspace of warp_workspace_bytes() for the LDS-staged kernel, or null
 };
-size_t warp_workspace_bytes(const WarpLaunch& L);
 hipError_t launch_warp(const WarpLaunch& L, hipStream_t s);
 // u8 CONSTANT warp of 3/4-channel NHWC batches with the source staged in LDS
 // and the geometry shared by kf frames per workgroup (k_warp_frames.hip)

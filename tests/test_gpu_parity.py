@@ -763,14 +763,15 @@ def test_warp_frames_kernel(ops, dev, oracle):
 
 
 def test_warp_kernels_agree(ops, dev, oracle):
-    """u8 BORDER_CONSTANT warps run on the LDS-staged tile kernel
-    (warp_tile_kernel, k_warp.hip) unless its source rectangle is over the LDS
-    budget; then on the batched gather kernel (warp_u8_kernel) where a
-    64-pixel output row spans few source rows, else on the per-pixel kernel
-    (warp_kernel).  VACV_TUNE_WARP_KERNEL = 3 / 2 / 0 forces one of them and
-    VACV_TUNE_WARP_PX switches the gather kernels' lane blocks per wave.
-    Identical outputs at full size for rotations, flips, shears, strong
-    down-scales, fused normalisation, NCHW planes and a pitched destination."""
+    """u8 BORDER_CONSTANT warps of 3/4-channel NHWC batches run on the
+    LDS-staged frames kernel (k_warp_frames.hip) unless its box plan does not
+    fit (e.g. a 4x down-scale); then, and for 1/2 channels or NCHW planes, on
+    the batched gather kernel (warp_u8_kernel) where a 64-pixel output row
+    spans few source rows, else on the per-pixel kernel (warp_kernel).
+    VACV_TUNE_WARP_KERNEL = 4 / 2 / 0 forces one of them and VACV_TUNE_WARP_PX
+    switches the gather kernels' lane blocks per wave.  Identical outputs at
+    full size for rotations, flips, shears, strong down-scales, fused
+    normalisation, NCHW planes and a pitched destination."""
     import torch
     from vacv_amd import NCHW
     imgs = np.stack([synthetic_image(80 + k, 720, 1280, 3) for k in range(2)])
@@ -786,7 +787,7 @@ def test_warp_kernels_agree(ops, dev, oracle):
             with ops.tuning(WARP_KERNEL=2):
                 a = ops.warp_affine(src, m, wo, ho)
                 an = ops.warp_affine_normalize(src, m, wo, ho, MEAN, STD)
-            with ops.tuning(WARP_KERNEL=3):
+            with ops.tuning(WARP_KERNEL=4):
                 t = ops.warp_affine(src, m, wo, ho)
                 tn = ops.warp_affine_normalize(src, m, wo, ho, MEAN, STD)
             with ops.tuning(WARP_KERNEL=0):
@@ -806,7 +807,7 @@ def test_warp_kernels_agree(ops, dev, oracle):
         for m in mats[:2] + mats[3:4]:
             for wo in (121, 128):  # byte stores / the aligned 4-pixel stores, partial tiles
                 want = oracle.warp_affine(im, m, wo, 83).reshape(83, wo, c)
-                for flag in (3, 2, 0):
+                for flag in (4, 2, 0):
                     with ops.tuning(WARP_KERNEL=flag):
                         got = host(ops.warp_affine(to_dev(im.reshape(1, 97, 143, c), dev), m, wo, 83))[0]
                     assert_same(got.reshape(83, wo, c), want, f"warp c={c} {wo} kernel={flag}")
