@@ -20,10 +20,9 @@
 // u16 dot products for the fixed-point sum.  Blocks are ordered so each XCD
 // walks a contiguous range (its L2 keeps the shared source rows).
 // These gather kernels serve fp32 sources, the non-CONSTANT border modes,
-// 1/2-channel and NCHW u8 planes, and geometries whose source box is over
-// the LDS plan of the u8 frames kernel (k_warp_frames.hip), which takes the
-// rest: it stages the source in LDS and computes the taps once for 8 frames
-// (DESIGN.md 3.3).
+// and geometries whose source box is over the LDS plan of the u8 frames
+// kernel (k_warp_frames.hip), which takes the rest: it stages the source in
+// LDS and computes the taps once for 8 frames.
 #pragma clang fp contract(off)
 
 #include <cmath>
@@ -436,8 +435,8 @@ hipError_t launch_px(const WarpLaunch& L, hipStream_t s) {
 template <int CC, typename TIn, int OUT>
 hipError_t launch_one(const WarpLaunch& L, hipStream_t s) {
     if constexpr (std::is_same<TIn, uint8_t>::value) {
-        // u8 CONSTANT, 3/4-channel NHWC: the LDS-staged frames kernel
-        // (k_warp_frames.hip), unless its box plan does not fit
+        // u8 CONSTANT: the LDS-staged frames kernel (k_warp_frames.hip),
+        // unless its box plan does not fit
         WarpFramesPlan P;
         if (warp_frames_plan(L, P)) return launch_warp_frames(L, P, s);
     }

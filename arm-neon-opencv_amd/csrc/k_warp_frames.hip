@@ -1,6 +1,7 @@
-// k_warp_frames.hip -- u8 affine bilinear warp, BORDER_CONSTANT, 3 or 4
-// interleaved channels: the source staged through LDS, the per-pixel geometry
-// computed once for many frames.
+// k_warp_frames.hip -- u8 affine bilinear warp, BORDER_CONSTANT, 1 to 4
+// interleaved channels or NCHW planes: the source staged through LDS, the
+// per-pixel geometry computed once for many frames.  A "frame" here is what
+// one sampler pass sees: a whole NHWC image, or one plane of an NCHW image.
 //
 // Reference: WarpAffineNaive::warp_affine_naive_hwc_u8 (warp_affine_naive.cpp:
 // 9-58) driven by WarpAffine::warp_affine_naive (warp_affine.cpp:111-169).
@@ -80,12 +81,12 @@ __device__ __forceinline__ void direct_taps(const WarpLaunch& L, const unsigned 
 // buffer ((rows_max + 2) * S: the rows, then the border pattern, two pixels
 // at rows_max * S and at (rows_max + 1) * S); dst_al: the destination allows dword
 // (u8 out) stores.
-template <int CC, int OUT, int NP>
+template <int CC, int OUT, int NP, bool PLANAR>
 __global__ void __launch_bounds__(kBlock)
 warp_frames_kernel(WarpLaunch L, int gx, int gy, int kf, int S, int rows_max, int buf, int dst_al) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     constexpr int TH = 4 * NP;
-    constexpr int kLd = CC == 3 ? 3 : 4;  // dwords loaded per 4-pixel group
+    constexpr int kLd = CC;  // dwords loaded per 4-pixel group (4 pixels x CC bytes)
     // staging loads: sc0 for byte output (neighbouring tiles' boxes share
     // rows through L2: 720p rot15 0.199 -> 0.190 ms), non-temporal for fp32
     // output, whose 4x larger stores want the L2 (0.426 vs 0.453 ms)
@@ -100,13 +101,21 @@ warp_frames_kernel(WarpLaunch L, int gx, int gy, int kf, int S, int rows_max, in
     // contiguous range of (frame group, tile) items, so neighbouring tiles of
     // the same frames -- whose boxes share edge rows -- meet in one L2
     const int tiles = gx * gy;
-    const int total = tiles * ((L.n + kf - 1) / kf);
+    const int nfr = L.n * L.src.planes;  // frames: images x planes
+    const int total = tiles * ((nfr + kf - 1) / kf);
     const int per_xcd = (total + 7) / 8;
     const int id = (int)(blockIdx.x % 8) * per_xcd + (int)(blockIdx.x / 8);
     if (id >= total) return;  // uniform
     const int fg = id / tiles, tile = id - fg * tiles;
     const int by = tile / gx, bx = tile - by * gx;
-    const int f0 = fg * kf, f1 = min(f0 + kf, L.n);
+    const int f0 = fg * kf, f1 = min(f0 + kf, nfr);
+    // byte offset of frame f in a batch of geometry g (PLANAR: NCHW planes
+    // are the frames; a compile-time split, so NHWC pays no division)
+    auto frame_img = [&](int f) { return PLANAR ? f / L.src.planes : f; };
+    auto frame_off = [&](int f, const PlaneGeom& g) {
+        const int img = frame_img(f), pl = f - img * L.src.planes;
+        return PLANAR ? (int64_t)img * g.img_pitch + (int64_t)pl * g.plane_pitch : (int64_t)f * g.img_pitch;
+    };
     const float* M = L.inv;
     const float wlim = (float)(L.src.w - 1), hlim = (float)(L.src.h - 1);
     const int x = bx * kFrTileW + lane;
@@ -270,12 +279,17 @@ warp_frames_kernel(WarpLaunch L, int gx, int gy, int kf, int S, int rows_max, in
     // out of range, so the loaded registers need no phi -- a conditional fetch
     // made the compiler copy them out right after the loads, i.e. wait for them
     auto fetch = [&](int f, bool live) {
-        const Rsrc rs = make_rsrc(L.src.base + (int64_t)f * L.src.img_pitch, L.src.plane_bytes);
+        const Rsrc rs = make_rsrc(L.src.base + frame_off(f, L.src), L.src.plane_bytes);
         const int lim = live ? nu : 0;
 #pragma unroll
         for (int u = 0; u < kFrMaxIt; ++u) {
             const int off = (u < lim && ((vm >> u) & 1u)) ? (int)(g0 + u * gstep + rs.delta) : (int)0x80000000;
-            if constexpr (CC == 3) {
+            if constexpr (CC == 1) {
+                pre[u][0] = __builtin_amdgcn_raw_buffer_load_b32(rs.r, off, 0, kAux);
+            } else if constexpr (CC == 2) {
+                const auto v = __builtin_amdgcn_raw_buffer_load_b64(rs.r, off, 0, kAux);
+                pre[u][0] = v[0]; pre[u][1] = v[1];
+            } else if constexpr (CC == 3) {
                 const auto v = __builtin_amdgcn_raw_buffer_load_b96(rs.r, off, 0, kAux);
                 pre[u][0] = v[0]; pre[u][1] = v[1]; pre[u][2] = v[2];
             } else {
@@ -284,10 +298,14 @@ warp_frames_kernel(WarpLaunch L, int gx, int gy, int kf, int S, int rows_max, in
             }
         }
     };
-    // 4 pixels x CC bytes -> one pixel per dword (byte 3 unused for CC = 3)
+    // 4 pixels x CC bytes -> one pixel per dword (the bytes above CC unused)
     auto spread = [&](const uint32_t (&d)[kLd]) {
         u32x4 q;
-        if constexpr (CC == 3) {
+        if constexpr (CC == 1) {
+            q[0] = d[0]; q[1] = d[0] >> 8; q[2] = d[0] >> 16; q[3] = d[0] >> 24;
+        } else if constexpr (CC == 2) {
+            q[0] = d[0]; q[1] = d[0] >> 16; q[2] = d[1]; q[3] = d[1] >> 16;
+        } else if constexpr (CC == 3) {
             q[0] = d[0];
             q[1] = __builtin_amdgcn_perm(d[1], d[0], 0x0C050403u);
             q[2] = __builtin_amdgcn_perm(d[2], d[1], 0x0C040302u);
@@ -302,7 +320,7 @@ warp_frames_kernel(WarpLaunch L, int gx, int gy, int kf, int S, int rows_max, in
         for (int u = 0; u < kFrMaxIt; ++u)
             if ((vm >> u) & 1u) *reinterpret_cast<u32x4*>(lds + boff + l0 + u * lstep) = spread(pre[u]);
         if (tailm) {  // rare: the plane's last group, bytewise
-            const Rsrc rs = make_rsrc(L.src.base + (int64_t)f * L.src.img_pitch, L.src.plane_bytes);
+            const Rsrc rs = make_rsrc(L.src.base + frame_off(f, L.src), L.src.plane_bytes);
 #pragma unroll
             for (int u = 0; u < kFrMaxIt; ++u) {
                 if ((tailm >> u) & 1u) {
@@ -339,7 +357,7 @@ warp_frames_kernel(WarpLaunch L, int gx, int gy, int kf, int S, int rows_max, in
         const int f = __builtin_amdgcn_readfirstlane(fv);
         const int y = yw + j;
         const bool inside = FULL || (x < L.dst.w && y < L.dst.h);
-        unsigned char* dbase = const_cast<unsigned char*>(L.dst.base) + (int64_t)f * L.dst.img_pitch;
+        unsigned char* dbase = const_cast<unsigned char*>(L.dst.base) + frame_off(f, L.dst);
         const Rsrc drs = make_rsrc(dbase, L.dst.plane_bytes);
         const us2 wx = __builtin_bit_cast(us2, wxp[j]);
         const uint32_t wA = wa4[j], wB = 8192u - wa4[j];
@@ -359,7 +377,11 @@ warp_frames_kernel(WarpLaunch L, int gx, int gy, int kf, int S, int rows_max, in
         const uint32_t drow = (uint32_t)y * dpitch + drs.delta;
         if constexpr (OUT == kOutSame) {
             uint32_t own;
-            if constexpr (CC == 3) {
+            if constexpr (CC == 1) {
+                own = vv[0] >> 24;
+            } else if constexpr (CC == 2) {
+                own = __builtin_amdgcn_perm(vv[1], vv[0], 0x0C0C0703u);
+            } else if constexpr (CC == 3) {
                 own = __builtin_amdgcn_perm(vv[2], __builtin_amdgcn_perm(vv[1], vv[0], 0x0C0C0703u), 0x0C070100u);
             } else {
                 own = __builtin_amdgcn_perm(__builtin_amdgcn_perm(vv[3], vv[2], 0x0C0C0703u),
@@ -401,13 +423,19 @@ warp_frames_kernel(WarpLaunch L, int gx, int gy, int kf, int S, int rows_max, in
                 if (OUT == kOutF32) {
                     fv = (float)v;
                 } else {
-                    const ChanNorm cn = chan_norm(L.norm, f, k);
+                    const int img = frame_img(f), pl = f - img * L.src.planes;
+                    const ChanNorm cn = chan_norm(L.norm, img, PLANAR ? pl : k);
                     fv = normalize_u8v(cn, v);
                 }
                 o[k] = __builtin_bit_cast(uint32_t, fv);
             }
             const int off = (int)(inside ? drow + (uint32_t)(x * CC * 4) : kOob);
-            if constexpr (CC == 3) {
+            if constexpr (CC == 1) {
+                __builtin_amdgcn_raw_buffer_store_b32(o[0], drs.r, off, 0, VACV_STORE_AUX);
+            } else if constexpr (CC == 2) {
+                typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+                __builtin_amdgcn_raw_buffer_store_b64(u32x2{o[0], o[1]}, drs.r, off, 0, VACV_STORE_AUX);
+            } else if constexpr (CC == 3) {
                 typedef unsigned int u32x3 __attribute__((ext_vector_type(3)));
                 const u32x3 o3 = {o[0], o[1], o[2]};
                 __builtin_amdgcn_raw_buffer_store_b96(o3, drs.r, off, 0, VACV_STORE_AUX);
@@ -421,7 +449,7 @@ warp_frames_kernel(WarpLaunch L, int gx, int gy, int kf, int S, int rows_max, in
     using edge_t = std::integral_constant<bool, false>;
     if (!staged) {  // uniform, rare: the box is over the LDS plan -- taps from memory
         for (int f = f0; f < f1; ++f) {
-            const unsigned char* sp = L.src.base + (int64_t)f * L.src.img_pitch;
+            const unsigned char* sp = L.src.base + frame_off(f, L.src);
             for (int j = 0; j < NP; ++j) {
                 uint32_t tl, tr, bl, br;
                 direct_taps<CC>(L, sp, x, yw + j, tl, tr, bl, br);
@@ -477,20 +505,20 @@ int64_t frames_resident(K kernel, size_t lds) {
     return r;
 }
 
-template <int CC, int OUT, int NP>
+template <int CC, int OUT, int NP, bool PLANAR>
 hipError_t launch_frames(const WarpLaunch& L, const WarpFramesPlan& P, hipStream_t s) {
     constexpr int TH = 4 * NP;
     const int gx = (L.dst.w + kFrTileW - 1) / kFrTileW, gy = (L.dst.h + TH - 1) / TH;
-    auto kern = warp_frames_kernel<CC, OUT, NP>;
+    auto kern = warp_frames_kernel<CC, OUT, NP, PLANAR>;
     int kf = P.kf;
     if (kf <= 0) {
         // at most 8 frames per workgroup (720p rot15: 4 / 8 / 16 frames 0.225 /
         // 0.200 / 0.210 ms), fewer when that leaves < ~3 rounds of residency
         const int64_t res = std::max<int64_t>(frames_resident(kern, (size_t)P.lds), 256);
         const int64_t tiles = (int64_t)gx * gy;
-        kf = (int)std::max<int64_t>(1, std::min<int64_t>(8, tiles * L.n / (3 * res)));
+        kf = (int)std::max<int64_t>(1, std::min<int64_t>(8, tiles * L.n * L.src.planes / (3 * res)));
     }
-    const int64_t total = (int64_t)gx * gy * ((L.n + kf - 1) / kf);
+    const int64_t total = (int64_t)gx * gy * ((L.n * L.src.planes + kf - 1) / kf);
     if (total >= 0x7FFFFFF0LL) return hipErrorInvalidValue;
     const int64_t blocks = (total + 7) / 8 * 8;
     hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(kBlock), (size_t)P.lds, s, L, gx, gy, kf, P.S, P.rows_max,
@@ -500,12 +528,19 @@ hipError_t launch_frames(const WarpLaunch& L, const WarpFramesPlan& P, hipStream
 
 template <int CC, int OUT>
 hipError_t launch_frames_np(const WarpLaunch& L, const WarpFramesPlan& P, hipStream_t s) {
-    return P.th == 16 ? launch_frames<CC, OUT, 4>(L, P, s) : launch_frames<CC, OUT, 8>(L, P, s);
+    if (CC == 1 && L.src.planes > 1)
+        return P.th == 16 ? launch_frames<CC, OUT, 4, true>(L, P, s) : launch_frames<CC, OUT, 8, true>(L, P, s);
+    return P.th == 16 ? launch_frames<CC, OUT, 4, false>(L, P, s) : launch_frames<CC, OUT, 8, false>(L, P, s);
 }
 
 template <int OUT>
 hipError_t launch_frames_cc(const WarpLaunch& L, const WarpFramesPlan& P, hipStream_t s) {
-    return L.src.cc == 3 ? launch_frames_np<3, OUT>(L, P, s) : launch_frames_np<4, OUT>(L, P, s);
+    switch (L.src.cc) {
+        case 1: return launch_frames_np<1, OUT>(L, P, s);
+        case 2: return launch_frames_np<2, OUT>(L, P, s);
+        case 3: return launch_frames_np<3, OUT>(L, P, s);
+        default: return launch_frames_np<4, OUT>(L, P, s);
+    }
 }
 
 }  // namespace
@@ -601,11 +636,12 @@ bool frames_layout(const WarpLaunch& L, WarpFramesPlan& P) {
 bool warp_frames_plan(const WarpLaunch& L, WarpFramesPlan& P) {
     const int knob = tune(VACV_TUNE_WARP_KERNEL);
     if (knob >= 0 && knob != 4) return false;
-    if (L.src.esize != 1 || L.border_mode != kBorderConstant || L.src.planes != 1) return false;
-    if (L.src.cc != 3 && L.src.cc != 4) return false;
+    if (L.src.esize != 1 || L.border_mode != kBorderConstant) return false;
+    if (L.src.planes > 1 && L.src.cc != 1) return false;
+    if (L.src.cc < 1 || L.src.cc > 4) return false;
     if (L.src.plane_bytes > kMaxPlaneBytes || L.dst.plane_bytes > kMaxPlaneBytes) return false;
     const auto al4 = [](const PlaneGeom& g) {
-        return !(g.row_pitch % 4 || g.img_pitch % 4 || reinterpret_cast<uintptr_t>(g.base) % 4);
+        return !(g.row_pitch % 4 || g.img_pitch % 4 || g.plane_pitch % 4 || reinterpret_cast<uintptr_t>(g.base) % 4);
     };
     if (!al4(L.src)) return false;
     if (L.out != kOutSame && !al4(L.dst)) return false;  // float stores

@@ -149,7 +149,7 @@ struct WarpLaunch {
     NormSpec norm;
 };
 hipError_t launch_warp(const WarpLaunch& L, hipStream_t s);
-// u8 CONSTANT warp of 3/4-channel NHWC batches with the source staged in LDS
+// u8 CONSTANT warp (1-4 interleaved channels, or NCHW planes) with the source staged in LDS
 // and the geometry shared by kf frames per workgroup (k_warp_frames.hip)
 struct WarpFramesPlan {
     int th;                      // tile rows (16 or 32; 64 columns)

@@ -710,7 +710,7 @@ def test_warp_border_modes(ops, dev, oracle):
 def test_warp_frames_kernel(ops, dev, oracle):
     """The LDS-staged frames kernel (k_warp_frames.hip: per-pixel taps computed
     once for kf frames, the source box staged per frame) is the default for u8
-    BORDER_CONSTANT warps of 3/4-channel NHWC batches.  Against the per-pixel
+    BORDER_CONSTANT warps (1-4 channels, NCHW planes as frames).  Against the per-pixel
     gather kernel (VACV_TUNE_WARP_KERNEL = 0) at full size over frames per
     workgroup 1, 2, 3, 16 and tile heights 16 / 32 (odd batch: a partial last
     frame group), u8 / fp32 / normalised outputs, a non-zero border value and a
@@ -746,27 +746,40 @@ def test_warp_frames_kernel(ops, dev, oracle):
             assert_same(g[k, 3:123, x0:x0 + 200], oracle.warp_affine(imgs[k], mats[2], 200, 120), f"pitched {x0}")
         g[:, 3:123, x0:x0 + 200] = 0
         assert not g.any(), "frames kernel wrote outside the window"
-    for c in (3, 4):  # odd sizes: the source box reaches the plane's last group
-        ims = np.stack([synthetic_image(600 + 7 * c + k, 97, 143, c) for k in range(3)])
-        mu = MEAN if c == 3 else np.append(MEAN, np.float32(1.0)).astype(np.float32)
-        sd = STD if c == 3 else np.append(STD, np.float32(2.0)).astype(np.float32)
+    for c in (1, 2, 3, 4):  # odd sizes: the source box reaches the plane's last group
+        ims = np.stack([synthetic_image(600 + 7 * c + k, 97, 143, c).reshape(97, 143, c) for k in range(3)])
+        mu = np.concatenate([MEAN, [1.0]]).astype(np.float32)[:c]
+        sd = np.concatenate([STD, [2.0]]).astype(np.float32)[:c]
         for m in mats:
             for wo, ho in ((143, 97), (121, 83)):
                 with ops.tuning(WARP_KERNEL=4, WARP_FRAMES=2):
                     got = host(ops.warp_affine(to_dev(ims, dev), m, wo, ho))
                     gotf = host(ops.warp_affine_normalize(to_dev(ims, dev), m, wo, ho, mu, sd))
                 for k in range(3):
-                    want = oracle.warp_affine(ims[k], m, wo, ho).reshape(ho, wo, c)
+                    want = oracle.warp_affine(ims[k] if c > 1 else ims[k, ..., 0], m, wo, ho).reshape(ho, wo, c)
                     assert_same(got[k].reshape(ho, wo, c), want, f"frames c={c} {wo}x{ho} {m.tolist()}")
                     wantf = oracle.normalize(oracle.u8_to_f32(want), mu, sd)
                     assert_same(gotf[k].reshape(ho, wo, c), wantf.reshape(ho, wo, c), f"frames norm c={c}")
 
 
+    # NCHW planes are frames of their own (3 planes x 3 images)
+    from vacv_amd import NCHW
+    ims = np.stack([synthetic_image(650 + k, 97, 143, 3) for k in range(3)])
+    chw = to_dev(np.ascontiguousarray(ims.transpose(0, 3, 1, 2)), dev)
+    with ops.tuning(WARP_KERNEL=4, WARP_FRAMES=2):
+        got = host(ops.warp_affine(chw, mats[0], 121, 83, layout=NCHW))
+        gotn = host(ops.warp_affine_normalize(chw, mats[0], 121, 83, MEAN, STD, layout=NCHW))
+    for k in range(3):
+        for ch in range(3):
+            want = oracle.warp_affine(np.ascontiguousarray(ims[k, ..., ch]), mats[0], 121, 83)
+            assert_same(got[k, ch], want.reshape(83, 121), f"frames chw {k} {ch}")
+            wn = oracle.normalize(oracle.u8_to_f32(want.reshape(83, 121, 1)), MEAN[ch:ch + 1], STD[ch:ch + 1])
+            assert_same(gotn[k, ch], wn.reshape(83, 121), f"frames chw norm {k} {ch}")
+
 def test_warp_kernels_agree(ops, dev, oracle):
-    """u8 BORDER_CONSTANT warps of 3/4-channel NHWC batches run on the
-    LDS-staged frames kernel (k_warp_frames.hip) unless its box plan does not
-    fit (e.g. a 4x down-scale); then, and for 1/2 channels or NCHW planes, on
-    the batched gather kernel (warp_u8_kernel) where a 64-pixel output row
+    """u8 BORDER_CONSTANT warps run on the LDS-staged frames kernel
+    (k_warp_frames.hip) unless its box plan does not fit (e.g. a 4x
+    down-scale); then on the batched gather kernel (warp_u8_kernel) where a 64-pixel output row
     spans few source rows, else on the per-pixel kernel (warp_kernel).
     VACV_TUNE_WARP_KERNEL = 4 / 2 / 0 forces one of them and VACV_TUNE_WARP_PX
     switches the gather kernels' lane blocks per wave.  Identical outputs at
