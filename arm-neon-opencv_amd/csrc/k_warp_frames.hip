@@ -198,10 +198,15 @@ warp_frames_kernel(WarpLaunch L, int gx, int gy, int kf, int S, int rows_max, in
     const int its = kr > 0 ? (R + 4 * kr - 1) / (4 * kr) : 0;
     const bool staged = kr > 0 && 16 * G <= S && R <= rows_max && its <= kFrMaxIt;  // uniform
     const uint32_t border_ra = (uint32_t)(rows_max * S);
-    uint32_t ra[NP];
+    // per pixel, packed: the LDS offset of its top-left tap (< 64 KiB) in
+    // bits 0..15, 4x its y-weight (<= 8192) in bits 16..31: a register per
+    // pixel less (123 -> 110 VGPRs).  A second staging register set for two
+    // frames in flight still spilled at 4 waves per SIMD and ran slower
+    // (0.2125 vs 0.187 ms at 720p rot15).
+    uint32_t rw[NP];
 #pragma unroll
     for (int j = 0; j < NP; ++j)
-        ra[j] = ((okm >> j) & 1u) ? (uint32_t)((syv[j] - ymin) * S + (sxv[j] - bx0) * 4) : border_ra;
+        rw[j] = (((okm >> j) & 1u) ? (uint32_t)((syv[j] - ymin) * S + (sxv[j] - bx0) * 4) : border_ra) | (wa4[j] << 16);
 
     // Row spans.  The box's rows near its top and bottom need only part of
     // its width (a rotated tile's source footprint is a parallelogram: ~0.6
@@ -274,11 +279,11 @@ warp_frames_kernel(WarpLaunch L, int gx, int gy, int kf, int S, int rows_max, in
         }
     }
 
-    uint32_t pre[kFrMaxIt][kLd];
+    typedef uint32_t Pre[kFrMaxIt][kLd];
     // branch-free: every step issues, idle lanes (and every lane when !live)
     // out of range, so the loaded registers need no phi -- a conditional fetch
     // made the compiler copy them out right after the loads, i.e. wait for them
-    auto fetch = [&](int f, bool live) {
+    auto fetch = [&](Pre& pre, int f, bool live) {
         const Rsrc rs = make_rsrc(L.src.base + frame_off(f, L.src), L.src.plane_bytes);
         const int lim = live ? nu : 0;
 #pragma unroll
@@ -315,7 +320,7 @@ warp_frames_kernel(WarpLaunch L, int gx, int gy, int kf, int S, int rows_max, in
         }
         return q;
     };
-    auto park = [&](int f, uint32_t boff) {
+    auto park = [&](const Pre& pre, int f, uint32_t boff) {
 #pragma unroll
         for (int u = 0; u < kFrMaxIt; ++u)
             if ((vm >> u) & 1u) *reinterpret_cast<u32x4*>(lds + boff + l0 + u * lstep) = spread(pre[u]);
@@ -360,7 +365,7 @@ warp_frames_kernel(WarpLaunch L, int gx, int gy, int kf, int S, int rows_max, in
         unsigned char* dbase = const_cast<unsigned char*>(L.dst.base) + frame_off(f, L.dst);
         const Rsrc drs = make_rsrc(dbase, L.dst.plane_bytes);
         const us2 wx = __builtin_bit_cast(us2, wxp[j]);
-        const uint32_t wA = wa4[j], wB = 8192u - wa4[j];
+        const uint32_t wA = rw[j] >> 16, wB = 8192u - (rw[j] >> 16);
         uint32_t vv[CC];
 #pragma unroll
         for (int k = 0; k < CC; ++k) {
@@ -462,26 +467,28 @@ warp_frames_kernel(WarpLaunch L, int gx, int gy, int kf, int S, int rows_max, in
     // (in groups of 4 pixels: all of a lane's 8 pixels' taps at once cost
     // 139 VGPRs, 3 waves per SIMD)
     auto sample = [&](auto full_c, int f, uint32_t boff) {
-        constexpr int kGrp = NP < 4 ? NP : 4;
+        constexpr int kGrp = 4;  // NP is 4 or 8
 #pragma unroll
         for (int j0 = 0; j0 < NP; j0 += kGrp) {
             uint32_t tp[kGrp][4];
 #pragma unroll
             for (int j = 0; j < kGrp; ++j) {
-                const uint32_t* t = reinterpret_cast<const uint32_t*>(lds + boff + ra[j0 + j]);
-                const uint32_t* b = reinterpret_cast<const uint32_t*>(lds + boff + ra[j0 + j] + S);
+                const uint32_t ra = rw[j0 + j] & 0xFFFFu;
+                const uint32_t* t = reinterpret_cast<const uint32_t*>(lds + boff + ra);
+                const uint32_t* b = reinterpret_cast<const uint32_t*>(lds + boff + ra + S);
                 tp[j][0] = t[0]; tp[j][1] = t[1]; tp[j][2] = b[0]; tp[j][3] = b[1];
             }
 #pragma unroll
             for (int j = 0; j < kGrp; ++j) emit(full_c, f, j0 + j, tp[j][0], tp[j][1], tp[j][2], tp[j][3]);
         }
     };
-    fetch(f0, true);
+    Pre pre;
+    fetch(pre, f0, true);
     for (int f = f0; f < f1; ++f) {
         const uint32_t boff = (uint32_t)(((f - f0) & 1) * buf);
-        park(f, boff);
+        park(pre, f, boff);
         __syncthreads();  // the box of frame f is in LDS; frame f - 1's reads of the other buffer are done
-        fetch(min(f + 1, f1 - 1), f + 1 < f1);  // in flight while frame f is sampled
+        fetch(pre, min(f + 1, f1 - 1), f + 1 < f1);  // in flight while frame f is sampled
         if (tile_full) sample(full_t(), f, boff);
         else sample(edge_t(), f, boff);
     }
@@ -622,8 +629,9 @@ bool frames_layout_th(const WarpLaunch& L, WarpFramesPlan& P, int th) {
     return P.lds <= 64 * 1024;
 }
 
-// 32-row tiles (measured faster: 0.200 vs 0.222 ms at 720p rot15) unless
-// their box is over the staging budget (e.g. 45 degrees), then 16
+// 32-row tiles (measured faster: 0.200 vs 0.222 ms at 720p rot15; 24-row
+// tiles, 5 workgroups per CU, 0.200 vs 0.193) unless their box is over the
+// staging budget (e.g. 45 degrees), then 16
 bool frames_layout(const WarpLaunch& L, WarpFramesPlan& P) {
     const int th_knob = tune(VACV_TUNE_WARP_TILE_H);
     if (th_knob == 16 || th_knob == 32) return frames_layout_th(L, P, th_knob);
