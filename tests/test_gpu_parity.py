@@ -762,6 +762,23 @@ def test_warp_frames_kernel(ops, dev, oracle):
                     assert_same(gotf[k].reshape(ho, wo, c), wantf.reshape(ho, wo, c), f"frames norm c={c}")
 
 
+    # pitched sources: rows padded to a multiple of 4 bytes (the frames
+    # kernel) and a source starting 1 byte into its allocation (dword-
+    # misaligned: the gather kernels)
+    bigs = to_dev(np.zeros((n, 100, 192, 3), np.uint8), dev)  # rows of 576 bytes
+    bigs[:, 2:99, 4:147] = to_dev(imgs[:, 100:197, 300:443], dev)
+    for view, tag in ((bigs[:, 2:99, 4:147], "row-padded"),
+                      (to_dev(np.ascontiguousarray(imgs[:, 100:197, 300:443]), dev), "dense")):
+        got = host(ops.warp_affine(view, mats[0], 121, 83))
+        for k in (0, n - 1):
+            assert_same(got[k], oracle.warp_affine(np.ascontiguousarray(imgs[k, 100:197, 300:443]), mats[0], 121, 83)
+                        .reshape(83, 121, 3), f"pitched source {tag}")
+    flat = torch.zeros(n * 97 * 143 * 3 + 1, dtype=torch.uint8, device=dev)
+    mis = flat[1:].view(n, 97, 143, 3)
+    mis.copy_(to_dev(np.ascontiguousarray(imgs[:, 100:197, 300:443]), dev))
+    got = host(ops.warp_affine(mis, mats[0], 121, 83))
+    assert_same(got[n - 1], oracle.warp_affine(np.ascontiguousarray(imgs[n - 1, 100:197, 300:443]), mats[0], 121, 83)
+                .reshape(83, 121, 3), "misaligned source")
     # NCHW planes are frames of their own (3 planes x 3 images)
     from vacv_amd import NCHW
     ims = np.stack([synthetic_image(650 + k, 97, 143, 3) for k in range(3)])
