@@ -28,6 +28,7 @@
 
 #include "vacv_device.hpp"
 
+
 namespace vacv {
 namespace {
 
@@ -48,6 +49,11 @@ resize_direct_kernel(ResizeLaunch L, int blocks_per_plane, int total, int xcd) {
     constexpr int NR = ONE_ROW ? 1 : 2;                // gathered rows per pixel
     constexpr int kWavePx = 64 * PXL;
     constexpr int kOutPx = CC * (int)sizeof(TOut);    // output bytes per pixel
+    // tap gathers: the default cache policy under fp32 output, so a 128-byte
+    // source line split between two waves is re-read from L2, not HBM
+    // (headline 0.2206 -> 0.2180 ms; sc0 0.2185); non-temporal under byte
+    // output, where the default policy measured slower (0.1232 -> 0.1267 ms)
+    constexpr int kLoadAux = OUT == kOutSame ? VACV_LOAD_AUX : 0;
     __shared__ __attribute__((aligned(16))) unsigned char xch[4][kGroupPx * kOutPx];
 
     // xcd: workgroup b runs on XCD b % 8; give each XCD one contiguous eighth
@@ -109,8 +115,8 @@ resize_direct_kernel(ResizeLaunch L, int blocks_per_plane, int total, int xcd) {
         const uint32_t oa = (uint32_t)ty.i * rp32 + (uint32_t)(tx.i * CC) + srs.delta;
         const uint32_t ob = oa + rp32;
         if ((ONE_ROW ? oa : ob) + 8u <= slimit) {  // the unaligned 8 bytes in range
-            if (ONE_ROW || ty.w0) load_taps<CC, false, VACV_LOAD_AUX>(srs, oa, tap[q][0][0], tap[q][0][1]);
-            if (!ONE_ROW && ty.w1) load_taps<CC, false, VACV_LOAD_AUX>(srs, ob, tap[q][NR - 1][0], tap[q][NR - 1][1]);
+            if (ONE_ROW || ty.w0) load_taps<CC, false, kLoadAux>(srs, oa, tap[q][0][0], tap[q][0][1]);
+            if (!ONE_ROW && ty.w1) load_taps<CC, false, kLoadAux>(srs, ob, tap[q][NR - 1][0], tap[q][NR - 1][1]);
         } else {
             // the plane's last pixels: an 8-byte load overhanging the end of
             // the buffer would read as zeros, so take the 2*CC bytes singly
