@@ -78,3 +78,53 @@ def test_global_stats_allreduce_gloo(n_images):
     for rank, m, s, count in res:
         assert count == n_images * 48 * 64
         assert np.array_equal(m, want_m) and np.array_equal(s, want_s), rank
+
+
+def _gpu_worker(rank, world, port, images, out_q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, os.path.join(repo, "arm-neon-opencv_amd"))
+    import torch.distributed as dist
+    from vacv_amd import ops
+    from vacv_amd.dist import allreduce_sums, shard_range, stats_from_moments
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dev = torch.device("cuda:0")  # both ranks on the one card of the box
+    b, e = shard_range(len(images), rank, world)
+    shard = torch.from_numpy(np.stack(images[b:e])).to(dev)
+    # vacv_channel_sums of this rank's shard on the GPU, all-reduced
+    local = ops.channel_sums(shard, per_image=False)[0].cpu()
+    h, w = images[0].shape[:2]
+    total, count = allreduce_sums(local, float((e - b) * h * w))
+    mean, std = stats_from_moments(total, count)
+    # the single-process answer: the whole batch on this rank's GPU
+    full = ops.channel_sums(torch.from_numpy(np.stack(images)).to(dev), per_image=False)[0].cpu()
+    fm, fs = stats_from_moments(full, float(len(images) * h * w))
+    out_q.put((rank, mean.numpy(), std.numpy(), count, bool(torch.equal(total, full)),
+               bool(torch.equal(mean, fm) and torch.equal(std, fs))))
+    dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_global_stats_two_ranks_on_gpu():
+    """The exchange step on real kernels: two ranks (gloo, both on cuda:0)
+    each reduce their shard with vacv_channel_sums on the GPU and all-reduce
+    the fp64 sums; the result equals the whole batch's sums on one rank
+    (exact: integer-valued fp64) and the oracle's exact mean / stddev."""
+    from oracle import Oracle, synthetic_image
+    images = [synthetic_image(700 + k, 90, 160, 3) for k in range(7)]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_gpu_worker, args=(r, 2, port, images, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=180) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    O = Oracle()
+    want_m, want_s = O.mean_stddev_exact(np.concatenate([im.reshape(-1, 3) for im in images])[None])
+    for rank, m, s, count, same_sums, same_stats in res:
+        assert count == 7 * 90 * 160
+        assert same_sums and same_stats, rank
+        assert np.array_equal(m, want_m) and np.array_equal(s, want_s), rank
