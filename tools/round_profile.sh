@@ -10,6 +10,9 @@
 #   5. tools/kbench.py over every operator (HIP events) and its rocprofv3
 #      --kernel-trace --stats summary
 # Every GPU step has its own time limit; the script stops at the first failure.
+# Only gpurun_out/ travels back from the GPU box: afterwards copy
+# gpurun_out/pmc_<workload>.json to profiles/ (bench.py's roofline.traffic)
+# and the <tag>_* files you keep.
 set -o pipefail
 T=${1:-rXX}
 R=$(pwd)
