@@ -81,7 +81,8 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(OUT
 resize_strip_kernel(ResizeLaunch L, int strips_x, int groups, int rows_per_group, int ring, int stride, int dst_al,
                     int total) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform, and said so
     // XCD-contiguous order: neighbouring strips share the 128-byte lines at
     // their edges; on one XCD those come from one L2
     const int per_xcd = (total + 7) / 8;
@@ -182,20 +183,37 @@ resize_strip_kernel(ResizeLaunch L, int strips_x, int groups, int rows_per_group
         hi_row = tap_of<MODE>(y1, L.src.h, H, L.scale_yf, L.scale_yd).i + 1;  // <= h - 1 (linear_tap)
     };
 
+    // a batch's vertical taps, computed once per workgroup (lanes 0 .. BR - 1
+    // of wave 0) into a table after the ring, one per batch parity: per row
+    // the ring offsets of its two source rows and its weight pair (16 bytes).
+    // Each wave computing its own rows' taps cost ~25 VALU per output row.
+    unsigned char* rtab = lds + ring * stride + 16;
+    auto put_rows = [&](int b) {
+        if (tid < BR) {
+            const int oy = min(oy_begin + b * BR + tid, H - 1);
+            const FixedTap ty = tap_of<MODE>(oy, L.src.h, H, L.scale_yf, L.scale_yd);
+            *reinterpret_cast<uint4*>(rtab + ((b & 1) * BR + tid) * 16) =
+                make_uint4(slot((uint32_t)ty.i) * (uint32_t)stride, slot((uint32_t)ty.i + 1u) * (uint32_t)stride,
+                           (uint32_t)ty.w0 | ((uint32_t)ty.w1 << 16), 0u);
+        }
+    };
+
     const int batches = (oy_end - oy_begin + BR - 1) / BR;
     if (batches <= 0) return;  // uniform
     int lo_row, hi_row;
     rows_of(0, lo_row, hi_row);
     fetch(lo_row, hi_row);
+    put_rows(0);
     int loaded = hi_row;
     for (int b = 0; b < batches; ++b) {
         park();
-        __syncthreads();
+        __syncthreads();  // batch b's rows and taps are in LDS; batch b - 1's reads are done
         if (b + 1 < batches) {  // the next batch's new rows, in flight while this one blends
             int l1, h1;
             rows_of(b + 1, l1, h1);
             fetch(max(l1, loaded + 1), h1);
             loaded = max(loaded, h1);
+            put_rows(b + 1);
         }
         // ---- blend: wave w takes rows w, w + 4, ... of the batch, 2 at a time ---
 #pragma unroll
@@ -203,11 +221,10 @@ resize_strip_kernel(ResizeLaunch L, int strips_x, int groups, int rows_per_group
             uint32_t wyv[2], ra[2], rb[2];
 #pragma unroll
             for (int j = 0; j < 2; ++j) {
-                const int oy = min(oy_begin + b * BR + 8 * g + wave + 4 * j, H - 1);
-                const FixedTap ty = tap_of<MODE>(oy, L.src.h, H, L.scale_yf, L.scale_yd);  // wave-uniform
-                wyv[j] = (uint32_t)ty.w0 | ((uint32_t)ty.w1 << 16);
-                ra[j] = slot((uint32_t)ty.i) * (uint32_t)stride;
-                rb[j] = slot((uint32_t)ty.i + 1u) * (uint32_t)stride;
+                const uint4 e = *reinterpret_cast<const uint4*>(rtab + ((b & 1) * BR + 8 * g + wave + 4 * j) * 16);
+                ra[j] = __builtin_amdgcn_readfirstlane(e.x);  // wave-uniform
+                rb[j] = __builtin_amdgcn_readfirstlane(e.y);
+                wyv[j] = __builtin_amdgcn_readfirstlane(e.z);
             }
 #pragma unroll
             for (int q = 0; q < PXL; ++q) {
@@ -274,7 +291,7 @@ bool strip_plan(const ResizeLaunch& L, StripPlan& p) {
     if (ring >= 256 || L.src.h >= (1 << 16)) return false;
     p.stride = chunks * 16;
     p.ring = ring;
-    p.lds = ring * p.stride + 16;  // + the last tap dword's overhang
+    p.lds = ring * p.stride + 16 + 2 * p.br * 16;  // + the last tap dword's overhang, the row-tap tables
     if (p.lds > kMaxLds) return false;
     p.strips_x = (L.dst.w + p.sw - 1) / p.sw;
     // enough workgroups for the chip: split the rows when the strips are few
