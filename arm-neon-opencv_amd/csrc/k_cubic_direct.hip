@@ -71,12 +71,18 @@ cubic_direct_kernel(ResizeLaunch L, int blocks_per_plane) {
         const int d = x_first + j * 64 + lane;
         const int dy = wide ? (d >= W ? 1 : 0) : d / W;
         const int x = wide ? (dy ? d - W : d) : d - dy * W;
-        const int tyi = wide ? (dy ? ty1.i : ty0.i) : cubic_tap(y_first + dy, L.src.h, L.scale_yd).i;
+        const CubicTap tyn = wide ? (dy ? ty1 : ty0) : cubic_tap(y_first + dy, L.src.h, L.scale_yd);
         const int txi = cubic_tap(x, L.src.w, L.scale_xd).i;
-        const uint32_t o0 = (uint32_t)(tyi - 1) * rp + (uint32_t)((txi - 1) * CC) + srs.delta;
+        const uint32_t o0 = (uint32_t)(tyn.i - 1) * rp + (uint32_t)((txi - 1) * CC) + srs.delta;
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
             const uint32_t a4 = (o0 + (uint32_t)r * rp) & ~3u;
+            // a tap row of weight 0 (every 7th output row of 1440 -> 224 has
+            // three: f = 0 exactly) is not read.  Its term is h * 0 in the
+            // reference and 0 * 0 here: both zeros, and a zero addend leaves
+            // the sum's bits alone (x + 0 = x; an all-zero sum is +0 either
+            // way, since the row of weight 1 contributes +0).
+            if (tyn.c[r] == 0.f) continue;
             if (a4 + 16u <= slimit) {
                 const auto v = __builtin_amdgcn_raw_buffer_load_b128(srs.r, (int)a4, 0, VACV_LOAD_AUX);
                 ch[j][r][0] = v[0];
