@@ -197,15 +197,20 @@ void area_up_tab(int n_in, int n_out, double scale, double inv, std::vector<int>
 }
 
 struct CachedTabs {
+    int device = 0;  // owner of dev
     void* dev = nullptr;
     AreaTabsDev t{};
 };
 std::mutex g_area_mu;
-std::map<std::tuple<int, int, int, int, int, double, double, int>, CachedTabs> g_area_tabs;
+// keyed by device first: the C++ layer leases any device, and a table lives on one
+std::map<std::tuple<int, int, int, int, int, int, double, double, int>, CachedTabs> g_area_tabs;
+bool free_tabs(CachedTabs& c) { return hipFree(c.dev) == hipSuccess; }
 
 int area_tables(const ResizeLaunch& R, double inv_x, double inv_y, bool up, int cc, hipStream_t s,
                 AreaTabsDev& out) {
-    const auto key = std::make_tuple(R.src.w, R.src.h, R.dst.w, R.dst.h, cc, inv_x, inv_y, (int)up);
+    int device = 0;
+    if (hipGetDevice(&device) != hipSuccess) return VACV_ERR_HIP;
+    const auto key = std::make_tuple(device, R.src.w, R.src.h, R.dst.w, R.dst.h, cc, inv_x, inv_y, (int)up);
     std::lock_guard<std::mutex> lk(g_area_mu);
     auto it = g_area_tabs.find(key);
     if (it == g_area_tabs.end()) {
@@ -244,12 +249,10 @@ int area_tables(const ResizeLaunch& R, double inv_x, double inv_y, bool up, int 
             o[10] = put(uya.data(), uya.size() * 4);
             o[11] = put(uyi.data(), uyi.size() * 4);
         }
-        if (g_area_tabs.size() > 64) {  // bounded cache
-            (void)hipDeviceSynchronize();
-            for (auto& kv : g_area_tabs) (void)hipFree(kv.second.dev);
-            g_area_tabs.clear();
-        }
+        if (g_area_tabs.size() > 64)  // bounded cache
+            (void)evict_device_cache(g_area_tabs, free_tabs);
         CachedTabs c;
+        c.device = device;
         if (hipMalloc(&c.dev, img.size() + 16) != hipSuccess) return VACV_ERR_NO_MEMORY;
         // one upload per geometry; synchronised so any stream may use it next
         if (hipMemcpyAsync(c.dev, img.data(), img.size(), hipMemcpyHostToDevice, s) != hipSuccess ||
@@ -325,12 +328,7 @@ int launch_resize_area_general(const ResizeLaunch& R, double inv_x, double inv_y
 
 int release_area_tables() {
     std::lock_guard<std::mutex> lk(g_area_mu);
-    int st = VACV_OK;
-    if (!g_area_tabs.empty() && hipDeviceSynchronize() != hipSuccess) st = VACV_ERR_HIP;
-    for (auto& kv : g_area_tabs)
-        if (hipFree(kv.second.dev) != hipSuccess) st = VACV_ERR_HIP;
-    g_area_tabs.clear();
-    return st;
+    return evict_device_cache(g_area_tabs, free_tabs);
 }
 
 }  // namespace vacv

@@ -408,8 +408,10 @@ namespace {
 // = sum_kappa A[r][kappa] * B[kappa][x] where A is the image block (rows r,
 // columns cn*x0 + kappa) and B the Toeplitz matrix B[kappa][x] = b(yy,
 // kappa - cn*x) (0 outside [0, K)).  Then sum a*b = 16*D_hi + D_lo + 128*T, T
-// = the template's byte sum -- exact in int32 (|16*D_hi| <= 2^31 / 2 for
-// K*h <= 2^20 / 2).  v_mfma_i32_32x32x32_i8, a wave owns 32 x 32 outputs; B
+// = the template's byte sum.  Each accumulator is exact in int32: |D_hi|,
+// |D_lo| <= 128 * 15 * K*h < 2^31 for K*h <= 2^19 (match_mfma_plan's guard);
+// the recombination, up to 255^2 * K*h, is done in int64.
+// v_mfma_i32_32x32x32_i8, a wave owns 32 x 32 outputs; B
 // depends only on (yy, kappa - cn*x), so its fragments are built once per
 // launch (match_bfrag_kernel) and read from L2 by every wave.
 typedef int v4i __attribute__((ext_vector_type(4)));
@@ -514,15 +516,16 @@ __global__ void __launch_bounds__(kBlock) match_corr_mfma_kernel(MatchLaunch M, 
             acc_lo = __builtin_amdgcn_mfma_i32_32x32x32_i8(a, b_lo, acc_lo, 0, 0, 0);
         }
     }
-    const int t128 = 128 * *tsum;
+    const int64_t t128 = 128 * (int64_t)*tsum;  // T <= 255 * K*h: past int32 once multiplied
     const int x = x0 + ni * 32 + i;
     if (x >= M.rw) return;
 #pragma unroll
     for (int reg = 0; reg < 16; ++reg) {
         const int r = r0 + mi * 32 + (reg & 3) + 8 * (reg >> 2) + 4 * h;
         if (r >= M.rh) continue;
-        const int d = 16 * acc_hi[reg] + acc_lo[reg] + t128;
-        reinterpret_cast<float*>(M.res + (int64_t)img * M.res_pitch + (int64_t)r * M.res_row)[x] = (float)d;
+        // the recombined sum is up to 255^2 * K * th: int64 (each accumulator stays in int32, see above)
+        const int64_t d = 16 * (int64_t)acc_hi[reg] + (int64_t)acc_lo[reg] + t128;
+        reinterpret_cast<float*>(M.res + (int64_t)img * M.res_pitch + (int64_t)r * M.res_row)[x] = (float)(double)d;
     }
 }
 

@@ -655,15 +655,20 @@ bool warp_frames_plan(const WarpLaunch& L, WarpFramesPlan& P) {
     if (L.out != kOutSame && !al4(L.dst)) return false;  // float stores
     for (int i = 0; i < 6; ++i)
         if (!std::isfinite(L.inv[i])) return false;
+    // everything frames_layout reads: the matrix, the sizes, the tile-height
+    // knob, the channel count and whether the output is bytes (the LDS
+    // layout of byte output carries the store exchange)
     struct Key {
         float inv[6];
-        int sw, sh, dw, dh, th;
+        int sw, sh, dw, dh, th, cc, bytes_out;
         bool operator<(const Key& o) const { return std::memcmp(this, &o, sizeof(Key)) < 0; }
     };
     Key k;
     std::memset(&k, 0, sizeof(k));
     std::memcpy(k.inv, L.inv, sizeof(k.inv));
     k.sw = L.src.w; k.sh = L.src.h; k.dw = L.dst.w; k.dh = L.dst.h; k.th = tune(VACV_TUNE_WARP_TILE_H);
+    k.cc = L.src.cc;
+    k.bytes_out = L.out == kOutSame ? 1 : 0;
     static std::mutex mu;
     static std::map<Key, std::pair<bool, WarpFramesPlan>> cache;
     bool ok;

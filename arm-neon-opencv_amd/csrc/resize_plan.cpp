@@ -162,6 +162,7 @@ bool evaluate_rows(const ResizeLaunch& L, const std::vector<Taps>& yt, int tile_
 }
 
 struct CachedPlan {
+    int device = 0;              // owner of dev
     void* dev = nullptr;
     void* host = nullptr;
     size_t bytes = 0;
@@ -171,6 +172,11 @@ struct CachedPlan {
 
 std::mutex g_mu;
 std::map<std::string, CachedPlan> g_plans;
+
+bool free_plan(CachedPlan& p) {
+    const bool a = hipFree(p.dev) == hipSuccess;
+    return (hipHostFree(p.host) == hipSuccess) && a;
+}
 
 template <typename T>
 void put(std::string& k, const T& v) {
@@ -328,15 +334,10 @@ int plan_resize(ResizeLaunch& L, hipStream_t stream, int rows) {
             for (int k = 0; k < L.norm.c_total; ++k)
                 for (int v = 0; v < 256; ++v) F(o_lut)[k * 256 + v] = normalize_value((float)v, L.norm.mean[k], L.norm.stdv[k]);
 
-        if (g_plans.size() > 256) {  // bounded cache
-            (void)hipDeviceSynchronize();
-            for (auto& kv : g_plans) {
-                (void)hipFree(kv.second.dev);
-                (void)hipHostFree(kv.second.host);
-            }
-            g_plans.clear();
-        }
+        if (g_plans.size() > 256)  // bounded cache
+            (void)evict_device_cache(g_plans, free_plan);
         CachedPlan cp;
+        cp.device = device;
         cp.bytes = bytes;
         cp.g = g;
         if (hipHostMalloc(&cp.host, bytes, hipHostMallocDefault) != hipSuccess) return VACV_ERR_NO_MEMORY;
@@ -396,14 +397,7 @@ void set_strips(ResizeLaunch& L, int64_t resident) {
 
 int release_plans() {
     std::lock_guard<std::mutex> lk(g_mu);
-    int st = VACV_OK;
-    if (!g_plans.empty() && hipDeviceSynchronize() != hipSuccess) st = VACV_ERR_HIP;
-    for (auto& kv : g_plans) {
-        if (hipFree(kv.second.dev) != hipSuccess) st = VACV_ERR_HIP;
-        if (hipHostFree(kv.second.host) != hipSuccess) st = VACV_ERR_HIP;
-    }
-    g_plans.clear();
-    return st;
+    return evict_device_cache(g_plans, free_plan);
 }
 
 }  // namespace vacv

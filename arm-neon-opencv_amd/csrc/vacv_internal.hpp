@@ -4,6 +4,7 @@
 
 #include <hip/hip_runtime.h>
 #include <cstdint>
+#include <set>
 
 #include "../../include/vacv_hip.h"
 
@@ -115,6 +116,25 @@ struct ResizeLaunch {
 int plan_resize(ResizeLaunch& L, hipStream_t s, int rows = 0);
 void set_strips(ResizeLaunch& L, int64_t resident_workgroups);
 int release_plans();
+
+// Frees every entry of a device-side cache whose entries record their owning
+// device (`.device`): each owner is synchronised and its allocations freed
+// with that device current; the caller's device is restored.  Returns
+// VACV_OK or VACV_ERR_HIP; the map is cleared either way.
+template <class Map, class FreeFn>
+int evict_device_cache(Map& m, FreeFn free_entry) {
+    int cur = 0, st = VACV_OK;
+    if (hipGetDevice(&cur) != hipSuccess) st = VACV_ERR_HIP;
+    std::set<int> owners;
+    for (auto& kv : m) owners.insert(kv.second.device);
+    for (int d : owners)
+        if (hipSetDevice(d) != hipSuccess || hipDeviceSynchronize() != hipSuccess) st = VACV_ERR_HIP;
+    for (auto& kv : m)
+        if (hipSetDevice(kv.second.device) != hipSuccess || !free_entry(kv.second)) st = VACV_ERR_HIP;
+    if (!m.empty() && hipSetDevice(cur) != hipSuccess) st = VACV_ERR_HIP;
+    m.clear();
+    return st;
+}
 
 hipError_t launch_resize(const ResizeLaunch& L, hipStream_t s);
 // u8 bilinear as per-pixel gathers (k_resize_direct.hip); needs no plan.

@@ -127,11 +127,13 @@ vacv_image Staging::in(const Tensor& t, int slot) {
     return describe(t, d);
 }
 
-vacv_image Staging::out(Tensor& dst, int w, int h, int c, DType dtype, DLayout layout, int slot) {
+vacv_image Staging::out(Tensor& dst, int w, int h, int c, DType dtype, DLayout layout, int slot, bool keep) {
     dst.create_on(_placement, w, h, c, dtype, layout);
     if (dst.len() > 0 && !dst.data) fail(_fn, "out of memory creating the output tensor");
     if (dst.on_device()) return describe(dst);
     void* d = _lease.scratch(slot, dst.len());
+    if (keep && dst.len() > 0)  // the scratch slot holds an earlier call's bytes: seed it with dst's
+        check_hip(_fn, hipMemcpyAsync(d, dst.data, dst.len(), hipMemcpyHostToDevice, _lease.stream()));
     _d2h.push_back({dst.data, d, dst.len()});
     _keep.push_back(dst);
     return describe(dst, d);

@@ -74,7 +74,9 @@ public:
     Staging(const Staging&) = delete;
     Staging& operator=(const Staging&) = delete;
     vacv_image in(const Tensor& t, int slot);
-    vacv_image out(Tensor& dst, int w, int h, int c, DType dtype, DLayout layout, int slot);
+    /// keep = the kernel reads dst's current bytes (BORDER_TRANSPARENT): a
+    /// host dst is first copied into its device scratch
+    vacv_image out(Tensor& dst, int w, int h, int c, DType dtype, DLayout layout, int slot, bool keep = false);
     /// fail loudly on a non-OK status from the C ABI
     void run(int status) { check(_fn, status); }
     void finish();

@@ -106,7 +106,9 @@ void warp_into(const char* fn, const Tensor& src, Tensor& dst, const float* m, V
     const double border[4] = {bv.v0, bv.v1, bv.v2, bv.v3};
     Staging st(fn, src);
     const vacv_image s = st.in(src, 0);
-    const vacv_image d = st.out(dst, dsize.w, dsize.h, src.c, normalize ? FP32 : src.dtype, src.layout, 1);
+    // BORDER_TRANSPARENT keeps dst's bytes where the sampler has no taps
+    const vacv_image d = st.out(dst, dsize.w, dsize.h, src.c, normalize ? FP32 : src.dtype, src.layout, 1,
+                                borderMode == BORDER_TRANSPARENT);
     if (normalize) {
         st.run(vacv_warp_affine_normalize(&s, &d, m, flags, borderMode, border, stats->m(), stats->s(),
                                           st.stream()));
@@ -276,13 +278,20 @@ void resize(const std::vector<Tensor>& src, std::vector<Tensor>& dst, VSize dsiz
     static const char* fn = "va_cv::resize";
     check_batch(fn, src, dst);
     const DType out = resize_out_dtype(fn, src[0], interpolation);
-    if (dsize.w < 1 || dsize.h < 1) fail(fn, "dsize must be positive");
-    (void)fx;
-    (void)fy;
+    // dsize = 0 with fx, fy: cv::resize's form, per frame (see the single-frame overload)
+    const bool scaled = dsize.w == 0 && dsize.h == 0 && fx > 0 && fy > 0 &&
+                        (interpolation == INTER_NEAREST || interpolation == INTER_AREA);
+    std::vector<VSize> sizes(src.size(), dsize);
+    if (scaled)
+        for (size_t i = 0; i < src.size(); ++i)
+            sizes[i] = VSize(static_cast<int>(std::nearbyint(src[i].w * fx)), static_cast<int>(std::nearbyint(src[i].h * fy)));
+    for (const VSize& z : sizes)
+        if (z.w < 1 || z.h < 1) fail(fn, "dsize must be positive");
     FramePipeline p(fn, detail::compute_device(src[0]));
     for (size_t i = 0; i < src.size(); ++i)
-        p.frame(src[i], dst[i], dsize.w, dsize.h, src[i].c, out, src[i].layout,
+        p.frame(src[i], dst[i], sizes[i].w, sizes[i].h, src[i].c, out, src[i].layout,
                 [&](const vacv_image& s, const vacv_image& d, hipStream_t st) {
+                    if (scaled) return vacv_resize_scaled(&s, &d, interpolation, VACV_LINEAR_REFERENCE, fx, fy, st);
                     return vacv_resize(&s, &d, interpolation, VACV_LINEAR_REFERENCE, st);
                 });
     p.finish();

@@ -469,6 +469,15 @@ Result batch_frames_case() {
         if (std::memcmp(o2[i].data, a.data, a.len())) err += "batched resize differs; ";
         if (std::memcmp(o3[i].data, b.data, b.len())) err += "batched warp differs; ";
     }
+    // dsize = 0 with fx / fy (cv::resize's form) through the batched overload
+    std::vector<Tensor> o4;
+    va_cv::resize(src, o4, VSize(0, 0), 0.5, 0.25, INTER_AREA);
+    for (int i = 0; i < n; ++i) {
+        Tensor a;
+        va_cv::resize(src[i], a, VSize(0, 0), 0.5, 0.25, INTER_AREA);
+        if (o4[i].w != 960 || o4[i].h != 270 || a.len() != o4[i].len() || std::memcmp(o4[i].data, a.data, a.len()))
+            err += "batched fx/fy resize differs; ";
+    }
     std::vector<Tensor> dev(n), od;
     for (int i = 0; i < n; ++i) dev[i] = src[i].to_device(0);
     va_cv::resize_normalize(dev, od, VSize(640, 360), 0, 0, INTER_LINEAR, tm, ts);
@@ -611,6 +620,24 @@ Result tensor_semantics_case() {
                     const int want_v = (sum + 2) >> 2;  // ResizeAreaFastVec fast_mode: half up
                     if (d[(y * 160 + x) * 3 + k] != want_v) { err += "INTER_AREA value; "; y = 90; x = 160; break; }
                 }
+    }
+    {
+        // BORDER_TRANSPARENT on a host dst: pixels without taps keep dst's
+        // bytes, not whatever an earlier call left in the device scratch slot
+        const float mv[6] = {0.6f, 0.1f, -60.f, -0.1f, 0.6f, 30.f};  // much of the output maps outside
+        Tensor M(3, 2, 1, FP32, NHWC);
+        std::memcpy(M.data, mv, sizeof(mv));
+        Tensor stale;
+        va_cv::warp_affine(img, stale, M, VSize(320, 180));  // fills the scratch slot with other bytes
+        Tensor keep(320, 180, 3, INT8, NHWC);
+        std::memset(keep.data, 77, keep.len());
+        std::vector<unsigned char> want(keep.len(), 77);
+        float inv[6];
+        oracle_invert_affine(mv, inv);
+        oracle_warp_affine_u8((const uint8_t*)img.data, img.w, img.h, 3, want.data(), 320, 180, inv);
+        va_cv::warp_affine(img, keep, M, VSize(320, 180), INTER_LINEAR, BORDER_TRANSPARENT);
+        if (keep.on_device() || std::memcmp(keep.data, want.data(), want.size()) != 0)
+            err += "BORDER_TRANSPARENT on a host dst lost dst's bytes; ";
     }
     try {
         Tensor o;

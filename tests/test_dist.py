@@ -104,6 +104,63 @@ def _gpu_worker(rank, world, port, images, out_q):
     dist.destroy_process_group()
 
 
+def _rccl_worker(port, images, out_q):
+    """One rank over the "nccl" backend (RCCL on ROCm), in a fresh process:
+    the cfg5 exchange exactly as bench.py's cubic_stats step runs it --
+    vacv_channel_sums of the shard on the device, all_reduce(SUM) of the fp64
+    device tensor over RCCL, vacv_stats_from_sums -- with no host round trip."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, os.path.join(repo, "arm-neon-opencv_amd"))
+    try:
+        import torch.distributed as dist
+        dev = torch.device("cuda:0")
+        torch.cuda.set_device(dev)
+        dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
+        from vacv_amd import ops
+        backend = dist.get_backend()
+        batch = torch.from_numpy(np.stack(images)).to(dev)
+        local = ops.channel_sums(batch, per_image=False)  # (1, c, 2) fp64 on the device
+        sums = local.clone()
+        dist.all_reduce(sums, op=dist.ReduceOp.SUM)
+        h, w = images[0].shape[:2]
+        mean, std = ops.stats_from_sums(sums, float(len(images) * h * w))
+        torch.cuda.synchronize()
+        out_q.put((backend, str(sums.device), bool(torch.equal(sums, local)), sums.cpu().numpy(),
+                   mean.cpu().numpy(), std.cpu().numpy()))
+        dist.destroy_process_group()
+    except Exception as e:  # report, do not hang the parent on q.get
+        out_q.put(("error", repr(e)))
+        raise
+
+
+@pytest.mark.gpu
+def test_global_stats_rccl_one_rank():
+    """The design's only collective (cfg5's global mean/stddev)
+    on RCCL itself: init_process_group("nccl") in a freshly spawned process,
+    all_reduce of vacv_channel_sums' fp64 device output, vacv_stats_from_sums.
+    At world size 1 the all-reduce must return the local sums unchanged, and
+    the statistics must equal the oracle's exact mean / stddev bit for bit."""
+    from oracle import Oracle, synthetic_image
+    images = [synthetic_image(710 + k, 96, 160, 3) for k in range(5)]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_rccl_worker, args=(_free_port(), images, q))
+    p.start()
+    res = q.get(timeout=180)
+    p.join(timeout=60)
+    assert res[0] != "error", res
+    assert p.exitcode == 0
+    backend, device, unchanged, sums, mean, std = res
+    assert backend == "nccl" and device == "cuda:0"
+    assert unchanged, "all_reduce at world size 1 changed the sums"
+    O = Oracle()
+    flat = np.concatenate([im.reshape(-1, 3) for im in images])
+    assert np.array_equal(sums.reshape(-1), O.channel_sums(flat[None])), "sums exact"
+    want_m, want_s = O.mean_stddev_exact(flat[None])
+    assert np.array_equal(mean[0], want_m) and np.array_equal(std[0], want_s)
+
+
 @pytest.mark.gpu
 def test_global_stats_two_ranks_on_gpu():
     """The exchange step on real kernels: two ranks (gloo, both on cuda:0)

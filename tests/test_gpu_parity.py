@@ -597,6 +597,75 @@ def test_warp_affine_config_and_harness(ops, dev, oracle, golden):
     assert_same(got[1], want, "warp_affine_normalize")
 
 
+def test_warp_cfg4_as_benchmarked(ops, dev, oracle, golden):
+    """cfg4 exactly as `bench.py --workload warp` runs it: 720p u8 frames,
+    rotation 15 / scale 0.9 about (640, 360), default dispatch (the frames
+    kernel with its default frames per workgroup: 128 frames are full groups,
+    131 leave a partial last group).  Frame 0 is the reference's own
+    1280x720.jpg and must give the cfg4 digest made by the reference's
+    warp_affine_naive (warp_affine_naive.cpp:9-58); frames 1, 63, 64, 127 and
+    130 are compared with the oracle; the whole batch with the per-pixel
+    gather kernel (VACV_TUNE_WARP_KERNEL = 0); the fused normalize likewise."""
+    import torch
+    meta, _ = golden
+    d = meta["digests"]
+    b720 = load_bgr("1280x720.jpg")
+    if sha(b720) != d["input_1280x720"]["sha256"]:
+        pytest.skip("PIL decodes differently here")
+    rot = ops.rotation_matrix(0.9, 15.0, (640, 360, 640, 360))
+    g = torch.Generator(device=dev)
+    g.manual_seed(1234)
+    for n in (128, 131):
+        src = torch.randint(0, 256, (n, 720, 1280, 3), dtype=torch.uint8, device=dev, generator=g)
+        src[0].copy_(to_dev(b720, dev))
+        dst = torch.empty_like(src)
+        ops.warp_affine(src, rot, 1280, 720, out=dst)  # the bench call
+        got = host(dst)
+        assert sha(got[0]) == d["cfg4_warp_1280x720_rot15_u8"]["sha256"], f"cfg4 digest, batch {n}"
+        for k in (1, 63, 64, 127, 130):
+            if k < n:
+                assert_same(got[k], oracle.warp_affine(host(src[k]), rot, 1280, 720), f"cfg4 frame {k} of {n}")
+        with ops.tuning(WARP_KERNEL=0):
+            want = ops.warp_affine(src, rot, 1280, 720)
+        assert torch.equal(dst, want), f"cfg4 batch {n}: frames kernel vs gather kernel"
+        del want
+        gotn = ops.warp_affine_normalize(src, rot, 1280, 720, MEAN, STD)
+        for k in (0, 64, n - 1):
+            wn = oracle.normalize(oracle.u8_to_f32(got[k]), MEAN, STD)
+            assert_same(host(gotn[k]), wn, f"cfg4 normalize frame {k} of {n}")
+        with ops.tuning(WARP_KERNEL=0):
+            assert torch.equal(gotn, ops.warp_affine_normalize(src, rot, 1280, 720, MEAN, STD)), \
+                f"cfg4 normalize batch {n}"
+        del src, dst, gotn
+        torch.cuda.empty_cache()
+
+
+def test_warp_frames_plan_cache_keys(ops, dev, oracle):
+    """The frames kernel's LDS plan depends on the channel count and on the
+    output kind (byte output adds a store-exchange area).  Calls that share a
+    matrix and sizes but differ in those must not share a plan: fp32 output
+    first, then u8 output; 1 channel first, then 4; each compared with the
+    gather kernel at 720p x 8 frames (full-size tiles, many workgroups per CU)."""
+    import torch
+    rng = np.random.default_rng(77)
+    for a, (first, then) in enumerate([(("norm", 3), ("u8", 3)), (("u8", 1), ("u8", 4)), (("f32", 4), ("u8", 4))]):
+        m = ops.rotation_matrix(0.9, 11.0 + a + 0.37, (640, 360, 640, 360))  # a matrix no other test uses
+        for kind, c in (first, then):
+            src = to_dev(rng.integers(0, 256, (8, 720, 1280, c), dtype=np.uint8), dev)
+            mu = np.concatenate([MEAN, [1.0]]).astype(np.float32)[:c]
+            sd = np.concatenate([STD, [2.0]]).astype(np.float32)[:c]
+
+            def run():
+                if kind == "norm":
+                    return ops.warp_affine_normalize(src, m, 1280, 720, mu, sd)
+                s = src if kind == "u8" else src.float()
+                return ops.warp_affine(s, m, 1280, 720)
+            got = run()
+            with ops.tuning(WARP_KERNEL=0):
+                want = run()
+            assert torch.equal(got, want), f"{kind} c={c} after {first}"
+
+
 def test_match_template(ops, dev, oracle):
     """match_template (match_template.cpp:13-41 -> cv::matchTemplate; OpenCV
     2.4's six methods restated in oracle/vacv_oracle.c, parity unpinned):
@@ -645,6 +714,16 @@ def test_match_template(ops, dev, oracle):
         tp = np.ascontiguousarray(im[10:43, 20:77])
         got = host(ops.match_template(to_dev(im[None], dev), to_dev(tp, dev), 2))
         assert_same(got[0], oracle.match_template(im, tp, 2), f"match mfma c{c}")
+    # the largest sums the matrix-core plan takes: all-255 image and a
+    # 226 x 141 template (K*h = 31,866, the LDS plan's limit is about 32k;
+    # 255^2 * 31,866 = 2.07e9, next to 2^31), recombined in int64
+    sat = np.full((300, 400), 255, np.uint8)
+    stpl = np.full((141, 226), 255, np.uint8)
+    got = host(ops.match_template(to_dev(sat, dev), to_dev(stpl, dev), 2))
+    assert_same(got, oracle.match_template(sat, stpl, 2), "match mfma int32 limit")
+    assert (got == np.float32(255.0 * 255.0 * 226 * 141)).all()
+    with ops.tuning(MATCH_KERNEL=0):
+        assert_same(host(ops.match_template(to_dev(sat, dev), to_dev(stpl, dev), 2)), got, "match dot4 int32 limit")
     # minMaxIdx on a match result finds the template's position
     got = ops.match_template(to_dev(img, dev), to_dev(small, dev), 0)
     mn, mx, imn, imx = ops.min_max_idx(got)
