@@ -494,6 +494,500 @@ warp_frames_kernel(WarpLaunch L, int gx, int gy, int kf, int S, int rows_max, in
     }
 }
 
+// ---------------------------------------------------------------------------
+// warp_ring_kernel: the frames kernel with its staging moved off the
+// registers.  Boxes are copied HBM -> LDS by LDS-DMA (buffer_load_dwordx4 ...
+// lds: 16 bytes per lane straight into LDS, no VGPR destination) as raw pixel
+// bytes, into a ring of ns LDS slots, so ns - 1 frames' boxes are in flight
+// while a frame is sampled (the register-staged kernel had one, and its blend
+// and staging halves serialised on that one HBM round trip: DESIGN.md §3.3).
+// A tap row's 2 CC bytes are read as the dwords covering them and shifted
+// into place (v_alignbyte), so there is no re-spread pass either.
+//
+// Synchronisation (the compiler does not track LDS-DMA, so it is explicit):
+// every wave issues, per frame, exactly n_w DMA instructions and, per sampled
+// frame, exactly kStores stores (every store is issued, out-of-range lanes at
+// an offset past the buffer), so before frame f's barrier the wave waits for
+// vmcnt <= (ns - 2) n_w + (stores issued since frame f's DMA): its own DMA of
+// frame f has landed, the later frames' stay in flight (gfx950 retires
+// vector-memory operations in issue order).  The barrier then publishes every
+// wave's part, and frame f + ns - 1's DMA reuses the slot that frame f - 1
+// was sampled from -- every wave has consumed those reads before the barrier.
+constexpr int kRingMaxIt = 6;  // DMA instructions per wave and frame, at most (a box of 24 KiB)
+// Diagnosis builds (make EXTRA=-DVACV_RING_DBG=n LIB=... OBJ=...; tools/kbench_lib.py):
+// bit 0 no sampling and stores, bit 1 no DMA.  Results are wrong in those builds.
+#ifndef VACV_RING_DBG
+#define VACV_RING_DBG 0
+#endif
+
+// s_waitcnt vmcnt(n) lgkmcnt(0), n a uniform runtime value (clamped to 63:
+// waiting for fewer outstanding operations is always safe)
+template <int N>
+__device__ __forceinline__ void waitcnt_vm() {
+    // gfx9 encoding: vmcnt [3:0] and [15:14], expcnt [6:4] (7: none), lgkmcnt [11:8]
+    __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4));
+}
+template <int... Ns>
+__device__ __forceinline__ void wait_vm_impl(int n, std::integer_sequence<int, Ns...>) {
+    (void)((n == Ns ? (waitcnt_vm<Ns>(), true) : false) || ...);
+}
+__device__ __forceinline__ void wait_vm(int n) {
+    n = n < 0 ? 0 : (n > 63 ? 63 : n);
+    n = __builtin_amdgcn_readfirstlane(n);
+    wait_vm_impl(n, std::make_integer_sequence<int, 64>());
+}
+
+typedef __attribute__((address_space(3))) void lds_void;
+
+// L: launch block; gx, gy: tiles per frame; kf: frames per workgroup; S: LDS
+// bytes per staged row (a multiple of 16); rows_max: staged rows per slot;
+// ns, slot: LDS slots and their bytes; dst_al: the destination allows dword
+// (u8 out) stores; ginv = ceil(2^20 / (S / 16)) (row of chunk c = c ginv >> 20,
+// exact for c < 4096 and S / 16 <= 256).
+#ifndef VACV_RING_WPE
+#define VACV_RING_WPE 1
+#endif
+#ifndef VACV_RING_GRP
+#define VACV_RING_GRP 4  // pixels whose taps are read before their blends
+#endif
+template <int CC, int OUT, int NP, bool PLANAR>
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(VACV_RING_WPE)))
+warp_ring_kernel(WarpLaunch L, int gx, int gy, int kf, int S, int rows_max, int ns, int slot, int dst_al,
+                 uint32_t ginv) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+    constexpr int TH = 4 * NP;
+    constexpr int kAux = OUT == kOutSame ? 1 : VACV_LOAD_AUX;  // sc0 / nt, as the frames kernel
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    int* red = reinterpret_cast<int*>(lds + ns * slot);  // 4 waves x 4 ints
+    unsigned char* xch = lds + ns * slot + 64 + (tid >> 6) * (2 * 64 * CC);
+
+    const int tiles = gx * gy;
+    const int nfr = L.n * L.src.planes;
+    const int total = tiles * ((nfr + kf - 1) / kf);
+    const int per_xcd = (total + 7) / 8;
+    const int id = (int)(blockIdx.x % 8) * per_xcd + (int)(blockIdx.x / 8);
+    if (id >= total) return;  // uniform
+    const int fg = id / tiles, tile = id - fg * tiles;
+    const int by = tile / gx, bx = tile - by * gx;
+    const int f0 = fg * kf, f1 = min(f0 + kf, nfr);
+    auto frame_img = [&](int f) { return PLANAR ? f / L.src.planes : f; };
+    auto frame_off = [&](int f, const PlaneGeom& g) {
+        const int img = frame_img(f), pl = f - img * L.src.planes;
+        return PLANAR ? (int64_t)img * g.img_pitch + (int64_t)pl * g.plane_pitch : (int64_t)f * g.img_pitch;
+    };
+    const float* M = L.inv;
+    const float wlim = (float)(L.src.w - 1), hlim = (float)(L.src.h - 1);
+    const int x = bx * kFrTileW + lane;
+    const int yw = by * TH + wave * NP;
+    const uint32_t rp = (uint32_t)L.src.row_pitch;
+
+    // ---- 1. per-pixel taps, once for every frame (as warp_frames_kernel) ---
+    const float axm = M[0] * (float)x, aym = M[3] * (float)x;
+    // per pixel until the box is known: sx | sy << 16 and v0 | wa4 << 16
+    // (16 registers instead of 32 at the kernel's register peak)
+    uint32_t sxy[NP], vwa[NP], okm = 0;
+    int xmin = INT_MAX, xmax = INT_MIN, ymin = INT_MAX, ymax = INT_MIN;
+#pragma unroll
+    for (int j = 0; j < NP; ++j) {
+        const int y = yw + j;
+        // warp_affine_naive.cpp:23-24: (m0*x + m1*y) + m2, all float
+        const float fx = (axm + M[1] * (float)y) + M[2];
+        const float fy = (aym + M[4] * (float)y) + M[5];
+        // warp_affine_naive.cpp:26-39: floor(f) in [0, n-2] <=> 0 <= f < n-1
+        const bool ok = (x < L.dst.w) & (y < L.dst.h) & (fx >= 0.f) & (fx < wlim) & (fy >= 0.f) & (fy < hlim);
+        const int sx = ok ? (int)fx : 0, sy = ok ? (int)fy : 0;
+        const float ax = fx - (float)sx, ay = fy - (float)sy;
+        const uint32_t w0 = (uint32_t)(int)((1.f - ay) * 2048.f + 0.5f);
+        const uint32_t v0 = (uint32_t)(int)((1.f - ax) * 2048.f + 0.5f);
+        sxy[j] = (uint32_t)sx | ((uint32_t)sy << 16);
+        vwa[j] = ok ? (v0 | ((4u * w0) << 16)) : (2048u | (8192u << 16));
+        okm |= (uint32_t)ok << j;
+        if (ok) {
+            xmin = min(xmin, sx);
+            xmax = max(xmax, sx);
+            ymin = min(ymin, sy);
+            ymax = max(ymax, sy);
+        }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        xmin = min(xmin, __shfl_xor(xmin, o, 64));
+        xmax = max(xmax, __shfl_xor(xmax, o, 64));
+        ymin = min(ymin, __shfl_xor(ymin, o, 64));
+        ymax = max(ymax, __shfl_xor(ymax, o, 64));
+    }
+    if (lane == 0) {
+        red[4 * wave + 0] = xmin;
+        red[4 * wave + 1] = xmax;
+        red[4 * wave + 2] = ymin;
+        red[4 * wave + 3] = ymax;
+    }
+    // each slot's 16-byte head: the border pixel repeated (a border pixel
+    // reads its taps there, with weights (2048,0) x (2048,0))
+    if (tid < 4 * ns) {
+        uint32_t bp = 0;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) bp |= (uint32_t)(int)L.border[(4 * (tid & 3) + e) % CC] << (8 * e);
+        *reinterpret_cast<uint32_t*>(lds + (tid >> 2) * slot + 4 * (tid & 3)) = bp;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+        xmin = min(xmin, red[4 * w + 0]);
+        xmax = max(xmax, red[4 * w + 1]);
+        ymin = min(ymin, red[4 * w + 2]);
+        ymax = max(ymax, red[4 * w + 3]);
+    }
+    xmin = __builtin_amdgcn_readfirstlane(xmin);
+    xmax = __builtin_amdgcn_readfirstlane(xmax);
+    ymin = __builtin_amdgcn_readfirstlane(ymin);
+    ymax = __builtin_amdgcn_readfirstlane(ymax);
+    const bool any = xmax >= 0;
+    const int bx0 = any ? (xmin & ~3) : 0;                         // first staged column (bx0 * CC dword-aligned)
+    const int G = any ? ((xmax + 2 - bx0) * CC + 15) >> 4 : 0;     // 16-byte chunks per staged row
+    const int R = any ? ymax + 2 - ymin : 0;                       // staged rows ymin .. ymax + 1
+    const int Gs = S >> 4;                                         // chunks per LDS row
+    const int n_inst = (R * Gs + 63) >> 6;                         // 1 KiB DMA instructions per frame
+    const bool staged = any && G <= Gs && R <= rows_max && n_inst <= 4 * kRingMaxIt;  // uniform
+    // this wave's DMA instructions per frame: i = wave, wave + 4, ...
+    const int n_w = staged && n_inst > wave ? (n_inst - wave + 3) >> 2 : 0;
+    uint32_t rw[NP], wxp[NP];
+#pragma unroll
+    for (int j = 0; j < NP; ++j) {
+        const bool ok = (okm >> j) & 1u;
+        const int sx = (int)(sxy[j] & 0xFFFFu), sy = (int)(sxy[j] >> 16);
+        rw[j] = (ok ? (uint32_t)(16 + (sy - ymin) * S + (sx - bx0) * CC) : 0u) | (vwa[j] & 0xFFFF0000u);
+        const uint32_t v0 = vwa[j] & 0xFFFFu;  // outside: (2048, 0)
+        wxp[j] = ok ? (v0 | ((2048u - v0) << 16)) : 2048u;
+    }
+
+    // Row spans in chunks (as warp_frames_kernel, in bytes): thread t < R
+    // clips the tile's source parallelogram to the rows that tap row ymin + t.
+    // The table lives in the last slot's data, which no DMA writes before
+    // frame f0's barrier.
+    uint32_t* spans = reinterpret_cast<uint32_t*>(lds + (ns - 1) * slot + 16);  // after that slot's border head
+    if (staged && tid < R) {
+        const float X0 = (float)(bx * kFrTileW), X1 = (float)(min(bx * kFrTileW + kFrTileW, L.dst.w) - 1);
+        const float Y0 = (float)(by * TH), Y1 = (float)(min(by * TH + TH, L.dst.h) - 1);
+        float cx[4], cy[4];
+        const float px[4] = {X0, X1, X1, X0}, py[4] = {Y0, Y0, Y1, Y1};
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            cx[i] = (M[0] * px[i] + M[1] * py[i]) + M[2];
+            cy[i] = (M[3] * px[i] + M[4] * py[i]) + M[5];
+        }
+        const float r = (float)(ymin + tid), ya = r - 1.05f, yb = r + 1.05f;
+        float lo = 3.0e38f, hi = -3.0e38f;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int i2 = (i + 1) & 3;
+            if (cy[i] >= ya && cy[i] <= yb) { lo = fminf(lo, cx[i]); hi = fmaxf(hi, cx[i]); }
+#pragma unroll
+            for (int e = 0; e < 2; ++e) {
+                const float yl = e ? yb : ya;
+                if ((cy[i] - yl) * (cy[i2] - yl) < 0.f) {
+                    const float xc = cx[i] + (yl - cy[i]) / (cy[i2] - cy[i]) * (cx[i2] - cx[i]);
+                    lo = fminf(lo, xc);
+                    hi = fmaxf(hi, xc);
+                }
+            }
+        }
+        uint32_t sp = 1u;  // empty: lo = 1 > hi = 0
+        if (lo <= hi) {
+            const int clo = (int)floorf(fmaxf(lo - 0.05f, -1.0e9f)) - bx0;       // left tap column
+            const int chi = (int)floorf(fminf(hi + 0.05f, 1.0e9f)) + 1 - bx0;    // right tap column
+            if (chi >= 0 && clo * CC <= 16 * G - 1) {
+                const int glo = (max(clo, 0) * CC) >> 4, ghi = min(((chi + 1) * CC - 1) >> 4, G - 1);
+                sp = (uint32_t)glo | ((uint32_t)ghi << 16);
+            }
+        }
+        spans[tid] = sp;
+    }
+    __syncthreads();
+
+    // this lane's DMA source offsets (frame-relative), frame-independent:
+    // instruction u of this wave covers the slot's chunks 64 (wave + 4u) + lane.
+    // vm: chunks inside their row's span; tailm: those reaching past the
+    // plane's last byte (loaded bytewise after the DMA instead)
+    uint32_t goff[kRingMaxIt];
+    uint32_t vm = 0, tailm = 0;
+#pragma unroll
+    for (int u = 0; u < kRingMaxIt; ++u) {
+        goff[u] = 0;
+        if (u < n_w) {
+            const int c = 64 * (wave + 4 * u) + lane;
+            const int row = (int)(__umul24((uint32_t)c, ginv) >> 20), col = c - row * Gs;  // c / Gs
+            if (row < R && col < G) {
+                const uint32_t sp = spans[row];
+                if ((int)(sp & 0xFFFFu) <= col && col <= (int)(sp >> 16)) {
+                    goff[u] = (uint32_t)(ymin + row) * rp + (uint32_t)(bx0 * CC + 16 * col);
+                    if ((int64_t)goff[u] + 16 > L.src.plane_bytes) tailm |= 1u << u;
+                    else vm |= 1u << u;
+                }
+            }
+        }
+    }
+    // frame f's box -> slot s: n_w instructions, idle lanes out of range
+    // (an out-of-range lane writes zeros to its own 16 bytes of the slot)
+    auto dma = [&](int f, int s, bool live) {
+        if (VACV_RING_DBG & 2) return;
+        const Rsrc rs = make_rsrc(L.src.base + frame_off(min(f, nfr - 1), L.src), L.src.plane_bytes);
+        unsigned char* base = lds + s * slot + 16 + 1024 * wave;
+#pragma unroll
+        for (int u = 0; u < kRingMaxIt; ++u) {
+            if (u < n_w) {
+                const int off = (live && ((vm >> u) & 1u)) ? (int)(goff[u] + rs.delta) : (int)0x80000000;
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(rs.r, (lds_void*)(base + 4096 * u), 16, off, 0, 0, kAux);
+            }
+        }
+    };
+    // the rare chunks at the plane's end, bytewise (after frame f's DMA landed)
+    auto fix_tail = [&](int f, int s) {
+        const Rsrc rs = make_rsrc(L.src.base + frame_off(f, L.src), L.src.plane_bytes);
+#pragma unroll
+        for (int u = 0; u < kRingMaxIt; ++u) {
+            if ((tailm >> u) & 1u) {
+                uint32_t d[4];
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    uint32_t w = 0;
+#pragma unroll
+                    for (int e = 0; e < 4; ++e)
+                        w |= (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(rs.r, (int)(goff[u] + rs.delta) + 4 * q + e,
+                                                                           0, 0) << (8 * e);
+                    d[q] = w;
+                }
+                const int c = 64 * (wave + 4 * u) + lane;
+                *reinterpret_cast<u32x4*>(lds + s * slot + 16 + 16 * c) = u32x4{d[0], d[1], d[2], d[3]};
+            }
+        }
+    };
+
+    const uint32_t dpitch = (uint32_t)L.dst.row_pitch;
+    const bool tile_full = bx * kFrTileW + kFrTileW <= L.dst.w && by * TH + TH <= L.dst.h &&
+                           (OUT != kOutSame || dst_al);
+    constexpr uint32_t kOob = 0x80000000u;
+    // vector-memory stores per sampled frame, every one issued (the wait count)
+    const int n_st = (VACV_RING_DBG & 1) ? 0 : OUT != kOutSame ? NP : (tile_full ? NP / 2 : NP * CC);
+
+    auto emit = [&](auto full_c, int fv, int j, uint32_t tlo, uint32_t thi, uint32_t blo, uint32_t bhi) {
+        constexpr bool FULL = decltype(full_c)::value;
+        const int f = __builtin_amdgcn_readfirstlane(fv);
+        const int y = yw + j;
+        const bool inside = FULL || (x < L.dst.w && y < L.dst.h);
+        unsigned char* dbase = const_cast<unsigned char*>(L.dst.base) + frame_off(f, L.dst);
+        const Rsrc drs = make_rsrc(dbase, L.dst.plane_bytes);
+        const us2 wx = __builtin_bit_cast(us2, wxp[j]);
+        const uint32_t wA = rw[j] >> 16, wB = 8192u - (rw[j] >> 16);
+        uint32_t vv[CC];
+#pragma unroll
+        for (int k = 0; k < CC; ++k) {
+            // channel k of the left tap (byte k) and of the right tap (byte CC + k)
+            const uint32_t sel = (uint32_t)k | (0x0Cu << 8) | ((uint32_t)(CC + k) << 16) | (0x0Cu << 24);
+            const uint32_t top = __builtin_amdgcn_perm(thi, tlo, sel);
+            const uint32_t bot = __builtin_amdgcn_perm(bhi, blo, sel);
+            const uint32_t ht = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, top), wx, 0u, false);
+            const uint32_t hb = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, bot), wx, 0u, false);
+            vv[k] = __umul24(ht, wA) + __umul24(hb, wB);  // warp_affine_naive.cpp:50-54, x4
+        }
+        const uint32_t drow = (uint32_t)y * dpitch + drs.delta;
+        if constexpr (OUT == kOutSame) {
+            uint32_t own;
+            if constexpr (CC == 1) {
+                own = vv[0] >> 24;
+            } else if constexpr (CC == 2) {
+                own = __builtin_amdgcn_perm(vv[1], vv[0], 0x0C0C0703u);
+            } else if constexpr (CC == 3) {
+                own = __builtin_amdgcn_perm(vv[2], __builtin_amdgcn_perm(vv[1], vv[0], 0x0C0C0703u), 0x0C070100u);
+            } else {
+                own = __builtin_amdgcn_perm(__builtin_amdgcn_perm(vv[3], vv[2], 0x0C0C0703u),
+                                            __builtin_amdgcn_perm(vv[1], vv[0], 0x0C0C0703u), 0x05040100u);
+            }
+            if constexpr (FULL) {
+                const uint32_t word = quad_pack<CC>(own, lane & 3);
+                constexpr int kRowB = 64 * CC;
+                unsigned char* xw = xch + (j & 1) * kRowB;
+                if ((lane & 3) < CC) *reinterpret_cast<uint32_t*>(xw + 4 * ((lane >> 2) * CC + (lane & 3))) = word;
+                if (j & 1) {
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                    __builtin_amdgcn_wave_barrier();
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                    constexpr int kChunks = kRowB / 16;
+                    const int m = lane % (2 * kChunks);
+                    const u32x4 v = *reinterpret_cast<const u32x4*>(xch + 16 * m);
+                    const uint32_t rowoff = (uint32_t)(y - 1 + (m >= kChunks)) * dpitch + drs.delta;
+                    const uint32_t off = lane < 2 * kChunks
+                                             ? rowoff + (uint32_t)(bx * kFrTileW * CC + 16 * (m % kChunks))
+                                             : kOob;
+                    __builtin_amdgcn_raw_buffer_store_b128(v, drs.r, (int)off, 0, VACV_STORE_AUX);
+                }
+            } else {  // the edges, or a byte-aligned destination: CC byte stores, all issued
+                const uint32_t off = inside ? drow + (uint32_t)(x * CC) : kOob;
+#pragma unroll
+                for (int k = 0; k < CC; ++k)
+                    __builtin_amdgcn_raw_buffer_store_b8((unsigned char)(own >> (8 * k)), drs.r,
+                                                         (int)(inside ? off + k : kOob), 0, VACV_STORE_AUX);
+            }
+        } else {
+            u32x4 o;
+#pragma unroll
+            for (int k = 0; k < CC; ++k) {
+                const int v = (int)(vv[k] >> 24);
+                float fv;
+                if (OUT == kOutF32) {
+                    fv = (float)v;
+                } else {
+                    const int img = frame_img(f), pl = f - img * L.src.planes;
+                    const ChanNorm cn = chan_norm(L.norm, img, PLANAR ? pl : k);
+                    fv = normalize_u8v(cn, v);
+                }
+                o[k] = __builtin_bit_cast(uint32_t, fv);
+            }
+            const int off = (int)(inside ? drow + (uint32_t)(x * CC * 4) : kOob);
+            if constexpr (CC == 1) {
+                __builtin_amdgcn_raw_buffer_store_b32(o[0], drs.r, off, 0, VACV_STORE_AUX);
+            } else if constexpr (CC == 2) {
+                typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+                __builtin_amdgcn_raw_buffer_store_b64(u32x2{o[0], o[1]}, drs.r, off, 0, VACV_STORE_AUX);
+            } else if constexpr (CC == 3) {
+                typedef unsigned int u32x3 __attribute__((ext_vector_type(3)));
+                const u32x3 o3 = {o[0], o[1], o[2]};
+                __builtin_amdgcn_raw_buffer_store_b96(o3, drs.r, off, 0, VACV_STORE_AUX);
+            } else {
+                __builtin_amdgcn_raw_buffer_store_b128(o, drs.r, off, 0, VACV_STORE_AUX);
+            }
+        }
+    };
+
+    using full_t = std::integral_constant<bool, true>;
+    using edge_t = std::integral_constant<bool, false>;
+    if (!any) {
+        // uniform: no pixel of the tile taps the source (a rotated warp's
+        // corners: 80 of cfg4's 460 tiles) -- every pixel is the border value,
+        // with no staging and no per-pixel arithmetic per frame
+        auto border_byte = [&](int i) { return (uint32_t)(int)L.border[i % CC]; };
+        if constexpr (OUT == kOutSame) {
+            if (tile_full) {
+                // the 2-row store segments of the byte path, constant: built once
+                constexpr int kRowB = 64 * CC, kChunks = kRowB / 16;
+                const int m = lane % (2 * kChunks);
+                u32x4 v;
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    uint32_t w = 0;
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) w |= border_byte(16 * (m % kChunks) + 4 * q + e) << (8 * e);
+                    v[q] = w;
+                }
+                for (int fv = f0; fv < f1; ++fv) {
+                    const int f = __builtin_amdgcn_readfirstlane(fv);
+                    const Rsrc drs = make_rsrc(L.dst.base + frame_off(f, L.dst), L.dst.plane_bytes);
+#pragma unroll
+                    for (int j = 1; j < NP; j += 2) {
+                        const uint32_t rowoff = (uint32_t)(yw + j - 1 + (m >= kChunks)) * dpitch + drs.delta;
+                        const uint32_t off = lane < 2 * kChunks
+                                                 ? rowoff + (uint32_t)(bx * kFrTileW * CC + 16 * (m % kChunks))
+                                                 : kOob;
+                        __builtin_amdgcn_raw_buffer_store_b128(v, drs.r, (int)off, 0, VACV_STORE_AUX);
+                    }
+                }
+                return;
+            }
+        }
+        // the blend of the border pattern (weights (2048,0) x (2048,0))
+        uint32_t bl = 0, bh = 0;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            bl |= border_byte(e) << (8 * e);
+            bh |= border_byte(4 + e) << (8 * e);
+        }
+        for (int f = f0; f < f1; ++f) {
+            // opaque per frame: hoisting the 8 blends out of the frame loop
+            // kept them all live (103 -> 127 VGPRs for the whole kernel)
+            asm volatile("" : "+v"(bl), "+v"(bh));
+            if (OUT != kOutSame && tile_full) {  // (byte output took the path above)
+                for (int j = 0; j < NP; ++j) emit(full_t(), f, j, bl, bh, bl, bh);
+            } else {
+                for (int j = 0; j < NP; ++j) emit(edge_t(), f, j, bl, bh, bl, bh);
+            }
+        }
+        return;
+    }
+    if (!staged) {  // uniform, rare: the box is over the plan -- taps from memory
+        for (int f = f0; f < f1; ++f) {
+            const unsigned char* sp = L.src.base + frame_off(f, L.src);
+            for (int j = 0; j < NP; ++j) {
+                uint32_t tl, tr, bl, br;
+                direct_taps<CC>(L, sp, x, yw + j, tl, tr, bl, br);
+                // as a (lo, hi) byte stream: left tap's CC bytes, then the right tap's
+                uint32_t tlo, thi, blo, bhi;
+                if constexpr (CC == 4) {
+                    tlo = tl; thi = tr; blo = bl; bhi = br;
+                } else {
+                    const uint64_t t = (uint64_t)tl | ((uint64_t)tr << (8 * CC));
+                    const uint64_t b = (uint64_t)bl | ((uint64_t)br << (8 * CC));
+                    tlo = (uint32_t)t; thi = (uint32_t)(t >> 32); blo = (uint32_t)b; bhi = (uint32_t)(b >> 32);
+                }
+                emit(edge_t(), f, j, tlo, thi, blo, bhi);
+            }
+        }
+        return;
+    }
+    // A tap row's 2 CC bytes start at any byte: read the dwords that cover
+    // them (dword-aligned ds_read2_b32 / ds_read_b32 -- an unaligned
+    // ds_read_b64 is replayed at 64 cycles) and shift by the byte offset.
+    constexpr int kDw = CC == 3 ? 3 : 2;  // dwords covering 2 CC bytes at any byte offset
+    auto taps_at = [&](const unsigned char* row, uint32_t sh, uint32_t& lo, uint32_t& hi) {
+        const uint32_t* t = reinterpret_cast<const uint32_t*>(row);
+        uint32_t d[kDw];
+#pragma unroll
+        for (int q = 0; q < kDw; ++q) d[q] = t[q];
+        if constexpr (CC == 4) {
+            lo = d[0];
+            hi = d[1];
+        } else {
+            lo = __builtin_amdgcn_alignbyte(d[1], d[0], sh);
+            hi = kDw == 3 ? __builtin_amdgcn_alignbyte(d[kDw - 1], d[1], sh) : 0u;
+        }
+    };
+    auto sample = [&](auto full_c, int f, uint32_t sbase) {
+        constexpr int kGrp = VACV_RING_GRP;
+#pragma unroll
+        for (int j0 = 0; j0 < NP; j0 += kGrp) {
+            uint32_t tp[kGrp][4];
+#pragma unroll
+            for (int j = 0; j < kGrp; ++j) {
+                const uint32_t ra = rw[j0 + j] & 0xFFFFu;
+                const unsigned char* a = lds + sbase + (ra & ~3u);
+                taps_at(a, ra & 3u, tp[j][0], tp[j][1]);
+                taps_at(a + S, ra & 3u, tp[j][2], tp[j][3]);
+            }
+#pragma unroll
+            for (int j = 0; j < kGrp; ++j) emit(full_c, f, j0 + j, tp[j][0], tp[j][1], tp[j][2], tp[j][3]);
+        }
+    };
+    // prologue: frames f0 .. f0 + ns - 2 in flight
+    for (int k = 0; k < ns - 1; ++k) dma(f0 + k, k, f0 + k < f1);
+    int s = 0;
+    for (int f = f0; f < f1; ++f) {
+        // this wave's DMA of frame f has landed: later operations still in
+        // flight are the DMAs of frames f + 1 .. f + ns - 2 and the stores of
+        // the (at most ns - 1) frames sampled since frame f's DMA was issued
+        wait_vm((ns - 2) * n_w + min(f - f0, ns - 1) * n_st);
+        if (tailm) fix_tail(f, s);
+        __builtin_amdgcn_s_barrier();  // every wave's part of frame f is in; frame f - 1's reads are done
+        const int sn = s == 0 ? ns - 1 : s - 1;  // (f + ns - 1) mod ns: the slot frame f - 1 used
+        dma(f + ns - 1, sn, f + ns - 1 < f1);
+        if (!(VACV_RING_DBG & 1)) {
+            if (tile_full) sample(full_t(), f, (uint32_t)(s * slot));
+            else sample(edge_t(), f, (uint32_t)(s * slot));
+        }
+        s = s + 1 == ns ? 0 : s + 1;
+    }
+    wait_vm(0);  // no LDS-DMA may outlive the workgroup's LDS
+}
+
 template <typename K>
 int64_t frames_resident(K kernel, size_t lds) {
     static std::mutex mu;
@@ -521,15 +1015,24 @@ hipError_t launch_frames(const WarpLaunch& L, const WarpFramesPlan& P, hipStream
     if (kf <= 0) {
         // at most 8 frames per workgroup (720p rot15: 4 / 8 / 16 frames 0.225 /
         // 0.200 / 0.210 ms), fewer when that leaves < ~3 rounds of residency
-        const int64_t res = std::max<int64_t>(frames_resident(kern, (size_t)P.lds), 256);
+        const int64_t res = std::max<int64_t>(
+            P.ring ? frames_resident(warp_ring_kernel<CC, OUT, NP, PLANAR>, (size_t)P.lds)
+                   : frames_resident(kern, (size_t)P.lds),
+            256);
         const int64_t tiles = (int64_t)gx * gy;
         kf = (int)std::max<int64_t>(1, std::min<int64_t>(8, tiles * L.n * L.src.planes / (3 * res)));
     }
     const int64_t total = (int64_t)gx * gy * ((L.n * L.src.planes + kf - 1) / kf);
     if (total >= 0x7FFFFFF0LL) return hipErrorInvalidValue;
     const int64_t blocks = (total + 7) / 8 * 8;
-    hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(kBlock), (size_t)P.lds, s, L, gx, gy, kf, P.S, P.rows_max,
-                       P.buf, P.dst_al);
+    if (P.ring) {
+        const uint32_t gs = (uint32_t)(P.S / 16), ginv = ((1u << 20) + gs - 1) / gs;
+        hipLaunchKernelGGL((warp_ring_kernel<CC, OUT, NP, PLANAR>), dim3((unsigned)blocks), dim3(kBlock),
+                           (size_t)P.lds, s, L, gx, gy, kf, P.S, P.rows_max, P.ns, P.slot, P.dst_al, ginv);
+    } else {
+        hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(kBlock), (size_t)P.lds, s, L, gx, gy, kf, P.S,
+                           P.rows_max, P.buf, P.dst_al);
+    }
     return hipGetLastError();
 }
 
@@ -629,11 +1132,113 @@ bool frames_layout_th(const WarpLaunch& L, WarpFramesPlan& P, int th) {
     return P.lds <= 64 * 1024;
 }
 
+// The ring kernel's LDS row stride (bytes, a multiple of 16, >= 16 G): the
+// same search as frames_stride for its access, per tap row the 2 (3 for
+// CC = 3) dwords from byte address 16 + row S + col CC rounded down, each
+// a ds_read_b32 (bank = dword mod 32 within each half-wave).
+int ring_stride(const WarpLaunch& L, int G, int s_max) {
+    const float* M = L.inv;
+    const int CC = L.src.cc;
+    int best_s = 16 * G;
+    long best_cost = -1;
+    for (int k = 0; k < 8; ++k) {
+        const int S = 16 * (G + k);
+        if (k > 0 && S > s_max) break;
+        long cost = 0;
+        for (int yi = 1; yi <= 3; ++yi) {
+            const int y = L.dst.h * yi / 4;
+            for (int xi = 0; xi < 3; ++xi) {
+                const int x0 = std::max(0, std::min(L.dst.w - 64, (L.dst.w - 64) * xi / 2));
+                for (int half = 0; half < 2; ++half) {
+                    long a0[32];
+                    for (int l = 0; l < 32; ++l) {
+                        const int x = x0 + 32 * half + l;
+                        const float fx = (M[0] * (float)x + M[1] * (float)y) + M[2];
+                        const float fy = (M[3] * (float)x + M[4] * (float)y) + M[5];
+                        long a = 0;  // outside: the slot's border head
+                        if (fx >= 0.f && fx < (float)(L.src.w - 1) && fy >= 0.f && fy < (float)(L.src.h - 1))
+                            a = 16 + (long)(int)fy * S + (long)(int)fx * CC;
+                        a0[l] = a >> 2;
+                    }
+                    for (int q = 0; q < (CC == 3 ? 3 : 2); ++q) {  // one ds_read_b32 per covering dword
+                        int worst = 1;
+                        for (int l = 0; l < 32; ++l) {  // distinct dwords on lane l's bank
+                            int n = 0;
+                            for (int m = 0; m < 32; ++m) {
+                                if (((a0[m] - a0[l]) & 31) != 0) continue;
+                                bool first = true;
+                                for (int t = 0; t < m; ++t) first = first && a0[t] != a0[m];
+                                n += first;
+                            }
+                            worst = std::max(worst, n);
+                        }
+                        cost += worst;
+                    }
+                }
+            }
+        }
+        if (best_cost < 0 || cost < best_cost) {
+            best_cost = cost;
+            best_s = S;
+        }
+    }
+    return best_s;
+}
+
+// The ring kernel's LDS layout: rows_max as frames_layout_th; raw pixel rows
+// of G 16-byte chunks; ns slots, each a 16-byte border head and whole 1 KiB
+// DMA instructions.  ns (2-4, VACV_TUNE_WARP_SLOTS) defaults to the count
+// with the most boxes in flight per CU, (ns - 1) x resident workgroups.
+bool ring_layout_th(const WarpLaunch& L, WarpFramesPlan& P, int th) {
+    P.th = th;
+    const int CC = L.src.cc;
+    const double sx = std::fabs(L.inv[0]) * (kFrTileW - 1) + std::fabs(L.inv[1]) * (P.th - 1);
+    const double sy = std::fabs(L.inv[3]) * (kFrTileW - 1) + std::fabs(L.inv[4]) * (P.th - 1);
+    const int W = (int)std::ceil(sx * (1 + 1e-5) + 1e-3) + 6;  // + floor spread, right tap, 4-alignment
+    const int G = (W * CC + 15) / 16;
+    P.rows_max = (int)std::ceil(sy * (1 + 1e-5) + 1e-3) + 3;
+    const int extra = 64 + (L.out == kOutSame ? 4 * 2 * 64 * CC : 0);
+    auto slot_of = [&](int S) { return 16 + (P.rows_max * (S / 16) + 63) / 64 * 1024; };
+    if ((P.rows_max * G + 63) / 64 > 4 * kRingMaxIt) return false;
+    const int knob = tune(VACV_TUNE_WARP_SLOTS);
+    int best_ns = 0;
+    long best_fl = -1;
+    for (int ns = 2; ns <= 4; ++ns) {
+        if (knob >= 2 && knob <= 4 && ns != knob) continue;
+        const int lds = ns * slot_of(16 * G) + extra;
+        if (lds > 64 * 1024) continue;
+        const long fl = (long)(ns - 1) * (160 * 1024 / lds);
+        if (fl > best_fl) {
+            best_fl = fl;
+            best_ns = ns;
+        }
+    }
+    if (!best_ns) return false;
+    P.ns = best_ns;
+    // strides that keep the same resident workgroups per CU
+    const int per_cu = 160 * 1024 / (P.ns * slot_of(16 * G) + extra);
+    int s_max = 16 * G;
+    for (int S = 16 * G; S <= 16 * (G + 7); S += 16)
+        if (160 * 1024 / (P.ns * slot_of(S) + extra) >= per_cu && (P.rows_max * (S / 16) + 63) / 64 <= 4 * kRingMaxIt)
+            s_max = S;
+    P.S = ring_stride(L, G, s_max);
+    P.slot = slot_of(P.S);
+    P.buf = P.slot;
+    P.lds = P.ns * P.slot + extra;
+    P.ring = 1;
+    return P.lds <= 64 * 1024;
+}
+
 // 32-row tiles (measured faster: 0.200 vs 0.222 ms at 720p rot15; 24-row
 // tiles, 5 workgroups per CU, 0.200 vs 0.193) unless their box is over the
 // staging budget (e.g. 45 degrees), then 16
 bool frames_layout(const WarpLaunch& L, WarpFramesPlan& P) {
     const int th_knob = tune(VACV_TUNE_WARP_TILE_H);
+    if (tune(VACV_TUNE_WARP_KERNEL) == 5) {
+        if (th_knob == 16 || th_knob == 32) return ring_layout_th(L, P, th_knob);
+        return ring_layout_th(L, P, 32) || ring_layout_th(L, P, 16);
+    }
+    P.ring = 0;
     if (th_knob == 16 || th_knob == 32) return frames_layout_th(L, P, th_knob);
     return frames_layout_th(L, P, 32) || frames_layout_th(L, P, 16);
 }
@@ -643,7 +1248,7 @@ bool frames_layout(const WarpLaunch& L, WarpFramesPlan& P) {
 // time); the alignment checks are per call.
 bool warp_frames_plan(const WarpLaunch& L, WarpFramesPlan& P) {
     const int knob = tune(VACV_TUNE_WARP_KERNEL);
-    if (knob >= 0 && knob != 4) return false;
+    if (knob >= 0 && knob != 4 && knob != 5) return false;
     if (L.src.esize != 1 || L.border_mode != kBorderConstant) return false;
     if (L.src.planes > 1 && L.src.cc != 1) return false;
     if (L.src.cc < 1 || L.src.cc > 4) return false;
@@ -660,7 +1265,7 @@ bool warp_frames_plan(const WarpLaunch& L, WarpFramesPlan& P) {
     // layout of byte output carries the store exchange)
     struct Key {
         float inv[6];
-        int sw, sh, dw, dh, th, cc, bytes_out;
+        int sw, sh, dw, dh, th, cc, bytes_out, kernel, slots;
         bool operator<(const Key& o) const { return std::memcmp(this, &o, sizeof(Key)) < 0; }
     };
     Key k;
@@ -669,6 +1274,8 @@ bool warp_frames_plan(const WarpLaunch& L, WarpFramesPlan& P) {
     k.sw = L.src.w; k.sh = L.src.h; k.dw = L.dst.w; k.dh = L.dst.h; k.th = tune(VACV_TUNE_WARP_TILE_H);
     k.cc = L.src.cc;
     k.bytes_out = L.out == kOutSame ? 1 : 0;
+    k.kernel = knob;
+    k.slots = tune(VACV_TUNE_WARP_SLOTS);
     static std::mutex mu;
     static std::map<Key, std::pair<bool, WarpFramesPlan>> cache;
     bool ok;

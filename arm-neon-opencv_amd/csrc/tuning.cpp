@@ -36,6 +36,7 @@ const char* const kNames[VACV_TUNE_COUNT] = {
     "VACV_MATCH_KERNEL",       // VACV_TUNE_MATCH_KERNEL
     "VACV_WARP_FRAMES",        // VACV_TUNE_WARP_FRAMES
     "VACV_WARP_TILE_H",        // VACV_TUNE_WARP_TILE_H
+    "VACV_WARP_SLOTS",         // VACV_TUNE_WARP_SLOTS
 };
 
 struct Table {

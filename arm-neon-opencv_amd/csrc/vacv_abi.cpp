@@ -449,6 +449,53 @@ int color_impl(const vacv_image* src_d, const vacv_image* dst_d, int code, int o
     return hip_status(launch_color(L, s));
 }
 
+// The cvt_color codes the reference hands to cv::cvtColor (cvt_color.cpp:
+// 139-141), OpenCV 2.4's arithmetic (k_color_cv.hip).
+int color_cv_impl(const vacv_image* src_d, const vacv_image* dst_d, int code, hipStream_t s) {
+    Img src, dst;
+    int st = load(src_d, src);
+    if (st) return st;
+    if ((st = load(dst_d, dst))) return st;
+    if (src.layout != VACV_NHWC || dst.layout != VACV_NHWC || src.c != 1 || dst.n != src.n) return VACV_ERR_INVALID_ARG;
+    CvColorLaunch L{};
+    L.src = src.data;
+    L.src_img = src.batch;
+    L.src_row = src.row;
+    L.dst = dst.data;
+    L.dst_img = dst.batch;
+    L.dst_row = dst.row;
+    L.n = src.n;
+    L.w = src.w;
+    if (code == VACV_COLOR_GRAY2BGR) {
+        if (src.dtype != VACV_INT8 && src.dtype != VACV_FP32) return VACV_ERR_UNSUPPORTED;
+        if (dst.dtype != src.dtype || dst.w != src.w || dst.h != src.h || dst.c != 3) return VACV_ERR_INVALID_ARG;
+        if (src.es == 4 && ((src.row | dst.row | src.batch | dst.batch) % 4 ||
+                            reinterpret_cast<uintptr_t>(src.data) % 4 || reinterpret_cast<uintptr_t>(dst.data) % 4))
+            return VACV_ERR_INVALID_ARG;
+        L.gray = 1;
+        L.h = src.h;
+        L.dcn = 3;
+        L.esize = src.es;
+        return hip_status(launch_color_cv(L, s));
+    }
+    if (src.dtype != VACV_INT8 || dst.dtype != VACV_INT8) return VACV_ERR_INVALID_ARG;
+    const int h = src.h / 3 * 2;  // cvt_color.cpp:152, as cv::cvtColor's YUV420 sizes
+    if (src.w % 2 || h % 2 || h < 2 || src.h != h / 2 * 3) return VACV_ERR_INVALID_ARG;
+    L.h = h;
+    switch (code) {
+        case VACV_COLOR_YUV2RGBA_NV12: L.layout = 0; L.dcn = 4; L.bidx = 2; break;
+        case VACV_COLOR_YUV2BGRA_NV12: L.layout = 0; L.dcn = 4; L.bidx = 0; break;
+        case VACV_COLOR_YUV2RGBA_NV21: L.layout = 1; L.dcn = 4; L.bidx = 2; break;
+        case VACV_COLOR_YUV2BGRA_NV21: L.layout = 1; L.dcn = 4; L.bidx = 0; break;
+        default: L.layout = 2; L.dcn = 3; L.bidx = 0; break;  // YV12
+    }
+    if (L.layout == 2 && src.row != src.w) return VACV_ERR_INVALID_ARG;  // planar chroma: dense rows
+    if (dst.w != src.w || dst.h != h || dst.c != L.dcn) return VACV_ERR_INVALID_ARG;
+    const int al = L.dcn == 4 ? 8 : 2;
+    L.aligned = !((dst.row | dst.batch) % al) && !(reinterpret_cast<uintptr_t>(dst.data) % al);
+    return hip_status(launch_color_cv(L, s));
+}
+
 // YUV420sp -> BGR -> bilinear resize (-> fp32 / normalize) in one kernel
 // (k_yuv_resize.hip).  dst = (wo, ho, 3) NHWC or NCHW, INT8 (out_kind
 // kOutSame) or FP32.
@@ -725,7 +772,17 @@ int vacv_warp_affine(const vacv_image* src, const vacv_image* dst, const float m
 }
 
 int vacv_cvt_color(const vacv_image* src, const vacv_image* dst, int code, void* stream) {
-    return color_impl(src, dst, code, kOutSame, nullptr, (hipStream_t)stream);
+    switch (code) {
+        case VACV_COLOR_GRAY2BGR:
+        case VACV_COLOR_YUV2RGBA_NV12:
+        case VACV_COLOR_YUV2BGRA_NV12:
+        case VACV_COLOR_YUV2RGBA_NV21:
+        case VACV_COLOR_YUV2BGRA_NV21:
+        case VACV_COLOR_YUV2BGR_YV12:
+            return color_cv_impl(src, dst, code, (hipStream_t)stream);
+        default:
+            return color_impl(src, dst, code, kOutSame, nullptr, (hipStream_t)stream);
+    }
 }
 
 int vacv_normalize(const vacv_image* src_d, const vacv_image* dst_d, const float* mean, const float* stddev,

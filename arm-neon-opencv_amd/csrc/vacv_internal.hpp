@@ -179,6 +179,12 @@ struct WarpFramesPlan {
     int lds;                     // dynamic LDS per workgroup
     int kf;                      // frames per workgroup (<= 0: chosen at launch)
     int dst_al;                  // destination dword-aligned (u8 quad stores)
+    // LDS-DMA ring kernel (ring = 1): boxes kept as raw pixel bytes, S a
+    // multiple of 16; ns boxes of `slot` bytes (a 16-byte border head, then
+    // rows_max rows rounded up to whole 1 KiB DMA instructions)
+    int ring;
+    int ns;
+    int slot;
 };
 bool warp_frames_plan(const WarpLaunch& L, WarpFramesPlan& P);
 hipError_t launch_warp_frames(const WarpLaunch& L, const WarpFramesPlan& P, hipStream_t s);
@@ -220,6 +226,23 @@ struct ColorLaunch {
     NormSpec norm;
 };
 hipError_t launch_color(const ColorLaunch& L, hipStream_t s);
+
+// cv::cvtColor codes the reference delegates to OpenCV (k_color_cv.hip):
+// YUV420 -> BGR(A)/RGB(A) in OpenCV 2.4's BT.601 fixed point, GRAY -> BGR(A)
+struct CvColorLaunch {
+    const unsigned char* src;      // Y plane (or the gray image) of image 0
+    int64_t src_img, src_row;      // bytes
+    unsigned char* dst;
+    int64_t dst_img, dst_row;
+    int n, w, h;                   // output size
+    int gray;                      // 1: GRAY2BGR(A), else YUV420
+    int layout;                    // YUV: 0 NV12, 1 NV21, 2 YV12, 3 IYUV
+    int dcn;                       // 3 or 4 output channels
+    int bidx;                      // 0: BGR(A) order, 2: RGB(A)
+    int esize;                     // gray: 1 (u8) or 4 (fp32)
+    int aligned;                   // YUV: dst rows allow 8-byte (dcn 4) / 2-byte (dcn 3) stores
+};
+hipError_t launch_color_cv(const CvColorLaunch& L, hipStream_t s);
 
 // YUV420sp -> BGR -> u8 bilinear resize (-> fp32 / normalised fp32), NHWC or
 // NCHW output: the model-input pipeline of SURVEY.md §8(f)2 in one pass

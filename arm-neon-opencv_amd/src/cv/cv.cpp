@@ -155,11 +155,25 @@ void resize(const Tensor& src, Tensor& dst, VSize dsize, double fx, double fy, i
 
 void cvt_color(const Tensor& src, Tensor& dst, int code) {
     static const char* fn = "va_cv::cvt_color";
-    check_yuv_code(fn, code);
+    // the codes the reference hands to cv::cvtColor (cvt_color.cpp:139-141),
+    // with OpenCV 2.4's arithmetic: GRAY2BGR, YUV420 -> RGBA/BGRA, YV12
+    if (code == COLOR_GRAY2BGR) {
+        if ((src.dtype != INT8 && src.dtype != FP32) || src.c != 1 || src.layout != NHWC)
+            fail(fn, "COLOR_GRAY2BGR takes a (w, h, 1) INT8 or FP32 NHWC tensor");
+        Staging st(fn, src);
+        const vacv_image s = st.in(src, 0);
+        const vacv_image d = st.out(dst, src.w, src.h, 3, src.dtype, NHWC, 1);
+        st.run(vacv_cvt_color(&s, &d, code, st.stream()));
+        st.finish();
+        return;
+    }
+    const bool cv4 = code == COLOR_YUV2RGBA_NV12 || code == COLOR_YUV2BGRA_NV12 || code == COLOR_YUV2RGBA_NV21 ||
+                     code == COLOR_YUV2BGRA_NV21;
+    if (!cv4 && code != COLOR_YUV2BGR_YV12) check_yuv_code(fn, code);
     const int h = yuv_rows(fn, src);
     Staging st(fn, src);
     const vacv_image s = st.in(src, 0);
-    const vacv_image d = st.out(dst, src.w, h, 3, INT8, NHWC, 1);
+    const vacv_image d = st.out(dst, src.w, h, cv4 ? 4 : 3, INT8, NHWC, 1);
     st.run(vacv_cvt_color(&s, &d, code, st.stream()));
     st.finish();
 }

@@ -98,7 +98,10 @@ void resize(const vision::Tensor& src, vision::Tensor& dst,
 
 /// YUV420sp (w, h*3/2, 1) INT8 -> (w, h, 3) INT8 NHWC (cvt_color.cpp:137-157).
 /// COLOR_YUV2BGR_NV21 is bit-exact with nv_to_bgr_naive; NV12 and the RGB
-/// orders are also decoded.
+/// orders are also decoded.  The codes the reference hands to cv::cvtColor
+/// (cvt_color.cpp:139-141) follow OpenCV 2.4: COLOR_YUV2RGBA/BGRA_NV12/NV21
+/// -> (w, h, 4), COLOR_YUV2BGR_YV12 (planar V, U) -> (w, h, 3), and
+/// COLOR_GRAY2BGR (w, h, 1) INT8/FP32 -> (w, h, 3) of the same dtype.
 void cvt_color(const vision::Tensor& src, vision::Tensor& dst, int code);
 
 /// dst = (x - mean[k]) / (stddev[k] + 1e-6), FP32, same layout

@@ -26,6 +26,10 @@ NCHW, NHWC = 0, 1
 INTER_NEAREST, INTER_LINEAR, INTER_CUBIC, INTER_AREA = 0, 1, 2, 3
 BORDER_CONSTANT, BORDER_REPLICATE, BORDER_REFLECT, BORDER_WRAP, BORDER_REFLECT_101, BORDER_TRANSPARENT = 0, 1, 2, 3, 4, 5
 COLOR_YUV2RGB_NV12, COLOR_YUV2BGR_NV12, COLOR_YUV2RGB_NV21, COLOR_YUV2BGR_NV21 = 90, 91, 92, 93
+# the codes the reference hands to cv::cvtColor (OpenCV 2.4 arithmetic)
+COLOR_GRAY2BGR = 8
+COLOR_YUV2RGBA_NV12, COLOR_YUV2BGRA_NV12, COLOR_YUV2RGBA_NV21, COLOR_YUV2BGRA_NV21 = 94, 95, 96, 97
+COLOR_YUV2BGR_YV12 = 99
 LINEAR_REFERENCE, LINEAR_NEON, LINEAR_OPENCV = 0, 1, 2
 TM_SQDIFF, TM_SQDIFF_NORMED, TM_CCORR, TM_CCORR_NORMED, TM_CCOEFF, TM_CCOEFF_NORMED = 0, 1, 2, 3, 4, 5
 
@@ -96,7 +100,7 @@ TUNE = {"RESIZE_DIRECT": 0, "CUBIC_DIRECT": 1, "RESIZE_INTERLEAVE": 2, "RESIZE_R
         "WARP_PX": 5, "NEAREST_KERNEL": 6, "AREA_KERNEL": 7, "AREA_ROWS": 8, "COLOR_CHUNKS": 9,
         "RESIZE_WGS": 10, "RESIZE_TILE_H": 11, "RESIZE_TILE_W": 12, "RESIZE_WORK": 13, "RESIZE_ROWS_BYTES": 14,
         "WARP_KERNEL": 15, "RESIZE_STRIP": 16, "MATCH_KERNEL": 17,
-        "WARP_FRAMES": 18, "WARP_TILE_H": 19}
+        "WARP_FRAMES": 18, "WARP_TILE_H": 19, "WARP_SLOTS": 20}
 
 _lib = None
 

@@ -243,11 +243,22 @@ def _yuv_desc(yuv: torch.Tensor) -> VacvImage:
     return describe(y4.unsqueeze(-1), NHWC)
 
 
+_DCN4 = (L.COLOR_YUV2RGBA_NV12, L.COLOR_YUV2BGRA_NV12, L.COLOR_YUV2RGBA_NV21, L.COLOR_YUV2BGRA_NV21)
+
+
 def cvt_color(yuv: torch.Tensor, code: int = L.COLOR_YUV2BGR_NV21, stream=None) -> torch.Tensor:
-    """va_cv::cvt_color (cv.h:95): (n, h*3/2, w) u8 -> (n, h, w, 3) u8."""
+    """va_cv::cvt_color (cv.h:95): (n, h*3/2, w) u8 -> (n, h, w, 3) u8 (4
+    channels for the RGBA/BGRA codes; YV12 is Y then the V and U planes).
+    COLOR_GRAY2BGR: (n, h, w) u8/fp32 -> (n, h, w, 3) of the same dtype."""
+    if code == L.COLOR_GRAY2BGR:
+        g4 = yuv if yuv.dim() == 3 else yuv.unsqueeze(0)
+        out = torch.empty(tuple(g4.shape) + (3,), dtype=g4.dtype, device=yuv.device)
+        check("vacv_cvt_color", L.load().vacv_cvt_color(ctypes.byref(describe(g4.unsqueeze(-1), NHWC)),
+                                                        ctypes.byref(describe(out, NHWC)), code, _stream(stream)))
+        return out if yuv.dim() == 3 else out[0]
     y4 = yuv if yuv.dim() == 3 else yuv.unsqueeze(0)
     n, hh, w = y4.shape
-    out = torch.empty((n, hh // 3 * 2, w, 3), dtype=torch.uint8, device=yuv.device)
+    out = torch.empty((n, hh // 3 * 2, w, 4 if code in _DCN4 else 3), dtype=torch.uint8, device=yuv.device)
     check("vacv_cvt_color", L.load().vacv_cvt_color(ctypes.byref(_yuv_desc(y4)), ctypes.byref(describe(out, NHWC)),
                                                     code, _stream(stream)))
     return out if yuv.dim() == 3 else out[0]

@@ -57,7 +57,12 @@ enum {
 /* va_cv::InputImageFormat (cv.h:62-74) */
 enum {
     VACV_COLOR_YUV2RGB_NV12 = 90, VACV_COLOR_YUV2BGR_NV12 = 91,
-    VACV_COLOR_YUV2RGB_NV21 = 92, VACV_COLOR_YUV2BGR_NV21 = 93
+    VACV_COLOR_YUV2RGB_NV21 = 92, VACV_COLOR_YUV2BGR_NV21 = 93,
+    /* the codes the reference hands to cv::cvtColor (cvt_color.cpp:139-141) */
+    VACV_COLOR_GRAY2BGR = 8,
+    VACV_COLOR_YUV2RGBA_NV12 = 94, VACV_COLOR_YUV2BGRA_NV12 = 95,
+    VACV_COLOR_YUV2RGBA_NV21 = 96, VACV_COLOR_YUV2BGRA_NV21 = 97,
+    VACV_COLOR_YUV2BGR_YV12 = 99
 };
 /* Arithmetic of the u8 bilinear sampler.
  *  REFERENCE: the path the reference's public API actually dispatches to,
@@ -163,7 +168,15 @@ int vacv_invert_affine(const float m[6], float inv_out[6]);
  * NHWC.  src = (w, h*3/2, 1) INT8; dst = (w, h, 3) INT8 NHWC.  Codes:
  * COLOR_YUV2BGR_NV21 (bit-exact with nv_to_bgr_naive), COLOR_YUV2BGR_NV12
  * (correct UV order; the reference decodes it as NV21), and the two RGB
- * variants.  w and h must be even. */
+ * variants.  w and h must be even.
+ * The codes the reference hands to cv::cvtColor (cvt_color.cpp:139-141),
+ * with OpenCV 2.4's arithmetic (BT.601, 20-bit fixed point; parity
+ * unpinned):
+ *   COLOR_YUV2RGBA/BGRA_NV12/NV21  src as above, dst (w, h, 4) INT8 NHWC, alpha 255
+ *   COLOR_YUV2BGR_YV12             src = (w, h*3/2, 1) INT8 with dense rows:
+ *                                  Y, then the (w/2)x(h/2) V and U planes;
+ *                                  dst (w, h, 3) INT8 NHWC
+ *   COLOR_GRAY2BGR                 src (w, h, 1) INT8 or FP32, dst (w, h, 3) same dtype */
 int vacv_cvt_color(const vacv_image* src, const vacv_image* dst, int code, void* stream);
 
 /* ---- normalize / statistics ------------------------------------------- */
@@ -290,12 +303,13 @@ enum {
     VACV_TUNE_RESIZE_TILE_W = 12,    /* staged kernel planner: tile width */
     VACV_TUNE_RESIZE_WORK = 13,      /* staged kernel planner: work per thread */
     VACV_TUNE_RESIZE_ROWS_BYTES = 14,/* whole-row kernel planner: output bytes per workgroup */
-    VACV_TUNE_WARP_KERNEL = 15,      /* u8 CONSTANT warp: 0 per-pixel gathers, 2 batched gathers, 4 LDS-staged frames (k_warp_frames.hip) */
+    VACV_TUNE_WARP_KERNEL = 15,      /* u8 CONSTANT warp: 0 per-pixel gathers, 2 batched gathers, 4 LDS-staged frames, 5 LDS-DMA ring of frames (k_warp_frames.hip) */
     VACV_TUNE_RESIZE_STRIP = 16,     /* two-tap u8 bilinear: column strips with an LDS row ring, 1: 64 columns x 16-row batches, 2: 128 x 8; 0 staged kernel */
     VACV_TUNE_MATCH_KERNEL = 17,     /* u8 match_template correlation: 0 v_dot4 kernel, else i8 MFMA where it fits */
     VACV_TUNE_WARP_FRAMES = 18,      /* u8 CONSTANT warp, LDS-staged frames kernel: frames per workgroup */
     VACV_TUNE_WARP_TILE_H = 19,      /* u8 CONSTANT warp, LDS-staged frames kernel: tile rows (16 or 32) */
-    VACV_TUNE_COUNT = 20
+    VACV_TUNE_WARP_SLOTS = 20,       /* u8 CONSTANT warp, LDS-DMA ring kernel: source boxes in the LDS ring (2-4) */
+    VACV_TUNE_COUNT = 21
 };
 /* value < 0 restores the built-in choice.  Returns VACV_OK or INVALID_ARG. */
 int vacv_set_tuning(int key, int value);

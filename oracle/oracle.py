@@ -83,6 +83,8 @@ class Oracle:
             ("oracle_warp_affine_border", [_P, _I, _I, _I, _I, _P, _I, _I, _P, _I], None),
             ("oracle_yuv420sp_to_bgr", [_P, _P, _I, _I, _I, _I], None),
             ("oracle_bgr2nv21", [_P, _P, _I, _I], None),
+            ("oracle_yuv420_cv", [_P, _P, _I, _I, _I, _I, _I], None),
+            ("oracle_gray_to_bgr", [_P, _P, _L, _I, _I], None),
             ("oracle_hwc_to_chw", [_P, _P, _I, _I, _I, _I], None),
             ("oracle_chw_to_hwc", [_P, _P, _I, _I, _I, _I], None),
             ("oracle_u8_to_f32", [_P, _P, _L], None),
@@ -232,6 +234,27 @@ class Oracle:
         h, w = bgr.shape[:2]
         out = np.zeros((h * 3 // 2, w), np.uint8)
         self.lib.oracle_bgr2nv21(_ptr(bgr), _ptr(out), w, h)
+        return out
+
+    # cv::cvtColor codes the reference delegates to OpenCV (cvt_color.cpp:139-141)
+    CV_YUV_CODES = {94: (0, 4, 2), 95: (0, 4, 0), 96: (1, 4, 2), 97: (1, 4, 0), 99: (2, 3, 0)}
+
+    def yuv420_cv(self, yuv, code):
+        """OpenCV 2.4's YUV420 -> BGR(A)/RGB(A) for COLOR_YUV2RGBA/BGRA_NV12/NV21
+        (94-97) and COLOR_YUV2BGR_YV12 (99); yuv = (h*3/2, w) u8."""
+        layout, dcn, bidx = self.CV_YUV_CODES[code]
+        yuv = np.ascontiguousarray(yuv, np.uint8)
+        h = yuv.shape[0] // 3 * 2
+        w = yuv.shape[1]
+        out = np.zeros((h, w, dcn), np.uint8)
+        self.lib.oracle_yuv420_cv(_ptr(yuv), _ptr(out), w, h, layout, dcn, bidx)
+        return out
+
+    def gray_to_bgr(self, gray, dcn=3):
+        """cv::cvtColor COLOR_GRAY2BGR (dcn 3) / GRAY2BGRA (4), u8 or fp32."""
+        g = np.ascontiguousarray(gray)
+        out = np.zeros(g.shape[:2] + (dcn,), g.dtype)
+        self.lib.oracle_gray_to_bgr(_ptr(g), _ptr(out), g.shape[0] * g.shape[1], dcn, g.itemsize)
         return out
 
     # -- layout / dtype / crop -------------------------------------------------

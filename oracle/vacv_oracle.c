@@ -682,6 +682,73 @@ void oracle_yuv420sp_to_bgr(const uint8_t* src, uint8_t* dst, int w, int h, int 
     }
 }
 
+/* The cvt_color codes the reference hands to cv::cvtColor (cvt_color.cpp:
+ * 139-141; cv.h:62-74): OpenCV 2.4.13's YUV420 -> RGB(A) of YUV420sp2RGB8
+ * / YUV420p2RGB8 (ITU-R BT.601, 20-bit fixed point; the constants and the
+ * formula as OpenCV 2.4.13.4's own YUV2RGBA_NV12 kernel text states them,
+ * thirdparty/opencv_2.4.13.4/.../libopencv_ocl.so):
+ *   y' = max(0, Y - 16) * 1220542
+ *   R = sat((y' + 2^19 + 1673527 v) >> 20)
+ *   G = sat((y' + 2^19 - 852492 v - 409993 u) >> 20)
+ *   B = sat((y' + 2^19 + 2116026 u) >> 20),  u = U - 128, v = V - 128.
+ * layout 0: NV12 (UV pairs), 1: NV21 (VU pairs), 2: YV12 (planar: Y, then
+ * the (w/2)x(h/2) V plane, then U), 3: IYUV/I420 (Y, U, V).  dcn = 3 or 4
+ * (alpha 255); bidx = 0: BGR(A) order, 2: RGB(A).  Parity unpinned (no
+ * OpenCV runs here); w, h even. */
+void oracle_yuv420_cv(const uint8_t* src, uint8_t* dst, int w, int h, int layout, int dcn, int bidx) {
+    const uint8_t* yp = src;
+    const uint8_t* c0 = src + (int64_t)w * h;
+    const uint8_t* c1 = c0 + (int64_t)(w / 2) * (h / 2);
+    for (int y = 0; y < h; ++y) {
+        for (int x = 0; x < w; ++x) {
+            int U, V;
+            if (layout <= 1) {
+                const uint8_t* pair = c0 + (int64_t)(y / 2) * w + (x & ~1);
+                U = layout == 0 ? pair[0] : pair[1];
+                V = layout == 0 ? pair[1] : pair[0];
+            } else {
+                const int64_t k = (int64_t)(y / 2) * (w / 2) + x / 2;
+                U = layout == 2 ? c1[k] : c0[k];
+                V = layout == 2 ? c0[k] : c1[k];
+            }
+            const int u = U - 128, v = V - 128;
+            const int ruv = (1 << 19) + 1673527 * v;
+            const int guv = (1 << 19) - 852492 * v - 409993 * u;
+            const int buv = (1 << 19) + 2116026 * u;
+            int yy = (int)yp[(int64_t)y * w + x] - 16;
+            yy = (yy < 0 ? 0 : yy) * 1220542;
+            int r = (yy + ruv) >> 20, g = (yy + guv) >> 20, b = (yy + buv) >> 20;
+            r = r < 0 ? 0 : (r > 255 ? 255 : r);
+            g = g < 0 ? 0 : (g > 255 ? 255 : g);
+            b = b < 0 ? 0 : (b > 255 ? 255 : b);
+            uint8_t* o = dst + ((int64_t)y * w + x) * dcn;
+            o[bidx] = (uint8_t)b;
+            o[1] = (uint8_t)g;
+            o[2 - bidx] = (uint8_t)r;
+            if (dcn == 4) o[3] = 255;
+        }
+    }
+}
+
+/* cv::cvtColor COLOR_GRAY2BGR / GRAY2BGRA (OpenCV 2.4 Gray2RGB: the value
+ * in every colour channel, alpha = the type's maximum) for u8 (esize 1) and
+ * fp32 (esize 4, alpha 1.0). */
+void oracle_gray_to_bgr(const void* src, void* dst, int64_t pixels, int dcn, int esize) {
+    for (int64_t i = 0; i < pixels; ++i) {
+        const uint8_t* s = (const uint8_t*)src + i * esize;
+        uint8_t* d = (uint8_t*)dst + i * dcn * esize;
+        for (int k = 0; k < 3; ++k) memcpy(d + k * esize, s, esize);
+        if (dcn == 4) {
+            if (esize == 1) {
+                d[3] = 255;
+            } else {
+                const float one = 1.0f;
+                memcpy(d + 3 * esize, &one, 4);
+            }
+        }
+    }
+}
+
 /* BGR -> NV21 test-input generator, image_util.cpp:9-41 (14-bit fixed point,
  * unsigned wrap-around, VU order). */
 void oracle_bgr2nv21(const uint8_t* bgr, uint8_t* dst, int w, int h) {

@@ -62,6 +62,11 @@ void oracle_warp_affine_border(const void* src, int w_in, int h_in, int cc, int 
 /* --- colour ------------------------------------------------------------ */
 void oracle_yuv420sp_to_bgr(const uint8_t* src, uint8_t* dst, int w, int h, int v_first, int rgb_out);
 void oracle_bgr2nv21(const uint8_t* bgr, uint8_t* dst, int w, int h);
+/* cv::cvtColor's YUV420 (OpenCV 2.4 BT.601 fixed point): layout 0 NV12,
+ * 1 NV21, 2 YV12, 3 IYUV; dcn 3/4; bidx 0 BGR(A), 2 RGB(A) */
+void oracle_yuv420_cv(const uint8_t* src, uint8_t* dst, int w, int h, int layout, int dcn, int bidx);
+/* cv::cvtColor GRAY2BGR(A): esize 1 (u8) or 4 (fp32) */
+void oracle_gray_to_bgr(const void* src, void* dst, int64_t pixels, int dcn, int esize);
 
 /* --- layout / dtype / crop -------------------------------------------- */
 void oracle_hwc_to_chw(const void* src, void* dst, int w, int h, int c, int esize);

@@ -81,7 +81,11 @@ def test_argument_validation_without_device(lib):
     yuv = VacvImage(0x1000, 1, 7, 9, 1, 2, 1, 0, 0, 0)
     bgr = VacvImage(0x2000, 1, 7, 6, 3, 2, 1, 0, 0, 0)
     assert lib.vacv_cvt_color(ctypes.byref(yuv), ctypes.byref(bgr), 93, None) == -1   # odd width
-    assert lib.vacv_cvt_color(ctypes.byref(yuv), ctypes.byref(bgr), 8, None) == -2    # GRAY2BGR
+    assert lib.vacv_cvt_color(ctypes.byref(yuv), ctypes.byref(bgr), 98, None) == -2   # YUV2RGB_YV12 (not in cv.h)
+    assert lib.vacv_cvt_color(ctypes.byref(yuv), ctypes.byref(bgr), 8, None) == -1    # GRAY2BGR: dst is not (7, 9, 3)
+    rgba = VacvImage(0x2000, 1, 8, 6, 3, 2, 1, 0, 0, 0)
+    yuv8 = VacvImage(0x1000, 1, 8, 9, 1, 2, 1, 0, 0, 0)
+    assert lib.vacv_cvt_color(ctypes.byref(yuv8), ctypes.byref(rgba), 96, None) == -1  # RGBA needs 4 channels
     f = VacvImage(0x1000, 1, 8, 8, 3, 0, 1, 0, 0, 0)
     mean = (ctypes.c_float * 3)(1, 2, 3)
     assert lib.vacv_normalize(ctypes.byref(good), ctypes.byref(f), mean, None, None) == -1  # one of mean/std

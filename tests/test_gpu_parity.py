@@ -796,7 +796,14 @@ def test_warp_border_modes(ops, dev, oracle):
     assert_same(got, want, "border normalize")
 
 
-def test_warp_frames_kernel(ops, dev, oracle):
+# the LDS-staged warp kernels: register-staged frames (4) and the LDS-DMA ring
+# with 2, 3 and 4 boxes (5)
+FRAMES_VARIANTS = [dict(WARP_KERNEL=4), dict(WARP_KERNEL=5, WARP_SLOTS=2), dict(WARP_KERNEL=5, WARP_SLOTS=3),
+                   dict(WARP_KERNEL=5, WARP_SLOTS=4)]
+
+
+@pytest.mark.parametrize("variant", range(len(FRAMES_VARIANTS)))
+def test_warp_frames_kernel(ops, dev, oracle, variant):
     """The LDS-staged frames kernel (k_warp_frames.hip: per-pixel taps computed
     once for kf frames, the source box staged per frame) is the default for u8
     BORDER_CONSTANT warps (1-4 channels, NCHW planes as frames).  Against the per-pixel
@@ -806,6 +813,7 @@ def test_warp_frames_kernel(ops, dev, oracle):
     pitched destination; against the oracle at odd sizes where the source box
     reaches the plane's last bytes (the bytewise tail path)."""
     import torch
+    V = FRAMES_VARIANTS[variant]
     n = 7
     imgs = np.stack([synthetic_image(500 + k, 720, 1280, 3) for k in range(n)])
     src = to_dev(imgs, dev)
@@ -819,17 +827,18 @@ def test_warp_frames_kernel(ops, dev, oracle):
             wantn = ops.warp_affine_normalize(src, m, 1280, 720, MEAN, STD)
         for th in (16, 32):
             for kf in (1, 2, 3, 16):
-                with ops.tuning(WARP_KERNEL=4, WARP_FRAMES=kf, WARP_TILE_H=th):
+                with ops.tuning(**V, WARP_FRAMES=kf, WARP_TILE_H=th):
                     got = ops.warp_affine(src, m, 1280, 720, border_value=(7, 200, 31, 0))
                     assert torch.equal(got, want), f"frames kernel {m.tolist()} th={th} kf={kf}"
-            with ops.tuning(WARP_KERNEL=4, WARP_TILE_H=th):
+            with ops.tuning(**V, WARP_TILE_H=th):
                 assert torch.equal(ops.warp_affine_normalize(src, m, 1280, 720, MEAN, STD), wantn), \
                     f"frames kernel normalize {m.tolist()} th={th}"
     # pitched destination (dword-aligned quads and bytewise columns)
     for x0 in (4, 5):
         big = torch.zeros((n, 130, 230, 3), dtype=torch.uint8, device=dev)
         view = big[:, 3:123, x0:x0 + 200]
-        ops.warp_affine(src, mats[2], 200, 120, out=view)
+        with ops.tuning(**V):
+            ops.warp_affine(src, mats[2], 200, 120, out=view)
         g = host(big)
         for k in (0, n - 1):
             assert_same(g[k, 3:123, x0:x0 + 200], oracle.warp_affine(imgs[k], mats[2], 200, 120), f"pitched {x0}")
@@ -841,7 +850,7 @@ def test_warp_frames_kernel(ops, dev, oracle):
         sd = np.concatenate([STD, [2.0]]).astype(np.float32)[:c]
         for m in mats:
             for wo, ho in ((143, 97), (121, 83)):
-                with ops.tuning(WARP_KERNEL=4, WARP_FRAMES=2):
+                with ops.tuning(**V, WARP_FRAMES=2):
                     got = host(ops.warp_affine(to_dev(ims, dev), m, wo, ho))
                     gotf = host(ops.warp_affine_normalize(to_dev(ims, dev), m, wo, ho, mu, sd))
                 for k in range(3):
@@ -858,7 +867,8 @@ def test_warp_frames_kernel(ops, dev, oracle):
     bigs[:, 2:99, 4:147] = to_dev(imgs[:, 100:197, 300:443], dev)
     for view, tag in ((bigs[:, 2:99, 4:147], "row-padded"),
                       (to_dev(np.ascontiguousarray(imgs[:, 100:197, 300:443]), dev), "dense")):
-        got = host(ops.warp_affine(view, mats[0], 121, 83))
+        with ops.tuning(**V):
+            got = host(ops.warp_affine(view, mats[0], 121, 83))
         for k in (0, n - 1):
             assert_same(got[k], oracle.warp_affine(np.ascontiguousarray(imgs[k, 100:197, 300:443]), mats[0], 121, 83)
                         .reshape(83, 121, 3), f"pitched source {tag}")
@@ -872,7 +882,7 @@ def test_warp_frames_kernel(ops, dev, oracle):
     from vacv_amd import NCHW
     ims = np.stack([synthetic_image(650 + k, 97, 143, 3) for k in range(3)])
     chw = to_dev(np.ascontiguousarray(ims.transpose(0, 3, 1, 2)), dev)
-    with ops.tuning(WARP_KERNEL=4, WARP_FRAMES=2):
+    with ops.tuning(**V, WARP_FRAMES=2):
         got = host(ops.warp_affine(chw, mats[0], 121, 83, layout=NCHW))
         gotn = host(ops.warp_affine_normalize(chw, mats[0], 121, 83, MEAN, STD, layout=NCHW))
     for k in range(3):
@@ -1160,3 +1170,45 @@ def test_error_statuses(ops, dev):
     odd = torch.zeros((1, 9, 5), dtype=torch.uint8, device=dev)
     with pytest.raises(V.VacvError):
         ops.cvt_color(odd)
+
+
+def test_cvt_color_opencv_codes(ops, dev, oracle):
+    """The cvt_color codes the reference hands to cv::cvtColor (cvt_color.cpp:
+    139-141): NV12/NV21 -> RGBA/BGRA (94-97) and YV12 -> BGR (99) with OpenCV
+    2.4's BT.601 fixed point, GRAY2BGR (8) for u8 and fp32 -- bit-exact with
+    the oracle's restatement (parity unpinned: no OpenCV runs here), batches,
+    odd block counts, a pitched 4-channel destination (byte stores) and the
+    saturating extremes."""
+    import torch
+    from vacv_amd import (COLOR_GRAY2BGR, COLOR_YUV2BGR_YV12, COLOR_YUV2BGRA_NV12, COLOR_YUV2BGRA_NV21,
+                          COLOR_YUV2RGBA_NV12, COLOR_YUV2RGBA_NV21)
+    rng = np.random.default_rng(91)
+    for h, w in ((6, 10), (72, 130), (1080, 1920)):
+        yuv = rng.integers(0, 256, (3, h * 3 // 2, w), dtype=np.uint8)
+        yuv[0, :h // 2] = 255
+        yuv[0, h:] = 0
+        for code in (COLOR_YUV2RGBA_NV12, COLOR_YUV2BGRA_NV12, COLOR_YUV2RGBA_NV21, COLOR_YUV2BGRA_NV21,
+                     COLOR_YUV2BGR_YV12):
+            got = host(ops.cvt_color(to_dev(yuv, dev), code))
+            for k in range(3):
+                assert_same(got[k], oracle.yuv420_cv(yuv[k], code), f"cvt code {code} {w}x{h} image {k}")
+    # a pitched RGBA destination (rows not 8-byte aligned: the byte-store path)
+    yuv = rng.integers(0, 256, (2, 30, 26), dtype=np.uint8)
+    big = torch.zeros((2, 20, 31, 4), dtype=torch.uint8, device=dev)
+    view = big[:, 0:20, 1:27]
+    from vacv_amd import _lib as L
+    from vacv_amd.ops import NHWC, check, describe
+    import ctypes
+    src = to_dev(yuv, dev)
+    check("vacv_cvt_color", L.load().vacv_cvt_color(ctypes.byref(describe(src.unsqueeze(-1), NHWC)),
+                                                    ctypes.byref(describe(view, NHWC)), COLOR_YUV2BGRA_NV21, None))
+    g = host(big)
+    for k in range(2):
+        assert_same(g[k, :, 1:27], oracle.yuv420_cv(yuv[k], COLOR_YUV2BGRA_NV21), "pitched rgba")
+    g[:, :, 1:27] = 0
+    assert not g.any(), "cvt_color wrote outside the window"
+    for dt in (np.uint8, np.float32):
+        gray = (rng.integers(0, 256, (2, 37, 53)).astype(dt) * (dt(0.5) if dt == np.float32 else 1)).astype(dt)
+        got = host(ops.cvt_color(to_dev(gray, dev), COLOR_GRAY2BGR))
+        for k in range(2):
+            assert_same(got[k], oracle.gray_to_bgr(gray[k]), f"gray2bgr {dt}")

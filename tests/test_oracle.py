@@ -387,3 +387,43 @@ def test_match_template_restatement(oracle):
                     num = num / t if abs(num) < t else (np.sign(num) if abs(num) < t * 1.125 else (1 if method == 1 else 0))
                 want[y, x] = num
         np.testing.assert_allclose(got, want.astype(np.float32), rtol=2e-6, atol=1e-6, err_msg=str(method))
+
+
+def test_cv_color_restatement(oracle):
+    """cv::cvtColor codes the reference delegates to OpenCV (cvt_color.cpp:
+    139-141): YUV420sp -> RGBA/BGRA (94-97), YV12 -> BGR (99) and GRAY2BGR (8).
+    oracle/vacv_oracle.c restates OpenCV 2.4's BT.601 fixed point; here an
+    independent numpy statement of the same formula (vectorised, int64) over
+    random frames and the saturating extremes.  Parity unpinned: no OpenCV
+    runs here; the constants are those of OpenCV 2.4.13.4's own YUV2RGBA_NV12
+    kernel text."""
+    rng = np.random.default_rng(11)
+    h, w = 10, 14
+    for yuv in (rng.integers(0, 256, (h * 3 // 2, w), dtype=np.uint8),
+                np.tile(np.array([0, 255], np.uint8), (h * 3 // 2, w // 2))):
+        Y = yuv[:h].astype(np.int64)
+        for code, (layout, dcn, bidx) in oracle.CV_YUV_CODES.items():
+            if layout <= 1:
+                pairs = yuv[h:].reshape(h // 2, w // 2, 2).astype(np.int64)
+                U, V = (pairs[..., 0], pairs[..., 1]) if layout == 0 else (pairs[..., 1], pairs[..., 0])
+            else:
+                planes = yuv[h:].reshape(-1)
+                q = (h // 2) * (w // 2)
+                p0, p1 = planes[:q].reshape(h // 2, w // 2), planes[q:2 * q].reshape(h // 2, w // 2)
+                V, U = (p0, p1) if layout == 2 else (p1, p0)
+            u = np.repeat(np.repeat(U.astype(np.int64) - 128, 2, 0), 2, 1)
+            v = np.repeat(np.repeat(V.astype(np.int64) - 128, 2, 0), 2, 1)
+            yy = np.maximum(Y - 16, 0) * 1220542
+            r = np.clip((yy + (1 << 19) + 1673527 * v) >> 20, 0, 255)
+            g = np.clip((yy + (1 << 19) - 852492 * v - 409993 * u) >> 20, 0, 255)
+            b = np.clip((yy + (1 << 19) + 2116026 * u) >> 20, 0, 255)
+            want = np.zeros((h, w, dcn), np.uint8)
+            want[..., bidx], want[..., 1], want[..., 2 - bidx] = b, g, r
+            if dcn == 4:
+                want[..., 3] = 255
+            assert np.array_equal(oracle.yuv420_cv(yuv, code), want), code
+    gray = rng.integers(0, 256, (5, 7), dtype=np.uint8)
+    assert np.array_equal(oracle.gray_to_bgr(gray), np.repeat(gray[..., None], 3, 2))
+    gf = rng.standard_normal((5, 7)).astype(np.float32)
+    want4 = np.concatenate([np.repeat(gf[..., None], 3, 2), np.ones((5, 7, 1), np.float32)], 2)
+    assert np.array_equal(oracle.gray_to_bgr(gf, 4), want4)

@@ -1,8 +1,8 @@
 #!/bin/bash
 # Round-end measurement on the GPU box (run through gpurun from the repo root):
 #   tools/round_profile.sh <tag>      e.g. r02
-#   1. rocprofv3 PMC passes (tools/pmc_bench.txt) over bench.py for the
-#      headline and the warp workload -> corrected HBM bytes per launch
+#   1. rocprofv3 PMC passes (tools/pmc_bench.txt) over bench.py for every
+#      workload (its dominant kernel) -> corrected HBM bytes per launch
 #      (profiles/pmc_<workload>.json, read by bench.py as roofline.traffic)
 #   2. bench.py (the driver's command) -> gpurun_out/<tag>_bench.json
 #   3. rocprofv3 --kernel-trace --stats over the same bench.py command
@@ -19,7 +19,7 @@ R=$(pwd)
 export TMPDIR=/tmp
 mkdir -p gpurun_out
 step() { echo "=== $1 $(date +%T)"; }
-for W in resize_normalize:resize_ warp:warp_; do
+for W in resize_normalize:resize_direct warp:warp_ cvt_normalize:color_kernel cubic_stats:cubic_direct yuv_resize:yuv_resize; do
   wl=${W%%:*}; key=${W##*:}
   step "pmc $wl"
   timeout -k 10 400 rocprofv3 -i "$R/tools/pmc_bench.txt" -d "$R/gpurun_out/pmc_$wl" -o pmc --output-format csv \
