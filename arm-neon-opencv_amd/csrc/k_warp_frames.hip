@@ -1,7 +1,8 @@
 // k_warp_frames.hip -- u8 affine bilinear warp, BORDER_CONSTANT, 1 to 4
-// interleaved channels or NCHW planes: the source staged through LDS, the
-// per-pixel geometry computed once for many frames.  A "frame" here is what
-// one sampler pass sees: a whole NHWC image, or one plane of an NCHW image.
+// interleaved channels or NCHW planes: the per-pixel geometry computed once
+// for many frames, the source boxes copied HBM -> LDS by LDS-DMA.  A "frame"
+// here is what one sampler pass sees: a whole NHWC image, or one plane of an
+// NCHW image.
 //
 // Reference: WarpAffineNaive::warp_affine_naive_hwc_u8 (warp_affine_naive.cpp:
 // 9-58) driven by WarpAffine::warp_affine_naive (warp_affine.cpp:111-169).
@@ -11,25 +12,22 @@
 //
 // Why this shape.  The gather kernels of k_warp.hip are
 // bound by the vector cache's tag lookups (one per lane quad and cache line of
-// every gather instruction), and the earlier LDS-staged tile kernel by its
-// per-pixel arithmetic: coordinates, weights and LDS addresses (~90 VALU per
-// pixel).  But one launch warps a whole batch with ONE matrix, so all of that
-// arithmetic is the same for every frame.  Here a workgroup owns a 64 x TH
+// every gather instruction).  But one launch warps a whole batch with ONE
+// matrix, so everything but the source bytes -- coordinates, weights, LDS
+// addresses -- is the same for every frame.  A workgroup owns a 64 x TH
 // output tile of kf consecutive frames:
-//  1. once: each lane computes its NP pixels' taps -- the LDS address of the
-//     top-left tap, packed u16 x-weights, 4x the y-weight -- and the workgroup
-//     reduces them to the source box the tile's taps reach;
-//  2. per frame: the box is staged into LDS with coalesced dword loads (4
-//     pixels = 12 bytes per lane for 3 channels, re-spread to one dword per
-//     pixel so every tap pair is two aligned dwords), one frame ahead in
-//     registers, two LDS buffers, one barrier per frame; each pixel then reads
-//     its two tap pairs (2 x ds_read2_b32) and blends: ~24 VALU per pixel and
-//     frame instead of ~90.
-// Pixels outside the source point at a border pattern kept in each LDS
-// buffer, with weights (2048, 0) x (2048, 0), so they come out as the border
-// value with no select.  A tile whose box exceeds the planned LDS buffer
-// (never for the planned geometry; the plan's bound is conservative) takes its
-// taps from memory bytewise.
+//  1. once: each lane computes its NP pixels' taps and the workgroup reduces
+//     them to the source box the tile's taps reach, and per box row the span
+//     its parallelogram needs;
+//  2. per frame: the box rows' spans are copied into an LDS slot by
+//     buffer_load_dwordx4 ... lds (no VGPR staging; the next frame's copy is
+//     in flight while this one is sampled); each pixel reads the dwords under
+//     its two tap pairs and blends in the reference's fixed point.
+// Pixels outside the source read a border pattern kept at the head of each
+// slot, with weights (2048, 0) x (2048, 0), so they need no select.  A tile
+// no pixel of which taps the source writes the border value without any
+// sampling; a tile whose box exceeds the plan (never for the planned
+// geometry; the plan's bound is conservative) takes its taps from memory.
 #pragma clang fp contract(off)
 
 #include <climits>
@@ -44,7 +42,6 @@ namespace vacv {
 namespace {
 
 constexpr int kFrTileW = 64;   // output columns per tile (one per lane)
-constexpr int kFrMaxIt = 6;    // staging groups (4 pixels) per thread and frame, at most
 
 template <int CC>
 __device__ __forceinline__ uint32_t pack_bytes(const unsigned char* p) {
@@ -73,424 +70,6 @@ __device__ __forceinline__ void direct_taps(const WarpLaunch& L, const unsigned 
 #pragma unroll
         for (int k = 0; k < CC; ++k) bp |= (uint32_t)(int)L.border[k] << (8 * k);
         tl = tr = bl = br = bp;
-    }
-}
-
-// L: launch block; gx, gy: tiles per frame; kf: frames per workgroup; S: LDS
-// bytes per staged row; rows_max: staged rows per buffer; buf: bytes per LDS
-// buffer ((rows_max + 2) * S: the rows, then the border pattern, two pixels
-// at rows_max * S and at (rows_max + 1) * S); dst_al: the destination allows dword
-// (u8 out) stores.
-template <int CC, int OUT, int NP, bool PLANAR>
-__global__ void __launch_bounds__(kBlock)
-warp_frames_kernel(WarpLaunch L, int gx, int gy, int kf, int S, int rows_max, int buf, int dst_al) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
-    constexpr int TH = 4 * NP;
-    constexpr int kLd = CC;  // dwords loaded per 4-pixel group (4 pixels x CC bytes)
-    // staging loads: sc0 for byte output (neighbouring tiles' boxes share
-    // rows through L2: 720p rot15 0.199 -> 0.190 ms), non-temporal for fp32
-    // output, whose 4x larger stores want the L2 (0.426 vs 0.453 ms)
-    constexpr int kAux = OUT == kOutSame ? 1 : VACV_LOAD_AUX;
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: keeps rows and bases scalar
-    int* red = reinterpret_cast<int*>(lds + 2 * buf);  // 4 waves x 4 ints
-    // byte output: this wave's two-row exchange (after the 64 bytes of red)
-    unsigned char* xch = lds + 2 * buf + 64 + (tid >> 6) * (2 * 64 * CC);
-
-    // XCD-aware order: workgroup b runs on XCD b % 8 and each XCD walks a
-    // contiguous range of (frame group, tile) items, so neighbouring tiles of
-    // the same frames -- whose boxes share edge rows -- meet in one L2
-    const int tiles = gx * gy;
-    const int nfr = L.n * L.src.planes;  // frames: images x planes
-    const int total = tiles * ((nfr + kf - 1) / kf);
-    const int per_xcd = (total + 7) / 8;
-    const int id = (int)(blockIdx.x % 8) * per_xcd + (int)(blockIdx.x / 8);
-    if (id >= total) return;  // uniform
-    const int fg = id / tiles, tile = id - fg * tiles;
-    const int by = tile / gx, bx = tile - by * gx;
-    const int f0 = fg * kf, f1 = min(f0 + kf, nfr);
-    // byte offset of frame f in a batch of geometry g (PLANAR: NCHW planes
-    // are the frames; a compile-time split, so NHWC pays no division)
-    auto frame_img = [&](int f) { return PLANAR ? f / L.src.planes : f; };
-    auto frame_off = [&](int f, const PlaneGeom& g) {
-        const int img = frame_img(f), pl = f - img * L.src.planes;
-        return PLANAR ? (int64_t)img * g.img_pitch + (int64_t)pl * g.plane_pitch : (int64_t)f * g.img_pitch;
-    };
-    const float* M = L.inv;
-    const float wlim = (float)(L.src.w - 1), hlim = (float)(L.src.h - 1);
-    const int x = bx * kFrTileW + lane;
-    const int yw = by * TH + wave * NP;  // this wave's first output row
-    const uint32_t rp = (uint32_t)L.src.row_pitch;
-
-    // ---- 1. per-pixel taps, once for every frame ---------------------------
-    const float axm = M[0] * (float)x, aym = M[3] * (float)x;
-    int sxv[NP], syv[NP];
-    uint32_t wxp[NP], wa4[NP], okm = 0;
-    int xmin = INT_MAX, xmax = INT_MIN, ymin = INT_MAX, ymax = INT_MIN;
-#pragma unroll
-    for (int j = 0; j < NP; ++j) {
-        const int y = yw + j;
-        // warp_affine_naive.cpp:23-24: (m0*x + m1*y) + m2, all float
-        const float fx = (axm + M[1] * (float)y) + M[2];
-        const float fy = (aym + M[4] * (float)y) + M[5];
-        // warp_affine_naive.cpp:26-39: floor(f) in [0, n-2] <=> 0 <= f < n-1
-        const bool ok = (x < L.dst.w) & (y < L.dst.h) & (fx >= 0.f) & (fx < wlim) & (fy >= 0.f) & (fy < hlim);
-        const int sx = ok ? (int)fx : 0, sy = ok ? (int)fy : 0;  // floor where ok
-        const float ax = fx - (float)sx, ay = fy - (float)sy;
-        // SATURATE_CAST_SHORT of a value in (0, 2048]: the +0.5f branch, no clamp
-        const uint32_t w0 = (uint32_t)(int)((1.f - ay) * 2048.f + 0.5f);
-        const uint32_t v0 = (uint32_t)(int)((1.f - ax) * 2048.f + 0.5f);
-        sxv[j] = sx;
-        syv[j] = sy;
-        // outside the source: the border pattern with weights (2048,0) x (2048,0)
-        wxp[j] = ok ? (v0 | ((2048u - v0) << 16)) : 2048u;
-        wa4[j] = ok ? 4u * w0 : 8192u;  // x4: the sum's bits 24..31 are the result
-        okm |= (uint32_t)ok << j;
-        if (ok) {
-            xmin = min(xmin, sx);
-            xmax = max(xmax, sx);
-            ymin = min(ymin, sy);
-            ymax = max(ymax, sy);
-        }
-    }
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        xmin = min(xmin, __shfl_xor(xmin, o, 64));
-        xmax = max(xmax, __shfl_xor(xmax, o, 64));
-        ymin = min(ymin, __shfl_xor(ymin, o, 64));
-        ymax = max(ymax, __shfl_xor(ymax, o, 64));
-    }
-    if (lane == 0) {
-        red[4 * wave + 0] = xmin;
-        red[4 * wave + 1] = xmax;
-        red[4 * wave + 2] = ymin;
-        red[4 * wave + 3] = ymax;
-    }
-    // the border pattern (one pixel per dword) at rows_max and rows_max + 1 of both buffers
-    if (tid < 8) {
-        uint32_t bp = 0;
-#pragma unroll
-        for (int k = 0; k < CC; ++k) bp |= (uint32_t)(int)L.border[k] << (8 * k);
-        const int b = tid >> 2, r = (tid >> 1) & 1, d = tid & 1;
-        *reinterpret_cast<uint32_t*>(lds + b * buf + (rows_max + r) * S + 4 * d) = bp;
-    }
-    __syncthreads();
-#pragma unroll
-    for (int w = 0; w < 4; ++w) {
-        xmin = min(xmin, red[4 * w + 0]);
-        xmax = max(xmax, red[4 * w + 1]);
-        ymin = min(ymin, red[4 * w + 2]);
-        ymax = max(ymax, red[4 * w + 3]);
-    }
-    // uniform (the compiler cannot tell: LDS loads), so everything derived
-    // from the box -- staged, the staging shape, the frame loop -- stays scalar
-    xmin = __builtin_amdgcn_readfirstlane(xmin);
-    xmax = __builtin_amdgcn_readfirstlane(xmax);
-    ymin = __builtin_amdgcn_readfirstlane(ymin);
-    ymax = __builtin_amdgcn_readfirstlane(ymax);
-    const bool any = xmax >= 0;
-    const int bx0 = any ? (xmin & ~3) : 0;              // first staged column (4-aligned)
-    const int G = any ? (xmax + 2 - bx0 + 3) >> 2 : 0;  // 4-pixel groups per staged row: columns .. xmax + 1
-    const int R = any ? ymax + 2 - ymin : 0;            // staged rows ymin .. ymax + 1
-    // staging shape: one wave instruction loads kr = 64 / G whole staged rows
-    // (lane l: row l / G, group l % G), a step of the workgroup 4 kr rows
-    const int kr = (G > 0 && G <= 64) ? 64 / G : 0;
-    const int its = kr > 0 ? (R + 4 * kr - 1) / (4 * kr) : 0;
-    const bool staged = kr > 0 && 16 * G <= S && R <= rows_max && its <= kFrMaxIt;  // uniform
-    const uint32_t border_ra = (uint32_t)(rows_max * S);
-    // per pixel, packed: the LDS offset of its top-left tap (< 64 KiB) in
-    // bits 0..15, 4x its y-weight (<= 8192) in bits 16..31: a register per
-    // pixel less (123 -> 110 VGPRs).  A second staging register set for two
-    // frames in flight still spilled at 4 waves per SIMD and ran slower
-    // (0.2125 vs 0.187 ms at 720p rot15).
-    uint32_t rw[NP];
-#pragma unroll
-    for (int j = 0; j < NP; ++j)
-        rw[j] = (((okm >> j) & 1u) ? (uint32_t)((syv[j] - ymin) * S + (sxv[j] - bx0) * 4) : border_ra) | (wa4[j] << 16);
-
-    // Row spans.  The box's rows near its top and bottom need only part of
-    // its width (a rotated tile's source footprint is a parallelogram: ~0.6
-    // of its bounding box at 15 degrees).  Thread t < R clips the
-    // parallelogram of the tile's corners to the band of source rows whose
-    // pixels tap row ymin + t (fy in [r - 1, r + 1), widened by 0.05 px for
-    // the float rounding of the reference's coordinates) and records the
-    // 4-pixel groups it needs, columns floor(x) .. floor(x) + 1.  The table
-    // lives in LDS buffer 1 until the first frame is parked there.
-    uint32_t* spans = reinterpret_cast<uint32_t*>(lds + buf);
-    if (staged && tid < R) {
-        const float X0 = (float)(bx * kFrTileW), X1 = (float)(min(bx * kFrTileW + kFrTileW, L.dst.w) - 1);
-        const float Y0 = (float)(by * TH), Y1 = (float)(min(by * TH + TH, L.dst.h) - 1);
-        float cx[4], cy[4];
-        const float px[4] = {X0, X1, X1, X0}, py[4] = {Y0, Y0, Y1, Y1};
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            cx[i] = (M[0] * px[i] + M[1] * py[i]) + M[2];
-            cy[i] = (M[3] * px[i] + M[4] * py[i]) + M[5];
-        }
-        const float r = (float)(ymin + tid), ya = r - 1.05f, yb = r + 1.05f;
-        float lo = 3.0e38f, hi = -3.0e38f;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const int i2 = (i + 1) & 3;
-            if (cy[i] >= ya && cy[i] <= yb) { lo = fminf(lo, cx[i]); hi = fmaxf(hi, cx[i]); }
-#pragma unroll
-            for (int e = 0; e < 2; ++e) {
-                const float yl = e ? yb : ya;
-                if ((cy[i] - yl) * (cy[i2] - yl) < 0.f) {
-                    const float xc = cx[i] + (yl - cy[i]) / (cy[i2] - cy[i]) * (cx[i2] - cx[i]);
-                    lo = fminf(lo, xc);
-                    hi = fmaxf(hi, xc);
-                }
-            }
-        }
-        uint32_t sp = 1u;  // empty: glo = 1 > ghi = 0
-        if (lo <= hi) {
-            const int clo = (int)floorf(fmaxf(lo - 0.05f, -1.0e9f)) - bx0;
-            const int chi = (int)floorf(fminf(hi + 0.05f, 1.0e9f)) + 1 - bx0;
-            if (chi >= 0 && clo <= 4 * G - 1) {
-                const int glo = max(clo, 0) >> 2, ghi = min(chi >> 2, G - 1);
-                sp = (uint32_t)glo | ((uint32_t)ghi << 16);
-            }
-        }
-        spans[tid] = sp;
-    }
-    __syncthreads();
-
-    // this lane's staging offsets, frame-independent; step u adds 4 kr rows.
-    // vm: steps with a group this lane stages (inside its row's span; the
-    // others load out of range -- zeros, no memory traffic -- and are not
-    // parked).  tailm: steps whose group reaches past the plane's last byte
-    // (a partly out-of-range load returns zeros): re-read bytewise when parked.
-    const int rl = kr > 0 ? lane / G : 0, cl = lane - rl * G;
-    const int r0 = wave * kr + rl;
-    const int nu = (staged && rl < kr && r0 < R) ? (R - r0 + 4 * kr - 1) / (4 * kr) : 0;
-    const uint32_t g0 = (uint32_t)(ymin + r0) * rp + (uint32_t)((bx0 + 4 * cl) * CC);
-    const uint32_t l0 = (uint32_t)(r0 * S + 16 * cl);
-    const uint32_t gstep = 4u * (uint32_t)kr * rp, lstep = 4u * (uint32_t)(kr * S);
-    uint32_t tailm = 0, vm = 0;
-#pragma unroll
-    for (int u = 0; u < kFrMaxIt; ++u) {
-        if (u < nu) {
-            const uint32_t sp = spans[r0 + 4 * kr * u];
-            if ((int)(sp & 0xFFFFu) <= cl && cl <= (int)(sp >> 16)) {
-                vm |= 1u << u;
-                if ((int64_t)(g0 + u * gstep) + 4 * CC > L.src.plane_bytes) tailm |= 1u << u;
-            }
-        }
-    }
-
-    typedef uint32_t Pre[kFrMaxIt][kLd];
-    // branch-free: every step issues, idle lanes (and every lane when !live)
-    // out of range, so the loaded registers need no phi -- a conditional fetch
-    // made the compiler copy them out right after the loads, i.e. wait for them
-    auto fetch = [&](Pre& pre, int f, bool live) {
-        const Rsrc rs = make_rsrc(L.src.base + frame_off(f, L.src), L.src.plane_bytes);
-        const int lim = live ? nu : 0;
-#pragma unroll
-        for (int u = 0; u < kFrMaxIt; ++u) {
-            const int off = (u < lim && ((vm >> u) & 1u)) ? (int)(g0 + u * gstep + rs.delta) : (int)0x80000000;
-            if constexpr (CC == 1) {
-                pre[u][0] = __builtin_amdgcn_raw_buffer_load_b32(rs.r, off, 0, kAux);
-            } else if constexpr (CC == 2) {
-                const auto v = __builtin_amdgcn_raw_buffer_load_b64(rs.r, off, 0, kAux);
-                pre[u][0] = v[0]; pre[u][1] = v[1];
-            } else if constexpr (CC == 3) {
-                const auto v = __builtin_amdgcn_raw_buffer_load_b96(rs.r, off, 0, kAux);
-                pre[u][0] = v[0]; pre[u][1] = v[1]; pre[u][2] = v[2];
-            } else {
-                const auto v = __builtin_amdgcn_raw_buffer_load_b128(rs.r, off, 0, kAux);
-                pre[u][0] = v[0]; pre[u][1] = v[1]; pre[u][2] = v[2]; pre[u][3] = v[3];
-            }
-        }
-    };
-    // 4 pixels x CC bytes -> one pixel per dword (the bytes above CC unused)
-    auto spread = [&](const uint32_t (&d)[kLd]) {
-        u32x4 q;
-        if constexpr (CC == 1) {
-            q[0] = d[0]; q[1] = d[0] >> 8; q[2] = d[0] >> 16; q[3] = d[0] >> 24;
-        } else if constexpr (CC == 2) {
-            q[0] = d[0]; q[1] = d[0] >> 16; q[2] = d[1]; q[3] = d[1] >> 16;
-        } else if constexpr (CC == 3) {
-            q[0] = d[0];
-            q[1] = __builtin_amdgcn_perm(d[1], d[0], 0x0C050403u);
-            q[2] = __builtin_amdgcn_perm(d[2], d[1], 0x0C040302u);
-            q[3] = d[2] >> 8;
-        } else {
-            q[0] = d[0]; q[1] = d[1]; q[2] = d[2]; q[3] = d[3];
-        }
-        return q;
-    };
-    auto park = [&](const Pre& pre, int f, uint32_t boff) {
-#pragma unroll
-        for (int u = 0; u < kFrMaxIt; ++u)
-            if ((vm >> u) & 1u) *reinterpret_cast<u32x4*>(lds + boff + l0 + u * lstep) = spread(pre[u]);
-        if (tailm) {  // rare: the plane's last group, bytewise
-            const Rsrc rs = make_rsrc(L.src.base + frame_off(f, L.src), L.src.plane_bytes);
-#pragma unroll
-            for (int u = 0; u < kFrMaxIt; ++u) {
-                if ((tailm >> u) & 1u) {
-                    const int off = (int)(g0 + u * gstep + rs.delta);
-                    uint32_t d[kLd];
-#pragma unroll
-                    for (int q = 0; q < kLd; ++q) {
-                        uint32_t w = 0;
-#pragma unroll
-                        for (int e = 0; e < 4; ++e)
-                            w |= (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(rs.r, off + 4 * q + e, 0, 0) << (8 * e);
-                        d[q] = w;
-                    }
-                    *reinterpret_cast<u32x4*>(lds + boff + l0 + u * lstep) = spread(d);
-                }
-            }
-        }
-    };
-
-    const uint32_t dpitch = (uint32_t)L.dst.row_pitch;
-    const int qx = bx * kFrTileW + (lane & ~3);  // the lane quad's first column
-    // uniform: every pixel of the tile is inside the output (and, for byte
-    // output, every lane quad's 4*CC bytes are dword-aligned): the
-    // branch-free store path
-    const bool tile_full = bx * kFrTileW + kFrTileW <= L.dst.w && by * TH + TH <= L.dst.h &&
-                           (OUT != kOutSame || dst_al);
-    constexpr uint32_t kOob = 0x80000000u;  // a buffer offset past any plane: the access is dropped
-
-    // blend pixel j of frame f from its taps and store it; FULL: tile_full
-    auto emit = [&](auto full_c, int fv, int j, uint32_t tl, uint32_t tr, uint32_t bl, uint32_t br) {
-        constexpr bool FULL = decltype(full_c)::value;
-        // uniform, and said so: with it in VGPRs the compiler wrapped every
-        // store in a waterfall loop over the buffer resource
-        const int f = __builtin_amdgcn_readfirstlane(fv);
-        const int y = yw + j;
-        const bool inside = FULL || (x < L.dst.w && y < L.dst.h);
-        unsigned char* dbase = const_cast<unsigned char*>(L.dst.base) + frame_off(f, L.dst);
-        const Rsrc drs = make_rsrc(dbase, L.dst.plane_bytes);
-        const us2 wx = __builtin_bit_cast(us2, wxp[j]);
-        const uint32_t wA = rw[j] >> 16, wB = 8192u - (rw[j] >> 16);
-        uint32_t vv[CC];
-#pragma unroll
-        for (int k = 0; k < CC; ++k) {
-            // warp_affine_naive.cpp:50-54 as (tl*wx0 + tr*wx1)*wy0 + (bl*wx0 +
-            // br*wx1)*wy1: exact integers (<= 255 * 2^22), here x4 so that
-            // bits 24..31 are the >> 22 result
-            const uint32_t sel = (uint32_t)k | (0x0Cu << 8) | ((uint32_t)(4 + k) << 16) | (0x0Cu << 24);
-            const uint32_t top = __builtin_amdgcn_perm(tr, tl, sel);
-            const uint32_t bot = __builtin_amdgcn_perm(br, bl, sel);
-            const uint32_t ht = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, top), wx, 0u, false);
-            const uint32_t hb = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, bot), wx, 0u, false);
-            vv[k] = __umul24(ht, wA) + __umul24(hb, wB);
-        }
-        const uint32_t drow = (uint32_t)y * dpitch + drs.delta;
-        if constexpr (OUT == kOutSame) {
-            uint32_t own;
-            if constexpr (CC == 1) {
-                own = vv[0] >> 24;
-            } else if constexpr (CC == 2) {
-                own = __builtin_amdgcn_perm(vv[1], vv[0], 0x0C0C0703u);
-            } else if constexpr (CC == 3) {
-                own = __builtin_amdgcn_perm(vv[2], __builtin_amdgcn_perm(vv[1], vv[0], 0x0C0C0703u), 0x0C070100u);
-            } else {
-                own = __builtin_amdgcn_perm(__builtin_amdgcn_perm(vv[3], vv[2], 0x0C0C0703u),
-                                            __builtin_amdgcn_perm(vv[1], vv[0], 0x0C0C0703u), 0x05040100u);
-            }
-            const uint32_t word = quad_pack<CC>(own, lane & 3);  // every lane takes part (DPP)
-            if constexpr (FULL) {
-                // two rows at a time through the wave's LDS exchange, out as
-                // 16-byte stores: 4x fewer store instructions than a dword per
-                // lane quad member (the store issue cost 0.03 ms of 0.2 at
-                // 720p rot15)
-                constexpr int kRowB = 64 * CC;  // bytes of a wave's output row segment
-                unsigned char* xw = xch + (j & 1) * kRowB;
-                if ((lane & 3) < CC) *reinterpret_cast<uint32_t*>(xw + 4 * ((lane >> 2) * CC + (lane & 3))) = word;
-                if (j & 1) {
-                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-                    __builtin_amdgcn_wave_barrier();
-                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-                    constexpr int kChunks = kRowB / 16;  // per row
-                    const int m = lane % (2 * kChunks);
-                    const u32x4 v = *reinterpret_cast<const u32x4*>(xch + 16 * m);
-                    const uint32_t rowoff = (uint32_t)(y - 1 + (m >= kChunks)) * dpitch + drs.delta;
-                    const uint32_t off = lane < 2 * kChunks
-                                             ? rowoff + (uint32_t)(bx * kFrTileW * CC + 16 * (m % kChunks))
-                                             : kOob;
-                    __builtin_amdgcn_raw_buffer_store_b128(v, drs.r, (int)off, 0, VACV_STORE_AUX);
-                }
-            } else if (inside) {  // the edges, or a byte-aligned destination
-                unsigned char* o = dbase + (int64_t)y * L.dst.row_pitch + (int64_t)x * CC;
-#pragma unroll
-                for (int k = 0; k < CC; ++k) o[k] = (unsigned char)(own >> (8 * k));
-            }
-        } else {
-            u32x4 o;
-#pragma unroll
-            for (int k = 0; k < CC; ++k) {
-                const int v = (int)(vv[k] >> 24);
-                float fv;
-                if (OUT == kOutF32) {
-                    fv = (float)v;
-                } else {
-                    const int img = frame_img(f), pl = f - img * L.src.planes;
-                    const ChanNorm cn = chan_norm(L.norm, img, PLANAR ? pl : k);
-                    fv = normalize_u8v(cn, v);
-                }
-                o[k] = __builtin_bit_cast(uint32_t, fv);
-            }
-            const int off = (int)(inside ? drow + (uint32_t)(x * CC * 4) : kOob);
-            if constexpr (CC == 1) {
-                __builtin_amdgcn_raw_buffer_store_b32(o[0], drs.r, off, 0, VACV_STORE_AUX);
-            } else if constexpr (CC == 2) {
-                typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
-                __builtin_amdgcn_raw_buffer_store_b64(u32x2{o[0], o[1]}, drs.r, off, 0, VACV_STORE_AUX);
-            } else if constexpr (CC == 3) {
-                typedef unsigned int u32x3 __attribute__((ext_vector_type(3)));
-                const u32x3 o3 = {o[0], o[1], o[2]};
-                __builtin_amdgcn_raw_buffer_store_b96(o3, drs.r, off, 0, VACV_STORE_AUX);
-            } else {
-                __builtin_amdgcn_raw_buffer_store_b128(o, drs.r, off, 0, VACV_STORE_AUX);
-            }
-        }
-    };
-
-    using full_t = std::integral_constant<bool, true>;
-    using edge_t = std::integral_constant<bool, false>;
-    if (!staged) {  // uniform, rare: the box is over the LDS plan -- taps from memory
-        for (int f = f0; f < f1; ++f) {
-            const unsigned char* sp = L.src.base + frame_off(f, L.src);
-            for (int j = 0; j < NP; ++j) {
-                uint32_t tl, tr, bl, br;
-                direct_taps<CC>(L, sp, x, yw + j, tl, tr, bl, br);
-                emit(edge_t(), f, j, tl, tr, bl, br);
-            }
-        }
-        return;
-    }
-    // all NP pixels' LDS reads first, then the blends and stores
-    // (in groups of 4 pixels: all of a lane's 8 pixels' taps at once cost
-    // 139 VGPRs, 3 waves per SIMD)
-    auto sample = [&](auto full_c, int f, uint32_t boff) {
-        constexpr int kGrp = 4;  // NP is 4 or 8
-#pragma unroll
-        for (int j0 = 0; j0 < NP; j0 += kGrp) {
-            uint32_t tp[kGrp][4];
-#pragma unroll
-            for (int j = 0; j < kGrp; ++j) {
-                const uint32_t ra = rw[j0 + j] & 0xFFFFu;
-                const uint32_t* t = reinterpret_cast<const uint32_t*>(lds + boff + ra);
-                const uint32_t* b = reinterpret_cast<const uint32_t*>(lds + boff + ra + S);
-                tp[j][0] = t[0]; tp[j][1] = t[1]; tp[j][2] = b[0]; tp[j][3] = b[1];
-            }
-#pragma unroll
-            for (int j = 0; j < kGrp; ++j) emit(full_c, f, j0 + j, tp[j][0], tp[j][1], tp[j][2], tp[j][3]);
-        }
-    };
-    Pre pre;
-    fetch(pre, f0, true);
-    for (int f = f0; f < f1; ++f) {
-        const uint32_t boff = (uint32_t)(((f - f0) & 1) * buf);
-        park(pre, f, boff);
-        __syncthreads();  // the box of frame f is in LDS; frame f - 1's reads of the other buffer are done
-        fetch(pre, min(f + 1, f1 - 1), f + 1 < f1);  // in flight while frame f is sampled
-        if (tile_full) sample(full_t(), f, boff);
-        else sample(edge_t(), f, boff);
     }
 }
 
@@ -548,7 +127,9 @@ typedef __attribute__((address_space(3))) void lds_void;
 #define VACV_RING_WPE 1
 #endif
 #ifndef VACV_RING_GRP
-#define VACV_RING_GRP 4  // pixels whose taps are read before their blends
+// pixels whose taps are read before their blends: 2 keeps the kernel at 95
+// VGPRs, 5 waves per SIMD (4 pixels: 103, 4 waves; 720p rot15 0.159 vs 0.169 ms)
+#define VACV_RING_GRP 2
 #endif
 template <int CC, int OUT, int NP, bool PLANAR>
 __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(VACV_RING_WPE)))
@@ -556,7 +137,10 @@ warp_ring_kernel(WarpLaunch L, int gx, int gy, int kf, int S, int rows_max, int 
                  uint32_t ginv) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     constexpr int TH = 4 * NP;
-    constexpr int kAux = OUT == kOutSame ? 1 : VACV_LOAD_AUX;  // sc0 / nt, as the frames kernel
+    // staging loads: sc0 for byte output (neighbouring tiles' boxes share
+    // rows through L2), non-temporal for fp32 output, whose 4x larger stores
+    // want the L2
+    constexpr int kAux = OUT == kOutSame ? 1 : VACV_LOAD_AUX;
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     int* red = reinterpret_cast<int*>(lds + ns * slot);  // 4 waves x 4 ints
@@ -582,7 +166,7 @@ warp_ring_kernel(WarpLaunch L, int gx, int gy, int kf, int S, int rows_max, int 
     const int yw = by * TH + wave * NP;
     const uint32_t rp = (uint32_t)L.src.row_pitch;
 
-    // ---- 1. per-pixel taps, once for every frame (as warp_frames_kernel) ---
+    // ---- 1. per-pixel taps, once for every frame ---------------------------
     const float axm = M[0] * (float)x, aym = M[3] * (float)x;
     // per pixel until the box is known: sx | sy << 16 and v0 | wa4 << 16
     // (16 registers instead of 32 at the kernel's register peak)
@@ -662,8 +246,13 @@ warp_ring_kernel(WarpLaunch L, int gx, int gy, int kf, int S, int rows_max, int 
         wxp[j] = ok ? (v0 | ((2048u - v0) << 16)) : 2048u;
     }
 
-    // Row spans in chunks (as warp_frames_kernel, in bytes): thread t < R
-    // clips the tile's source parallelogram to the rows that tap row ymin + t.
+    // Row spans.  The box's rows near its top and bottom need only part of
+    // its width (a rotated tile's source footprint is a parallelogram: ~0.6
+    // of its bounding box at 15 degrees).  Thread t < R clips the
+    // parallelogram of the tile's corners to the band of source rows whose
+    // pixels tap row ymin + t (fy in [r - 1, r + 1), widened by 0.05 px for
+    // the float rounding of the reference's coordinates) and records the
+    // 16-byte chunks it needs, columns floor(x) .. floor(x) + 1.
     // The table lives in the last slot's data, which no DMA writes before
     // frame f0's barrier.
     uint32_t* spans = reinterpret_cast<uint32_t*>(lds + (ns - 1) * slot + 16);  // after that slot's border head
@@ -1010,29 +599,22 @@ template <int CC, int OUT, int NP, bool PLANAR>
 hipError_t launch_frames(const WarpLaunch& L, const WarpFramesPlan& P, hipStream_t s) {
     constexpr int TH = 4 * NP;
     const int gx = (L.dst.w + kFrTileW - 1) / kFrTileW, gy = (L.dst.h + TH - 1) / TH;
-    auto kern = warp_frames_kernel<CC, OUT, NP, PLANAR>;
+    auto kern = warp_ring_kernel<CC, OUT, NP, PLANAR>;
     int kf = P.kf;
     if (kf <= 0) {
-        // at most 8 frames per workgroup (720p rot15: 4 / 8 / 16 frames 0.225 /
-        // 0.200 / 0.210 ms), fewer when that leaves < ~3 rounds of residency
-        const int64_t res = std::max<int64_t>(
-            P.ring ? frames_resident(warp_ring_kernel<CC, OUT, NP, PLANAR>, (size_t)P.lds)
-                   : frames_resident(kern, (size_t)P.lds),
-            256);
+        // at most 16 frames per workgroup (the per-tile taps, box and spans
+        // amortised over more frames: 720p rot15 8 / 16 / 32 frames 0.183 /
+        // 0.175 / 0.185 ms), fewer when that leaves < ~3 rounds of residency
+        const int64_t res = std::max<int64_t>(frames_resident(kern, (size_t)P.lds), 256);
         const int64_t tiles = (int64_t)gx * gy;
-        kf = (int)std::max<int64_t>(1, std::min<int64_t>(8, tiles * L.n * L.src.planes / (3 * res)));
+        kf = (int)std::max<int64_t>(1, std::min<int64_t>(16, tiles * L.n * L.src.planes / (3 * res)));
     }
     const int64_t total = (int64_t)gx * gy * ((L.n * L.src.planes + kf - 1) / kf);
     if (total >= 0x7FFFFFF0LL) return hipErrorInvalidValue;
     const int64_t blocks = (total + 7) / 8 * 8;
-    if (P.ring) {
-        const uint32_t gs = (uint32_t)(P.S / 16), ginv = ((1u << 20) + gs - 1) / gs;
-        hipLaunchKernelGGL((warp_ring_kernel<CC, OUT, NP, PLANAR>), dim3((unsigned)blocks), dim3(kBlock),
-                           (size_t)P.lds, s, L, gx, gy, kf, P.S, P.rows_max, P.ns, P.slot, P.dst_al, ginv);
-    } else {
-        hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(kBlock), (size_t)P.lds, s, L, gx, gy, kf, P.S,
-                           P.rows_max, P.buf, P.dst_al);
-    }
+    const uint32_t gs = (uint32_t)(P.S / 16), ginv = ((1u << 20) + gs - 1) / gs;
+    hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(kBlock), (size_t)P.lds, s, L, gx, gy, kf, P.S, P.rows_max,
+                       P.ns, P.slot, P.dst_al, ginv);
     return hipGetLastError();
 }
 
@@ -1059,83 +641,11 @@ hipError_t launch_frames_cc(const WarpLaunch& L, const WarpFramesPlan& P, hipStr
 // bank conflicts for the tap reads.  A wave's 64 lanes read the taps of 64
 // consecutive output pixels of one row; rotated, they fall on several staged
 // rows, and the stride decides whether those rows' dwords land on distinct
-// banks (ds_read_b32: bank = dword mod 32 within each half-wave; distinct
-// dwords on one bank serialise).  Counted on a few sample rows of the output
-// for the 8 strides 16 G .. 16 G + 112 (those <= s_max); ties go to the
-// smaller stride.
-int frames_stride(const WarpLaunch& L, int G, int s_max) {
-    const float* M = L.inv;
-    int best_s = 16 * G;
-    long best_cost = -1;
-    for (int k = 0; k < 8; ++k) {
-        const int S = 16 * (G + k), sd = S / 4;
-        if (k > 0 && S > s_max) break;  // a wider stride would cost a workgroup per CU
-        long cost = 0;
-        for (int yi = 1; yi <= 3; ++yi) {
-            const int y = L.dst.h * yi / 4;
-            for (int xi = 0; xi < 3; ++xi) {
-                const int x0 = std::max(0, std::min(L.dst.w - 64, (L.dst.w - 64) * xi / 2));
-                for (int half = 0; half < 2; ++half) {
-                    for (int d = 0; d < 2; ++d) {  // the tap pair's two dwords
-                        long a[32];
-                        for (int l = 0; l < 32; ++l) {
-                            const int x = x0 + 32 * half + l;
-                            const float fx = (M[0] * (float)x + M[1] * (float)y) + M[2];
-                            const float fy = (M[3] * (float)x + M[4] * (float)y) + M[5];
-                            a[l] = -1 - d;  // outside: the shared border pattern
-                            if (fx >= 0.f && fx < (float)(L.src.w - 1) && fy >= 0.f && fy < (float)(L.src.h - 1))
-                                a[l] = (long)(int)fy * sd + (int)fx + d;
-                        }
-                        int worst = 1;
-                        for (int l = 0; l < 32; ++l) {  // distinct dwords on lane l's bank
-                            int n = 0;
-                            for (int m = 0; m < 32; ++m) {
-                                if ((((a[m] - a[l]) % 32) + 32) % 32 != 0) continue;
-                                bool first = true;
-                                for (int q = 0; q < m; ++q) first = first && a[q] != a[m];
-                                n += first;
-                            }
-                            worst = std::max(worst, n);
-                        }
-                        cost += worst;
-                    }
-                }
-            }
-        }
-        if (best_cost < 0 || cost < best_cost) {
-            best_cost = cost;
-            best_s = S;
-        }
-    }
-    return best_s;
-}
-
-// The LDS layout of one geometry (pointer-independent): tile rows, stride,
-// rows per buffer.  The bound is the tile's coordinate span (|m0|*63 +
-// |m1|*(TH-1) columns, |m3|*63 + |m4|*(TH-1) rows) plus floor, the second
-// tap, 4-alignment and slack; the kernel re-checks the real box and reads
-// memory if it is larger.
-bool frames_layout_th(const WarpLaunch& L, WarpFramesPlan& P, int th) {
-    P.th = th;
-    const double sx = std::fabs(L.inv[0]) * (kFrTileW - 1) + std::fabs(L.inv[1]) * (P.th - 1);
-    const double sy = std::fabs(L.inv[3]) * (kFrTileW - 1) + std::fabs(L.inv[4]) * (P.th - 1);
-    const int W = (int)std::ceil(sx * (1 + 1e-5) + 1e-3) + 6;  // + floor spread, right tap, 4-alignment
-    const int G = (W + 3) / 4;
-    P.rows_max = (int)std::ceil(sy * (1 + 1e-5) + 1e-3) + 3;
-    if (G > 64 || (P.rows_max + 4 * (64 / G) - 1) / (4 * (64 / G)) > kFrMaxIt) return false;
-    // strides that keep 4 workgroups per CU (160 KiB of LDS)
-    const int extra = 64 + (L.out == kOutSame ? 4 * 2 * 64 * L.src.cc : 0);
-    const int s_max = (40960 - extra) / (2 * (P.rows_max + 2)) / 16 * 16;
-    P.S = frames_stride(L, G, s_max);
-    P.buf = ((P.rows_max + 2) * P.S + 15) / 16 * 16;
-    P.lds = 2 * P.buf + 64 + (L.out == kOutSame ? 4 * 2 * 64 * L.src.cc : 0);  // + the byte output exchange
-    return P.lds <= 64 * 1024;
-}
-
-// The ring kernel's LDS row stride (bytes, a multiple of 16, >= 16 G): the
-// same search as frames_stride for its access, per tap row the 2 (3 for
-// CC = 3) dwords from byte address 16 + row S + col CC rounded down, each
-// a ds_read_b32 (bank = dword mod 32 within each half-wave).
+// banks.  Per tap row a pixel reads the 2 (3 for CC = 3) dwords from byte
+// address 16 + row S + col CC rounded down, each a ds_read_b32 (bank = dword
+// mod 32 within each half-wave; distinct dwords on one bank serialise).
+// Counted on a few sample rows of the output for the 8 strides 16 G ..
+// 16 G + 112 (those <= s_max); ties go to the smaller stride.
 int ring_stride(const WarpLaunch& L, int G, int s_max) {
     const float* M = L.inv;
     const int CC = L.src.cc;
@@ -1185,10 +695,14 @@ int ring_stride(const WarpLaunch& L, int G, int s_max) {
     return best_s;
 }
 
-// The ring kernel's LDS layout: rows_max as frames_layout_th; raw pixel rows
-// of G 16-byte chunks; ns slots, each a 16-byte border head and whole 1 KiB
-// DMA instructions.  ns (2-4, VACV_TUNE_WARP_SLOTS) defaults to the count
-// with the most boxes in flight per CU, (ns - 1) x resident workgroups.
+// The LDS layout of one geometry (pointer-independent).  The box bound is the
+// tile's coordinate span (|m0|*63 + |m1|*(TH-1) columns, |m3|*63 +
+// |m4|*(TH-1) rows) plus floor, the second tap, 4-alignment and slack; the
+// kernel re-checks the real box and reads memory if it is larger.  Raw pixel
+// rows of G 16-byte chunks; ns slots, each a 16-byte border head and whole
+// 1 KiB DMA instructions.  ns (2-4, VACV_TUNE_WARP_SLOTS) defaults to 2:
+// occupancy beats depth (720p rot15: 2 / 3 / 4 slots 0.159 / 0.183 / 0.29 ms,
+// 5 / 3 / 2 workgroups per CU).
 bool ring_layout_th(const WarpLaunch& L, WarpFramesPlan& P, int th) {
     P.th = th;
     const int CC = L.src.cc;
@@ -1201,20 +715,8 @@ bool ring_layout_th(const WarpLaunch& L, WarpFramesPlan& P, int th) {
     auto slot_of = [&](int S) { return 16 + (P.rows_max * (S / 16) + 63) / 64 * 1024; };
     if ((P.rows_max * G + 63) / 64 > 4 * kRingMaxIt) return false;
     const int knob = tune(VACV_TUNE_WARP_SLOTS);
-    int best_ns = 0;
-    long best_fl = -1;
-    for (int ns = 2; ns <= 4; ++ns) {
-        if (knob >= 2 && knob <= 4 && ns != knob) continue;
-        const int lds = ns * slot_of(16 * G) + extra;
-        if (lds > 64 * 1024) continue;
-        const long fl = (long)(ns - 1) * (160 * 1024 / lds);
-        if (fl > best_fl) {
-            best_fl = fl;
-            best_ns = ns;
-        }
-    }
-    if (!best_ns) return false;
-    P.ns = best_ns;
+    P.ns = knob >= 2 && knob <= 4 ? knob : 2;
+    if (P.ns * slot_of(16 * G) + extra > 64 * 1024) return false;
     // strides that keep the same resident workgroups per CU
     const int per_cu = 160 * 1024 / (P.ns * slot_of(16 * G) + extra);
     int s_max = 16 * G;
@@ -1223,24 +725,16 @@ bool ring_layout_th(const WarpLaunch& L, WarpFramesPlan& P, int th) {
             s_max = S;
     P.S = ring_stride(L, G, s_max);
     P.slot = slot_of(P.S);
-    P.buf = P.slot;
     P.lds = P.ns * P.slot + extra;
-    P.ring = 1;
     return P.lds <= 64 * 1024;
 }
 
-// 32-row tiles (measured faster: 0.200 vs 0.222 ms at 720p rot15; 24-row
-// tiles, 5 workgroups per CU, 0.200 vs 0.193) unless their box is over the
-// staging budget (e.g. 45 degrees), then 16
+// 32-row tiles (measured faster: 0.171 vs 0.182 ms at 720p rot15) unless
+// their box is over the staging budget, then 16
 bool frames_layout(const WarpLaunch& L, WarpFramesPlan& P) {
     const int th_knob = tune(VACV_TUNE_WARP_TILE_H);
-    if (tune(VACV_TUNE_WARP_KERNEL) == 5) {
-        if (th_knob == 16 || th_knob == 32) return ring_layout_th(L, P, th_knob);
-        return ring_layout_th(L, P, 32) || ring_layout_th(L, P, 16);
-    }
-    P.ring = 0;
-    if (th_knob == 16 || th_knob == 32) return frames_layout_th(L, P, th_knob);
-    return frames_layout_th(L, P, 32) || frames_layout_th(L, P, 16);
+    if (th_knob == 16 || th_knob == 32) return ring_layout_th(L, P, th_knob);
+    return ring_layout_th(L, P, 32) || ring_layout_th(L, P, 16);
 }
 
 // Host plan: does the frames kernel apply, and with which LDS layout?
@@ -1248,7 +742,7 @@ bool frames_layout(const WarpLaunch& L, WarpFramesPlan& P) {
 // time); the alignment checks are per call.
 bool warp_frames_plan(const WarpLaunch& L, WarpFramesPlan& P) {
     const int knob = tune(VACV_TUNE_WARP_KERNEL);
-    if (knob >= 0 && knob != 4 && knob != 5) return false;
+    if (knob >= 0 && knob != 4) return false;
     if (L.src.esize != 1 || L.border_mode != kBorderConstant) return false;
     if (L.src.planes > 1 && L.src.cc != 1) return false;
     if (L.src.cc < 1 || L.src.cc > 4) return false;
@@ -1265,7 +759,7 @@ bool warp_frames_plan(const WarpLaunch& L, WarpFramesPlan& P) {
     // layout of byte output carries the store exchange)
     struct Key {
         float inv[6];
-        int sw, sh, dw, dh, th, cc, bytes_out, kernel, slots;
+        int sw, sh, dw, dh, th, cc, bytes_out, slots;
         bool operator<(const Key& o) const { return std::memcmp(this, &o, sizeof(Key)) < 0; }
     };
     Key k;
@@ -1274,7 +768,6 @@ bool warp_frames_plan(const WarpLaunch& L, WarpFramesPlan& P) {
     k.sw = L.src.w; k.sh = L.src.h; k.dw = L.dst.w; k.dh = L.dst.h; k.th = tune(VACV_TUNE_WARP_TILE_H);
     k.cc = L.src.cc;
     k.bytes_out = L.out == kOutSame ? 1 : 0;
-    k.kernel = knob;
     k.slots = tune(VACV_TUNE_WARP_SLOTS);
     static std::mutex mu;
     static std::map<Key, std::pair<bool, WarpFramesPlan>> cache;

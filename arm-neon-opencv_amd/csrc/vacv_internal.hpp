@@ -169,22 +169,18 @@ struct WarpLaunch {
     NormSpec norm;
 };
 hipError_t launch_warp(const WarpLaunch& L, hipStream_t s);
-// u8 CONSTANT warp (1-4 interleaved channels, or NCHW planes) with the source staged in LDS
-// and the geometry shared by kf frames per workgroup (k_warp_frames.hip)
+// u8 CONSTANT warp (1-4 interleaved channels, or NCHW planes) with the source boxes
+// copied into an LDS ring by LDS-DMA and the geometry shared by kf frames per
+// workgroup (k_warp_frames.hip)
 struct WarpFramesPlan {
     int th;                      // tile rows (16 or 32; 64 columns)
-    int S;                       // LDS bytes per staged source row (one dword per pixel)
-    int rows_max;                // staged rows per LDS buffer
-    int buf;                     // bytes per LDS buffer (rows + border pattern)
+    int S;                       // LDS bytes per staged source row (raw pixel bytes, a multiple of 16)
+    int rows_max;                // staged rows per LDS slot
+    int ns;                      // LDS slots of the ring (boxes: one being sampled, ns - 1 in flight)
+    int slot;                    // bytes per slot (a 16-byte border head, rows in whole 1 KiB DMA units)
     int lds;                     // dynamic LDS per workgroup
     int kf;                      // frames per workgroup (<= 0: chosen at launch)
     int dst_al;                  // destination dword-aligned (u8 quad stores)
-    // LDS-DMA ring kernel (ring = 1): boxes kept as raw pixel bytes, S a
-    // multiple of 16; ns boxes of `slot` bytes (a 16-byte border head, then
-    // rows_max rows rounded up to whole 1 KiB DMA instructions)
-    int ring;
-    int ns;
-    int slot;
 };
 bool warp_frames_plan(const WarpLaunch& L, WarpFramesPlan& P);
 hipError_t launch_warp_frames(const WarpLaunch& L, const WarpFramesPlan& P, hipStream_t s);

@@ -258,7 +258,7 @@ def make_workload(name: str, batch: int, dev, rank: int, world: int, ops) -> dic
         src = u8(B, 720, 1280, 3)
         dst = torch.empty_like(src)
         m = ops.rotation_matrix(0.9, 15.0, (640, 360, 640, 360))
-        return {"batch": B, "px": 1280 * 720, "b_alg": B * 2 * 1280 * 720 * 3, "kernel": "warp_frames_kernel",
+        return {"batch": B, "px": 1280 * 720, "b_alg": B * 2 * 1280 * 720 * 3, "kernel": "warp_ring_kernel",
                 "frame": "1280x720x3", "output": "1280x720x3 u8",
                 "desc": "warp_affine INTER_LINEAR BORDER_CONSTANT 1280x720x3 u8, scale 0.9 rot 15 aux (640,360,640,360)",
                 "main": lambda stream=None: ops.warp_affine(src, m, 1280, 720, out=dst, stream=stream)}

@@ -303,12 +303,12 @@ enum {
     VACV_TUNE_RESIZE_TILE_W = 12,    /* staged kernel planner: tile width */
     VACV_TUNE_RESIZE_WORK = 13,      /* staged kernel planner: work per thread */
     VACV_TUNE_RESIZE_ROWS_BYTES = 14,/* whole-row kernel planner: output bytes per workgroup */
-    VACV_TUNE_WARP_KERNEL = 15,      /* u8 CONSTANT warp: 0 per-pixel gathers, 2 batched gathers, 4 LDS-staged frames, 5 LDS-DMA ring of frames (k_warp_frames.hip) */
+    VACV_TUNE_WARP_KERNEL = 15,      /* u8 CONSTANT warp: 0 per-pixel gathers, 2 batched gathers, 4 LDS-staged frames: an LDS-DMA ring of source boxes (k_warp_frames.hip) */
     VACV_TUNE_RESIZE_STRIP = 16,     /* two-tap u8 bilinear: column strips with an LDS row ring, 1: 64 columns x 16-row batches, 2: 128 x 8; 0 staged kernel */
     VACV_TUNE_MATCH_KERNEL = 17,     /* u8 match_template correlation: 0 v_dot4 kernel, else i8 MFMA where it fits */
-    VACV_TUNE_WARP_FRAMES = 18,      /* u8 CONSTANT warp, LDS-staged frames kernel: frames per workgroup */
-    VACV_TUNE_WARP_TILE_H = 19,      /* u8 CONSTANT warp, LDS-staged frames kernel: tile rows (16 or 32) */
-    VACV_TUNE_WARP_SLOTS = 20,       /* u8 CONSTANT warp, LDS-DMA ring kernel: source boxes in the LDS ring (2-4) */
+    VACV_TUNE_WARP_FRAMES = 18,      /* u8 CONSTANT warp, LDS-staged kernel: frames per workgroup */
+    VACV_TUNE_WARP_TILE_H = 19,      /* u8 CONSTANT warp, LDS-staged kernel: tile rows (16 or 32) */
+    VACV_TUNE_WARP_SLOTS = 20,       /* u8 CONSTANT warp, LDS-staged kernel: source boxes in the LDS ring (2-4) */
     VACV_TUNE_COUNT = 21
 };
 /* value < 0 restores the built-in choice.  Returns VACV_OK or INVALID_ARG. */

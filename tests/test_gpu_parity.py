@@ -796,17 +796,17 @@ def test_warp_border_modes(ops, dev, oracle):
     assert_same(got, want, "border normalize")
 
 
-# the LDS-staged warp kernels: register-staged frames (4) and the LDS-DMA ring
-# with 2, 3 and 4 boxes (5)
-FRAMES_VARIANTS = [dict(WARP_KERNEL=4), dict(WARP_KERNEL=5, WARP_SLOTS=2), dict(WARP_KERNEL=5, WARP_SLOTS=3),
-                   dict(WARP_KERNEL=5, WARP_SLOTS=4)]
+# the LDS-staged warp kernel with 2 (default), 3 and 4 boxes in its LDS ring
+FRAMES_VARIANTS = [dict(WARP_KERNEL=4, WARP_SLOTS=2), dict(WARP_KERNEL=4, WARP_SLOTS=3),
+                   dict(WARP_KERNEL=4, WARP_SLOTS=4)]
 
 
 @pytest.mark.parametrize("variant", range(len(FRAMES_VARIANTS)))
 def test_warp_frames_kernel(ops, dev, oracle, variant):
-    """The LDS-staged frames kernel (k_warp_frames.hip: per-pixel taps computed
-    once for kf frames, the source box staged per frame) is the default for u8
-    BORDER_CONSTANT warps (1-4 channels, NCHW planes as frames).  Against the per-pixel
+    """The LDS-staged kernel (k_warp_frames.hip: per-pixel taps computed once
+    for kf frames, the source boxes copied into an LDS ring of 2-4 slots by
+    LDS-DMA) is the default for u8 BORDER_CONSTANT warps (1-4 channels, NCHW
+    planes as frames); border-only tiles skip the sampling.  Against the per-pixel
     gather kernel (VACV_TUNE_WARP_KERNEL = 0) at full size over frames per
     workgroup 1, 2, 3, 16 and tile heights 16 / 32 (odd batch: a partial last
     frame group), u8 / fp32 / normalised outputs, a non-zero border value and a
