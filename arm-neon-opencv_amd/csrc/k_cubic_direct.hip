@@ -34,7 +34,17 @@ constexpr int kWavePx = 64 * kPxl;    // 128 output pixels per wave
 // spills; 80 still spills the normalised 3-channel kernel)
 constexpr int cubic_waves(int cc, int out) { return cc == 1 ? 8 : (cc == 3 && out == kOutNorm ? 5 : 6); }
 
-template <int CC, int OUT>
+// SUMS: the statistics half of cfg5 fused (normalize_naive.cpp:7-72 on the
+// resized image, here as fixed-order sums for the global mean_stddev): each
+// lane adds its (at most 2) pixels' values and squares per channel in fp32,
+// the wave reduces them in a fixed shuffle order, and lane 0 stores the
+// wave's (Sum x, Sum x^2) as fp64 partials; wave_sums_kernel sums those in
+// a fixed order (deterministic, run to run).  fp32 within a wave: 128 values
+// <= 255 (squares <= 65025) -- relative error ~1e-7, far inside SURVEY
+// 8(c)'s 1e-3 (mean) / 1e-4 (std) bar.  (Reducing inside the launch -- the
+// last wave of each image, found by an agent-scope release/acquire counter
+// -- took 2.2 ms: an agent-scope release per wave writes back the L2.)
+template <int CC, int OUT, bool SUMS>
 __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(cubic_waves(CC, OUT))))
 cubic_direct_kernel(ResizeLaunch L, int blocks_per_plane) {
     __shared__ __attribute__((aligned(16))) float xch[4][kWavePx * CC];
@@ -44,7 +54,15 @@ cubic_direct_kernel(ResizeLaunch L, int blocks_per_plane) {
     const int W = L.dst.w;
     const int P = W * L.dst.h;
     const int p0 = (blk * 4 + (int)threadIdx.y) * kWavePx;
-    if (p0 >= P) return;  // whole wave
+    // this wave's partials, value-major: [CC][2][image][wave of the image]
+    const int64_t n_waves = (int64_t)L.n * blocks_per_plane * 4;
+    double* part = SUMS ? L.sum_partials + (int64_t)pidx * blocks_per_plane * 4 + blk * 4 + (int)threadIdx.y : nullptr;
+    if (p0 >= P) {  // whole wave
+        if (SUMS) {
+            if (threadIdx.x < 2 * CC) part[threadIdx.x * n_waves] = 0.0;
+        }
+        return;
+    }
     const int npx = min(kWavePx, P - p0);
     const int lane = threadIdx.x;
     const int img = pidx / L.src.planes;
@@ -151,6 +169,38 @@ cubic_direct_kernel(ResizeLaunch L, int blocks_per_plane) {
             xo[(j * 64 + lane) * CC + k] = v;
         }
     }
+    if (SUMS) {
+        // this lane's own values back from LDS (summed in the blend loop they
+        // held 6 registers across it: a spill at the 80-VGPR cap)
+        float s1[CC], s2[CC];
+#pragma unroll
+        for (int k = 0; k < CC; ++k) s1[k] = s2[k] = 0.f;
+#pragma unroll
+        for (int j = 0; j < kPxl; ++j) {
+            if (j * 64 + lane >= npx) continue;
+#pragma unroll
+            for (int k = 0; k < CC; ++k) {
+                const float v = xo[(j * 64 + lane) * CC + k];
+                s1[k] += v;
+                s2[k] += v * v;
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < CC; ++k) {
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) {
+                s1[k] += __shfl_xor(s1[k], o, 64);
+                s2[k] += __shfl_xor(s2[k], o, 64);
+            }
+        }
+        if (lane == 0) {
+#pragma unroll
+            for (int k = 0; k < CC; ++k) {
+                part[(2 * k) * n_waves] = (double)s1[k];
+                part[(2 * k + 1) * n_waves] = (double)s2[k];
+            }
+        }
+    }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -191,6 +241,70 @@ cubic_direct_kernel(ResizeLaunch L, int blocks_per_plane) {
     }
 }
 
+// The fixed-order sum of the per-wave partials (value-major layout: a
+// value's partials are one contiguous run; interleaved with the other values
+// every workgroup fetched all of them, 24 us for cfg5).  One 1024-thread
+// workgroup per (group, value, split): thread t adds terms t, t + 1024, ...
+// of the split's range in order (8 loads issued ahead of their adds), then a
+// fixed LDS tree.  Per-image sums: one split per image.  The batch sum
+// (cfg5: 50K terms per value): kSplit splits per value, each writing its
+// sum; the last split of a value to finish (one agent-scope release /
+// acquire per workgroup -- a release per wave, 50K of them, took 2.2 ms)
+// adds the kSplit sums in split order.  Deterministic either way.
+constexpr int kSumThreads = 1024;
+constexpr int kSplit = 16;
+__global__ void __launch_bounds__(kSumThreads) wave_sums_kernel(const double* partials, int waves, int n, int vals,
+                                                               int per_image, double* sums, int* count) {
+    __shared__ double red[kSumThreads];
+    __shared__ int last;
+    const int splits = per_image ? 1 : kSplit;
+    const int g = blockIdx.x / (vals * splits);
+    const int r = blockIdx.x - g * vals * splits;
+    const int v = r / splits, sp = r - v * splits;
+    const int64_t run = per_image ? waves : (int64_t)n * waves;  // terms of this (group, value)
+    const int64_t b0 = run * sp / splits, b1 = run * (sp + 1) / splits;
+    const double* p = partials + (int64_t)v * n * waves + (per_image ? (int64_t)g * waves : 0);
+    constexpr int kDepth = 8;
+    double acc = 0.0;
+    int64_t t = b0 + threadIdx.x;
+    for (; t + (kDepth - 1) * kSumThreads < b1; t += kDepth * kSumThreads) {
+        double x[kDepth];
+#pragma unroll
+        for (int q = 0; q < kDepth; ++q) x[q] = p[t + (int64_t)q * kSumThreads];
+#pragma unroll
+        for (int q = 0; q < kDepth; ++q) acc += x[q];
+    }
+    for (; t < b1; t += kSumThreads) acc += p[t];
+    red[threadIdx.x] = acc;
+    __syncthreads();
+    for (int h = kSumThreads / 2; h > 0; h >>= 1) {
+        if ((int)threadIdx.x < h) red[threadIdx.x] += red[threadIdx.x + h];
+        __syncthreads();
+    }
+    if (per_image) {
+        if (threadIdx.x == 0) sums[g * vals + v] = red[0];
+        return;
+    }
+    // split sums right after the partials: split[v * kSplit + sp]
+    double* split = const_cast<double*>(partials) + (int64_t)vals * n * waves;
+    if (threadIdx.x == 0) {
+        split[v * kSplit + sp] = red[0];
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        const int old = __hip_atomic_fetch_add(count + v, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        last = old == kSplit - 1;
+    }
+    __syncthreads();
+    if (!last) return;
+    if (threadIdx.x == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        double a = 0.0;
+        for (int q = 0; q < kSplit; ++q) a += __hip_atomic_load(split + v * kSplit + q, __ATOMIC_RELAXED,
+                                                                 __HIP_MEMORY_SCOPE_AGENT);
+        sums[v] = a;
+        __hip_atomic_store(count + v, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // for the next launch
+    }
+}
+
 template <int CC>
 hipError_t launch_cc(const ResizeLaunch& L, hipStream_t s) {
     constexpr int kBlockPx = 4 * kWavePx;
@@ -199,10 +313,20 @@ hipError_t launch_cc(const ResizeLaunch& L, hipStream_t s) {
     const int64_t total = per_plane * L.n * L.src.planes;
     if (P >= 0x7FFFFFFF - kBlockPx || total > 0x7FFFFFF0LL) return hipErrorInvalidValue;
     if (L.out == kOutNorm)
-        hipLaunchKernelGGL((cubic_direct_kernel<CC, kOutNorm>), dim3((unsigned)total), dim3(64, 4), 0, s, L,
+        hipLaunchKernelGGL((cubic_direct_kernel<CC, kOutNorm, false>), dim3((unsigned)total), dim3(64, 4), 0, s, L,
                            (int)per_plane);
+    else if (L.sum_partials) {
+        hipLaunchKernelGGL((cubic_direct_kernel<CC, kOutF32, true>), dim3((unsigned)total), dim3(64, 4), 0, s, L,
+                           (int)per_plane);
+        const hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+        const int blocks = L.sum_per_image ? L.n * 2 * CC : 2 * CC * kSplit;
+        hipLaunchKernelGGL(wave_sums_kernel, dim3((unsigned)blocks), dim3(kSumThreads), 0, s,
+                           (const double*)L.sum_partials, (int)(per_plane * 4), L.n, 2 * CC, L.sum_per_image,
+                           L.sum_out, L.sum_count);
+    }
     else
-        hipLaunchKernelGGL((cubic_direct_kernel<CC, kOutF32>), dim3((unsigned)total), dim3(64, 4), 0, s, L,
+        hipLaunchKernelGGL((cubic_direct_kernel<CC, kOutF32, false>), dim3((unsigned)total), dim3(64, 4), 0, s, L,
                            (int)per_plane);
     return hipGetLastError();
 }
@@ -212,6 +336,12 @@ hipError_t launch_cc(const ResizeLaunch& L, hipStream_t s) {
 bool cubic_direct_applies(const ResizeLaunch& L) {
     if (tune(VACV_TUNE_CUBIC_DIRECT) == 0) return false;  // A/B: the staged kernel
     return L.kind == kCubic && L.src.esize == 1 && L.src.cc <= 3 && (L.out == kOutF32 || L.out == kOutNorm);
+}
+
+int cubic_direct_waves(const ResizeLaunch& L) {
+    constexpr int kBlockPx = 4 * kWavePx;
+    const int64_t P = (int64_t)L.dst.w * L.dst.h;
+    return (int)((P + kBlockPx - 1) / kBlockPx * 4);
 }
 
 hipError_t launch_cubic_direct(const ResizeLaunch& L, hipStream_t s) {

@@ -570,13 +570,26 @@ __global__ void __launch_bounds__(kBlock) stats_reduce_kernel(SumsLaunch L, int 
     const int k = (cc == 1) ? 0 : ch;
     const int img_lo = L.per_image ? g : 0, img_hi = L.per_image ? g + 1 : L.n;
     const int64_t terms = (int64_t)(img_hi - img_lo) * L.blocks_per_image;
-    double acc = 0.0;
-    for (int64_t t = threadIdx.x; t < terms; t += kBlock) {
+    auto term = [&](int64_t t) {
         const int img = img_lo + (int)(t / L.blocks_per_image);
         const int b = (int)(t - (int64_t)(img - img_lo) * L.blocks_per_image);
         const int64_t pidx = (int64_t)img * L.src.planes + plane;
-        acc += L.partials[((pidx * L.blocks_per_image) + b) * (2 * cc) + 2 * k + mom];
+        return L.partials[((pidx * L.blocks_per_image) + b) * (2 * cc) + 2 * k + mom];
+    };
+    // thread t adds terms t, t + 256, ... in that order; 16 loads are issued
+    // before their adds (a load-add chain per term took 78 us for cfg5's
+    // 50K per-wave partials), the order of the adds is unchanged
+    constexpr int kDepth = 16;
+    double acc = 0.0;
+    int64_t t = threadIdx.x;
+    for (; t + (kDepth - 1) * kBlock < terms; t += kDepth * kBlock) {
+        double v[kDepth];
+#pragma unroll
+        for (int q = 0; q < kDepth; ++q) v[q] = term(t + q * kBlock);
+#pragma unroll
+        for (int q = 0; q < kDepth; ++q) acc += v[q];
     }
+    for (; t < terms; t += kBlock) acc += term(t);
     red[threadIdx.x] = acc;
     __syncthreads();
     for (int h = kBlock / 2; h > 0; h >>= 1) {

@@ -461,6 +461,84 @@ hipError_t launch_cc(const WarpLaunch& L, hipStream_t s) {
 
 }  // namespace
 
+namespace {
+
+// ---------------------------------------------------------------------------
+// INTER_NEAREST: OpenCV 2.4.13's warpAffine (imgwarp.cpp) -- the map in fp64
+// fixed point with AB_BITS = 10:
+//   X0 = cvRound((M1 y + M2) 1024) + 512,  adelta = cvRound(M0 x 1024)
+//   X  = (X0 + adelta) >> 10            (the same for Y with M3, M4, M5)
+// then remap's nearest sampler: inside -> the source pixel; outside -> the
+// border value (CONSTANT), dst untouched (TRANSPARENT), or the pixel at
+// borderInterpolate(X), borderInterpolate(Y).  Parity unpinned (no OpenCV
+// runs here; oracle_warp_affine_nn restates the same).  One thread per
+// output pixel of one plane: a rarely used mode, gather-bound.
+template <int CC, typename TIn, int OUT>
+__global__ void __launch_bounds__(kBlock) warp_nearest_kernel(WarpLaunch L) {
+    using TOut = typename std::conditional<(OUT == kOutSame), TIn, float>::type;
+    const int x = blockIdx.x * kBlock + threadIdx.x, y = blockIdx.y, pidx = blockIdx.z;
+    if (x >= L.dst.w) return;
+    const int img = pidx / L.src.planes, pl = pidx - img * L.src.planes;
+    const double* M = L.invd;
+    const int X0 = (int)rint((M[1] * y + M[2]) * 1024.0) + 512;
+    const int Y0 = (int)rint((M[4] * y + M[5]) * 1024.0) + 512;
+    int X = (int)((uint32_t)X0 + (uint32_t)(int)rint(M[0] * x * 1024.0)) >> 10;
+    int Y = (int)((uint32_t)Y0 + (uint32_t)(int)rint(M[3] * x * 1024.0)) >> 10;
+    X = min(max(X, -32768), 32767);  // remap's short map (saturate_cast<short>)
+    Y = min(max(Y, -32768), 32767);
+    const bool inside = (unsigned)X < (unsigned)L.src.w && (unsigned)Y < (unsigned)L.src.h;
+    if (!inside && L.border_mode == kBorderTransparent) return;
+    TOut* d = reinterpret_cast<TOut*>(const_cast<unsigned char*>(L.dst.base) + (int64_t)img * L.dst.img_pitch +
+                                      (int64_t)pl * L.dst.plane_pitch + (int64_t)y * L.dst.row_pitch) + (int64_t)x * CC;
+    const TIn* sp = nullptr;
+    if (inside || L.border_mode != kBorderConstant) {
+        const int sx = inside ? X : border_index(X, L.src.w, L.border_mode);
+        const int sy = inside ? Y : border_index(Y, L.src.h, L.border_mode);
+        sp = reinterpret_cast<const TIn*>(L.src.base + (int64_t)img * L.src.img_pitch + (int64_t)pl * L.src.plane_pitch +
+                                          (int64_t)sy * L.src.row_pitch) + (int64_t)sx * CC;
+    }
+#pragma unroll
+    for (int k = 0; k < CC; ++k) {
+        const int ch = L.src.planes > 1 ? pl : k;
+        const TIn v = sp ? sp[k] : (TIn)L.border[ch];
+        if constexpr (OUT == kOutSame) {
+            d[k] = v;
+        } else if constexpr (OUT == kOutF32) {
+            d[k] = (float)v;
+        } else {
+            const ChanNorm cn = chan_norm(L.norm, img, ch);
+            if constexpr (std::is_same<TIn, uint8_t>::value) d[k] = normalize_u8v(cn, (int)v);
+            else d[k] = normalize_f(cn, (float)v);
+        }
+    }
+}
+
+template <typename TIn, int OUT>
+hipError_t launch_nearest_t(const WarpLaunch& L, hipStream_t s) {
+    const dim3 grid((unsigned)((L.dst.w + kBlock - 1) / kBlock), (unsigned)L.dst.h, (unsigned)(L.n * L.src.planes));
+    if ((int64_t)L.n * L.src.planes > 65535 || L.dst.h > 65535) return hipErrorInvalidValue;
+    switch (L.src.cc) {
+        case 1: hipLaunchKernelGGL((warp_nearest_kernel<1, TIn, OUT>), grid, dim3(kBlock), 0, s, L); break;
+        case 2: hipLaunchKernelGGL((warp_nearest_kernel<2, TIn, OUT>), grid, dim3(kBlock), 0, s, L); break;
+        case 3: hipLaunchKernelGGL((warp_nearest_kernel<3, TIn, OUT>), grid, dim3(kBlock), 0, s, L); break;
+        case 4: hipLaunchKernelGGL((warp_nearest_kernel<4, TIn, OUT>), grid, dim3(kBlock), 0, s, L); break;
+        default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+}  // namespace
+
+hipError_t launch_warp_nearest(const WarpLaunch& L, hipStream_t s) {
+    if (L.src.esize == 1) {
+        if (L.out == kOutSame) return launch_nearest_t<uint8_t, kOutSame>(L, s);
+        if (L.out == kOutF32) return launch_nearest_t<uint8_t, kOutF32>(L, s);
+        return launch_nearest_t<uint8_t, kOutNorm>(L, s);
+    }
+    if (L.out == kOutNorm) return launch_nearest_t<float, kOutNorm>(L, s);
+    return launch_nearest_t<float, kOutSame>(L, s);
+}
+
 hipError_t launch_warp(const WarpLaunch& L, hipStream_t s) {
     if (L.src.esize == 1) {
         if (L.out == kOutSame) return launch_cc<uint8_t, kOutSame>(L, s);

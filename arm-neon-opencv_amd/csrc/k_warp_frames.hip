@@ -94,7 +94,8 @@ __device__ __forceinline__ void direct_taps(const WarpLaunch& L, const unsigned 
 // was sampled from -- every wave has consumed those reads before the barrier.
 constexpr int kRingMaxIt = 6;  // DMA instructions per wave and frame, at most (a box of 24 KiB)
 // Diagnosis builds (make EXTRA=-DVACV_RING_DBG=n LIB=... OBJ=...; tools/kbench_lib.py):
-// bit 0 no sampling and stores, bit 1 no DMA.  Results are wrong in those builds.
+// bit 0 no sampling and stores, bit 1 no DMA, bit 2 every lane reads its taps at
+// one LDS address (no bank conflicts).  Results are wrong in those builds.
 #ifndef VACV_RING_DBG
 #define VACV_RING_DBG 0
 #endif
@@ -140,7 +141,11 @@ warp_ring_kernel(WarpLaunch L, int gx, int gy, int kf, int S, int rows_max, int 
     // staging loads: sc0 for byte output (neighbouring tiles' boxes share
     // rows through L2), non-temporal for fp32 output, whose 4x larger stores
     // want the L2
+#ifdef VACV_RING_AUX
+    constexpr int kAux = VACV_RING_AUX;
+#else
     constexpr int kAux = OUT == kOutSame ? 1 : VACV_LOAD_AUX;
+#endif
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     int* red = reinterpret_cast<int*>(lds + ns * slot);  // 4 waves x 4 ints
@@ -547,7 +552,7 @@ warp_ring_kernel(WarpLaunch L, int gx, int gy, int kf, int S, int rows_max, int 
             uint32_t tp[kGrp][4];
 #pragma unroll
             for (int j = 0; j < kGrp; ++j) {
-                const uint32_t ra = rw[j0 + j] & 0xFFFFu;
+                const uint32_t ra = (VACV_RING_DBG & 4) ? 16u : rw[j0 + j] & 0xFFFFu;
                 const unsigned char* a = lds + sbase + (ra & ~3u);
                 taps_at(a, ra & 3u, tp[j][0], tp[j][1]);
                 taps_at(a + S, ra & 3u, tp[j][2], tp[j][3]);

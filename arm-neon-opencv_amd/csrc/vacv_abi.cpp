@@ -16,6 +16,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <map>
+#include <set>
 #include <mutex>
 #include <tuple>
 #include <utility>
@@ -114,7 +115,8 @@ struct Workspace {
 std::mutex g_ws_mu;
 std::map<std::tuple<int, void*, int>, Workspace> g_ws;
 
-int workspace(hipStream_t s, size_t bytes, void** out, int slot = 0) {
+// zero_new: a new allocation is zeroed (queued on s, so before any use)
+int workspace(hipStream_t s, size_t bytes, void** out, int slot = 0, bool zero_new = false) {
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess) return VACV_ERR_HIP;
     std::lock_guard<std::mutex> lk(g_ws_mu);
@@ -130,6 +132,7 @@ int workspace(hipStream_t s, size_t bytes, void** out, int slot = 0) {
         size_t cap = std::max<size_t>(bytes, 1 << 20);
         if (hipMalloc(&w.buf, cap) != hipSuccess) return VACV_ERR_NO_MEMORY;
         w.cap = cap;
+        if (zero_new && hipMemsetAsync(w.buf, 0, cap, s) != hipSuccess) return VACV_ERR_HIP;
     }
     *out = w.buf;
     return VACV_OK;
@@ -225,8 +228,19 @@ int normalize_with(const Img& src, const Img& dst, const NormSpec& ns, hipStream
 
 // fx / fy > 0: cv::resize's inv_scale (the reference passes them through to
 // OpenCV for NEAREST / AREA, resize.cpp:35); 0: dsize / ssize
+// FusedSums: the cubic gather kernel's per-wave statistics epilogue
+// (vacv_resize_channel_sums); `used` tells whether that kernel ran with it.
+struct FusedSums {
+    double* partials;            // [cc][2][n][waves] + [cc][2][16] split sums, sized by the caller
+    double* sums;                // [n][cc][2] (per_image) or [cc][2]
+    int per_image;
+    int* count;                  // >= 2 cc zeroed ints (the batch sum's counters)
+    int waves;                   // out: waves per plane
+    bool used;                   // out
+};
+
 int resize_impl(const vacv_image* src_d, const vacv_image* dst_d, int interpolation, int mode, int out_kind,
-                const NormSpec* ns, hipStream_t s, double fx = 0.0, double fy = 0.0) {
+                const NormSpec* ns, hipStream_t s, double fx = 0.0, double fy = 0.0, FusedSums* fs = nullptr) {
     Img src, dst;
     int st = load(src_d, src);
     if (st) return st;
@@ -329,7 +343,17 @@ int resize_impl(const vacv_image* src_d, const vacv_image* dst_d, int interpolat
         return hip_status(launch_resize_strip(L, s));
     // u8 cubic (fused widen to fp32), c <= 3 interleaved: per-pixel gathers
     // (k_cubic_direct.hip); VACV_CUBIC_DIRECT=0 selects the staged kernel
-    if (cubic_direct_applies(L)) return hip_status(launch_cubic_direct(L, s));
+    if (cubic_direct_applies(L)) {
+        if (fs && L.out == kOutF32 && fs->partials && L.src.planes == 1) {
+            L.sum_partials = fs->partials;
+            L.sum_out = fs->sums;
+            L.sum_per_image = fs->per_image;
+            L.sum_count = fs->count;
+            fs->waves = cubic_direct_waves(L);
+            fs->used = true;
+        }
+        return hip_status(launch_cubic_direct(L, s));
+    }
     L.interleave = tune(VACV_TUNE_RESIZE_INTERLEAVE) != 0;
     L.rows_mode = tune(VACV_TUNE_RESIZE_ROWS) == 1;
     if (L.rows_mode) {
@@ -387,10 +411,17 @@ int warp_impl(const vacv_image* src_d, const vacv_image* dst_d, const float m[6]
     // warp_affine.cpp:114-118: anything but LINEAR + CONSTANT recurses into the
     // OpenCV stub; the other border modes are built here (vacv_semantics.hpp
     // border_index: the naive sampler with OpenCV's borderInterpolate taps)
-    if (flags != VACV_INTER_LINEAR) return VACV_ERR_UNSUPPORTED;
+    // flags as cv::warpAffine reads them (the reference hands every flag but
+    // INTER_LINEAR to OpenCV): the interpolation in bits 0-2, WARP_INVERSE_MAP
+    // (m is already the dst -> src map: no inversion).  INTER_LINEAR keeps the
+    // naive sampler; INTER_NEAREST is OpenCV 2.4's fixed-point nearest.
+    const int interp = flags & 7;
+    const bool inverse_map = (flags & VACV_WARP_INVERSE_MAP) != 0;
+    if (flags & ~(7 | VACV_WARP_INVERSE_MAP)) return VACV_ERR_UNSUPPORTED;
+    if (interp != VACV_INTER_LINEAR && interp != VACV_INTER_NEAREST) return VACV_ERR_UNSUPPORTED;
     if (border_mode < VACV_BORDER_CONSTANT || border_mode > VACV_BORDER_TRANSPARENT) return VACV_ERR_UNSUPPORTED;
     if (src.layout == VACV_NHWC && src.c > 4) return VACV_ERR_UNSUPPORTED;
-    if (src.w < 2 || src.h < 2) return VACV_ERR_INVALID_ARG;
+    if (interp == VACV_INTER_LINEAR && (src.w < 2 || src.h < 2)) return VACV_ERR_INVALID_ARG;
     WarpLaunch L{};
     L.src = geom(src);
     L.dst = geom(dst);
@@ -399,11 +430,32 @@ int warp_impl(const vacv_image* src_d, const vacv_image* dst_d, const float m[6]
     if (src.dtype == VACV_FP32 && out_kind == kOutF32) L.out = kOutSame;
     const int want = (L.out == kOutSame) ? src.dtype : VACV_FP32;
     if (dst.dtype != want) return VACV_ERR_INVALID_ARG;
-    vacv_invert_affine(m, L.inv);
+    if (inverse_map) std::memcpy(L.inv, m, sizeof(L.inv));
+    else vacv_invert_affine(m, L.inv);
     border_values(src, bv, L.border);
     L.border_mode = border_mode;
     if (border_mode == VACV_BORDER_TRANSPARENT && dst.data == src.data) return VACV_ERR_INVALID_ARG;  // in place
     if (ns) L.norm = *ns;
+    if (interp == VACV_INTER_NEAREST) {
+        // cv::warpAffine: the float map widened to double and, unless
+        // WARP_INVERSE_MAP, inverted in double (imgwarp.cpp)
+        double* M = L.invd;
+        for (int i = 0; i < 6; ++i) M[i] = (double)m[i];
+        if (!inverse_map) {
+            double D = M[0] * M[4] - M[1] * M[3];
+            D = D != 0 ? 1. / D : 0;
+            const double A11 = M[4] * D, A22 = M[0] * D;
+            M[0] = A11;
+            M[1] *= -D;
+            M[3] *= -D;
+            M[4] = A22;
+            const double b1 = -M[0] * M[2] - M[1] * M[5];
+            const double b2 = -M[3] * M[2] - M[4] * M[5];
+            M[2] = b1;
+            M[5] = b2;
+        }
+        return hip_status(launch_warp_nearest(L, s));
+    }
     return hip_status(launch_warp(L, s));
 }
 
@@ -823,14 +875,36 @@ int vacv_channel_sums(const vacv_image* src_d, double* sums, int per_image, void
     return channel_sums_into(src, sums, per_image ? 1 : 0, static_cast<double*>(ws), blocks, s);
 }
 
-int vacv_resize_channel_sums(const vacv_image* src, const vacv_image* dst, int interpolation, int mode,
+int vacv_resize_channel_sums(const vacv_image* src_d, const vacv_image* dst_d, int interpolation, int mode,
                              double* sums, int per_image, void* stream) {
     if (!sums) return VACV_ERR_INVALID_ARG;
-    // two passes: a per-wave fp64 sum epilogue in the cubic gather kernel was
-    // measured slower (0.253 ms vs 0.172 + 0.030)
-    const int st = resize_impl(src, dst, interpolation, mode, kOutSame, nullptr, (hipStream_t)stream);
+    hipStream_t s = (hipStream_t)stream;
+    Img src, dst;
+    int st = load(src_d, src);
     if (st) return st;
-    return vacv_channel_sums(dst, sums, per_image, stream);
+    if ((st = load(dst_d, dst))) return st;
+    // u8 -> fp32 cubic into a dense NHWC output (cfg5): the gather kernel's
+    // per-wave sums epilogue, then only the fixed-order reduction -- the output
+    // is not read back (a separate vacv_channel_sums pass re-read 77 MB per
+    // cfg5 batch).  Everything else: resize, then vacv_channel_sums.
+    if (interpolation == VACV_INTER_CUBIC && src.dtype == VACV_INT8 && dst.dtype == VACV_FP32 &&
+        dst.layout == VACV_NHWC && dst.c <= 3 && dense(dst) && src.n == dst.n) {
+        const int64_t P = (int64_t)dst.w * dst.h;
+        const int64_t waves = (P + 511) / 512 * 4;  // cubic_direct_waves() for this size
+        void* ws = nullptr;
+        // the per-wave partials [c][2][n][waves], then 2 c x 16 split sums
+        if ((st = workspace(s, (size_t)(dst.n * waves * 2 * dst.c + 2 * dst.c * 16) * sizeof(double), &ws))) return st;
+        // the batch sum's second level: 2c ints of counters, left zeroed by
+        // every launch (k_cubic_direct.hip)
+        void* cnt = nullptr;
+        if ((st = workspace(s, 64 * sizeof(int), &cnt, 2, true))) return st;
+        FusedSums fs{static_cast<double*>(ws), sums, per_image ? 1 : 0, static_cast<int*>(cnt), 0, false};
+        if ((st = resize_impl(src_d, dst_d, interpolation, mode, kOutSame, nullptr, s, 0.0, 0.0, &fs))) return st;
+        if (fs.used) return fs.waves == waves ? VACV_OK : VACV_ERR_HIP;  // (a layout mismatch cannot happen)
+        return vacv_channel_sums(dst_d, sums, per_image, stream);
+    }
+    if ((st = resize_impl(src_d, dst_d, interpolation, mode, kOutSame, nullptr, s))) return st;
+    return vacv_channel_sums(dst_d, sums, per_image, stream);
 }
 
 int vacv_stats_from_sums(const double* sums, int groups, int c, double count, float* mean, float* stddev,

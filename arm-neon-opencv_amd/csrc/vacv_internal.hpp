@@ -108,6 +108,14 @@ struct ResizeLaunch {
     int area_half_up;            // INTER_AREA u8 2x2, cn 1/3/4: (sum + 2) >> 2 (ResizeAreaFastVec fast_mode)
     ResizePlanDev plan;
     NormSpec norm;
+    // cubic gather kernel only (or null): the output's per-channel
+    // (Sum x, Sum x^2) -- per-wave partials [cc][2][image][wave]
+    // (cubic_direct_waves() waves, a workspace), then sum_out = [n][cc][2]
+    // (sum_per_image) or [cc][2] in a fixed order
+    double* sum_partials;
+    double* sum_out;
+    int sum_per_image;
+    int* sum_count;              // 2 cc zeroed ints, left zeroed (the batch sum)
 };
 
 // Fills tiles, strips and the cached device plan of L (host).  With rows = 1
@@ -157,18 +165,23 @@ int release_area_tables();
 // u8 -> fp32 cubic as per-pixel gathers (k_cubic_direct.hip); needs no plan
 bool cubic_direct_applies(const ResizeLaunch& L);
 hipError_t launch_cubic_direct(const ResizeLaunch& L, hipStream_t s);
+int cubic_direct_waves(const ResizeLaunch& L);  // waves per output plane (the sum_partials layout)
 
 struct WarpLaunch {
     PlaneGeom src;
     PlaneGeom dst;
     int n;
     float inv[6];
+    double invd[6];              // INTER_NEAREST: OpenCV's fp64 inverse map (warpAffine)
     float border[4];
     int border_mode;             // kBorder* (vacv_semantics.hpp)
     int out;                     // OutKind
     NormSpec norm;
 };
 hipError_t launch_warp(const WarpLaunch& L, hipStream_t s);
+// INTER_NEAREST (OpenCV 2.4 warpAffine + remapNearest; the reference hands
+// every flag but INTER_LINEAR to OpenCV, warp_affine.cpp:114-118)
+hipError_t launch_warp_nearest(const WarpLaunch& L, hipStream_t s);
 // u8 CONSTANT warp (1-4 interleaved channels, or NCHW planes) with the source boxes
 // copied into an LDS ring by LDS-DMA and the geometry shared by kf frames per
 // workgroup (k_warp_frames.hip)

@@ -84,7 +84,12 @@ std::vector<float> affine_of(const char* fn, const Tensor& M) { return host_floa
 void check_warp_modes(const char* fn, const Tensor& src, int flags, int borderMode) {
     // warp_affine.cpp:114-118
     if (src.dtype != INT8 && src.dtype != FP32) fail(fn, "warp_affine takes INT8 or FP32");
-    if (flags != INTER_LINEAR) fail(fn, "only INTER_LINEAR is supported");
+    // INTER_LINEAR / INTER_NEAREST, optionally | WARP_INVERSE_MAP (the
+    // reference hands all but INTER_LINEAR to cv::warpAffine; OpenCV 2.4's
+    // semantics here, vacv_hip.h)
+    const int interp = flags & INTER_MAX;
+    if ((flags & ~(INTER_MAX | WARP_INVERSE_MAP)) || (interp != INTER_LINEAR && interp != INTER_NEAREST))
+        fail(fn, "only INTER_LINEAR and INTER_NEAREST (optionally | WARP_INVERSE_MAP) are supported");
     // BORDER_CONSTANT is the reference's naive path; REPLICATE, REFLECT, WRAP,
     // REFLECT_101 and TRANSPARENT extend it (the reference hands them to
     // OpenCV: warp_affine.cpp:114-118); BORDER_ISOLATED has no meaning here

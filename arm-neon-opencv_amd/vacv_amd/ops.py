@@ -201,7 +201,9 @@ def invert_affine(m) -> np.ndarray:
 
 def warp_affine(src: torch.Tensor, m, w: int, h: int, flags: int = INTER_LINEAR, border_mode: int = BORDER_CONSTANT,
                 border_value=(0, 0, 0, 0), layout: int = NHWC, out=None, stream=None) -> torch.Tensor:
-    """va_cv::warp_affine (cv.h:118-122); m is the forward 2x3 map."""
+    """va_cv::warp_affine (cv.h:118-122); m is the forward 2x3 map, or the
+    inverse one with flags | WARP_INVERSE_MAP; flags INTER_LINEAR (the
+    reference's naive sampler) or INTER_NEAREST (OpenCV 2.4's)."""
     s4 = _as4d(src, layout)
     if out is None:
         out = _empty_like_shape(s4, layout, w, h, src.dtype, True, src.dim())

@@ -286,20 +286,25 @@ def make_workload(name: str, batch: int, dev, rank: int, world: int, ops) -> dic
         dst = torch.empty((B, 224, 224, 3), dtype=torch.float32, device=dev)
         stats = {}
 
+        def main(stream=None):
+            # the resize with the per-rank (Sum x, Sum x^2) fused into the
+            # cubic kernel (vacv_resize_channel_sums) and its fixed-order
+            # reduction
+            stats["sums"] = ops.resize_channel_sums(src, 224, 224, INTER_CUBIC, per_image=False, out=dst,
+                                                    stream=stream)[1]
+
         def extra(stream=None):
-            # the global mean/stddev of the whole sharded batch: exact per-rank
-            # sums (vacv_channel_sums), ONE all-reduce of the (c, 2) fp64 sums
-            # over RCCL, vacv_stats_from_sums -- identical on every rank, no
-            # host sync
-            sums = ops.channel_sums(dst, per_image=False)
+            # the global mean/stddev of the whole sharded batch: ONE all-reduce
+            # of the (c, 2) fp64 sums over RCCL, vacv_stats_from_sums --
+            # identical on every rank, no host sync
+            sums = stats["sums"]
             if world > 1:
                 torch.distributed.all_reduce(sums, op=torch.distributed.ReduceOp.SUM)
             stats["mean"], stats["std"] = ops.stats_from_sums(sums, float(B) * world * 224 * 224)
         return {"batch": B, "px": 2560 * 1440, "b_alg": B * resize_bytes(2560, 1440, 3, 224, 224, 1, 4, cubic=True),
                 "kernel": "cubic_direct_kernel", "frame": "2560x1440x3", "output": "224x224x3 fp32 + global mean/std",
                 "desc": "resize INTER_CUBIC 2560x1440x3 u8 -> 224x224x3 fp32 + global mean_stddev (RCCL all-reduce)",
-                "main": lambda stream=None: ops.resize(src, 224, 224, interpolation=INTER_CUBIC, out=dst, stream=stream),
-                "extra": extra}
+                "main": main, "extra": extra}
     B = batch or 256
     src = u8(B, H_IN, W_IN, C)
     dst = torch.empty((B, H_OUT, W_OUT, C), dtype=torch.float32, device=dev)

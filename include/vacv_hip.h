@@ -49,6 +49,8 @@ enum { VACV_FP32 = 0, VACV_FP16 = 1, VACV_INT8 = 2 /* unsigned bytes */, VACV_FP
 enum { VACV_NCHW = 0, VACV_NHWC = 1 };
 /* va_cv::VInterMode (cv.h:27-35) */
 enum { VACV_INTER_NEAREST = 0, VACV_INTER_LINEAR = 1, VACV_INTER_CUBIC = 2, VACV_INTER_AREA = 3 };
+/* warp flag (cv.h:35): m is already the inverse (dst -> src) map */
+enum { VACV_WARP_INVERSE_MAP = 16 };
 /* va_cv::VBorderMode (cv.h:38-48) */
 enum {
     VACV_BORDER_CONSTANT = 0, VACV_BORDER_REPLICATE = 1, VACV_BORDER_REFLECT = 2, VACV_BORDER_WRAP = 3,
@@ -141,7 +143,15 @@ int vacv_resize_scaled(const vacv_image* src, const vacv_image* dst, int interpo
 /* WarpAffine::warp_affine (warp_affine.cpp:16-36, :111-169, cv.h:118-122).
  * m = the FORWARD 2x3 map, row-major; it is inverted on the host with the
  * reference's arithmetic and is NOT modified (the reference inverts the
- * caller's M in place).  INTER_LINEAR only.  A pixel whose top-left tap is
+ * caller's M in place).  flags = INTER_LINEAR or INTER_NEAREST, optionally
+ * | VACV_WARP_INVERSE_MAP (m is then the dst -> src map, used as is); the
+ * reference hands every flag but INTER_LINEAR to cv::warpAffine
+ * (warp_affine.cpp:114-118), so those are restated from OpenCV 2.4 (parity
+ * unpinned):
+ *   INTER_NEAREST  cv::warpAffine's fp64 fixed point (AB_BITS = 10, round
+ *                  half to even), remap's nearest sampler; the border modes
+ *                  below on the mapped pixel
+ * INTER_LINEAR: a pixel whose top-left tap is
  * inside [0,w-2]x[0,h-2] is the reference's naive sampler bit for bit; the
  * others depend on border_mode:
  *   BORDER_CONSTANT     border_value (the reference leaves them untouched);

@@ -84,6 +84,7 @@ class Oracle:
             ("oracle_yuv420sp_to_bgr", [_P, _P, _I, _I, _I, _I], None),
             ("oracle_bgr2nv21", [_P, _P, _I, _I], None),
             ("oracle_yuv420_cv", [_P, _P, _I, _I, _I, _I, _I], None),
+            ("oracle_warp_affine_nn", [_P, _I, _I, _I, _I, _P, _I, _I, _P, _I, _I, _P], None),
             ("oracle_gray_to_bgr", [_P, _P, _L, _I, _I], None),
             ("oracle_hwc_to_chw", [_P, _P, _I, _I, _I, _I], None),
             ("oracle_chw_to_hwc", [_P, _P, _I, _I, _I, _I], None),
@@ -221,6 +222,18 @@ class Oracle:
         return out
 
     # -- colour ----------------------------------------------------------------
+    def warp_affine_nn(self, img, m, w_out, h_out, inverse_map=False, border_mode=0, border=(0, 0, 0, 0), dst=None):
+        """cv::warpAffine INTER_NEAREST (OpenCV 2.4), m forward (or inverse
+        with inverse_map); border_mode 5 keeps `dst` where unmapped."""
+        img = np.ascontiguousarray(img)
+        w, h, c = _shape(img)
+        out = np.ascontiguousarray(dst).copy() if dst is not None else _out(h_out, w_out, c, img.dtype)
+        mm = np.ascontiguousarray(m, np.float32)
+        bv = np.ascontiguousarray(border, np.float64)
+        self.lib.oracle_warp_affine_nn(_ptr(img), w, h, c, img.itemsize, _ptr(out), w_out, h_out, _ptr(mm),
+                                       int(inverse_map), int(border_mode), _ptr(bv))
+        return out
+
     def yuv420sp_to_bgr(self, yuv, v_first=True, rgb=False):
         yuv = np.ascontiguousarray(yuv, np.uint8)
         h = yuv.shape[0] // 3 * 2

@@ -653,6 +653,61 @@ void oracle_warp_affine_border(const void* src, int w_in, int h_in, int cc, int 
     }
 }
 
+/* cv::warpAffine with INTER_NEAREST (the reference hands every flag but
+ * INTER_LINEAR to OpenCV, warp_affine.cpp:114-118), as OpenCV 2.4.13's
+ * imgwarp.cpp computes it: the float map widened to double and, unless
+ * inverse_map (WARP_INVERSE_MAP), inverted in double; AB_BITS = 10 fixed
+ * point with cvRound (half to even)
+ *   X0 = cvRound((M1 y + M2) 1024) + 512, X = (X0 + cvRound(M0 x 1024)) >> 10
+ * (Y likewise with M3..M5), clamped to short as remap's map; then remap's
+ * nearest sampler: inside -> the source pixel; outside -> border (mode 0),
+ * dst untouched (5), else the pixel at borderInterpolate (modes 1-4).
+ * esize 1 (u8) or 4 (fp32); border[] already in the element type's range.
+ * Parity unpinned: no OpenCV runs here. */
+void oracle_warp_affine_nn(const void* src, int w_in, int h_in, int cc, int esize, void* dst, int w_out, int h_out,
+                           const float m[6], int inverse_map, int mode, const double border[4]) {
+    double M[6];
+    for (int i = 0; i < 6; ++i) M[i] = (double)m[i];
+    if (!inverse_map) {
+        double D = M[0] * M[4] - M[1] * M[3];
+        D = D != 0 ? 1. / D : 0;
+        const double A11 = M[4] * D, A22 = M[0] * D;
+        M[0] = A11;
+        M[1] *= -D;
+        M[3] *= -D;
+        M[4] = A22;
+        const double b1 = -M[0] * M[2] - M[1] * M[5];
+        const double b2 = -M[3] * M[2] - M[4] * M[5];
+        M[2] = b1;
+        M[5] = b2;
+    }
+    const uint8_t* s = (const uint8_t*)src;
+    uint8_t* d = (uint8_t*)dst;
+    for (int y = 0; y < h_out; ++y) {
+        const int X0 = (int)nearbyint((M[1] * y + M[2]) * 1024.0) + 512;
+        const int Y0 = (int)nearbyint((M[4] * y + M[5]) * 1024.0) + 512;
+        for (int x = 0; x < w_out; ++x) {
+            int X = (int)((uint32_t)X0 + (uint32_t)(int)nearbyint(M[0] * x * 1024.0)) >> 10;
+            int Y = (int)((uint32_t)Y0 + (uint32_t)(int)nearbyint(M[3] * x * 1024.0)) >> 10;
+            X = X < -32768 ? -32768 : (X > 32767 ? 32767 : X);
+            Y = Y < -32768 ? -32768 : (Y > 32767 ? 32767 : Y);
+            uint8_t* o = d + ((int64_t)y * w_out + x) * cc * esize;
+            const int inside = X >= 0 && X < w_in && Y >= 0 && Y < h_in;
+            if (!inside && mode == 5) continue;
+            if (!inside && mode == 0) {
+                for (int k = 0; k < cc; ++k) {
+                    if (esize == 1) o[k] = (uint8_t)border[k];
+                    else { const float f = (float)border[k]; memcpy(o + 4 * k, &f, 4); }
+                }
+                continue;
+            }
+            const int sx = inside ? X : oracle_border_index(X, w_in, mode);
+            const int sy = inside ? Y : oracle_border_index(Y, h_in, mode);
+            memcpy(o, s + ((int64_t)sy * w_in + sx) * cc * esize, (size_t)cc * esize);
+        }
+    }
+}
+
 /* ------------------------------------------------------------------------ */
 /* YUV420 semi-planar -> BGR, cvt_color.cpp:39-135 (BT.601 full range, 7-bit
  * integer coefficients, arithmetic shifts).  v_first=1: NV21 (VU pairs);

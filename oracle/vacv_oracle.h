@@ -59,6 +59,11 @@ void oracle_warp_affine_f32(const float* src, int w_in, int h_in, int cc,
 void oracle_warp_affine_border(const void* src, int w_in, int h_in, int cc, int esize,
                                void* dst, int w_out, int h_out, const float m[6], int mode);
 
+/* cv::warpAffine INTER_NEAREST (OpenCV 2.4 fixed point + remap nearest);
+ * inverse_map: m is the dst -> src map; modes 0-5; esize 1 or 4 */
+void oracle_warp_affine_nn(const void* src, int w_in, int h_in, int cc, int esize, void* dst, int w_out, int h_out,
+                           const float m[6], int inverse_map, int mode, const double border[4]);
+
 /* --- colour ------------------------------------------------------------ */
 void oracle_yuv420sp_to_bgr(const uint8_t* src, uint8_t* dst, int w, int h, int v_first, int rgb_out);
 void oracle_bgr2nv21(const uint8_t* bgr, uint8_t* dst, int w, int h);

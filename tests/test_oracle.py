@@ -427,3 +427,45 @@ def test_cv_color_restatement(oracle):
     gf = rng.standard_normal((5, 7)).astype(np.float32)
     want4 = np.concatenate([np.repeat(gf[..., None], 3, 2), np.ones((5, 7, 1), np.float32)], 2)
     assert np.array_equal(oracle.gray_to_bgr(gf, 4), want4)
+
+
+def test_warp_nearest_restatement(oracle):
+    """cv::warpAffine INTER_NEAREST (the reference hands it to OpenCV,
+    warp_affine.cpp:114-118): oracle_warp_affine_nn against an independent
+    numpy statement of OpenCV 2.4's fixed point (fp64 inverse, AB_BITS = 10,
+    half-to-even rounding) and remap's nearest sampler, for a forward and an
+    inverse map (WARP_INVERSE_MAP), CONSTANT / REPLICATE / WRAP borders.
+    Parity unpinned."""
+    rng = np.random.default_rng(17)
+    img = rng.integers(0, 256, (23, 31, 3), dtype=np.uint8)
+    m = oracle.rotation_matrix(0.8, 27.0, [15, 11, 18, 9])
+    inv32 = oracle.invert_affine(m)
+    for inverse in (False, True):
+        if inverse:
+            given = inv32
+            M = inv32.astype(np.float64)
+        else:
+            given = m
+            f = m.astype(np.float64)
+            D = f[0] * f[4] - f[1] * f[3]
+            D = 1.0 / D if D != 0 else 0.0
+            M = np.array([f[4] * D, f[1] * -D, 0.0, f[3] * -D, f[0] * D, 0.0])
+            M[2] = -M[0] * f[2] - M[1] * f[5]
+            M[5] = -M[3] * f[2] - M[4] * f[5]
+        ys, xs = np.mgrid[0:19, 0:29]
+        X0 = np.rint((M[1] * ys + M[2]) * 1024.0).astype(np.int64) + 512
+        Y0 = np.rint((M[4] * ys + M[5]) * 1024.0).astype(np.int64) + 512
+        X = np.clip((X0 + np.rint(M[0] * xs * 1024.0).astype(np.int64)) >> 10, -32768, 32767)
+        Y = np.clip((Y0 + np.rint(M[3] * xs * 1024.0).astype(np.int64)) >> 10, -32768, 32767)
+        inside = (X >= 0) & (X < 31) & (Y >= 0) & (Y < 23)
+        for mode in (0, 1, 3):
+            if mode == 0:
+                want = np.zeros((19, 29, 3), np.uint8)
+                want[...] = (7, 8, 9)
+                want[inside] = img[Y[inside], X[inside]]
+            else:
+                bx = np.clip(X, 0, 30) if mode == 1 else np.mod(X, 31)
+                by = np.clip(Y, 0, 22) if mode == 1 else np.mod(Y, 23)
+                want = img[by, bx]
+            got = oracle.warp_affine_nn(img, given, 29, 19, inverse_map=inverse, border_mode=mode, border=(7, 8, 9, 0))
+            assert np.array_equal(got, want), (inverse, mode)
