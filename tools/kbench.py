@@ -170,9 +170,16 @@ def run_cases(cases, iters, tag):
         torch.cuda.synchronize()
         ms = sorted(e0.elapsed_time(e1) for e0, e1 in ev)
         med = ms[len(ms) // 2]
-        print(json.dumps({"case": name, **({"knobs": tag} if tag else {}), "ms_median": round(med, 4), "ms_min": round(ms[0], 4),
-                          "alg_GBps": round(nbytes / med / 1e6, 1), "frac_8TBps": round(nbytes / med / 1e6 / 8000, 4),
-                          "Mpx_s": round(px / med / 1e3, 1)}), flush=True)
+        if name.endswith("_macs"):
+            # a compute rate, not bytes: u8 multiply-adds of the correlation
+            # per second, against the dense i8 MFMA peak (~5 POP/s = 2.5
+            # PMAC/s, MI355X_MICROARCH.md; the kernel's nibble split issues
+            # twice these MACs on the matrix cores)
+            rate = {"GMAC_s": round(nbytes / med / 1e6, 1), "frac_i8_mfma_dense": round(nbytes / med / 1e6 / 2.5e6, 4)}
+        else:
+            rate = {"alg_GBps": round(nbytes / med / 1e6, 1), "frac_8TBps": round(nbytes / med / 1e6 / 8000, 4)}
+        print(json.dumps({"case": name, **({"knobs": tag} if tag else {}), "ms_median": round(med, 4),
+                          "ms_min": round(ms[0], 4), **rate, "Mpx_s": round(px / med / 1e3, 1)}), flush=True)
 
 
 if __name__ == "__main__":
