@@ -521,261 +521,8 @@ resize_kernel(ResizeLaunch L) {
     }
 }
 
-// ---------------------------------------------------------------------------
-// resize_rows_kernel: the streaming form.  A tile is tile_h WHOLE output rows
-// of one plane (the planner sizes it at ~8 KiB of output); tiles are numbered
-// in address order (image, plane, row group) and a grid of resident
-// workgroups walks them grid-stride, so at any moment the chip's in-flight
-// reads and writes cover a compact, monotonically advancing window of HBM.
-// Measured on MI355X, that traffic shape moves 5.98 TB/s for the 3x-downscale
-// mix where strip-persistent workgroups (resize_kernel: each walks its own
-// contiguous region) top out near 5.0 (tools/membench2.hip).
-// Per tile:
-//   1. the tile's source rows with a non-zero vertical weight (planner list,
-//      scalar loads) are read whole by 16-byte non-temporal buffer loads,
-//      all of a thread's loads issued before any LDS write;
-//   2. each lane owns fixed 4-element output chunks j = tid + m*256 of the
-//      tile (lane-stationary: the column taps, channel and LDS offsets of its
-//      elements are resolved once per workgroup from the planner's per-pixel
-//      table), samples the staged rows, applies the epilogue and writes each
-//      chunk with one non-temporal store (16 B fp32 / 4 B u8).
-// ---------------------------------------------------------------------------
 namespace {
-constexpr int kRowsAux = 2;  // nt (gfx950 aux bit 1): source rows and outputs are touched once
-}  // namespace
 
-template <int KIND, int CC, typename TIn, int OUT, int MODE>
-__global__ void __launch_bounds__(kBlock)
-resize_rows_kernel(ResizeLaunch L) {
-    constexpr int TAPS = (KIND == kCubic) ? 4 : 2;
-    constexpr int ES = sizeof(TIn);
-    using TOut = typename std::conditional<(OUT == kOutSame), TIn, float>::type;
-    constexpr int OS = sizeof(TOut);
-    constexpr int E = 4;                   // elements per chunk
-    constexpr int M = kRowsMaxChunksPerLane;
-    using Smp = Sampler<KIND, CC, TIn, MODE>;
-    using XW = typename Smp::XW;
-    constexpr bool kHoldXW = sizeof(XW) <= 8;
-
-    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
-    int* rowinfo_l = reinterpret_cast<int*>(lds);  // [tile_h][8]
-    unsigned char* rows_l = lds + 32 * 8 * 4 + ((L.max_slots * 4 + 15) & ~15);
-    const int tid = threadIdx.x;
-
-    // ---- lane-stationary chunk constants ---------------------------------------
-    const int rl = L.dst.w * CC;        // elements per output row
-    const int cpo = (rl + E - 1) / E;   // chunks per output row
-    const int tile_chunks = L.tile_h * cpo;
-    int c_t[M];                         // tile row of chunk slot m (tile_h = none)
-    int c_off[M][E];                    // LDS column offset (bits 0-23) | channel << 24
-    XW c_xw[M][kHoldXW ? E : 1];
-    int c_px[M][kHoldXW ? 1 : E];
-#pragma unroll
-    for (int m = 0; m < M; ++m) {
-        const int j = tid + m * kBlock;
-        const bool live = j < tile_chunks;
-        const int t = live ? j / cpo : 0;
-        c_t[m] = live ? t : L.tile_h;
-        const int e0 = (j - t * cpo) * E;
-#pragma unroll
-        for (int i = 0; i < E; ++i) {
-            const int e = live ? min(e0 + i, rl - 1) : 0;
-            const int px = e / CC;
-            const int k = e - px * CC;
-            c_off[m][i] = (L.plan.xoff[px] + ES * k) | (k << 24);
-            if constexpr (kHoldXW) c_xw[m][i] = reinterpret_cast<const XW*>(L.plan.xw)[px];
-            else c_px[m][i] = px;
-        }
-    }
-
-    const int tiles_total = L.n * L.src.planes * L.tiles_y;
-    const int64_t rp = L.src.row_pitch;
-    const int cpr = L.slot_stride >> 4;
-    int cur_img = -1;
-    ChanNorm cn[CC] = {};
-    bool all_mul = false;
-
-    // One tile's addressing (uniform).
-    struct TileRef {
-        int task, img, plane, ns, nchunks, y0, ny;
-        const int* trow;
-        Rsrc rs;
-        uint32_t limit;
-    };
-    auto tile_ref = [&](int tile) {
-        TileRef r;
-        r.task = tile % L.tiles_y;
-        const int pidx = tile / L.tiles_y;  // image * planes + plane
-        r.img = pidx / L.src.planes;
-        r.plane = pidx - r.img * L.src.planes;
-        const unsigned char* src_plane =
-            L.src.base + (int64_t)r.img * L.src.img_pitch + (int64_t)r.plane * L.src.plane_pitch;
-        r.rs = make_rsrc(src_plane, L.src.plane_bytes);
-        r.limit = (uint32_t)L.src.plane_bytes + r.rs.delta;
-        r.ns = L.plan.task_nslots[r.task];
-        r.trow = L.plan.task_rows + (int64_t)r.task * L.max_slots;
-        r.nchunks = r.ns * cpr;
-        r.y0 = r.task * L.tile_h;
-        r.ny = min(L.tile_h, L.dst.h - r.y0);
-        return r;
-    };
-    auto chunk_load = [&](const TileRef& r, int k) {
-        const int sl = k / cpr;
-        const uint32_t o = ((((uint32_t)((int64_t)r.trow[sl] * rp)) + r.rs.delta) & ~15u) + 16u * (k - sl * cpr);
-        uint4 v;
-        if (o + 16u <= r.limit) {
-            auto x = __builtin_amdgcn_raw_buffer_load_b128(r.rs.r, (int)o, 0, kRowsAux);
-            v = *reinterpret_cast<uint4*>(&x);
-        } else {
-            v = load16_safe(r.rs, o, r.limit);
-        }
-        return v;
-    };
-    // Software pipeline: the first kPF*256 chunks of the NEXT tile's rows and
-    // its row info are loaded into registers before the current tile is
-    // computed, so their HBM / L2 latency hides under the compute and stores.
-    constexpr int kPF = 2;
-    uint4 pf[kPF];
-    int pf_ri[8];
-    auto prefetch = [&](const TileRef& r) {
-#pragma unroll
-        for (int m = 0; m < kPF; ++m) {
-            const int k = tid + m * kBlock;
-            if (k < r.nchunks) pf[m] = chunk_load(r, k);
-        }
-        if (tid < r.ny) {
-            // rowinfo[t]: LDS offset of each tap's row (a zero weight points
-            // at a valid staged row: the sampler multiplies it by 0, as the
-            // reference does), then the weights (int bits for fixed point)
-            const int nc = L.tile_h * TAPS;
-#pragma unroll
-            for (int q = 0; q < TAPS; ++q) {
-                const int sl = L.plan.task_cand[(int64_t)r.task * nc + tid * TAPS + q];
-                const int s = sl >= 0 ? sl : 0;
-                pf_ri[q] = s * L.slot_stride + (int)((((uint32_t)((int64_t)r.trow[s] * rp)) + r.rs.delta) & 15u);
-            }
-            if (KIND == kCubic) {
-                const int4 w = reinterpret_cast<const int4*>(L.plan.yw)[r.y0 + tid];
-                pf_ri[4] = w.x; pf_ri[5] = w.y; pf_ri[6] = w.z; pf_ri[7] = w.w;
-            } else {
-                const int2 w = reinterpret_cast<const int2*>(L.plan.yw)[r.y0 + tid];  // int or float bits
-                pf_ri[4] = w.x; pf_ri[5] = w.y;
-            }
-        }
-    };
-
-    int tile = blockIdx.x;
-    if (tile < tiles_total) prefetch(tile_ref(tile));
-    for (; tile < tiles_total; tile += gridDim.x) {
-        const TileRef cur = tile_ref(tile);
-        const int img = cur.img, plane = cur.plane, y0 = cur.y0, ny = cur.ny;
-        if (OUT == kOutNorm && img != cur_img) {  // uniform
-            cur_img = img;
-            all_mul = KIND == kLinearFixed;
-#pragma unroll
-            for (int k = 0; k < CC; ++k) {
-                cn[k] = chan_norm(L.norm, img, CC == 1 ? plane % L.norm.c_total : k);
-                all_mul = all_mul && cn[k].mul;
-            }
-        }
-        __syncthreads();  // the previous tile is consumed
-        // ---- 1. stage the tile's weighted source rows (whole rows) -----------
-#pragma unroll
-        for (int m = 0; m < kPF; ++m) {
-            const int k = tid + m * kBlock;
-            if (k < cur.nchunks) *reinterpret_cast<uint4*>(rows_l + 16 * k) = pf[m];  // slot_stride = 16 * cpr
-        }
-        constexpr int kStage = 4;  // chunks beyond the prefetch depth: loaded now
-        for (int base = kPF * kBlock; base < cur.nchunks; base += kStage * kBlock) {
-            uint4 v[kStage];
-#pragma unroll
-            for (int m = 0; m < kStage; ++m) {
-                const int k = base + tid + m * kBlock;
-                if (k < cur.nchunks) v[m] = chunk_load(cur, k);
-            }
-#pragma unroll
-            for (int m = 0; m < kStage; ++m) {
-                const int k = base + tid + m * kBlock;
-                if (k < cur.nchunks) *reinterpret_cast<uint4*>(rows_l + 16 * k) = v[m];
-            }
-        }
-        if (tid < ny) {
-            int* ri = rowinfo_l + tid * 8;
-#pragma unroll
-            for (int q = 0; q < 8; ++q) ri[q] = pf_ri[q];
-        }
-        __syncthreads();  // rows + row info visible
-        if (tile + (int)gridDim.x < tiles_total) prefetch(tile_ref(tile + gridDim.x));
-
-        // ---- 2. compute + store ------------------------------------------------
-        unsigned char* dst_plane = const_cast<unsigned char*>(L.dst.base) + (int64_t)img * L.dst.img_pitch +
-                                   (int64_t)plane * L.dst.plane_pitch;
-        const Rsrc rd = make_rsrc(dst_plane, L.dst.plane_bytes);
-        auto pass = [&](auto mul_tag) {
-            constexpr bool MUL = decltype(mul_tag)::value;
-#pragma unroll
-            for (int m = 0; m < M; ++m) {
-                if (c_t[m] >= ny) continue;
-                const RowTaps rt = row_taps(rowinfo_l + c_t[m] * 8);
-                TOut out[E];
-                auto elems = [&](auto two_tag) {
-                    constexpr bool TWO = decltype(two_tag)::value;
-#pragma unroll
-                    for (int i = 0; i < E; ++i) {
-                        XW xw;
-                        if constexpr (kHoldXW) xw = c_xw[m][i];
-                        else xw = reinterpret_cast<const XW*>(L.plan.xw)[c_px[m][i]];
-                        const auto v = Smp::template at<TWO>(rows_l, c_off[m][i] & 0xFFFFFF, xw, rt);
-                        if constexpr (OUT == kOutNorm) {
-                            const ChanNorm c = pick(cn, c_off[m][i] >> 24);
-                            if constexpr (KIND == kLinearFixed) {
-                                // normalize_naive.cpp:74-90 on a u8-valued result
-                                const double d = (double)((float)v - c.mean);
-                                if constexpr (MUL) out[i] = (float)(d * c.inv);
-                                else out[i] = (float)(d / ((double)c.stdv + 1e-6));
-                            } else {
-                                out[i] = normalize_f(c, (float)v);
-                            }
-                        } else {
-                            out[i] = (TOut)v;
-                        }
-                    }
-                };
-                if (KIND == kCubic || rt.w[1] != 0) elems(std::true_type{});
-                else elems(std::false_type{});
-                const int e0 = (tid + m * kBlock - c_t[m] * cpo) * E;
-                const int64_t ob = (int64_t)(y0 + c_t[m]) * L.dst.row_pitch + (int64_t)e0 * OS;
-                const uint32_t boff = (uint32_t)ob + rd.delta;
-                const int valid = min(E, rl - e0);
-                if constexpr (OS == 4) {
-                    if (valid == E && (boff & 15u) == 0) {
-                        u32x4 d = {__float_as_uint(out[0]), __float_as_uint(out[1]), __float_as_uint(out[2]),
-                                   __float_as_uint(out[3])};
-                        __builtin_amdgcn_raw_buffer_store_b128(d, rd.r, (int)boff, 0, kRowsAux);
-                        continue;
-                    }
-                } else {
-                    if (valid == E && (boff & 3u) == 0) {
-                        const uint32_t d = (uint32_t)out[0] | ((uint32_t)out[1] << 8) | ((uint32_t)out[2] << 16) |
-                                           ((uint32_t)out[3] << 24);
-                        __builtin_amdgcn_raw_buffer_store_b32(d, rd.r, (int)boff, 0, kRowsAux);
-                        continue;
-                    }
-                }
-                TOut* dp = reinterpret_cast<TOut*>(dst_plane + ob);
-#pragma unroll
-                for (int i = 0; i < E; ++i)
-                    if (i < valid) dp[i] = out[i];
-            }
-        };
-        if (OUT == kOutNorm && KIND == kLinearFixed && all_mul) pass(std::true_type{});
-        else pass(std::false_type{});
-    }
-}
-
-namespace {
-// Workgroups of this kernel instance the device holds at once, for an LDS
-// footprint (cached: the occupancy query is not free).
 template <typename K>
 int64_t resident_workgroups(K kernel, int lds_bytes) {
     static std::mutex mu;
@@ -796,20 +543,6 @@ int64_t resident_workgroups(K kernel, int lds_bytes) {
 
 template <int KIND, int CC, typename TIn, int OUT, int MODE>
 hipError_t launch_one(ResizeLaunch L, hipStream_t s) {
-    if (L.rows_mode) {
-        // grid-stride over address-ordered tiles with one wave of resident
-        // workgroups (VACV_RESIZE_WGS overrides, for measurement)
-        auto rk = resize_rows_kernel<KIND, CC, TIn, OUT, MODE>;
-        const int64_t tiles = (int64_t)L.n * L.src.planes * L.tiles_y;
-        if (tiles > 0x7FFFFFFF) return hipErrorInvalidValue;
-        const int64_t resident = resident_workgroups(rk, L.lds_bytes);
-        if (resident <= 0) return hipErrorInvalidValue;
-        const int wgs = tune(VACV_TUNE_RESIZE_WGS);
-        const int64_t want = wgs > 0 ? wgs : resident;
-        const int64_t blocks = std::min<int64_t>(tiles, want);
-        hipLaunchKernelGGL(rk, dim3((unsigned)blocks), dim3(kBlock), L.lds_bytes, s, L);
-        return hipGetLastError();
-    }
     auto kernel = resize_kernel<KIND, CC, TIn, OUT, MODE>;
     const int64_t resident = resident_workgroups(kernel, L.lds_bytes);
     if (resident <= 0) return hipErrorInvalidValue;

@@ -123,44 +123,6 @@ bool evaluate(const ResizeLaunch& L, const std::vector<Taps>& xt, const std::vec
 
 int knob(int key, int def) { return tune_or(key, def); }
 
-// Rows mode (resize_rows_kernel): a tile is `tile_h` whole output rows; the
-// staged rows are whole source rows (column 0 on, the kernel evaluates the
-// column taps itself).  LDS: row info + per-slot heads + the slots.
-constexpr int kRowsLdsBudget = 48 * 1024;
-
-bool evaluate_rows(const ResizeLaunch& L, const std::vector<Taps>& yt, int tile_h, Geometry& g) {
-    const int taps = L.kind == kCubic ? 4 : 2;
-    const int bp = L.src.cc * L.src.esize;
-    if (tile_h * taps > 64) return false;
-    // every lane owns at most kRowsMaxChunksPerLane 4-element chunks of a tile
-    const int64_t cpo = ((int64_t)L.dst.w * L.dst.cc + 3) / 4;
-    if ((int64_t)tile_h * cpo > (int64_t)kRowsMaxChunksPerLane * kBlock) return false;
-    if ((int64_t)(L.src.w + 4) * bp >= (1 << 24)) return false;  // LDS offsets packed in 24 bits
-    g.tile_w = L.dst.w;
-    g.tile_h = tile_h;
-    g.tiles_x = 1;
-    g.tiles_y = (L.dst.h + tile_h - 1) / tile_h;
-    g.sparse = ((double)L.src.h / L.dst.h) >= taps ? 1 : 0;
-    g.max_cpr = (int)(((int64_t)L.src.w * bp + 30) / 16);
-    g.slot_stride = g.max_cpr * 16;
-    int slots = 1;
-    for (int ty = 0; ty < g.tiles_y; ++ty) {
-        const int y0 = ty * tile_h, ny = std::min(tile_h, L.dst.h - y0);
-        int cnt = 0;
-        if (g.sparse) {
-            for (int t = 0; t < ny; ++t)
-                for (int j = 0; j < taps; ++j) cnt += weight_nonzero(L, yt[y0 + t], j);
-        } else {
-            cnt = yt[y0 + ny - 1].origin + taps - 1 - yt[y0].origin + 1;
-        }
-        slots = std::max(slots, cnt);
-    }
-    g.max_slots = slots;
-    const int64_t lds = 32 * 8 * 4 + a16((size_t)slots * 4) + (int64_t)slots * g.slot_stride;
-    g.lds = (int)std::min<int64_t>(lds, 1 << 30);
-    return lds <= kRowsLdsBudget;
-}
-
 struct CachedPlan {
     int device = 0;              // owner of dev
     void* dev = nullptr;
@@ -185,7 +147,7 @@ void put(std::string& k, const T& v) {
 
 }  // namespace
 
-int plan_resize(ResizeLaunch& L, hipStream_t stream, int rows) {
+int plan_resize(ResizeLaunch& L, hipStream_t stream) {
     const int taps = L.kind == kCubic ? 4 : 2;
     const bool lut = false;  // kernels normalise arithmetically (NormSpec.inv / mul_ok)
 
@@ -200,9 +162,7 @@ int plan_resize(ResizeLaunch& L, hipStream_t stream, int rows) {
     const int force_h = knob(VACV_TUNE_RESIZE_TILE_H, 0);
     const int force_w = knob(VACV_TUNE_RESIZE_TILE_W, 0);
     const int work = std::max(1, knob(VACV_TUNE_RESIZE_WORK, kWorkPerThread));
-    // rows mode: ~8 KiB of output per workgroup (VACV_RESIZE_ROWS_BYTES)
-    const int rows_bytes = std::max(1, knob(VACV_TUNE_RESIZE_ROWS_BYTES, 8192));
-    put(key, force_h); put(key, force_w); put(key, work); put(key, rows); put(key, rows_bytes);
+    put(key, force_h); put(key, force_w); put(key, work);
 
     std::lock_guard<std::mutex> lk(g_mu);
     auto it = g_plans.find(key);
@@ -217,19 +177,11 @@ int plan_resize(ResizeLaunch& L, hipStream_t stream, int rows) {
         int tile_w = L.dst.w;
         Geometry g{};
         bool ok = false;
-        if (rows) {
-            const int64_t out_row = (int64_t)L.dst.w * L.dst.cc * L.dst.esize;
-            int th = (int)std::max<int64_t>(1, std::min<int64_t>(32, (rows_bytes + out_row / 2) / out_row));
-            if (force_h > 0) th = std::min(force_h, 32);
-            th = std::min(th, L.dst.h);
-            for (; th >= 1 && !ok; --th) ok = evaluate_rows(L, yt, th, g);
-            if (!ok) return VACV_ERR_UNSUPPORTED;
-        }
-        if (!rows && (int64_t)(L.src.w + taps) * bp > 12288) {
+        if ((int64_t)(L.src.w + taps) * bp > 12288) {
             const double sx = (double)L.src.w / L.dst.w;
             tile_w = std::min(L.dst.w, std::max(64, (int)(8192.0 / (sx * bp)) / 64 * 64));
         }
-        if (!rows && L.dst.esize == 4) {
+        if (L.dst.esize == 4) {
             // fp32 output: a tile row is at most kResizeMaxChunksPerLane
             // 4-element chunks per lane (k_resize.hip); split evenly
             const int max_w = std::max(4, (4 * kResizeMaxChunksPerLane * kBlock / L.dst.cc) / 4 * 4);
@@ -238,8 +190,8 @@ int plan_resize(ResizeLaunch& L, hipStream_t stream, int rows) {
                 tile_w = std::min(max_w, ((L.dst.w + nt - 1) / nt + 3) / 4 * 4);
             }
         }
-        if (!rows && force_w > 0) tile_w = std::min(force_w, L.dst.w);
-        for (; !rows;) {
+        if (force_w > 0) tile_w = std::min(force_w, L.dst.w);
+        for (;;) {
             // work items per output row: 4-pixel groups (byte output) or
             // 4-element chunks (fp32 output), see k_resize.hip
             const int per_row = L.dst.esize == 1 ? (tile_w + 3) / 4 : (tile_w * L.dst.cc + 3) / 4;
@@ -276,7 +228,7 @@ int plan_resize(ResizeLaunch& L, hipStream_t stream, int rows) {
         auto F = [&](size_t o) { return reinterpret_cast<float*>(img.data() + o); };
         for (int tx = 0; tx < g.tiles_x; ++tx) {
             const int x0 = tx * g.tile_w, nx = std::min(g.tile_w, L.dst.w - x0);
-            const int cf = rows ? 0 : xt[x0].origin;  // rows mode stages whole rows
+            const int cf = xt[x0].origin;
             I(o_cf)[tx] = cf;
             I(o_cpr)[tx] = ((xt[x0 + nx - 1].origin + taps - 1 - cf + 1) * bp + 30) / 16;
             for (int i = 0; i < nx; ++i) {

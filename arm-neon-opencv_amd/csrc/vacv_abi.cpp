@@ -329,8 +329,7 @@ int resize_impl(const vacv_image* src_d, const vacv_image* dst_d, int interpolat
     // kernel measured faster (1280x720: 0.63 vs 0.69 ms).  VACV_TUNE_RESIZE_DIRECT
     // = 0 never / 2 always uses the gather kernel, for A/B tests.
     // Otherwise resize_kernel with interleaved (address-ordered) tasks;
-    // VACV_TUNE_RESIZE_INTERLEAVE = 0 selects its strip order and
-    // VACV_TUNE_RESIZE_ROWS = 1 the whole-row kernel.
+    // VACV_TUNE_RESIZE_INTERLEAVE = 0 selects its strip order.
     const int direct = tune_or(VACV_TUNE_RESIZE_DIRECT, 1);
     if (L.kind == kLinearFixed && L.src.cc <= 4 && dst.w < (1 << 23) && dst.h < (1 << 23) &&
         (direct == 2 || (direct == 1 && resize_one_tap_rows(L))))
@@ -355,13 +354,7 @@ int resize_impl(const vacv_image* src_d, const vacv_image* dst_d, int interpolat
         return hip_status(launch_cubic_direct(L, s));
     }
     L.interleave = tune(VACV_TUNE_RESIZE_INTERLEAVE) != 0;
-    L.rows_mode = tune(VACV_TUNE_RESIZE_ROWS) == 1;
-    if (L.rows_mode) {
-        st = plan_resize(L, s, 1);
-        if (st == VACV_ERR_UNSUPPORTED) L.rows_mode = 0;
-        else if (st) return st;
-    }
-    if (!L.rows_mode && (st = plan_resize(L, s, 0))) return st;
+    if ((st = plan_resize(L, s))) return st;
     return hip_status(launch_resize(L, s));
 }
 

@@ -13,7 +13,6 @@ namespace vacv {
 constexpr int kBlock = 256;         // threads per workgroup (4 waves)
 constexpr int kMaxC = VACV_MAX_CHANNELS;
 constexpr int kResizeMaxChunksPerLane = 1;        // fp32 resize: 4-element chunks per lane per row
-constexpr int kRowsMaxChunksPerLane = 2;          // resize_rows_kernel: 4-element chunks per lane per tile
 constexpr int64_t kMaxPlaneBytes = 0x7FFFFFF0LL;  // buffer-resource addressing limit of one plane
 
 // A kernel-variant knob (tuning.cpp, VACV_TUNE_*): -1 = the built-in choice.
@@ -101,7 +100,6 @@ struct ResizeLaunch {
     int lds_bytes;               // dynamic LDS per workgroup
     int strips;                  // workgroups per (plane, tile column)
     int tasks_per_strip;         // row tiles per workgroup (software-pipelined)
-    int rows_mode;               // 1: resize_rows_kernel (whole output rows, one tile per workgroup)
     int interleave;              // resize_kernel: 1 = tasks grid-stride in address order, 0 = strips
     int area_x, area_y;          // INTER_AREA integer block (launch_resize_area)
     float area_scale;            // INTER_AREA: 1.f / (area_x * area_y)
@@ -118,10 +116,8 @@ struct ResizeLaunch {
     int* sum_count;              // 2 cc zeroed ints, left zeroed (the batch sum)
 };
 
-// Fills tiles, strips and the cached device plan of L (host).  With rows = 1
-// it plans for resize_rows_kernel (tile = rows_per_block whole output rows)
-// and fails with VACV_ERR_UNSUPPORTED when the rows do not fit its LDS budget.
-int plan_resize(ResizeLaunch& L, hipStream_t s, int rows = 0);
+// Fills tiles, strips and the cached device plan of L (host).
+int plan_resize(ResizeLaunch& L, hipStream_t s);
 void set_strips(ResizeLaunch& L, int64_t resident_workgroups);
 int release_plans();
 

@@ -301,7 +301,7 @@ enum {
     VACV_TUNE_RESIZE_DIRECT = 0,     /* u8 bilinear: 0 staged, 1 gather kernel for one-tap rows, 2 gather always */
     VACV_TUNE_CUBIC_DIRECT = 1,      /* u8 cubic: 0 staged kernel, else the gather kernel */
     VACV_TUNE_RESIZE_INTERLEAVE = 2, /* staged kernel: 0 strip order, else address-ordered tasks */
-    VACV_TUNE_RESIZE_ROWS = 3,       /* 1: the whole-row staged kernel */
+    VACV_TUNE_RESIZE_ROWS = 3,       /* retired (the whole-row staged kernel, never faster, was removed): no effect */
     VACV_TUNE_DIRECT_XCD = 4,        /* gather kernel block order: 0 plain, 1 XCD-contiguous */
     VACV_TUNE_WARP_PX = 5,           /* warp gather kernel: lane blocks per wave (4, 5, 8, 10) */
     VACV_TUNE_NEAREST_KERNEL = 6,    /* INTER_NEAREST: 0 per-pixel kernel, 1 row per workgroup, else row per wave (when they apply) */
@@ -312,7 +312,7 @@ enum {
     VACV_TUNE_RESIZE_TILE_H = 11,    /* staged kernel planner: tile height */
     VACV_TUNE_RESIZE_TILE_W = 12,    /* staged kernel planner: tile width */
     VACV_TUNE_RESIZE_WORK = 13,      /* staged kernel planner: work per thread */
-    VACV_TUNE_RESIZE_ROWS_BYTES = 14,/* whole-row kernel planner: output bytes per workgroup */
+    VACV_TUNE_RESIZE_ROWS_BYTES = 14,/* retired with VACV_TUNE_RESIZE_ROWS: no effect */
     VACV_TUNE_WARP_KERNEL = 15,      /* u8 CONSTANT warp: 0 per-pixel gathers, 2 batched gathers, 4 LDS-staged frames: an LDS-DMA ring of source boxes (k_warp_frames.hip) */
     VACV_TUNE_RESIZE_STRIP = 16,     /* two-tap u8 bilinear: column strips with an LDS row ring, 1: 64 columns x 16-row batches, 2: 128 x 8; 0 staged kernel */
     VACV_TUNE_MATCH_KERNEL = 17,     /* u8 match_template correlation: 0 v_dot4 kernel, else i8 MFMA where it fits */
