@@ -9,7 +9,8 @@
 // row-major order within a frame, frames outer, blocks dealt XCD-contiguously
 // (as the vacv kernels do).  One JSON line per (L, TR, mode): GB/s of bytes
 // read + written.  mode 0 copy, 1 read only (a checksum written per tile),
-// 2 read by LDS-DMA.
+// 2 read by LDS-DMA, 3 write only (16 bytes per lane), 4 write only (4 bytes
+// per lane: the store width of the u8 strip / area kernels).
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
@@ -40,11 +41,25 @@ __global__ __launch_bounds__(256) void seg_copy(const unsigned char* src, unsign
     const int chunks = L / 16;  // per row
     const int64_t fbase = (int64_t)f * H * pitch;
     unsigned acc = 0;
+    if (mode == 4) {  // dword e of the tile (row-major), lanes contiguous
+        const int dw = L / 4;
+        for (int e = threadIdx.x; e < TR * dw; e += 256) {
+            const int r = e / dw, c = e - r * dw;
+            const int row = ty * TR + r;
+            if (row >= H) break;
+            __builtin_nontemporal_store((unsigned)e, reinterpret_cast<unsigned*>(dst + fbase + (int64_t)row * pitch + (int64_t)tx * L + 4 * c));
+        }
+        return;
+    }
     for (int e = threadIdx.x; e < TR * chunks; e += 256) {
         const int r = e / chunks, c = e - r * chunks;
         const int row = ty * TR + r;
         if (row >= H) break;
         const int64_t off = fbase + (int64_t)row * pitch + (int64_t)tx * L + 16 * c;
+        if (mode == 3) {
+            __builtin_nontemporal_store(u32x4{(unsigned)e, 1u, 2u, 3u}, reinterpret_cast<u32x4*>(dst + off));
+            continue;
+        }
         const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(src + off));
         if (mode == 0) __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(dst + off));
         else acc ^= v[0] ^ v[1] ^ v[2] ^ v[3];
@@ -97,7 +112,7 @@ int main() {
     CHECK(hipEventCreate(&e1));
     const int Ls[] = {192, 256, 320, 384, 640, 1280, 3840};
     const int TRs[] = {32, 8};
-    for (int mode = 0; mode < 3; ++mode) {
+    for (int mode = 0; mode < 5; ++mode) {
         for (int TR : TRs) {
             for (int L : Ls) {
                 const int tiles_x = pitch / L, tiles_y = (H + TR - 1) / TR;
@@ -125,8 +140,9 @@ int main() {
                 }
                 std::sort(ms.begin(), ms.end());
                 const double moved = (double)bytes * (mode == 0 ? 2 : 1);
+                const char* names[] = {"copy", "read", "read_dma", "write16", "write4"};
                 std::printf("{\"L\": %d, \"TR\": %d, \"mode\": \"%s\", \"ms\": %.4f, \"GBps\": %.1f}\n", L, TR,
-                            mode == 0 ? "copy" : mode == 1 ? "read" : "read_dma", ms[5], moved / ms[5] / 1e6);
+                            names[mode], ms[5], moved / ms[5] / 1e6);
                 std::fflush(stdout);
             }
         }
