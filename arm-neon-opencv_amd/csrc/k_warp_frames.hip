@@ -100,24 +100,6 @@ constexpr int kRingMaxIt = 6;  // DMA instructions per wave and frame, at most (
 #define VACV_RING_DBG 0
 #endif
 
-// s_waitcnt vmcnt(n) lgkmcnt(0), n a uniform runtime value (clamped to 63:
-// waiting for fewer outstanding operations is always safe)
-template <int N>
-__device__ __forceinline__ void waitcnt_vm() {
-    // gfx9 encoding: vmcnt [3:0] and [15:14], expcnt [6:4] (7: none), lgkmcnt [11:8]
-    __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4));
-}
-template <int... Ns>
-__device__ __forceinline__ void wait_vm_impl(int n, std::integer_sequence<int, Ns...>) {
-    (void)((n == Ns ? (waitcnt_vm<Ns>(), true) : false) || ...);
-}
-__device__ __forceinline__ void wait_vm(int n) {
-    n = n < 0 ? 0 : (n > 63 ? 63 : n);
-    n = __builtin_amdgcn_readfirstlane(n);
-    wait_vm_impl(n, std::make_integer_sequence<int, 64>());
-}
-
-typedef __attribute__((address_space(3))) void lds_void;
 
 // L: launch block; gx, gy: tiles per frame; kf: frames per workgroup; S: LDS
 // bytes per staged row (a multiple of 16); rows_max: staged rows per slot;

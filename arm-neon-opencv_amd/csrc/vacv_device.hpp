@@ -4,6 +4,7 @@
 
 #include <hip/hip_runtime.h>
 #include <cstdint>
+#include <utility>
 
 #include "vacv_internal.hpp"
 #include "vacv_semantics.hpp"
@@ -128,6 +129,32 @@ __device__ __forceinline__ float normalize_f(const ChanNorm& c, float x) {
 }
 
 // ---- u8 bilinear fixed point (k_resize_direct.hip, k_yuv_resize.hip) ----
+
+// ---- LDS-DMA (buffer_load ... lds) bookkeeping (k_warp_frames.hip, k_resize_strip.hip) ----
+
+typedef __attribute__((address_space(3))) void lds_void;
+
+// s_waitcnt vmcnt(n) lgkmcnt(0), n a uniform runtime value (clamped to 63:
+// waiting for fewer outstanding operations is always safe).  The compiler
+// does not track LDS-DMA writes, so the kernels wait for them themselves:
+// gfx9 retires vector memory operations in issue order, so "the last n
+// operations may still be in flight" means everything before them landed.
+template <int N>
+__device__ __forceinline__ void waitcnt_vm() {
+    // gfx9 encoding: vmcnt [3:0] and [15:14], expcnt [6:4] (7: none), lgkmcnt [11:8]
+    __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4));
+}
+template <int... Ns>
+__device__ __forceinline__ void wait_vm_impl(int n, std::integer_sequence<int, Ns...>) {
+    (void)((n == Ns ? (waitcnt_vm<Ns>(), true) : false) || ...);
+}
+__device__ __forceinline__ void wait_vm(int n) {
+    n = n < 0 ? 0 : (n > 63 ? 63 : n);
+    n = __builtin_amdgcn_readfirstlane(n);
+    wait_vm_impl(n, std::make_integer_sequence<int, 64>());
+}
+// s_waitcnt lgkmcnt(0) alone
+__device__ __forceinline__ void wait_lgkm() { __builtin_amdgcn_s_waitcnt(0xF | (3 << 14) | (7 << 4)); }
 
 typedef unsigned short us2 __attribute__((ext_vector_type(2)));
 
