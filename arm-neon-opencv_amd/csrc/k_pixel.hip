@@ -1010,6 +1010,235 @@ __global__ void __launch_bounds__(kBlock) area_u8_colsum_kernel(ResizeLaunch L, 
     }
 }
 
+// u8 INTER_AREA at integer scales, streaming (round 3): a lane owns a UNIT of
+// PX output pixels of one row -- U = lcm(16, AX*CC) source bytes of each of
+// its ay source rows (16-byte loads, the rows' loads in flight together),
+// summed down the rows into packed u16 column sums in registers, then across
+// each pixel's AX columns with compile-time byte positions.  No LDS, no
+// barrier: the memory shape of a copy (a wave reads 64 consecutive units of
+// a row and writes their outputs contiguously).  The LDS column-sum kernel
+// above alternated a load phase and an LDS/output phase per workgroup that
+// never overlapped (diagnosis builds at 2x2: loads alone 0.263 ms, the rest
+// alone 0.250, both 0.519).  Integer sums: bit-identical to it.
+// cache policy of the unit kernel's stores (A/B builds: EXTRA=-DVACV_AREA_STORE_AUX=n)
+#ifndef VACV_AREA_STORE_AUX
+#define VACV_AREA_STORE_AUX 0
+#endif
+template <int AX, int CC>
+struct AreaUnit {
+    static constexpr int gcd(int a, int b) { return b == 0 ? a : gcd(b, a % b); }
+    static constexpr int U = 16 / gcd(16, AX * CC) * AX * CC;  // lcm(16, AX * CC)
+    static constexpr int NCH = U / 16;                         // 16-byte chunks per row
+    static constexpr int PX = U / (AX * CC);                   // output pixels per unit
+    static constexpr int OB = PX * CC;                         // output elements per unit
+};
+
+template <int OUT, int AX, int CC>
+__global__ void __launch_bounds__(kBlock) area_u8_unit_kernel(ResizeLaunch L, int units_per_row, int total, int dst_al) {
+    using A = AreaUnit<AX, CC>;
+    constexpr int NCH = A::NCH, ND = 4 * NCH, PX = A::PX, OB = A::OB;
+    // the wave's 64 units' column sums, chunk-major: 32 bytes (ev, od) per chunk
+    __shared__ __attribute__((aligned(16))) uint32_t xch[kBlock / 64][64 * NCH * 8];
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
+    const int wu0 = (int)blockIdx.x * kBlock + wave * 64;  // the wave's first unit (uniform)
+    if (wu0 >= total) return;  // uniform
+    const int per_plane = L.dst.h * units_per_row;
+    const int ay = L.area_y;
+    const uint32_t rp = (uint32_t)L.src.row_pitch;
+    // ---- loads: instruction c moves chunk q = 64c + lane of the wave's units
+    // (unit q / NCH, its chunk q % NCH), so each is a contiguous run of source
+    // bytes, not 64 strided pieces (a unit-per-lane load: 0.60 ms at 2x2 vs
+    // 0.52 for the LDS column sums); the column sums are summed per chunk
+    // down the rows, then exchanged through the wave's LDS slice
+    uint32_t ev[ND], od[ND];
+    const unsigned char* cbase[NCH];
+    uint32_t coff[NCH];
+    bool cok[NCH];
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+        const int q = 64 * c + lane;
+        const int uq = wu0 + q / NCH, cq = q % NCH;
+        cok[c] = uq < total;
+        const int g = min(uq, total - 1);
+        const int pidx = g / per_plane;
+        const int rem = g - pidx * per_plane;
+        const int y = rem / units_per_row, u = rem - y * units_per_row;
+        const int img = pidx / L.src.planes, plane = pidx - img * L.src.planes;
+        cbase[c] = L.src.base + (int64_t)img * L.src.img_pitch + (int64_t)plane * L.src.plane_pitch;
+        coff[c] = (uint32_t)(y * ay) * rp + (uint32_t)(u * A::U + 16 * cq);
+    }
+#pragma unroll
+    for (int d = 0; d < ND; ++d) ev[d] = od[d] = 0u;
+    auto add = [&](int c, const uint4& t) {
+        const uint32_t w[4] = {t.x, t.y, t.z, t.w};
+#pragma unroll
+        for (int d = 0; d < 4; ++d) {
+            ev[4 * c + d] += w[d] & 0x00FF00FFu;
+            od[4 * c + d] += (w[d] >> 8) & 0x00FF00FFu;
+        }
+    };
+    auto load = [&](int c, uint32_t roff) -> uint4 {
+        const Rsrc srs = make_rsrc(cbase[c], L.src.plane_bytes);
+        const uint32_t lim = (uint32_t)L.src.plane_bytes + srs.delta;
+        const uint32_t oc = coff[c] + roff + srs.delta;
+        if (!cok[c]) return make_uint4(0u, 0u, 0u, 0u);
+        if (oc + 16u <= lim) return load16(srs, oc);
+        uint32_t d[4] = {0u, 0u, 0u, 0u};  // the plane's last bytes: a straddling 16-byte load reads as zeros
+#pragma unroll 1
+        for (uint32_t e = 0; e < 16u; ++e)
+            if (oc + e < lim) d[e >> 2] |= (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(srs.r, (int)(oc + e), 0, 0) << (8 * (e & 3));
+        return make_uint4(d[0], d[1], d[2], d[3]);
+    };
+    int r = 0;
+    for (; r + 2 <= ay; r += 2) {  // two rows of every chunk in flight
+        uint4 t0[NCH], t1[NCH];
+#pragma unroll
+        for (int c = 0; c < NCH; ++c) {
+            t0[c] = load(c, (uint32_t)r * rp);
+            t1[c] = load(c, (uint32_t)(r + 1) * rp);
+        }
+#pragma unroll
+        for (int c = 0; c < NCH; ++c) {
+            add(c, t0[c]);
+            add(c, t1[c]);
+        }
+    }
+    if (r < ay) {
+#pragma unroll
+        for (int c = 0; c < NCH; ++c) add(c, load(c, (uint32_t)r * rp));
+    }
+    // ---- exchange: chunk q's sums -> slot q; lane l takes its unit's chunks
+    uint32_t* xw = xch[wave];
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+        const int q = 64 * c + lane;
+        *reinterpret_cast<uint4*>(xw + 8 * q) = make_uint4(ev[4 * c], ev[4 * c + 1], ev[4 * c + 2], ev[4 * c + 3]);
+        *reinterpret_cast<uint4*>(xw + 8 * q + 4) = make_uint4(od[4 * c], od[4 * c + 1], od[4 * c + 2], od[4 * c + 3]);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+        const int q = NCH * lane + c;
+        const uint4 e4 = *reinterpret_cast<const uint4*>(xw + 8 * q);
+        const uint4 o4 = *reinterpret_cast<const uint4*>(xw + 8 * q + 4);
+        ev[4 * c] = e4.x; ev[4 * c + 1] = e4.y; ev[4 * c + 2] = e4.z; ev[4 * c + 3] = e4.w;
+        od[4 * c] = o4.x; od[4 * c + 1] = o4.y; od[4 * c + 2] = o4.z; od[4 * c + 3] = o4.w;
+    }
+    const int gid = wu0 + lane;
+    if (gid >= total) return;
+    const int pidx = gid / per_plane;
+    const int rem = gid - pidx * per_plane;
+    const int y = rem / units_per_row, u = rem - y * units_per_row;
+    const int img = pidx / L.src.planes, plane = pidx - img * L.src.planes;
+    // output element e: pixel p = e / CC, channel k; its source bytes
+    // j = (p * AX + a) * CC + k, a < AX -- all positions compile-time
+    auto colsum = [&](int j) -> int {
+        const uint32_t w = (j & 1) ? od[j >> 2] : ev[j >> 2];
+        return (int)((w >> (16 * ((j >> 1) & 1))) & 0xFFFFu);
+    };
+    const int vx = min(PX, L.dst.w - u * PX);  // valid pixels (the row's last unit may be partial)
+    unsigned char* dp = const_cast<unsigned char*>(L.dst.base) + (int64_t)img * L.dst.img_pitch +
+                        (int64_t)plane * L.dst.plane_pitch;
+    const Rsrc drs = make_rsrc(dp, L.dst.plane_bytes);
+    constexpr int ES = OUT == kOutSame ? 1 : 4;
+    const uint32_t ro = (uint32_t)y * (uint32_t)L.dst.row_pitch + (uint32_t)(u * OB * ES) + drs.delta;
+    uint32_t outw[OUT == kOutSame ? OB / 4 : OB];
+#pragma unroll
+    for (int e = 0; e < OB; ++e) {
+        const int p = e / CC, k = e - p * CC;
+        int sum = 0;
+#pragma unroll
+        for (int a = 0; a < AX; ++a) sum += colsum((p * AX + a) * CC + k);
+        const int v = L.area_half_up ? (sum + 2) >> 2 : (int)rintf(__fmul_rn((float)sum, L.area_scale));
+        if constexpr (OUT == kOutSame) {
+            if (e % 4 == 0) outw[e / 4] = 0u;
+            outw[e / 4] |= (uint32_t)(v & 0xFF) << (8 * (e % 4));
+        } else if constexpr (OUT == kOutF32) {
+            outw[e] = __builtin_bit_cast(uint32_t, (float)v);
+        } else {
+            const ChanNorm cn = chan_norm(L.norm, img, CC == 1 ? plane % L.norm.c_total : k);
+            outw[e] = __builtin_bit_cast(uint32_t, normalize_u8v(cn, v));
+        }
+    }
+    if (vx == PX && dst_al) {  // dword stores (OB * ES is a multiple of 4)
+        constexpr int NW = OUT == kOutSame ? OB / 4 : OB;
+        if constexpr (NW % 4 == 0) {
+#pragma unroll
+            for (int i = 0; i < NW; i += 4)
+                __builtin_amdgcn_raw_buffer_store_b128(u32x4{outw[i], outw[i + 1], outw[i + 2], outw[i + 3]}, drs.r,
+                                                       (int)(ro + 4u * (uint32_t)i), 0, VACV_AREA_STORE_AUX);
+        } else if constexpr (NW % 2 == 0) {
+            typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+#pragma unroll
+            for (int i = 0; i < NW; i += 2)
+                __builtin_amdgcn_raw_buffer_store_b64(u32x2{outw[i], outw[i + 1]}, drs.r, (int)(ro + 4u * (uint32_t)i), 0,
+                                                      VACV_AREA_STORE_AUX);
+        } else {
+#pragma unroll
+            for (int i = 0; i < NW; ++i)
+                __builtin_amdgcn_raw_buffer_store_b32(outw[i], drs.r, (int)(ro + 4u * (uint32_t)i), 0, VACV_AREA_STORE_AUX);
+        }
+    } else {  // the row's partial last unit or an unaligned destination: element by element
+#pragma unroll
+        for (int e = 0; e < OB; ++e) {
+            if (e >= vx * CC) break;
+            if constexpr (OUT == kOutSame)
+                __builtin_amdgcn_raw_buffer_store_b8((unsigned char)(outw[e / 4] >> (8 * (e % 4))), drs.r, (int)(ro + (uint32_t)e), 0,
+                                                     VACV_AREA_STORE_AUX);
+            else
+                __builtin_amdgcn_raw_buffer_store_b32(outw[e], drs.r, (int)(ro + 4u * (uint32_t)e), 0, VACV_AREA_STORE_AUX);
+        }
+    }
+}
+
+template <int AX, int CC>
+hipError_t launch_area_u8_unit_c(const ResizeLaunch& L, hipStream_t s) {
+    using A = AreaUnit<AX, CC>;
+    const int upr = (L.dst.w + A::PX - 1) / A::PX;
+    const int64_t total = (int64_t)upr * L.dst.h * L.n * L.src.planes;
+    if (total >= 0x7FFFFF00LL) return hipErrorInvalidValue;
+    const int es = L.out == kOutSame ? 1 : 4;
+    const uintptr_t dbits = reinterpret_cast<uintptr_t>(L.dst.base) | (uintptr_t)L.dst.img_pitch |
+                            (uintptr_t)L.dst.plane_pitch | (uintptr_t)L.dst.row_pitch;
+    // the vector stores need their own width's alignment: a unit's bytes
+    // start at u * OB * es within the row
+    const int ob = A::OB * es;
+    const int wst = ob % 16 == 0 ? 16 : ob % 8 == 0 ? 8 : 4;
+    const int dst_al = (dbits % (uintptr_t)wst) == 0;
+    const dim3 grid((unsigned)((total + kBlock - 1) / kBlock));
+    if (L.out == kOutSame) hipLaunchKernelGGL((area_u8_unit_kernel<kOutSame, AX, CC>), grid, dim3(kBlock), 0, s, L, upr, (int)total, dst_al);
+    else if (L.out == kOutF32) hipLaunchKernelGGL((area_u8_unit_kernel<kOutF32, AX, CC>), grid, dim3(kBlock), 0, s, L, upr, (int)total, dst_al);
+    else hipLaunchKernelGGL((area_u8_unit_kernel<kOutNorm, AX, CC>), grid, dim3(kBlock), 0, s, L, upr, (int)total, dst_al);
+    return hipGetLastError();
+}
+
+// the unit kernel's (AX, CC) instances: U = lcm(16, AX*CC) <= 48 bytes per
+// row, so a unit's column sums fit in 24 registers; plane bytes < 2^31
+bool area_unit_applies(const ResizeLaunch& L) {
+    const int ax = L.area_x, cc = L.src.cc;
+    const bool inst = (ax == 2 && cc >= 1 && cc <= 4) || (ax == 3 && cc == 1) || (ax == 4 && cc >= 1 && cc <= 4);
+    return inst && L.area_y >= 1 && L.area_y <= 257 && L.src.plane_bytes < (1LL << 31) - 64 &&
+           L.dst.plane_bytes < (1LL << 31) - 64;
+}
+
+hipError_t launch_area_u8_unit(const ResizeLaunch& L, hipStream_t s) {
+    switch (L.area_x * 8 + L.src.cc) {
+        case 17: return launch_area_u8_unit_c<2, 1>(L, s);
+        case 18: return launch_area_u8_unit_c<2, 2>(L, s);
+        case 19: return launch_area_u8_unit_c<2, 3>(L, s);
+        case 20: return launch_area_u8_unit_c<2, 4>(L, s);
+        case 25: return launch_area_u8_unit_c<3, 1>(L, s);
+        case 33: return launch_area_u8_unit_c<4, 1>(L, s);
+        case 34: return launch_area_u8_unit_c<4, 2>(L, s);
+        case 35: return launch_area_u8_unit_c<4, 3>(L, s);
+        case 36: return launch_area_u8_unit_c<4, 4>(L, s);
+        default: return hipErrorInvalidValue;
+    }
+}
+
 template <int VB, int CC>
 hipError_t launch_area_u8_colsum_c(const ResizeLaunch& L, hipStream_t s, int tw, int rows, dim3 grid) {
     if (L.out == kOutSame) hipLaunchKernelGGL((area_u8_colsum_kernel<kOutSame, VB, CC>), grid, dim3(kBlock), 0, s, L, tw, rows);
@@ -1077,7 +1306,9 @@ hipError_t launch_resize_area(const ResizeLaunch& L, hipStream_t s) {
     if (L.src.esize == 1) {
         const uintptr_t bits = reinterpret_cast<uintptr_t>(L.src.base) | (uintptr_t)L.src.img_pitch |
                                (uintptr_t)L.src.plane_pitch | (uintptr_t)L.src.row_pitch;
-        const int knob = tune(VACV_TUNE_AREA_KERNEL);  // A/B: 1 per-pixel, 2 dword column sums
+        // A/B: 1 per-pixel, 2 dword column sums, 3 16-byte column sums (LDS)
+        const int knob = tune(VACV_TUNE_AREA_KERNEL);
+        if ((bits & 15) == 0 && knob <= 0 && area_unit_applies(L)) return launch_area_u8_unit(L, s);
         const int vb = (bits & 15) == 0 && L.area_x * L.src.cc <= 256 ? 16 : (bits & 3) == 0 ? 4 : 0;
         if (vb && L.area_x * L.src.cc <= 1024 && L.area_y <= 257 && knob != 1)  // u16 column sums: 255 * ay < 2^16
             return launch_area_u8_colsum(L, s, knob == 2 ? 4 : vb);

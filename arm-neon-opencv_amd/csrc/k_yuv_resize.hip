@@ -63,12 +63,16 @@ __device__ __forceinline__ uint32_t chroma_sel(int w, int tx) {
 }
 
 // yo / co: byte offsets (from the 16-byte aligned base) of the Y row and of
-// its chroma row.
+// its chroma row.  Default cache policy, not non-temporal: a 64-pixel gather
+// shares its 128-byte lines with the neighbouring wave's, and the chroma row
+// serves two Y rows; in L2 they are fetched once (256 x NV21 1080p ->
+// 640x360: u8 0.1447 -> 0.1361 ms, CHW fp32 0.1986 -> 0.1950 ms).
+constexpr int kYuvAux = 0;
 __device__ __forceinline__ void gather_row(const Rsrc& rs, uint32_t yo, uint32_t co, int w, int tx, RowTaps& t) {
-    t.y = __builtin_amdgcn_raw_buffer_load_b32(rs.r, (int)(yo + (uint32_t)tx), 0, VACV_LOAD_AUX);
+    t.y = __builtin_amdgcn_raw_buffer_load_b32(rs.r, (int)(yo + (uint32_t)tx), 0, kYuvAux);
     const int ca = tx & ~1;
     const int c0 = min(ca, w - 4);
-    t.c = __builtin_amdgcn_raw_buffer_load_b32(rs.r, (int)(co + (uint32_t)c0), 0, VACV_LOAD_AUX);
+    t.c = __builtin_amdgcn_raw_buffer_load_b32(rs.r, (int)(co + (uint32_t)c0), 0, kYuvAux);
 }
 
 struct RowOffs {

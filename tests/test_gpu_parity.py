@@ -261,7 +261,8 @@ def test_nearest_area_kernel_variants_agree(ops, dev, oracle):
     source is 16-byte aligned, its row fits 16 KiB and the sample stride is
     short) vs row-staged per workgroup (VACV_TUNE_NEAREST_KERNEL = 1) vs the
     per-pixel kernel (0); area 16-byte column
-    sums (default) vs dword column sums (2) vs per-pixel (1); plus an fp32 row
+    units (default) vs 16-byte LDS column sums (3) vs dword column sums (2) vs
+    per-pixel (1); plus an fp32 row
     past 64 KiB (5600 px x 3 ch: the per-pixel fallback) and a strong
     horizontal downscale (wide stride: the per-pixel kernel) vs the oracle."""
     import torch
@@ -283,7 +284,7 @@ def test_nearest_area_kernel_variants_agree(ops, dev, oracle):
     assert_same(host(a)[1], oracle.resize_nearest(imgs[1], 3000, 1500), "nearest upscale")
     for wo, ho in [(640, 360), (960, 540), (480, 270)]:
         a = ops.resize(src, wo, ho, interpolation=INTER_AREA)
-        for knob in (1, 2):
+        for knob in (1, 2, 3):
             with ops.tuning(AREA_KERNEL=knob):
                 b = ops.resize(src, wo, ho, interpolation=INTER_AREA)
             assert torch.equal(a, b), f"area variant {knob} differs -> {wo}x{ho}"
@@ -350,6 +351,52 @@ def test_resize_area(ops, dev, oracle):
         big = np.tile(blk, (64, 96, 1))  # the column-sum kernel (16-byte aligned rows)
         got = host(ops.resize(to_dev(big[None], dev), 384, 64, interpolation=INTER_AREA))[0]
         assert_same(got.reshape(64, 384, c), oracle.resize_area(big, 384, 64).reshape(64, 384, c), f"area tie c{c}")
+
+
+def test_area_unit_kernel(ops, dev, oracle):
+    """The streaming u8 INTER_AREA kernel (area_u8_unit_kernel, k_pixel.hip:
+    16-byte aligned rows, AX in {2, 4} with 1-4 channels, AX = 3 with one):
+    bit-exact against the oracle and against the LDS column-sum kernel
+    (VACV_TUNE_AREA_KERNEL = 3) for every instance, with row pitches padded
+    so that a row's last unit is partial (and, on the last row, its chunks
+    reach past the plane's end), u8 / fp32 / normalised output, NCHW planes
+    and a destination that forbids the vector stores."""
+    import torch
+    from vacv_amd import INTER_AREA, NCHW
+    cases = [(2, 2, 1), (2, 2, 2), (2, 2, 3), (2, 2, 4), (3, 3, 1), (3, 1, 1), (4, 4, 1), (4, 2, 2), (4, 4, 3),
+             (4, 3, 4), (2, 3, 3), (2, 5, 1)]
+    for i, (ax, ay, c) in enumerate(cases):
+        for wo, ho in [(37, 11), (64, 9)]:
+            w, h = wo * ax, ho * ay
+            pitch = -(-(w * c + 1) // 16) * 16  # 16-byte rows, padded
+            imgs = [synthetic_image(790 + 10 * i + k, h, w, c).reshape(h, w, c) for k in range(2)]
+            flat = np.zeros(2 * h * pitch, np.uint8)
+            for k in range(2):
+                for y in range(h):
+                    o = (k * h + y) * pitch
+                    flat[o:o + w * c] = imgs[k][y].reshape(-1)
+            view = to_dev(flat, dev).as_strided((2, h, w, c), (h * pitch, pitch, c, 1))
+            got = ops.resize(view, wo, ho, interpolation=INTER_AREA)
+            gh = host(got)
+            for k in range(2):
+                want = oracle.resize_area(imgs[k] if c > 1 else imgs[k][..., 0], wo, ho)
+                assert_same(gh[k].reshape(want.shape), want, f"area unit {ax}x{ay} c{c} -> {wo}x{ho}")
+            with ops.tuning(AREA_KERNEL=3):
+                ref = ops.resize(view, wo, ho, interpolation=INTER_AREA)
+                refn = ops.resize_normalize(view, wo, ho, MEAN[:c], STD[:c], interpolation=INTER_AREA) if c in (1, 3) else None
+            assert torch.equal(got, ref), f"unit vs colsum {ax}x{ay} c{c}"
+            if refn is not None:
+                gotn = ops.resize_normalize(view, wo, ho, MEAN[:c], STD[:c], interpolation=INTER_AREA)
+                assert torch.equal(gotn, refn), f"unit vs colsum normalize {ax}x{ay} c{c}"
+            # a destination at an odd offset: element-wise stores
+            out = torch.zeros((2, ho, wo + 1, c), dtype=torch.uint8, device=dev)[:, :, 1:]
+            ops.resize(view, wo, ho, interpolation=INTER_AREA, out=out)
+            assert torch.equal(out, ref), f"unit unaligned dst {ax}x{ay} c{c}"
+    img = synthetic_image(799, 64, 96, 3)
+    chw = to_dev(np.ascontiguousarray(img.transpose(2, 0, 1))[None], dev)
+    got = host(ops.resize(chw, 48, 32, interpolation=INTER_AREA, layout=NCHW))[0]
+    for k in range(3):
+        assert_same(got[k], oracle.resize_area(np.ascontiguousarray(img[..., k]), 48, 32), "area unit chw")
 
 
 def test_resize_area_any_scale(ops, dev, oracle):
