@@ -19,6 +19,10 @@
 // once per wave.  Results are re-assembled in LDS and leave as 16-byte
 // non-temporal stores.
 #pragma clang fp contract(off)
+// A/B builds: EXTRA=-DVACV_CUBIC_NT_STORES=0 (write-back output stores)
+#ifndef VACV_CUBIC_NT_STORES
+#define VACV_CUBIC_NT_STORES 1
+#endif
 
 #include <cstdlib>
 
@@ -226,8 +230,12 @@ cubic_direct_kernel(ResizeLaunch L, int blocks_per_plane) {
                 off = r * rowp + (b - r * out_row);
             }
             if (c * 16 + 16 <= vbytes) {
+#if VACV_CUBIC_NT_STORES
                 __builtin_nontemporal_store(*reinterpret_cast<const u32x4*>(xs + 16 * c),
                                             reinterpret_cast<u32x4*>(dp + off));
+#else
+                *reinterpret_cast<u32x4*>(dp + off) = *reinterpret_cast<const u32x4*>(xs + 16 * c);
+#endif
             } else {
                 for (uint32_t e = c * 16; e < vbytes; ++e) dp[off + (e - c * 16)] = xs[e];
             }
