@@ -316,6 +316,16 @@ int resize_impl(const vacv_image* src_d, const vacv_image* dst_d, int interpolat
             return hip_status(launch_resize_area(L, s));
         }
         return launch_resize_area_general(L, ifx, ify, s);
+    } else if (interpolation == VACV_INTER_LANCZOS4) {
+        // resize.cpp:46-48 hands it to cv::resize; OpenCV 2.4's 8x8 Lanczos
+        // (k_lanczos.hip), u8 in fixed point, fp32 in float
+        if (src.dtype != VACV_INT8 && src.dtype != VACV_FP32) return VACV_ERR_UNSUPPORTED;
+        L.out = out_kind;
+        if (src.dtype == VACV_FP32 && L.out == kOutF32) L.out = kOutSame;
+        const int want = L.out == kOutSame ? src.dtype : VACV_FP32;
+        if (dst.dtype != want) return VACV_ERR_INVALID_ARG;
+        const double ifx = fx > 0 ? fx : (double)dst.w / src.w, ify = fy > 0 ? fy : (double)dst.h / src.h;
+        return launch_resize_lanczos(L, ifx, ify, s);
     } else {
         return VACV_ERR_UNSUPPORTED;  // resize.cpp:46-49 recurses forever for other modes
     }
@@ -768,7 +778,8 @@ int vacv_resize(const vacv_image* src_d, const vacv_image* dst_d, int interpolat
 int vacv_resize_scaled(const vacv_image* src, const vacv_image* dst, int interpolation, int mode, double fx,
                        double fy, void* stream) {
     if (!(fx > 0) || !(fy > 0)) return VACV_ERR_INVALID_ARG;
-    if (interpolation != VACV_INTER_NEAREST && interpolation != VACV_INTER_AREA) return VACV_ERR_UNSUPPORTED;
+    if (interpolation != VACV_INTER_NEAREST && interpolation != VACV_INTER_AREA && interpolation != VACV_INTER_LANCZOS4)
+        return VACV_ERR_UNSUPPORTED;
     return resize_impl(src, dst, interpolation, mode, kOutSame, nullptr, (hipStream_t)stream, fx, fy);
 }
 
@@ -1059,7 +1070,8 @@ int vacv_release_workspace(void) {
     g_ws.clear();
     const int pst = release_plans();
     const int ast = release_area_tables();
-    return st ? st : (pst ? pst : ast);
+    const int lst = release_lanczos_tables();
+    return st ? st : (pst ? pst : (ast ? ast : lst));
 }
 
 }  // extern "C"

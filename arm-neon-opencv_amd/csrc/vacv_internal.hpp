@@ -158,6 +158,10 @@ hipError_t launch_resize_area(const ResizeLaunch& L, hipStream_t s);
 // cv::resize's inv_scale.  Returns a vacv_status.
 int launch_resize_area_general(const ResizeLaunch& L, double inv_x, double inv_y, hipStream_t s);
 int release_area_tables();
+// INTER_LANCZOS4 (k_lanczos.hip): OpenCV 2.4 cv::resize restated; inv_x /
+// inv_y = dsize / ssize (or fx / fy)
+int launch_resize_lanczos(const ResizeLaunch& L, double inv_x, double inv_y, hipStream_t s);
+int release_lanczos_tables();
 // u8 -> fp32 cubic as per-pixel gathers (k_cubic_direct.hip); needs no plan
 bool cubic_direct_applies(const ResizeLaunch& L);
 hipError_t launch_cubic_direct(const ResizeLaunch& L, hipStream_t s);

@@ -74,9 +74,14 @@ DType resize_out_dtype(const char* fn, const Tensor& src, int interpolation) {
         if (src.dtype != INT8 && src.dtype != FP32) fail(fn, "INTER_AREA takes INT8 or FP32");
         return src.dtype;
     }
+    if (interpolation == INTER_LANCZOS4) {
+        // resize.cpp:46-49 hands it to cv::resize; OpenCV 2.4's 8x8 Lanczos here
+        if (src.dtype != INT8 && src.dtype != FP32) fail(fn, "INTER_LANCZOS4 takes INT8 or FP32");
+        return src.dtype;
+    }
     // every other mode goes to OpenCV in the reference, which this build
     // does not ship (the reference without OpenCV recurses forever)
-    fail(fn, "only INTER_NEAREST, INTER_LINEAR, INTER_CUBIC and INTER_AREA are supported");
+    fail(fn, "only INTER_NEAREST, INTER_LINEAR, INTER_CUBIC, INTER_AREA and INTER_LANCZOS4 are supported");
 }
 
 std::vector<float> affine_of(const char* fn, const Tensor& M) { return host_floats(fn, M, 6); }
@@ -144,7 +149,7 @@ void resize(const Tensor& src, Tensor& dst, VSize dsize, double fx, double fy, i
     // half to even) and inv_scale = fx, fy.  The naive LINEAR / CUBIC paths
     // use dsize alone (resize.cpp:77-135).
     const bool scaled = dsize.w == 0 && dsize.h == 0 && fx > 0 && fy > 0 &&
-                        (interpolation == INTER_NEAREST || interpolation == INTER_AREA);
+                        (interpolation == INTER_NEAREST || interpolation == INTER_AREA || interpolation == INTER_LANCZOS4);
     if (scaled) {
         dsize.w = static_cast<int>(std::nearbyint(src.w * fx));
         dsize.h = static_cast<int>(std::nearbyint(src.h * fy));
@@ -299,7 +304,7 @@ void resize(const std::vector<Tensor>& src, std::vector<Tensor>& dst, VSize dsiz
     const DType out = resize_out_dtype(fn, src[0], interpolation);
     // dsize = 0 with fx, fy: cv::resize's form, per frame (see the single-frame overload)
     const bool scaled = dsize.w == 0 && dsize.h == 0 && fx > 0 && fy > 0 &&
-                        (interpolation == INTER_NEAREST || interpolation == INTER_AREA);
+                        (interpolation == INTER_NEAREST || interpolation == INTER_AREA || interpolation == INTER_LANCZOS4);
     std::vector<VSize> sizes(src.size(), dsize);
     if (scaled)
         for (size_t i = 0; i < src.size(); ++i)

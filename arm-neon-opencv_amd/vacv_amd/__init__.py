@@ -9,7 +9,7 @@ from ._lib import (BORDER_CONSTANT, BORDER_REFLECT, BORDER_REFLECT_101, BORDER_R
                    BORDER_WRAP, COLOR_GRAY2BGR, COLOR_YUV2BGR_NV12, COLOR_YUV2BGR_NV21, COLOR_YUV2BGR_YV12,
                    COLOR_YUV2BGRA_NV12, COLOR_YUV2BGRA_NV21, COLOR_YUV2RGB_NV12, COLOR_YUV2RGB_NV21,
                    COLOR_YUV2RGBA_NV12, COLOR_YUV2RGBA_NV21,
-                   FP16, FP32, FP64, INT8, INTER_AREA, INTER_CUBIC, INTER_LINEAR, INTER_NEAREST, LINEAR_NEON, LINEAR_OPENCV,
+                   FP16, FP32, FP64, INT8, INTER_AREA, INTER_CUBIC, INTER_LANCZOS4, INTER_LINEAR, INTER_NEAREST, LINEAR_NEON, LINEAR_OPENCV,
                    LINEAR_REFERENCE, NCHW, NHWC, WARP_INVERSE_MAP, VacvError, build)
 
 __all__ = ["ops", "dist", "build", "VacvError"]

@@ -23,7 +23,7 @@ HEADER = REPO_ROOT / "include" / "vacv_hip.h"
 OK, ERR_INVALID_ARG, ERR_UNSUPPORTED, ERR_HIP, ERR_NO_MEMORY = 0, -1, -2, -3, -4
 FP32, FP16, INT8, FP64 = 0, 1, 2, 3
 NCHW, NHWC = 0, 1
-INTER_NEAREST, INTER_LINEAR, INTER_CUBIC, INTER_AREA = 0, 1, 2, 3
+INTER_NEAREST, INTER_LINEAR, INTER_CUBIC, INTER_AREA, INTER_LANCZOS4 = 0, 1, 2, 3, 4
 BORDER_CONSTANT, BORDER_REPLICATE, BORDER_REFLECT, BORDER_WRAP, BORDER_REFLECT_101, BORDER_TRANSPARENT = 0, 1, 2, 3, 4, 5
 WARP_INVERSE_MAP = 16  # warp flag: m is the dst -> src map
 COLOR_YUV2RGB_NV12, COLOR_YUV2BGR_NV12, COLOR_YUV2RGB_NV21, COLOR_YUV2BGR_NV21 = 90, 91, 92, 93

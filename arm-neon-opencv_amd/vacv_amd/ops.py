@@ -148,7 +148,7 @@ def change_dtype(src: torch.Tensor, dtype: torch.dtype, layout: int = NHWC, stre
 def resize(src: torch.Tensor, w: int, h: int, interpolation: int = INTER_LINEAR, mode: int = LINEAR_REFERENCE,
            layout: int = NHWC, out=None, stream=None, fx: float = 0.0, fy: float = 0.0) -> torch.Tensor:
     """va_cv::resize (cv.h:85-87).  INTER_CUBIC on u8 input returns fp32.
-    w = h = 0 with fx, fy > 0 (INTER_NEAREST / INTER_AREA): cv::resize's
+    w = h = 0 with fx, fy > 0 (INTER_NEAREST / INTER_AREA / INTER_LANCZOS4): cv::resize's
     dsize = (round(w_in * fx), round(h_in * fy)) and inv_scale = (fx, fy)."""
     s4 = _as4d(src, layout)
     dt = torch.float32 if (interpolation == INTER_CUBIC) else src.dtype

@@ -48,7 +48,7 @@ enum { VACV_FP32 = 0, VACV_FP16 = 1, VACV_INT8 = 2 /* unsigned bytes */, VACV_FP
 /* vision::DLayout (tensor.h:21-24) */
 enum { VACV_NCHW = 0, VACV_NHWC = 1 };
 /* va_cv::VInterMode (cv.h:27-35) */
-enum { VACV_INTER_NEAREST = 0, VACV_INTER_LINEAR = 1, VACV_INTER_CUBIC = 2, VACV_INTER_AREA = 3 };
+enum { VACV_INTER_NEAREST = 0, VACV_INTER_LINEAR = 1, VACV_INTER_CUBIC = 2, VACV_INTER_AREA = 3, VACV_INTER_LANCZOS4 = 4 };
 /* warp flag (cv.h:35): m is already the inverse (dst -> src) map */
 enum { VACV_WARP_INVERSE_MAP = 16 };
 /* va_cv::VBorderMode (cv.h:38-48) */

@@ -78,6 +78,7 @@ class Oracle:
             ("oracle_warp_affine_u8", [_P, _I, _I, _I, _P, _I, _I, _P], None),
             ("oracle_warp_affine_f32", [_P, _I, _I, _I, _P, _I, _I, _P], None),
             ("oracle_resize_area_any", [_P, _I, _I, _I, _I, _P, _I, _I, ctypes.c_double, ctypes.c_double], None),
+            ("oracle_resize_lanczos4", [_P, _I, _I, _I, _I, _P, _I, _I, ctypes.c_double, ctypes.c_double], None),
             ("oracle_match_template", [_P, _I, _I, _P, _I, _I, _I, _I, _I, _P], None),
             ("oracle_min_max_idx", [_P, _I, _I, _I, _P, _P, _P], None),
             ("oracle_warp_affine_border", [_P, _I, _I, _I, _I, _P, _I, _I, _P, _I], None),
@@ -167,6 +168,16 @@ class Oracle:
         w, h, c = _shape(img)
         out = _out(h_out, w_out, c, img.dtype)
         self.lib.oracle_resize_area_any(_ptr(img), w, h, c, img.dtype.itemsize, _ptr(out), w_out, h_out,
+                                        float(inv_x), float(inv_y))
+        return out
+
+    def resize_lanczos4(self, img, w_out, h_out, inv_x=0.0, inv_y=0.0):
+        """INTER_LANCZOS4 (OpenCV 2.4 cv::resize restated; parity unpinned,
+        vacv_oracle.c).  inv_x / inv_y: fx / fy when dsize derives from them."""
+        img = np.ascontiguousarray(img)
+        w, h, c = _shape(img)
+        out = _out(h_out, w_out, c, img.dtype)
+        self.lib.oracle_resize_lanczos4(_ptr(img), w, h, c, img.dtype.itemsize, _ptr(out), w_out, h_out,
                                         float(inv_x), float(inv_y))
         return out
 

@@ -1119,3 +1119,136 @@ void oracle_min_max_idx(const void* src, int w, int h, int esize, const uint8_t*
     idx[3] = imx < 0 ? -1 : (int)(imx % w);
 }
 
+
+/* ---- INTER_LANCZOS4 (OpenCV 2.4.13 imgwarp.cpp restated; parity unpinned) ----
+ * The reference hands the mode to cv::resize (resize.cpp:46-48).  resize():
+ * per output column fx = (float)((dx + 0.5) * scale_x - 0.5), sx = cvFloor(fx),
+ * fx -= sx, interpolateLanczos4(fx) -> 8 coefficients (u8: saturate_cast<short>
+ * (c * INTER_RESIZE_COEF_SCALE)); rows the same.  resizeGeneric_: every source
+ * row is resized horizontally into a WT buffer (HResizeLanczos4: taps sx - 3
+ * .. sx + 4, an out-of-range tap walks by cn to the nearest pixel of its
+ * channel; columns outside [xmin, xmax) sum from 0, the others unrolled),
+ * then output row dy combines rows clip(sy - 3 + k, 0, h) (VResizeLanczos4:
+ * (b0 r0 + .. + b3 r3) + (b4 r4 + .. + b7 r7), u8 by FixedPtCast<int, uchar, 22>). */
+static void lz_coeffs(float x, float* coeffs) {
+    static const double s45 = 0.70710678118654752440084436210485;
+    static const double cs[8][2] = {{1, 0}, {-s45, -s45}, {0, 1}, {s45, -s45}, {-1, 0}, {s45, s45}, {0, -1}, {-s45, s45}};
+    const double pi = 3.1415926535897932384626433832795;
+    int i;
+    float sum = 0.f;
+    double y0, s0, c0;
+    if (x < FLT_EPSILON) {
+        for (i = 0; i < 8; i++) coeffs[i] = 0.f;
+        coeffs[3] = 1.f;
+        return;
+    }
+    y0 = -(x + 3) * pi * 0.25;
+    s0 = sin(y0);
+    c0 = cos(y0);
+    for (i = 0; i < 8; i++) {
+        double y = -(x + 3 - i) * pi * 0.25;
+        coeffs[i] = (float)((cs[i][0] * s0 + cs[i][1] * c0) / (y * y));
+        sum += coeffs[i];
+    }
+    sum = 1.f / sum;
+    for (i = 0; i < 8; i++) coeffs[i] *= sum;
+}
+
+static short lz_sat_short(float v) {
+    long r = lrintf(v);
+    return (short)(r < -32768 ? -32768 : r > 32767 ? 32767 : r);
+}
+
+void oracle_resize_lanczos4(const void* src, int w_in, int h_in, int cc, int esize, void* dst, int w_out, int h_out,
+                            double inv_x, double inv_y) {
+    const double scale_x = 1. / (inv_x > 0 ? inv_x : (double)w_out / w_in);
+    const double scale_y = 1. / (inv_y > 0 ? inv_y : (double)h_out / h_in);
+    const int sw = w_in * cc, dw = w_out * cc;
+    int* xofs = (int*)malloc(sizeof(int) * dw);
+    float* xa = (float*)malloc(sizeof(float) * 8 * w_out);
+    short* xai = (short*)malloc(sizeof(short) * 8 * w_out);
+    int* yofs = (int*)malloc(sizeof(int) * h_out);
+    float* ya = (float*)malloc(sizeof(float) * 8 * h_out);
+    short* yai = (short*)malloc(sizeof(short) * 8 * h_out);
+    /* the horizontal pass of every source row: int (u8) or float (fp32) */
+    int* bi = esize == 1 ? (int*)malloc(sizeof(int) * (size_t)dw * h_in) : NULL;
+    float* bf = esize == 1 ? NULL : (float*)malloc(sizeof(float) * (size_t)dw * h_in);
+    int xmin = 0, xmax = w_out, dx, dy, k, r, j;
+    for (dx = 0; dx < w_out; dx++) {
+        float fx = (float)((dx + 0.5) * scale_x - 0.5);
+        int sx = (int)floorf(fx);
+        fx -= sx;
+        if (sx < 3) xmin = dx + 1;
+        if (sx + 4 >= w_in && dx < xmax) xmax = dx;
+        for (k = 0; k < cc; k++) xofs[dx * cc + k] = sx * cc + k;
+        lz_coeffs(fx, xa + 8 * dx);
+        for (k = 0; k < 8; k++) xai[8 * dx + k] = lz_sat_short(xa[8 * dx + k] * 2048.f);
+    }
+    for (dy = 0; dy < h_out; dy++) {
+        float fy = (float)((dy + 0.5) * scale_y - 0.5);
+        int sy = (int)floorf(fy);
+        fy -= sy;
+        yofs[dy] = sy;
+        lz_coeffs(fy, ya + 8 * dy);
+        for (k = 0; k < 8; k++) yai[8 * dy + k] = lz_sat_short(ya[8 * dy + k] * 2048.f);
+    }
+    for (r = 0; r < h_in; r++) {
+        for (dx = 0; dx < dw; dx++) {
+            const int px = dx / cc, fast = px >= xmin && px < xmax;
+            const int sx = xofs[dx] - cc * 3;
+            if (esize == 1) {
+                const uint8_t* S = (const uint8_t*)src + (size_t)r * sw;
+                int v = 0;
+                for (j = 0; j < 8; j++) {
+                    int sxj = sx + j * cc;
+                    while (sxj < 0) sxj += cc;
+                    while (sxj >= sw) sxj -= cc;
+                    v += S[sxj] * xai[8 * px + j];
+                }
+                bi[(size_t)r * dw + dx] = v;
+            } else {
+                const float* S = (const float*)src + (size_t)r * sw;
+                float v = 0.f, t[8];
+                for (j = 0; j < 8; j++) {
+                    int sxj = sx + j * cc;
+                    while (sxj < 0) sxj += cc;
+                    while (sxj >= sw) sxj -= cc;
+                    t[j] = S[sxj] * xa[8 * px + j];
+                }
+                if (fast) {
+                    v = t[0];
+                    for (j = 1; j < 8; j++) v = v + t[j];
+                } else {
+                    for (j = 0; j < 8; j++) v += t[j];
+                }
+                bf[(size_t)r * dw + dx] = v;
+            }
+        }
+    }
+    for (dy = 0; dy < h_out; dy++) {
+        int rows[8];
+        for (k = 0; k < 8; k++) {
+            int sy = yofs[dy] - 3 + k;
+            rows[k] = sy < 0 ? 0 : sy >= h_in ? h_in - 1 : sy;
+        }
+        for (dx = 0; dx < dw; dx++) {
+            if (esize == 1) {
+                const short* b = yai + 8 * dy;
+                int s0 = bi[(size_t)rows[0] * dw + dx] * b[0] + bi[(size_t)rows[1] * dw + dx] * b[1] +
+                         bi[(size_t)rows[2] * dw + dx] * b[2] + bi[(size_t)rows[3] * dw + dx] * b[3];
+                int s1 = bi[(size_t)rows[4] * dw + dx] * b[4] + bi[(size_t)rows[5] * dw + dx] * b[5] +
+                         bi[(size_t)rows[6] * dw + dx] * b[6] + bi[(size_t)rows[7] * dw + dx] * b[7];
+                int v = (s0 + s1 + (1 << 21)) >> 22;
+                ((uint8_t*)dst)[(size_t)dy * dw + dx] = (uint8_t)(v < 0 ? 0 : v > 255 ? 255 : v);
+            } else {
+                const float* b = ya + 8 * dy;
+                float s0 = bf[(size_t)rows[0] * dw + dx] * b[0] + bf[(size_t)rows[1] * dw + dx] * b[1] +
+                           bf[(size_t)rows[2] * dw + dx] * b[2] + bf[(size_t)rows[3] * dw + dx] * b[3];
+                float s1 = bf[(size_t)rows[4] * dw + dx] * b[4] + bf[(size_t)rows[5] * dw + dx] * b[5] +
+                           bf[(size_t)rows[6] * dw + dx] * b[6] + bf[(size_t)rows[7] * dw + dx] * b[7];
+                ((float*)dst)[(size_t)dy * dw + dx] = s0 + s1;
+            }
+        }
+    }
+    free(xofs); free(xa); free(xai); free(yofs); free(ya); free(yai); free(bi); free(bf);
+}

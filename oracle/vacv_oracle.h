@@ -48,6 +48,10 @@ void oracle_resize_area_any(const void* src, int w_in, int h_in, int cc, int esi
                             int h_out, double inv_x, double inv_y);
 int oracle_area_table(int ssize, int dsize, int cn, double scale, int* di, int* si, float* alpha);
 void oracle_area_linear_tap(int d, int n_in, double scale, double inv_scale, int* i, float* f);
+/* INTER_LANCZOS4 (OpenCV 2.4 cv::resize, 8x8 taps, replicate borders);
+ * esize 1 (fixed point) or 4; inv_x / inv_y <= 0: dsize / ssize */
+void oracle_resize_lanczos4(const void* src, int w_in, int h_in, int cc, int esize, void* dst, int w_out, int h_out,
+                            double inv_x, double inv_y);
 void oracle_resize_cubic_f32(const float* src, int w_in, int h_in, int cc,
                              float* dst, int w_out, int h_out);
 void oracle_warp_affine_u8(const uint8_t* src, int w_in, int h_in, int cc,

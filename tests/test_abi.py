@@ -69,7 +69,7 @@ def test_argument_validation_without_device(lib):
     assert lib.vacv_resize(ctypes.byref(small_pitch), ctypes.byref(good), 1, 0, None) == -1
     dst = VacvImage(0x2000, 1, 4, 4, 3, 2, 1, 0, 0, 0)
     assert lib.vacv_crop(ctypes.byref(good), ctypes.byref(dst), 6, 0, None) == -1      # rect outside
-    assert lib.vacv_resize(ctypes.byref(good), ctypes.byref(dst), 4, 0, None) == -2    # INTER_LANCZOS4
+    assert lib.vacv_resize(ctypes.byref(good), ctypes.byref(dst), 5, 0, None) == -2    # no such mode (LANCZOS4 = 4 runs)
     dst3 = VacvImage(0x2000, 1, 3, 3, 3, 2, 1, 0, 0, 0)
     assert lib.vacv_resize_scaled(ctypes.byref(good), ctypes.byref(dst3), 3, 0, 0.0, 0.5, None) == -1  # fx <= 0
     assert lib.vacv_resize_scaled(ctypes.byref(good), ctypes.byref(dst3), 1, 0, 0.5, 0.5, None) == -2  # LINEAR

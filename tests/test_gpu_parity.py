@@ -399,6 +399,41 @@ def test_area_unit_kernel(ops, dev, oracle):
         assert_same(got[k], oracle.resize_area(np.ascontiguousarray(img[..., k]), 48, 32), "area unit chw")
 
 
+def test_resize_lanczos4(ops, dev, oracle):
+    """INTER_LANCZOS4 (k_lanczos.hip; the reference hands it to cv::resize,
+    resize.cpp:46-48, cv.h:33): bit-exact against the oracle's OpenCV 2.4
+    restatement (parity unpinned) for u8 and fp32, 1-4 channels, down- and
+    up-scales, NCHW planes, the normalise epilogue, and cv::resize's fx / fy
+    form."""
+    import torch
+    from vacv_amd import INTER_LANCZOS4, NCHW
+    rng = np.random.default_rng(41)
+    for i, ((h, w), c) in enumerate([((60, 84), 1), ((45, 70), 2), ((64, 96), 3), ((33, 50), 4)]):
+        img = synthetic_image(820 + i, h, w, c)
+        img = img if c > 1 else img[..., None]
+        f = (img.astype(np.float32) + rng.standard_normal(img.shape).astype(np.float32)).astype(np.float32)
+        sq = (lambda a: a) if c > 1 else (lambda a: a[..., 0])
+        for wo, ho in [(w // 3, h // 2), (w * 2 + 1, h + 7), (w - 1, h * 3)]:
+            got = host(ops.resize(to_dev(img[None], dev), wo, ho, interpolation=INTER_LANCZOS4))[0]
+            assert_same(sq(got), oracle.resize_lanczos4(sq(img), wo, ho), f"lanczos u8 {h}x{w}x{c}->{ho}x{wo}")
+            gotf = host(ops.resize(to_dev(f[None], dev), wo, ho, interpolation=INTER_LANCZOS4))[0]
+            assert_same(sq(gotf), oracle.resize_lanczos4(sq(f), wo, ho), f"lanczos f32 {h}x{w}x{c}->{ho}x{wo}")
+        if c == 3:
+            chw = np.ascontiguousarray(img.transpose(2, 0, 1))
+            got = host(ops.resize(to_dev(chw[None], dev), 41, 37, interpolation=INTER_LANCZOS4, layout=NCHW))[0]
+            for k in range(c):
+                assert_same(got[k], oracle.resize_lanczos4(chw[k], 41, 37), "lanczos chw")
+            got = host(ops.resize_normalize(to_dev(img[None], dev), 50, 30, MEAN, STD, interpolation=INTER_LANCZOS4))[0]
+            want = oracle.normalize(oracle.u8_to_f32(oracle.resize_lanczos4(img, 50, 30)), MEAN, STD)
+            assert_same(got, want, "lanczos normalize")
+            got = host(ops.resize(to_dev(img[None], dev), 0, 0, interpolation=INTER_LANCZOS4, fx=0.7, fy=0.45))[0]
+            wo, ho = int(round(w * 0.7)), int(round(h * 0.45))
+            assert_same(got, oracle.resize_lanczos4(img, wo, ho, 0.7, 0.45), "lanczos fx/fy")
+    big = np.stack([synthetic_image(830 + k, 1080, 1920, 3) for k in range(2)])
+    got = host(ops.resize(to_dev(big, dev), 640, 360, interpolation=INTER_LANCZOS4))
+    assert_same(got[1], oracle.resize_lanczos4(big[1], 640, 360), "lanczos 1080p -> 640x360")
+
+
 def test_resize_area_any_scale(ops, dev, oracle):
     """INTER_AREA at non-integer scales (OpenCV 2.4 cv::resize restated,
     parity unpinned -- oracle/vacv_oracle.c oracle_resize_area_any):

@@ -469,3 +469,68 @@ def test_warp_nearest_restatement(oracle):
                 want = img[by, bx]
             got = oracle.warp_affine_nn(img, given, 29, 19, inverse_map=inverse, border_mode=mode, border=(7, 8, 9, 0))
             assert np.array_equal(got, want), (inverse, mode)
+
+
+def _lanczos_numpy(img, w_out, h_out):
+    """An independent numpy statement of OpenCV 2.4's INTER_LANCZOS4
+    (interpolateLanczos4 + resize()'s tables + replicate borders), u8 only:
+    separable integer sums in fixed point, the column pass on every source
+    row first, then the 8-row pass."""
+    h, w, c = img.shape
+    f32 = np.float32
+
+    def coeffs(x):
+        x = f32(x)
+        if x < np.finfo(np.float32).eps:
+            out = np.zeros(8, np.float32)
+            out[3] = 1
+            return out
+        s45 = 0.70710678118654752440084436210485
+        cs = [(1, 0), (-s45, -s45), (0, 1), (s45, -s45), (-1, 0), (s45, s45), (0, -1), (-s45, s45)]
+        y0 = -float(x + f32(3)) * 3.1415926535897932384626433832795 * 0.25
+        s0, c0 = np.sin(y0), np.cos(y0)
+        out = np.zeros(8, np.float32)
+        tot = f32(0)
+        for i in range(8):
+            y = -float(x + f32(3) - f32(i)) * 3.1415926535897932384626433832795 * 0.25
+            out[i] = f32((cs[i][0] * s0 + cs[i][1] * c0) / (y * y))
+            tot = f32(tot + out[i])
+        return (out * f32(f32(1) / tot)).astype(np.float32)
+
+    def table(n_in, n_out):
+        sc = 1.0 / (n_out / n_in)
+        idx, wts = [], []
+        for d in range(n_out):
+            fx = f32((d + 0.5) * sc - 0.5)
+            s = int(np.floor(fx))
+            fx = f32(fx - f32(s))
+            cf = coeffs(fx)
+            wts.append(np.clip(np.rint(cf * f32(2048)), -32768, 32767).astype(np.int64))
+            idx.append(np.clip(np.arange(s - 3, s + 5), 0, n_in - 1))
+        return np.array(idx), np.array(wts)
+
+    xi, xw = table(w, w_out)
+    yi, yw = table(h, h_out)
+    src = img.astype(np.int64)
+    rows = (src[:, xi, :] * xw[None, :, :, None]).sum(axis=2)          # (h, w_out, c)
+    acc = (rows[yi, :, :] * yw[:, :, None, None]).sum(axis=1)         # (h_out, w_out, c)
+    return np.clip((acc + (1 << 21)) >> 22, 0, 255).astype(np.uint8)
+
+
+def test_lanczos4_restatement(oracle):
+    """INTER_LANCZOS4 (the reference hands it to cv::resize, resize.cpp:46-48;
+    cv.h:33): oracle_resize_lanczos4 against an independent numpy statement
+    for u8 down- and up-scales with 1 and 3 channels, and the identity at
+    equal size (coefficients (0, 0, 0, 1, 0, ...)) for u8 and fp32.  Parity
+    unpinned: OpenCV is not runnable here."""
+    rng = np.random.default_rng(23)
+    for (h, w, c), (wo, ho) in [((21, 34, 3), (13, 9)), ((17, 12, 1), (29, 40)), ((32, 48, 3), (48, 20)),
+                                ((9, 9, 3), (5, 7))]:
+        img = rng.integers(0, 256, (h, w, c), dtype=np.uint8)
+        got = oracle.resize_lanczos4(img if c > 1 else img[..., 0], wo, ho)
+        want = _lanczos_numpy(img, wo, ho)
+        assert np.array_equal(got.reshape(want.shape), want), (h, w, c, wo, ho)
+    img = rng.integers(0, 256, (15, 22, 3), dtype=np.uint8)
+    assert np.array_equal(oracle.resize_lanczos4(img, 22, 15), img)
+    f = rng.standard_normal((15, 22, 3)).astype(np.float32)
+    assert np.array_equal(oracle.resize_lanczos4(f, 22, 15), f)
