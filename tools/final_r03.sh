@@ -25,4 +25,10 @@ for W in "resize:1280x720:resize_strip" "resize_other:area_1080p_960:area_u8_uni
   python3 tools/pmc_summary.py "gpurun_out/pmc_k_$key" "$key" --out "gpurun_out/pmc_k_$key.json" \
       > "gpurun_out/pmc_k_${key}_summary.txt" || exit 1
 done
+step "cubic store policy A/B"
+if [ -d arm-neon-opencv_amd/lib_cwb ]; then
+  for i in 1 2; do for l in lib lib_cwb; do
+    timeout -k 10 200 python3 tools/kbench_lib.py arm-neon-opencv_amd/$l --op cubic --iters 30 | sed "s/^/$l /" || exit 1
+  done; done
+fi
 step done
