@@ -1255,7 +1255,7 @@ def test_error_statuses(ops, dev):
         ops.crop(x, (4, 4, 12, 12))           # rect outside the image
     assert e.value.status == V._lib.ERR_INVALID_ARG
     with pytest.raises(V.VacvError) as e:
-        ops.resize(x, 4, 4, interpolation=4)  # INTER_LANCZOS4
+        ops.resize(x, 4, 4, interpolation=5)  # no such mode (resize.cpp:46-49 recurses on it)
     assert e.value.status == V._lib.ERR_UNSUPPORTED
     with pytest.raises(V.VacvError) as e:  # BORDER_ISOLATED has no meaning for warp_affine
         ops.warp_affine(x, np.eye(2, 3, dtype=np.float32), 8, 8, border_mode=16)
