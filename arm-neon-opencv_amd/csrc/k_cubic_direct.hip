@@ -40,30 +40,38 @@ constexpr int cubic_waves(int cc, int out) { return cc == 1 ? 8 : (cc == 3 && ou
 
 // SUMS: the statistics half of cfg5 fused (normalize_naive.cpp:7-72 on the
 // resized image, here as fixed-order sums for the global mean_stddev): each
-// lane adds its (at most 2) pixels' values and squares per channel in fp32,
-// the wave reduces them in a fixed shuffle order, and lane 0 stores the
-// wave's (Sum x, Sum x^2) as fp64 partials; wave_sums_kernel sums those in
-// a fixed order (deterministic, run to run).  fp32 within a wave: 128 values
-// <= 255 (squares <= 65025) -- relative error ~1e-7, far inside SURVEY
-// 8(c)'s 1e-3 (mean) / 1e-4 (std) bar.  (Reducing inside the launch -- the
-// last wave of each image, found by an agent-scope release/acquire counter
-// -- took 2.2 ms: an agent-scope release per wave writes back the L2.)
+// lane adds its (at most 2) pixels' values and squares per channel in fp32
+// (fp32 only over <= 2 pixels), the wave reduces those in fp64 in
+// a fixed shuffle order, the workgroup adds its 4 waves in order (one LDS
+// exchange, one barrier), and thread v stores value v of the workgroup's
+// (Sum x, Sum x^2) as an fp64 partial; group_sums_kernel sums those in a fixed
+// order (deterministic, run to run).  (Reducing across workgroups inside the
+// launch -- the last wave of each image, found by an agent-scope
+// release/acquire counter -- took 2.2 ms: an agent-scope release per wave
+// writes back the L2.)
 template <int CC, int OUT, bool SUMS>
 __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(cubic_waves(CC, OUT))))
 cubic_direct_kernel(ResizeLaunch L, int blocks_per_plane) {
     __shared__ __attribute__((aligned(16))) float xch[4][kWavePx * CC];
 
+    __shared__ double wsum[SUMS ? 4 : 1][2 * CC];
     const int pidx = blockIdx.x / blocks_per_plane;  // image * planes + plane
     const int blk = blockIdx.x - pidx * blocks_per_plane;
     const int W = L.dst.w;
     const int P = W * L.dst.h;
     const int p0 = (blk * 4 + (int)threadIdx.y) * kWavePx;
-    // this wave's partials, value-major: [CC][2][image][wave of the image]
-    const int64_t n_waves = (int64_t)L.n * blocks_per_plane * 4;
-    double* part = SUMS ? L.sum_partials + (int64_t)pidx * blocks_per_plane * 4 + blk * 4 + (int)threadIdx.y : nullptr;
     if (p0 >= P) {  // whole wave
         if (SUMS) {
-            if (threadIdx.x < 2 * CC) part[threadIdx.x * n_waves] = 0.0;
+            // no pixels: zero sums, then the workgroup's barrier below
+            if (threadIdx.x < 2 * CC) wsum[threadIdx.y][threadIdx.x] = 0.0;
+            __syncthreads();
+            if (threadIdx.y == 0 && threadIdx.x < 2 * CC) {
+                const int64_t groups = (int64_t)L.n * blocks_per_plane;
+                double a = 0.0;
+#pragma unroll
+                for (int w = 0; w < 4; ++w) a += wsum[w][threadIdx.x];
+                L.sum_partials[threadIdx.x * groups + blockIdx.x] = a;
+            }
         }
         return;
     }
@@ -189,26 +197,32 @@ cubic_direct_kernel(ResizeLaunch L, int blocks_per_plane) {
                 s2[k] += v * v;
             }
         }
+        double d[2 * CC];
 #pragma unroll
         for (int k = 0; k < CC; ++k) {
+            d[2 * k] = (double)s1[k];
+            d[2 * k + 1] = (double)s2[k];
+        }
 #pragma unroll
-            for (int o = 32; o > 0; o >>= 1) {
-                s1[k] += __shfl_xor(s1[k], o, 64);
-                s2[k] += __shfl_xor(s2[k], o, 64);
-            }
+        for (int o = 32; o > 0; o >>= 1) {
+#pragma unroll
+            for (int v = 0; v < 2 * CC; ++v) d[v] += __shfl_xor(d[v], o, 64);
         }
         if (lane == 0) {
 #pragma unroll
-            for (int k = 0; k < CC; ++k) {
-                part[(2 * k) * n_waves] = (double)s1[k];
-                part[(2 * k + 1) * n_waves] = (double)s2[k];
-            }
+            for (int v = 0; v < 2 * CC; ++v) wsum[threadIdx.y][v] = d[v];
+        }
+        __syncthreads();
+        if (threadIdx.y == 0 && lane < 2 * CC) {
+            // value-major [CC][2][image][workgroup]: a value's partials are one
+            // contiguous run for group_sums_kernel
+            const int64_t groups = (int64_t)L.n * blocks_per_plane;
+            double a = 0.0;
+#pragma unroll
+            for (int w = 0; w < 4; ++w) a += wsum[w][lane];
+            L.sum_partials[lane * groups + blockIdx.x] = a;
         }
     }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-
     // ---- LDS -> HBM: dense byte b of the plane's output lives at row
     // b / out_row, column byte b % out_row --------------------------------------
     unsigned char* dp = const_cast<unsigned char*>(L.dst.base) + (int64_t)img * L.dst.img_pitch +
@@ -249,67 +263,67 @@ cubic_direct_kernel(ResizeLaunch L, int blocks_per_plane) {
     }
 }
 
-// The fixed-order sum of the per-wave partials (value-major layout: a
-// value's partials are one contiguous run; interleaved with the other values
-// every workgroup fetched all of them, 24 us for cfg5).  One 1024-thread
-// workgroup per (group, value, split): thread t adds terms t, t + 1024, ...
-// of the split's range in order (8 loads issued ahead of their adds), then a
-// fixed LDS tree.  Per-image sums: one split per image.  The batch sum
-// (cfg5: 50K terms per value): kSplit splits per value, each writing its
-// sum; the last split of a value to finish (one agent-scope release /
-// acquire per workgroup -- a release per wave, 50K of them, took 2.2 ms)
-// adds the kSplit sums in split order.  Deterministic either way.
+// The fixed-order sum of the per-workgroup partials and, optionally, the
+// population mean / stddev (stats_kernel's formula, k_pixel.hip): one
+// 1024-thread workgroup per (group, channel) sums both of the channel's
+// values -- thread t adds terms t, t + 1024, ... in order (8 loads issued
+// ahead of their adds), then a fixed LDS tree -- so the statistics need no
+// communication between workgroups (cfg5: 12,544 terms per value, 3
+// workgroups; round 3's per-wave partials took 16 split workgroups per value,
+// an agent-scope counter and a separate stats launch).
 constexpr int kSumThreads = 1024;
-constexpr int kSplit = 16;
-__global__ void __launch_bounds__(kSumThreads) wave_sums_kernel(const double* partials, int waves, int n, int vals,
-                                                               int per_image, double* sums, int* count) {
-    __shared__ double red[kSumThreads];
-    __shared__ int last;
-    const int splits = per_image ? 1 : kSplit;
-    const int g = blockIdx.x / (vals * splits);
-    const int r = blockIdx.x - g * vals * splits;
-    const int v = r / splits, sp = r - v * splits;
-    const int64_t run = per_image ? waves : (int64_t)n * waves;  // terms of this (group, value)
-    const int64_t b0 = run * sp / splits, b1 = run * (sp + 1) / splits;
-    const double* p = partials + (int64_t)v * n * waves + (per_image ? (int64_t)g * waves : 0);
+__global__ void __launch_bounds__(kSumThreads) group_sums_kernel(const double* partials, int groups, int n, int cc,
+                                                                int per_image, double count, double* sums,
+                                                                float* mean, float* stddev) {
+    __shared__ double red[2][kSumThreads];
+    const int g = blockIdx.x / cc;  // output group (image, or 0)
+    const int k = blockIdx.x - g * cc;
+    const int64_t run = per_image ? groups : (int64_t)n * groups;  // terms of this (group, value)
+    const int64_t vstride = (int64_t)n * groups;
+    const double* p1 = partials + (int64_t)(2 * k) * vstride + (per_image ? (int64_t)g * groups : 0);
+    const double* p2 = p1 + vstride;
     constexpr int kDepth = 8;
-    double acc = 0.0;
-    int64_t t = b0 + threadIdx.x;
-    for (; t + (kDepth - 1) * kSumThreads < b1; t += kDepth * kSumThreads) {
-        double x[kDepth];
+    double a1 = 0.0, a2 = 0.0;
+    int64_t t = threadIdx.x;
+    for (; t + (kDepth - 1) * kSumThreads < run; t += kDepth * kSumThreads) {
+        double x[kDepth], y[kDepth];
 #pragma unroll
-        for (int q = 0; q < kDepth; ++q) x[q] = p[t + (int64_t)q * kSumThreads];
+        for (int q = 0; q < kDepth; ++q) {
+            x[q] = p1[t + (int64_t)q * kSumThreads];
+            y[q] = p2[t + (int64_t)q * kSumThreads];
+        }
 #pragma unroll
-        for (int q = 0; q < kDepth; ++q) acc += x[q];
+        for (int q = 0; q < kDepth; ++q) {
+            a1 += x[q];
+            a2 += y[q];
+        }
     }
-    for (; t < b1; t += kSumThreads) acc += p[t];
-    red[threadIdx.x] = acc;
+    for (; t < run; t += kSumThreads) {
+        a1 += p1[t];
+        a2 += p2[t];
+    }
+    red[0][threadIdx.x] = a1;
+    red[1][threadIdx.x] = a2;
     __syncthreads();
     for (int h = kSumThreads / 2; h > 0; h >>= 1) {
-        if ((int)threadIdx.x < h) red[threadIdx.x] += red[threadIdx.x + h];
+        if ((int)threadIdx.x < h) {
+            red[0][threadIdx.x] += red[0][threadIdx.x + h];
+            red[1][threadIdx.x] += red[1][threadIdx.x + h];
+        }
         __syncthreads();
     }
-    if (per_image) {
-        if (threadIdx.x == 0) sums[g * vals + v] = red[0];
-        return;
-    }
-    // split sums right after the partials: split[v * kSplit + sp]
-    double* split = const_cast<double*>(partials) + (int64_t)vals * n * waves;
     if (threadIdx.x == 0) {
-        split[v * kSplit + sp] = red[0];
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        const int old = __hip_atomic_fetch_add(count + v, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        last = old == kSplit - 1;
-    }
-    __syncthreads();
-    if (!last) return;
-    if (threadIdx.x == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        double a = 0.0;
-        for (int q = 0; q < kSplit; ++q) a += __hip_atomic_load(split + v * kSplit + q, __ATOMIC_RELAXED,
-                                                                 __HIP_MEMORY_SCOPE_AGENT);
-        sums[v] = a;
-        __hip_atomic_store(count + v, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // for the next launch
+        const int idx = g * cc + k;
+        const double s1 = red[0][0], s2 = red[1][0];
+        sums[2 * idx] = s1;
+        sums[2 * idx + 1] = s2;
+        if (mean) {
+            const double m = s1 / count;
+            double var = s2 / count - m * m;
+            if (var < 0) var = 0;
+            mean[idx] = (float)m;
+            stddev[idx] = (float)sqrt(var);
+        }
     }
 }
 
@@ -328,10 +342,11 @@ hipError_t launch_cc(const ResizeLaunch& L, hipStream_t s) {
                            (int)per_plane);
         const hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
-        const int blocks = L.sum_per_image ? L.n * 2 * CC : 2 * CC * kSplit;
-        hipLaunchKernelGGL(wave_sums_kernel, dim3((unsigned)blocks), dim3(kSumThreads), 0, s,
-                           (const double*)L.sum_partials, (int)(per_plane * 4), L.n, 2 * CC, L.sum_per_image,
-                           L.sum_out, L.sum_count);
+        const int blocks = (L.sum_per_image ? L.n : 1) * CC;
+        const double count = (double)P * (L.sum_per_image ? 1 : L.n);
+        hipLaunchKernelGGL(group_sums_kernel, dim3((unsigned)blocks), dim3(kSumThreads), 0, s,
+                           (const double*)L.sum_partials, (int)per_plane, L.n, CC, L.sum_per_image, count,
+                           L.sum_out, L.sum_mean, L.sum_std);
     }
     else
         hipLaunchKernelGGL((cubic_direct_kernel<CC, kOutF32, false>), dim3((unsigned)total), dim3(64, 4), 0, s, L,
@@ -346,10 +361,10 @@ bool cubic_direct_applies(const ResizeLaunch& L) {
     return L.kind == kCubic && L.src.esize == 1 && L.src.cc <= 3 && (L.out == kOutF32 || L.out == kOutNorm);
 }
 
-int cubic_direct_waves(const ResizeLaunch& L) {
+int cubic_direct_groups(const ResizeLaunch& L) {
     constexpr int kBlockPx = 4 * kWavePx;
     const int64_t P = (int64_t)L.dst.w * L.dst.h;
-    return (int)((P + kBlockPx - 1) / kBlockPx * 4);
+    return (int)((P + kBlockPx - 1) / kBlockPx);
 }
 
 hipError_t launch_cubic_direct(const ResizeLaunch& L, hipStream_t s) {

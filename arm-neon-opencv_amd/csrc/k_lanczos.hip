@@ -13,20 +13,30 @@
 //    (fx = (float)((dx + 0.5) * scale_x - 0.5)) and 8 coefficients, per
 //    output row sy and 8 coefficients.  u8: coefficients
 //    saturate_cast<short>(c * 2048); fp32: the float coefficients.
-//  * Per output element: 8 source rows clip(sy - 3 + k, 0, h - 1), per row
-//    the 8 horizontal taps of columns sx - 3 + j clamped to [0, w - 1] (the
-//    `while (sxj < 0) sxj += cn` walk of HResizeLanczos4), summed in tap
-//    order -- int for u8, fp32 for fp32 (columns in [xmin, xmax) take the
-//    unrolled sum without the leading 0 +, as OpenCV's fast path does);
-//    then the 8 rows as (b0 h0 + b1 h1 + b2 h2 + b3 h3) + (b4 h4 + ... b7 h7),
-//    u8 rounded by FixedPtCast<int, uchar, 22>.
-// One thread per output element; the taps of neighbouring threads share
-// cache lines, so the gathers hit L1 / L2.  A correctness path for a mode
-// the reference cannot run, not a tuned kernel.
+//  * Horizontal pass (HResizeLanczos4): per source row and output column the
+//    8 taps sx - 3 .. sx + 4 of each channel (an out-of-range tap walks by cn
+//    to the nearest pixel of its channel: a clamp), summed in tap order --
+//    int for u8, fp32 for fp32 (columns outside [xmin, xmax) start from
+//    0 +, as OpenCV's border loop does).
+//  * Vertical pass (VResizeLanczos4): rows clip(sy - 3 + k, 0, h - 1); u8 in
+//    int (order immaterial), rounded by FixedPtCast<int, uchar, 22>; fp32:
+//    elements e < (dst.w * cn & ~3) as the 4-wide NEON loop of
+//    VResizeLanczos4Vec_32f, (b0 h0 + .. + b3 h3) + (b4 h4 + .. + b7 h7),
+//    the rest as the scalar tail, b0 h0 + b1 h1 + .. + b7 h7 left to right.
+// Shape (as resizeGeneric_ itself): a wave owns a strip of 64 output columns
+// (one per lane) and a band of output rows and walks down it.  Each source
+// row the band needs is resized horizontally ONCE -- per lane one
+// dword-aligned window load of its 8 CC tap bytes (u8) or 8 CC floats --
+// into the lane's own slot of an 8-row LDS ring (row r -> slot r mod 8);
+// an output row then reads its 8 rows' values from the ring.  Every lane
+// reads and writes only its own ring entries: no barriers.  At a 3x
+// downscale that is ~3 horizontal rows per output row instead of the 8 a
+// per-output-element gather pays, and no table reads per tap.
 #pragma clang fp contract(off)
 
 #include <algorithm>
 #include <cfloat>
+#include <climits>
 #include <cmath>
 #include <cstring>
 #include <map>
@@ -58,63 +68,243 @@ struct LanczosLaunch {
 };
 
 template <typename TIn, int OUT, int CC>
-__global__ void __launch_bounds__(kBlock) lanczos_kernel(LanczosLaunch L) {
+__global__ void __launch_bounds__(kBlock) lanczos_kernel(LanczosLaunch L, int strips, int bands, int band_rows) {
     constexpr bool U8 = std::is_same<TIn, uint8_t>::value;
     using TW = typename std::conditional<U8, int, float>::type;
-    const int e = (int)(blockIdx.x * kBlock + threadIdx.x);
-    const int y = blockIdx.y;
-    const int pidx = blockIdx.z;
-    if (e >= L.dst.w * CC) return;
-    const int x = e / CC, k = e - x * CC;
+    using TOut = typename std::conditional<(OUT == kOutSame), TIn, float>::type;
+    __shared__ TW ring[4][8][64 * CC];  // per wave: 8 source rows x 64 columns x CC
+
+    // wave-uniform, and said so: the plane's buffer resource stays in SGPRs
+    // (derived from a per-lane value it would be waterfalled at every load)
+    const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)), lane = (int)(threadIdx.x & 63);
+    const int task = (int)blockIdx.x * 4 + wave;  // (plane, band, strip), strip fastest
+    const int strip = task % strips;
+    const int rest = task / strips;
+    const int band = rest % bands;
+    const int pidx = rest / bands;
+    if (pidx >= L.n * L.src.planes) return;  // whole wave
+    const int y0 = band * band_rows, y1 = min(y0 + band_rows, L.dst.h);
+    const int x = strip * 64 + lane;
+    const bool live = x < L.dst.w;
+    const int xc = live ? x : L.dst.w - 1;  // idle lanes resize a valid column and store nothing
     const int img = pidx / L.src.planes;
     const int plane = pidx - img * L.src.planes;
-    const unsigned char* sp = L.src.base + (int64_t)img * L.src.img_pitch + (int64_t)plane * L.src.plane_pitch;
     const int w = L.src.w, h = L.src.h;
-    const int sx = L.t.xofs[x], sy = L.t.yofs[y];
-    int cols[8];
+    const unsigned char* sp = L.src.base + (int64_t)img * L.src.img_pitch + (int64_t)plane * L.src.plane_pitch;
+    const Rsrc srs = make_rsrc(sp, L.src.plane_bytes);
+    const uint32_t slimit = (uint32_t)L.src.plane_bytes + srs.delta;
+    const uint32_t rp = (uint32_t)L.src.row_pitch;  // plane < 2^31 bytes (kMaxPlaneBytes)
+
+    // this column's taps: origin, coefficients, fast (unrolled, unclamped) or not
+    const int sx = L.t.xofs[xc];
+    const bool fast = xc >= L.t.xmin && xc < L.t.xmax;
+    TW c[8];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) cols[j] = min(max(sx - 3 + j, 0), w - 1) * CC + k;
-    const bool fast = x >= L.t.xmin && x < L.t.xmax;
-    TW hs[8];
+    for (int j = 0; j < 8; ++j) {
+        if constexpr (U8) c[j] = (int)L.t.xai[8 * xc + j];
+        else c[j] = L.t.xaf[8 * xc + j];
+    }
+
+    // HResizeLanczos4 of source row r for this lane's column -> ring slot
+    auto hrow = [&](int r, int slot) {
+        TW hv[CC];
+        const uint32_t row0 = (uint32_t)r * rp;
+        if constexpr (U8) {
+            constexpr int ND = (8 * CC + 6) / 4;  // dwords covering 8 CC bytes at any byte offset
+            const uint32_t off = row0 + (uint32_t)((sx - 3) * CC) + srs.delta;
+            const uint32_t a = off & ~3u, sh = off & 3u;
+            uint32_t d[ND];
+            if (fast && a + 4u * ND <= slimit) {
+                int q = 0;
 #pragma unroll
-    for (int r = 0; r < 8; ++r) {
-        const TIn* row = reinterpret_cast<const TIn*>(sp + (int64_t)min(max(sy - 3 + r, 0), h - 1) * L.src.row_pitch);
-        TW a[8];
+                for (; q + 4 <= ND; q += 4) {
+                    const auto v = __builtin_amdgcn_raw_buffer_load_b128(srs.r, (int)(a + 4 * q), 0, 0);
+                    d[q] = v[0]; d[q + 1] = v[1]; d[q + 2] = v[2]; d[q + 3] = v[3];
+                }
+                if constexpr (ND % 4 == 3) {
+                    const auto v = __builtin_amdgcn_raw_buffer_load_b96(srs.r, (int)(a + 4 * q), 0, 0);
+                    d[q] = v[0]; d[q + 1] = v[1]; d[q + 2] = v[2];
+                } else if constexpr (ND % 4 == 2) {
+                    const auto v = __builtin_amdgcn_raw_buffer_load_b64(srs.r, (int)(a + 4 * q), 0, 0);
+                    d[q] = v[0]; d[q + 1] = v[1];
+                } else if constexpr (ND % 4 == 1) {
+                    d[q] = __builtin_amdgcn_raw_buffer_load_b32(srs.r, (int)(a + 4 * q), 0, 0);
+                }
+            } else {
+                // border columns (clamped taps) and the plane's last bytes: the
+                // 8 CC tap bytes one by one, placed where the window load puts them
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            if constexpr (U8) a[j] = (int)row[cols[j]] * (int)L.t.xai[8 * x + j];
-            else a[j] = row[cols[j]] * L.t.xaf[8 * x + j];
+                for (int q = 0; q < ND; ++q) d[q] = 0u;
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    const int col = min(max(sx - 3 + j, 0), w - 1);
+#pragma unroll
+                    for (int k = 0; k < CC; ++k) {
+                        const uint32_t e = sh + (uint32_t)(j * CC + k);
+                        const uint32_t b = __builtin_amdgcn_raw_buffer_load_b8(
+                            srs.r, (int)(row0 + (uint32_t)(col * CC + k) + srs.delta), 0, 0);
+                        d[e >> 2] |= b << (8 * (e & 3));
+                    }
+                }
+            }
+            uint32_t wv[ND - 1];
+#pragma unroll
+            for (int q = 0; q < ND - 1; ++q) wv[q] = __builtin_amdgcn_alignbyte(d[q + 1], d[q], sh);
+#pragma unroll
+            for (int k = 0; k < CC; ++k) {
+                int v = 0;  // int sums: the order is immaterial
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    const int e = j * CC + k;
+                    v += (int)((wv[e >> 2] >> (8 * (e & 3))) & 0xFFu) * c[j];
+                }
+                hv[k] = v;
+            }
+        } else {
+            float t[8][CC];
+            const uint32_t off = row0 + (uint32_t)((sx - 3) * CC * 4) + srs.delta;
+            if (fast && off + 32u * CC <= slimit) {
+#pragma unroll
+                for (int q = 0; q < 2 * CC; ++q) {
+                    const auto v = __builtin_amdgcn_raw_buffer_load_b128(srs.r, (int)(off + 16 * q), 0, 0);
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        const int e = 4 * q + i;
+                        // (__builtin_bit_cast(float, v[i]) of a vector element reads
+                        // element 0 for every i with this compiler: ROCm 7.2 clang)
+                        t[e / CC][e % CC] = __uint_as_float(v[i]);
+                    }
+                }
+            } else {
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    const int col = min(max(sx - 3 + j, 0), w - 1);
+#pragma unroll
+                    for (int k = 0; k < CC; ++k)
+                        t[j][k] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                                                                srs.r, (int)(row0 + (uint32_t)(col * CC + k) * 4 + srs.delta), 0, 0));
+                }
+            }
+#pragma unroll
+            for (int k = 0; k < CC; ++k) {
+                float a[8];
+#pragma unroll
+                for (int j = 0; j < 8; ++j) a[j] = t[j][k] * c[j];
+                // HResizeLanczos4: the border loop starts from v = 0, the unrolled one does not
+                float v = fast ? a[0] : 0.f + a[0];
+#pragma unroll
+                for (int j = 1; j < 8; ++j) v = v + a[j];
+                hv[k] = v;
+            }
         }
-        // HResizeLanczos4: the border loop starts from v = 0, the unrolled one does not
-        TW v = fast ? a[0] : (TW)0 + a[0];
 #pragma unroll
-        for (int j = 1; j < 8; ++j) v = v + a[j];
-        hs[r] = v;
+        for (int k = 0; k < CC; ++k) ring[wave][slot][lane * CC + k] = hv[k];
+    };
+
+    const int dw = L.dst.w * CC;
+    unsigned char* dp = const_cast<unsigned char*>(L.dst.base) + (int64_t)img * L.dst.img_pitch +
+                        (int64_t)plane * L.dst.plane_pitch;
+    const Rsrc drs = make_rsrc(dp, L.dst.plane_bytes);
+    const bool dst_al = ((reinterpret_cast<uintptr_t>(dp) | (uintptr_t)L.dst.row_pitch) & 3) == 0;
+    ChanNorm cn[CC] = {};
+    if (OUT == kOutNorm) {
+#pragma unroll
+        for (int k = 0; k < CC; ++k) cn[k] = chan_norm(L.norm, img, CC == 1 ? plane % L.norm.c_total : k);
     }
-    float f = 0.f;
-    int vi = 0;
-    if constexpr (U8) {
-        const short* b = L.t.yai + 8 * y;
-        const int s0 = hs[0] * b[0] + hs[1] * b[1] + hs[2] * b[2] + hs[3] * b[3];
-        const int s1 = hs[4] * b[4] + hs[5] * b[5] + hs[6] * b[6] + hs[7] * b[7];
-        vi = min(max((s0 + s1 + (1 << 21)) >> 22, 0), 255);  // FixedPtCast<int, uchar, 22>
-    } else {
-        const float* b = L.t.yaf + 8 * y;
-        const float s0 = ((hs[0] * b[0] + hs[1] * b[1]) + hs[2] * b[2]) + hs[3] * b[3];
-        const float s1 = ((hs[4] * b[4] + hs[5] * b[5]) + hs[6] * b[6]) + hs[7] * b[7];
-        f = s0 + s1;
-    }
-    using TOut = typename std::conditional<(OUT == kOutSame), TIn, float>::type;
-    TOut* d = reinterpret_cast<TOut*>(const_cast<unsigned char*>(L.dst.base) + (int64_t)img * L.dst.img_pitch +
-                                      (int64_t)plane * L.dst.plane_pitch + (int64_t)y * L.dst.row_pitch) + e;
-    if (OUT == kOutSame) {
-        if constexpr (U8) *d = (TOut)vi;
-        else *d = (TOut)f;
-    } else if (OUT == kOutF32) {
-        *d = (TOut)(U8 ? (float)vi : f);
-    } else {
-        const ChanNorm cn = chan_norm(L.norm, img, CC == 1 ? plane % L.norm.c_total : k);
-        *d = (TOut)(U8 ? normalize_u8v(cn, vi) : normalize_f(cn, f));
+
+    int next = INT_MIN;  // first source row (unclamped) not yet in the ring
+    for (int y = y0; y < y1; ++y) {
+        const int sy = L.t.yofs[y];  // uniform, non-decreasing in y
+        for (int r = max(next, sy - 3); r <= sy + 4; ++r) hrow(min(max(r, 0), h - 1), r & 7);
+        next = max(next, sy + 5);
+        TW hs[8][CC];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+#pragma unroll
+            for (int q = 0; q < CC; ++q) hs[k][q] = ring[wave][(sy - 3 + k) & 7][lane * CC + q];
+        }
+        TOut o[CC];
+        if constexpr (U8) {
+            const short* b = L.t.yai + 8 * y;
+            int bb[8];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) bb[k] = b[k];
+#pragma unroll
+            for (int q = 0; q < CC; ++q) {
+                const int s0 = hs[0][q] * bb[0] + hs[1][q] * bb[1] + hs[2][q] * bb[2] + hs[3][q] * bb[3];
+                const int s1 = hs[4][q] * bb[4] + hs[5][q] * bb[5] + hs[6][q] * bb[6] + hs[7][q] * bb[7];
+                const int vi = min(max((s0 + s1 + (1 << 21)) >> 22, 0), 255);  // FixedPtCast<int, uchar, 22>
+                if (OUT == kOutSame) o[q] = (TOut)vi;
+                else if (OUT == kOutF32) o[q] = (TOut)(float)vi;
+                else o[q] = (TOut)normalize_u8v(cn[q], vi);
+            }
+        } else {
+            const float* b = L.t.yaf + 8 * y;
+            float bb[8];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) bb[k] = b[k];
+#pragma unroll
+            for (int q = 0; q < CC; ++q) {
+                float v;
+                if (x * CC + q < (dw & ~3)) {  // VResizeLanczos4Vec_32f's 4-wide loop
+                    const float s0 = ((hs[0][q] * bb[0] + hs[1][q] * bb[1]) + hs[2][q] * bb[2]) + hs[3][q] * bb[3];
+                    const float s1 = ((hs[4][q] * bb[4] + hs[5][q] * bb[5]) + hs[6][q] * bb[6]) + hs[7][q] * bb[7];
+                    v = s0 + s1;
+                } else {  // the scalar tail
+                    v = hs[0][q] * bb[0];
+#pragma unroll
+                    for (int k = 1; k < 8; ++k) v = v + hs[k][q] * bb[k];
+                }
+                if (OUT == kOutNorm) v = normalize_f(cn[q], v);
+                o[q] = (TOut)v;
+            }
+        }
+        const uint32_t orow = (uint32_t)y * (uint32_t)L.dst.row_pitch + drs.delta;
+        if constexpr (sizeof(TOut) == 1) {
+            // u8: the quad's 4 CC bytes as CC dword stores (quad_pack) where the
+            // quad is whole and the destination dword-aligned, else bytes
+            uint32_t own = 0;
+#pragma unroll
+            for (int q = 0; q < CC; ++q) own |= (uint32_t)(uint8_t)o[q] << (8 * q);
+            const int xq = x & ~3;
+            const bool quad = dst_al && xq + 4 <= L.dst.w;  // uniform per quad
+            const uint32_t word = quad_pack<CC>(own, lane & 3);
+            if (quad) {
+                if ((lane & 3) < CC)
+                    __builtin_amdgcn_raw_buffer_store_b32(word, drs.r, (int)(orow + (uint32_t)(xq * CC + 4 * (lane & 3))),
+                                                          0, 0);
+            } else if (live) {
+#pragma unroll
+                for (int q = 0; q < CC; ++q)
+                    __builtin_amdgcn_raw_buffer_store_b8((unsigned char)(own >> (8 * q)), drs.r,
+                                                         (int)(orow + (uint32_t)(x * CC + q)), 0, 0);
+            }
+        } else if (live) {
+            const uint32_t off = orow + (uint32_t)(x * CC) * 4u;
+            TOut* dq = reinterpret_cast<TOut*>(dp + (off - drs.delta));
+            if (dst_al) {
+                if constexpr (CC == 1) {
+                    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, o[0]), drs.r, (int)off, 0, 0);
+                } else if constexpr (CC == 2) {
+                    typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+                    __builtin_amdgcn_raw_buffer_store_b64(
+                        u32x2{__builtin_bit_cast(uint32_t, o[0]), __builtin_bit_cast(uint32_t, o[1])}, drs.r, (int)off, 0, 0);
+                } else if constexpr (CC == 3) {
+                    typedef unsigned int u32x3 __attribute__((ext_vector_type(3)));
+                    __builtin_amdgcn_raw_buffer_store_b96(
+                        u32x3{__builtin_bit_cast(uint32_t, o[0]), __builtin_bit_cast(uint32_t, o[1]),
+                              __builtin_bit_cast(uint32_t, o[2])}, drs.r, (int)off, 0, 0);
+                } else {
+                    __builtin_amdgcn_raw_buffer_store_b128(
+                        u32x4{__builtin_bit_cast(uint32_t, o[0]), __builtin_bit_cast(uint32_t, o[1]),
+                              __builtin_bit_cast(uint32_t, o[2]), __builtin_bit_cast(uint32_t, o[3])},
+                        drs.r, (int)off, 0, 0);
+                }
+            } else {
+#pragma unroll
+                for (int q = 0; q < CC; ++q) dq[q] = o[q];
+            }
+        }
     }
 }
 
@@ -228,30 +418,34 @@ int lanczos_tables(const ResizeLaunch& R, double inv_x, double inv_y, hipStream_
     return VACV_OK;
 }
 
+struct LzGrid {
+    int blocks, strips, bands, band_rows;
+};
+
 template <typename TIn, int OUT>
-hipError_t launch_out(const LanczosLaunch& A, dim3 grid, hipStream_t s) {
+hipError_t launch_out(const LanczosLaunch& A, const LzGrid& g, hipStream_t s) {
+    const dim3 grid((unsigned)g.blocks), block(kBlock);
     switch (A.src.cc) {
-        case 1: hipLaunchKernelGGL((lanczos_kernel<TIn, OUT, 1>), grid, dim3(kBlock), 0, s, A); break;
-        case 2: hipLaunchKernelGGL((lanczos_kernel<TIn, OUT, 2>), grid, dim3(kBlock), 0, s, A); break;
-        case 3: hipLaunchKernelGGL((lanczos_kernel<TIn, OUT, 3>), grid, dim3(kBlock), 0, s, A); break;
-        case 4: hipLaunchKernelGGL((lanczos_kernel<TIn, OUT, 4>), grid, dim3(kBlock), 0, s, A); break;
+        case 1: hipLaunchKernelGGL((lanczos_kernel<TIn, OUT, 1>), grid, block, 0, s, A, g.strips, g.bands, g.band_rows); break;
+        case 2: hipLaunchKernelGGL((lanczos_kernel<TIn, OUT, 2>), grid, block, 0, s, A, g.strips, g.bands, g.band_rows); break;
+        case 3: hipLaunchKernelGGL((lanczos_kernel<TIn, OUT, 3>), grid, block, 0, s, A, g.strips, g.bands, g.band_rows); break;
+        case 4: hipLaunchKernelGGL((lanczos_kernel<TIn, OUT, 4>), grid, block, 0, s, A, g.strips, g.bands, g.band_rows); break;
         default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
 }
 
 template <typename TIn>
-hipError_t launch_t(const LanczosLaunch& A, dim3 grid, hipStream_t s) {
-    if (A.out == kOutSame) return launch_out<TIn, kOutSame>(A, grid, s);
-    if (A.out == kOutF32) return launch_out<TIn, kOutF32>(A, grid, s);
-    return launch_out<TIn, kOutNorm>(A, grid, s);
+hipError_t launch_t(const LanczosLaunch& A, const LzGrid& g, hipStream_t s) {
+    if (A.out == kOutSame) return launch_out<TIn, kOutSame>(A, g, s);
+    if (A.out == kOutF32) return launch_out<TIn, kOutF32>(A, g, s);
+    return launch_out<TIn, kOutNorm>(A, g, s);
 }
 
 }  // namespace
 
 int launch_resize_lanczos(const ResizeLaunch& R, double inv_x, double inv_y, hipStream_t s) {
     if (R.src.cc > 4) return VACV_ERR_UNSUPPORTED;
-    if (R.dst.h > 65535 || (int64_t)R.n * R.src.planes > 65535) return VACV_ERR_UNSUPPORTED;
     LanczosLaunch A{};
     A.src = R.src;
     A.dst = R.dst;
@@ -260,8 +454,20 @@ int launch_resize_lanczos(const ResizeLaunch& R, double inv_x, double inv_y, hip
     A.norm = R.norm;
     const int st = lanczos_tables(R, inv_x, inv_y, s, A.t);
     if (st) return st;
-    const dim3 grid((R.dst.w * R.src.cc + kBlock - 1) / kBlock, R.dst.h, R.n * R.src.planes);
-    const hipError_t e = R.src.esize == 1 ? launch_t<uint8_t>(A, grid, s) : launch_t<float>(A, grid, s);
+    // wave tasks: 64-column strips x bands of output rows x planes; bands
+    // shrink until there are ~16K tasks (a band's first row resizes all 8 of
+    // its source rows, later rows only the new ones)
+    LzGrid g;
+    const int64_t planes = (int64_t)R.n * R.src.planes;
+    g.strips = (R.dst.w + 63) / 64;
+    const int64_t want = (16384 + g.strips * planes - 1) / (g.strips * planes);
+    g.bands = (int)std::max<int64_t>(1, std::min<int64_t>(want, (R.dst.h + 15) / 16));
+    g.band_rows = (R.dst.h + g.bands - 1) / g.bands;
+    g.bands = (R.dst.h + g.band_rows - 1) / g.band_rows;
+    const int64_t tasks = (int64_t)g.strips * g.bands * planes;
+    if ((tasks + 3) / 4 > 0x7FFFFFF0LL) return VACV_ERR_UNSUPPORTED;
+    g.blocks = (int)((tasks + 3) / 4);
+    const hipError_t e = R.src.esize == 1 ? launch_t<uint8_t>(A, g, s) : launch_t<float>(A, g, s);
     return e == hipSuccess ? VACV_OK : VACV_ERR_HIP;
 }
 

@@ -305,80 +305,6 @@ __global__ void __launch_bounds__(kBlock) color_kernel(ColorLaunch L) {
     }  // row pairs
 }
 
-// --------------------------------------------------------------------------
-// YUV420sp -> BGR with an fp32 output (+ normalize), the BASELINE cfg3 path.
-// Output-stationary: one thread = one 16-byte output chunk (4 consecutive
-// elements of a row), chunks numbered in address order over the batch, so
-// every wave stores 1 KiB contiguously (non-temporal) and the grid sweeps
-// HBM in order.  The chunk's (at most two) pixels read their Y and chroma
-// bytes from the L1/L2-resident input rows; each input byte leaves HBM once.
-template <int OUT>
-__global__ void __launch_bounds__(kBlock) color_f32_kernel(ColorLaunch L, uint32_t cpo) {
-    const uint32_t g = blockIdx.x * kBlock + threadIdx.x;
-    const uint32_t r = g / cpo;  // image * h + y
-    if (r >= (uint32_t)L.n * L.h) return;
-    const int e0 = (int)(g - r * cpo) * 4;
-    const int img = (int)(r / L.h);
-    const int y = (int)r - img * L.h;
-    const int rl = 3 * L.w;
-
-    const unsigned char* yrow = L.src + (int64_t)img * L.src_img + (int64_t)y * L.src_row;
-    const unsigned char* uvrow = L.src + (int64_t)img * L.src_img + (int64_t)(L.h + (y >> 1)) * L.src_row;
-    const int p0 = e0 / 3;
-    const int p1 = min((e0 + 3) / 3, L.w - 1);
-    int bgr[2][3];
-#pragma unroll
-    for (int q = 0; q < 2; ++q) {
-        const int px = q ? p1 : p0;
-        const int pair = px & ~1;
-        const int Y = yrow[px];
-        const int a = uvrow[pair], b = uvrow[pair + 1];
-        const Chroma ch = chroma_terms(L.v_first ? b : a, L.v_first ? a : b);  // (u, v)
-        const int R = clamp_u8(Y + ch.ra), G = clamp_u8(Y - ch.ga), B = clamp_u8(Y + ch.ba);
-        bgr[q][0] = L.rgb ? R : B;
-        bgr[q][1] = G;
-        bgr[q][2] = L.rgb ? B : R;
-    }
-    float m[3] = {0.f, 0.f, 0.f}, sd[3] = {1.f, 1.f, 1.f};
-    if (OUT == kOutNorm) {
-#pragma unroll
-        for (int k = 0; k < 3; ++k) norm_params(L.norm, img, k, m[k], sd[k]);
-    }
-    float o[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        const int e = min(e0 + i, rl - 1);
-        const int px = e / 3;
-        const int k = e - px * 3;
-        const int q = px != p0;
-        const int v = q ? (k == 0 ? bgr[1][0] : (k == 1 ? bgr[1][1] : bgr[1][2]))
-                        : (k == 0 ? bgr[0][0] : (k == 1 ? bgr[0][1] : bgr[0][2]));
-        if (OUT == kOutNorm) {
-            const float mk = k == 0 ? m[0] : (k == 1 ? m[1] : m[2]);
-            const double d = (double)((float)v - mk);
-            if (L.norm.mode == 1 && ((L.norm.mul_ok >> k) & 1u)) {
-                // host-verified exact for every u8 value (NormSpec.mul_ok)
-                o[i] = (float)(d * (k == 0 ? L.norm.inv[0] : (k == 1 ? L.norm.inv[1] : L.norm.inv[2])));
-            } else {
-                const float sk = k == 0 ? sd[0] : (k == 1 ? sd[1] : sd[2]);
-                o[i] = (float)(d / ((double)sk + 1e-6));  // normalize_naive.cpp:84-87
-            }
-        } else {
-            o[i] = (float)v;
-        }
-    }
-    unsigned char* drow = L.dst + (int64_t)img * L.dst_img + (int64_t)y * L.dst_row;
-    float* dp = reinterpret_cast<float*>(drow) + e0;
-    if (e0 + 4 <= rl && (reinterpret_cast<uintptr_t>(dp) & 15) == 0) {
-        __builtin_nontemporal_store(u32x4{__float_as_uint(o[0]), __float_as_uint(o[1]), __float_as_uint(o[2]),
-                                          __float_as_uint(o[3])},
-                                    reinterpret_cast<u32x4*>(dp));
-    } else {
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-            if (e0 + i < rl) dp[i] = o[i];
-    }
-}
 
 // --------------------------------------------------------------------------
 // normalize (normalize_naive.cpp:74-90) over rows of (w * cc) elements.
@@ -1366,14 +1292,6 @@ hipError_t launch_dtype(const DtypeLaunch& L, hipStream_t s) {
 }
 
 hipError_t launch_color(const ColorLaunch& L, hipStream_t s) {
-    const uint32_t cpo = (uint32_t)((3LL * L.w + 3) / 4);
-    const uint64_t chunks = (uint64_t)cpo * L.n * L.h;
-    if (L.out != kOutSame && chunks < (1ull << 32) - kBlock && tune(VACV_TUNE_COLOR_CHUNKS) == 1) {  // opt-in: measured slower (VALU-bound)
-        const uint32_t blocks = (uint32_t)((chunks + kBlock - 1) / kBlock);
-        if (L.out == kOutF32) hipLaunchKernelGGL(color_f32_kernel<kOutF32>, dim3(blocks), dim3(kBlock), 0, s, L, cpo);
-        else hipLaunchKernelGGL(color_f32_kernel<kOutNorm>, dim3(blocks), dim3(kBlock), 0, s, L, cpo);
-        return hipGetLastError();
-    }
     dim3 block(64, 4);
     dim3 grid((L.w / 4 + 64) / 64, (L.h / 2 + 4 * kColorPairs - 1) / (4 * kColorPairs), L.n);
     if (L.out == kOutSame) hipLaunchKernelGGL(color_kernel<kOutSame>, grid, block, 0, s, L);

@@ -34,6 +34,22 @@ namespace {
 
 constexpr int kGroupPx = 256;  // pixels per LDS exchange round (4 per lane)
 
+// Diagnosis builds (make EXTRA=-DVACV_DIRECT_DBG=n LIB=... OBJ=...;
+// tools/kbench_lib.py), results wrong: bit 0 no normalisation (the u8 value
+// converted), bit 1 no blend either (the tap bytes stored as they are),
+// bit 2 no output stores.
+#ifndef VACV_DIRECT_DBG
+#define VACV_DIRECT_DBG 0
+#endif
+// cache policy of the fp32-output stores and tap gathers (aux bits:
+// 1 sc0, 2 nt, 16 sc1)
+#ifndef VACV_DIRECT_SAUX
+#define VACV_DIRECT_SAUX VACV_STORE_AUX
+#endif
+#ifndef VACV_DIRECT_LAUX
+#define VACV_DIRECT_LAUX 0
+#endif
+
 // Pixels per lane: 8 when one tap row is gathered and the kernel still fits
 // 64 VGPRs (8 waves per SIMD) at 8, else 4 (measured: spills otherwise).
 constexpr int direct_pxl(int cc, int out, bool one_row) {
@@ -53,7 +69,8 @@ resize_direct_kernel(ResizeLaunch L, int blocks_per_plane, int total, int xcd) {
     // source line split between two waves is re-read from L2, not HBM
     // (headline 0.2206 -> 0.2180 ms; sc0 0.2185); non-temporal under byte
     // output, where the default policy measured slower (0.1232 -> 0.1267 ms)
-    constexpr int kLoadAux = OUT == kOutSame ? VACV_LOAD_AUX : 0;
+    constexpr int kLoadAux = OUT == kOutSame ? VACV_LOAD_AUX : VACV_DIRECT_LAUX;
+    constexpr int kStoreAux = OUT == kOutSame ? VACV_STORE_AUX : VACV_DIRECT_SAUX;
     __shared__ __attribute__((aligned(16))) unsigned char xch[4][kGroupPx * kOutPx];
 
     // xcd: workgroup b runs on XCD b % 8; give each XCD one contiguous eighth
@@ -161,9 +178,9 @@ resize_direct_kernel(ResizeLaunch L, int blocks_per_plane, int total, int xcd) {
                 const uint32_t sel = (uint32_t)k | (0x0Cu << 8) | ((uint32_t)(CC + k) << 16) | (0x0Cu << 24);
                 const uint32_t top = __builtin_amdgcn_perm(tap[q][0][1], tap[q][0][0], sel);
                 const uint32_t bot = ONE_ROW ? 0u : __builtin_amdgcn_perm(tap[q][NR - 1][1], tap[q][NR - 1][0], sel);
-                const int v = blend_fixed<MODE>(top, bot, wx, wA, wB);
+                const int v = (VACV_DIRECT_DBG & 2) ? (int)top : blend_fixed<MODE>(top, bot, wx, wA, wB);
                 if (OUT == kOutSame) o[k] = (TOut)v;
-                else if (OUT == kOutF32) o[k] = (TOut)(float)v;
+                else if (OUT == kOutF32 || (VACV_DIRECT_DBG & 3)) o[k] = (TOut)(float)v;
                 else o[k] = (TOut)normalize_u8v(cn[k], v);
             }
         }
@@ -174,7 +191,7 @@ resize_direct_kernel(ResizeLaunch L, int blocks_per_plane, int total, int xcd) {
         // ---- LDS -> HBM: dense byte b of the plane's output lives at row
         // b / out_row, column byte b % out_row ---------------------------------
         const int gp = npx - g * kGroupPx;  // valid pixels of this round (uniform)
-        if (gp > 0) {
+        if (gp > 0 && !(VACV_DIRECT_DBG & 4)) {
             // 32-bit offsets: the plane is < 2^31 bytes (kMaxPlaneBytes)
             const uint32_t vbytes = (uint32_t)(min(gp, kGroupPx) * kOutPx);
             const uint32_t b0 = (uint32_t)(p0 + g * kGroupPx) * kOutPx;  // 16-byte aligned (256 | p0)
@@ -187,7 +204,8 @@ resize_direct_kernel(ResizeLaunch L, int blocks_per_plane, int total, int xcd) {
                         off = r * rowp + (b - r * out_row);
                     }
                     if (c * 16 + 16 <= vbytes) {
-                        store16(rd, off + rd.delta, *reinterpret_cast<const uint4*>(xs + 16 * c));
+                        const u32x4 v = *reinterpret_cast<const u32x4*>(xs + 16 * c);
+                        __builtin_amdgcn_raw_buffer_store_b128(v, rd.r, (int)(off + rd.delta), 0, kStoreAux);
                     } else {
                         for (uint32_t e = c * 16; e < vbytes; ++e) dp[off + (e - c * 16)] = xs[e];
                     }

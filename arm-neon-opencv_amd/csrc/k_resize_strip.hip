@@ -44,6 +44,10 @@ constexpr int kMaxLds = 64 * 1024;
 #ifndef VACV_STRIP_AUX
 #define VACV_STRIP_AUX 0
 #endif
+// cache policy of the output stores (A/B builds: EXTRA=-DVACV_STRIP_SAUX=n)
+#ifndef VACV_STRIP_SAUX
+#define VACV_STRIP_SAUX VACV_STORE_AUX
+#endif
 
 // one output pixel (lane-quad packed for u8) at row byte offset row_off
 template <int CC, int OUT>
@@ -57,12 +61,12 @@ __device__ __forceinline__ void store_pixel(const int (&v)[CC], const ChanNorm (
         if (quad_full) {
             if ((lane & 3) < CC)
                 __builtin_amdgcn_raw_buffer_store_b32(word, drs.r, (int)(row_off + (uint32_t)(qx * CC + 4 * (lane & 3))), 0,
-                                                      VACV_STORE_AUX);
+                                                      VACV_STRIP_SAUX);
         } else if (ox < W) {
 #pragma unroll
             for (int k = 0; k < CC; ++k)
                 __builtin_amdgcn_raw_buffer_store_b8((unsigned char)v[k], drs.r, (int)(row_off + (uint32_t)(ox * CC + k)), 0,
-                                                     VACV_STORE_AUX);
+                                                     VACV_STRIP_SAUX);
         }
     } else if (ox < W) {
         uint32_t f[CC];
@@ -71,15 +75,15 @@ __device__ __forceinline__ void store_pixel(const int (&v)[CC], const ChanNorm (
             f[k] = __builtin_bit_cast(uint32_t, OUT == kOutF32 ? (float)v[k] : normalize_u8v(cn[k], v[k]));
         const int off = (int)(row_off + (uint32_t)(ox * CC * 4));
         if constexpr (CC == 1) {
-            __builtin_amdgcn_raw_buffer_store_b32(f[0], drs.r, off, 0, VACV_STORE_AUX);
+            __builtin_amdgcn_raw_buffer_store_b32(f[0], drs.r, off, 0, VACV_STRIP_SAUX);
         } else if constexpr (CC == 2) {
             typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
-            __builtin_amdgcn_raw_buffer_store_b64(u32x2{f[0], f[1]}, drs.r, off, 0, VACV_STORE_AUX);
+            __builtin_amdgcn_raw_buffer_store_b64(u32x2{f[0], f[1]}, drs.r, off, 0, VACV_STRIP_SAUX);
         } else if constexpr (CC == 3) {
             typedef unsigned int u32x3 __attribute__((ext_vector_type(3)));
-            __builtin_amdgcn_raw_buffer_store_b96(u32x3{f[0], f[1], f[2]}, drs.r, off, 0, VACV_STORE_AUX);
+            __builtin_amdgcn_raw_buffer_store_b96(u32x3{f[0], f[1], f[2]}, drs.r, off, 0, VACV_STRIP_SAUX);
         } else {
-            __builtin_amdgcn_raw_buffer_store_b128(u32x4{f[0], f[1], f[2], f[3]}, drs.r, off, 0, VACV_STORE_AUX);
+            __builtin_amdgcn_raw_buffer_store_b128(u32x4{f[0], f[1], f[2], f[3]}, drs.r, off, 0, VACV_STRIP_SAUX);
         }
     }
 }

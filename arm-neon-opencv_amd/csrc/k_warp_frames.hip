@@ -106,6 +106,10 @@ constexpr int kRingMaxIt = 6;  // DMA instructions per wave and frame, at most (
 // ns, slot: LDS slots and their bytes; dst_al: the destination allows dword
 // (u8 out) stores; ginv = ceil(2^20 / (S / 16)) (row of chunk c = c ginv >> 20,
 // exact for c < 4096 and S / 16 <= 256).
+// cache policy of the ring kernel's output stores (A/B builds: EXTRA=-DVACV_RING_SAUX=n)
+#ifndef VACV_RING_SAUX
+#define VACV_RING_SAUX VACV_STORE_AUX
+#endif
 #ifndef VACV_RING_WPE
 #define VACV_RING_WPE 1
 #endif
@@ -344,8 +348,12 @@ warp_ring_kernel(WarpLaunch L, int gx, int gy, int kf, int S, int rows_max, int 
     const bool tile_full = bx * kFrTileW + kFrTileW <= L.dst.w && by * TH + TH <= L.dst.h &&
                            (OUT != kOutSame || dst_al);
     constexpr uint32_t kOob = 0x80000000u;
-    // vector-memory stores per sampled frame, every one issued (the wait count)
-    const int n_st = (VACV_RING_DBG & 1) ? 0 : OUT != kOutSame ? NP : (tile_full ? NP / 2 : NP * CC);
+    // vector-memory stores per sampled frame, every one issued (the wait
+    // count).  Full tiles issue only 16-byte (u8) or one-per-row fp32 stores
+    // at per-row addresses, which the compiler cannot merge, so the count is
+    // exact; edge tiles count 0, i.e. their wait also drains the previous
+    // frame's byte stores (conservative: ~9 % of cfg4's tiles).
+    const int n_st = (VACV_RING_DBG & 1) || !tile_full ? 0 : OUT != kOutSame ? NP : NP / 2;
 
     auto emit = [&](auto full_c, int fv, int j, uint32_t tlo, uint32_t thi, uint32_t blo, uint32_t bhi) {
         constexpr bool FULL = decltype(full_c)::value;
@@ -396,14 +404,14 @@ warp_ring_kernel(WarpLaunch L, int gx, int gy, int kf, int S, int rows_max, int 
                     const uint32_t off = lane < 2 * kChunks
                                              ? rowoff + (uint32_t)(bx * kFrTileW * CC + 16 * (m % kChunks))
                                              : kOob;
-                    __builtin_amdgcn_raw_buffer_store_b128(v, drs.r, (int)off, 0, VACV_STORE_AUX);
+                    __builtin_amdgcn_raw_buffer_store_b128(v, drs.r, (int)off, 0, VACV_RING_SAUX);
                 }
             } else {  // the edges, or a byte-aligned destination: CC byte stores, all issued
                 const uint32_t off = inside ? drow + (uint32_t)(x * CC) : kOob;
 #pragma unroll
                 for (int k = 0; k < CC; ++k)
                     __builtin_amdgcn_raw_buffer_store_b8((unsigned char)(own >> (8 * k)), drs.r,
-                                                         (int)(inside ? off + k : kOob), 0, VACV_STORE_AUX);
+                                                         (int)(inside ? off + k : kOob), 0, VACV_RING_SAUX);
             }
         } else {
             u32x4 o;
@@ -422,16 +430,16 @@ warp_ring_kernel(WarpLaunch L, int gx, int gy, int kf, int S, int rows_max, int 
             }
             const int off = (int)(inside ? drow + (uint32_t)(x * CC * 4) : kOob);
             if constexpr (CC == 1) {
-                __builtin_amdgcn_raw_buffer_store_b32(o[0], drs.r, off, 0, VACV_STORE_AUX);
+                __builtin_amdgcn_raw_buffer_store_b32(o[0], drs.r, off, 0, VACV_RING_SAUX);
             } else if constexpr (CC == 2) {
                 typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
-                __builtin_amdgcn_raw_buffer_store_b64(u32x2{o[0], o[1]}, drs.r, off, 0, VACV_STORE_AUX);
+                __builtin_amdgcn_raw_buffer_store_b64(u32x2{o[0], o[1]}, drs.r, off, 0, VACV_RING_SAUX);
             } else if constexpr (CC == 3) {
                 typedef unsigned int u32x3 __attribute__((ext_vector_type(3)));
                 const u32x3 o3 = {o[0], o[1], o[2]};
-                __builtin_amdgcn_raw_buffer_store_b96(o3, drs.r, off, 0, VACV_STORE_AUX);
+                __builtin_amdgcn_raw_buffer_store_b96(o3, drs.r, off, 0, VACV_RING_SAUX);
             } else {
-                __builtin_amdgcn_raw_buffer_store_b128(o, drs.r, off, 0, VACV_STORE_AUX);
+                __builtin_amdgcn_raw_buffer_store_b128(o, drs.r, off, 0, VACV_RING_SAUX);
             }
         }
     };
@@ -465,7 +473,7 @@ warp_ring_kernel(WarpLaunch L, int gx, int gy, int kf, int S, int rows_max, int 
                         const uint32_t off = lane < 2 * kChunks
                                                  ? rowoff + (uint32_t)(bx * kFrTileW * CC + 16 * (m % kChunks))
                                                  : kOob;
-                        __builtin_amdgcn_raw_buffer_store_b128(v, drs.r, (int)off, 0, VACV_STORE_AUX);
+                        __builtin_amdgcn_raw_buffer_store_b128(v, drs.r, (int)off, 0, VACV_RING_SAUX);
                     }
                 }
                 return;
@@ -551,7 +559,10 @@ warp_ring_kernel(WarpLaunch L, int gx, int gy, int kf, int S, int rows_max, int 
         // flight are the DMAs of frames f + 1 .. f + ns - 2 and the stores of
         // the (at most ns - 1) frames sampled since frame f's DMA was issued
         wait_vm((ns - 2) * n_w + min(f - f0, ns - 1) * n_st);
-        if (tailm) fix_tail(f, s);
+        if (tailm) {
+            fix_tail(f, s);
+            wait_lgkm();  // its LDS stores land before the barrier (s_barrier does not wait for them)
+        }
         __builtin_amdgcn_s_barrier();  // every wave's part of frame f is in; frame f - 1's reads are done
         const int sn = s == 0 ? ns - 1 : s - 1;  // (f + ns - 1) mod ns: the slot frame f - 1 used
         dma(f + ns - 1, sn, f + ns - 1 < f1);

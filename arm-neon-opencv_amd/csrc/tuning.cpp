@@ -19,18 +19,15 @@ const char* const kNames[VACV_TUNE_COUNT] = {
     "VACV_RESIZE_DIRECT",      // VACV_TUNE_RESIZE_DIRECT
     "VACV_CUBIC_DIRECT",       // VACV_TUNE_CUBIC_DIRECT
     "VACV_RESIZE_INTERLEAVE",  // VACV_TUNE_RESIZE_INTERLEAVE
-    "VACV_RESIZE_ROWS",        // VACV_TUNE_RESIZE_ROWS (retired)
     "VACV_DIRECT_XCD",         // VACV_TUNE_DIRECT_XCD
     "VACV_WARP_PX",            // VACV_TUNE_WARP_PX
     "VACV_NEAREST_KERNEL",     // VACV_TUNE_NEAREST_KERNEL
     "VACV_AREA_KERNEL",        // VACV_TUNE_AREA_KERNEL
     "VACV_AREA_ROWS",          // VACV_TUNE_AREA_ROWS
-    "VACV_COLOR_CHUNKS",       // VACV_TUNE_COLOR_CHUNKS
     "VACV_RESIZE_WGS",         // VACV_TUNE_RESIZE_WGS
     "VACV_RESIZE_TILE_H",      // VACV_TUNE_RESIZE_TILE_H
     "VACV_RESIZE_TILE_W",      // VACV_TUNE_RESIZE_TILE_W
     "VACV_RESIZE_WORK",        // VACV_TUNE_RESIZE_WORK
-    "VACV_RESIZE_ROWS_BYTES",  // VACV_TUNE_RESIZE_ROWS_BYTES (retired)
     "VACV_WARP_KERNEL",        // VACV_TUNE_WARP_KERNEL
     "VACV_RESIZE_STRIP",       // VACV_TUNE_RESIZE_STRIP
     "VACV_MATCH_KERNEL",       // VACV_TUNE_MATCH_KERNEL

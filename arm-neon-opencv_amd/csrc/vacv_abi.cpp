@@ -201,16 +201,24 @@ int norm_spec(const Img& shape, const float* mean, const float* stdv, NormSpec& 
     if (shape.c > kMaxC) return VACV_ERR_UNSUPPORTED;
     ns.mode = 1;
     ns.mul_ok = 0;
+    ns.f32_ok = 0;
     for (int k = 0; k < shape.c; ++k) {
         ns.mean[k] = mean[k];
         ns.stdv[k] = stdv[k];
         ns.inv[k] = 1.0 / ((double)stdv[k] + 1e-6);
-        bool ok = true;
-        for (int v = 0; v < 256 && ok; ++v) {
+        ns.inv_hi[k] = (float)ns.inv[k];
+        ns.inv_lo[k] = (float)(ns.inv[k] - (double)ns.inv_hi[k]);
+        bool ok = true, ok32 = true;
+        for (int v = 0; v < 256; ++v) {
             const float d = (float)v - mean[k];
-            ok = (float)((double)d * ns.inv[k]) == normalize_value((float)v, mean[k], stdv[k]);
+            const float want = normalize_value((float)v, mean[k], stdv[k]);
+            ok = ok && (float)((double)d * ns.inv[k]) == want;
+            const float lo = d * ns.inv_lo[k];  // -ffp-contract=off: rounded, then the fma
+            const float got = std::fma(d, ns.inv_hi[k], lo);
+            ok32 = ok32 && std::memcmp(&got, &want, sizeof(float)) == 0;
         }
         if (ok) ns.mul_ok |= 1u << k;
+        if (ok32) ns.f32_ok |= 1u << k;
     }
     return VACV_OK;
 }
@@ -228,14 +236,16 @@ int normalize_with(const Img& src, const Img& dst, const NormSpec& ns, hipStream
 
 // fx / fy > 0: cv::resize's inv_scale (the reference passes them through to
 // OpenCV for NEAREST / AREA, resize.cpp:35); 0: dsize / ssize
-// FusedSums: the cubic gather kernel's per-wave statistics epilogue
-// (vacv_resize_channel_sums); `used` tells whether that kernel ran with it.
+// FusedSums: the cubic gather kernel's per-workgroup statistics epilogue
+// (vacv_resize_channel_sums / vacv_resize_mean_stddev); `used` tells whether
+// that kernel ran with it.
 struct FusedSums {
-    double* partials;            // [cc][2][n][waves] + [cc][2][16] split sums, sized by the caller
+    double* partials;            // [cc][2][n][workgroups], sized by the caller
     double* sums;                // [n][cc][2] (per_image) or [cc][2]
     int per_image;
-    int* count;                  // >= 2 cc zeroed ints (the batch sum's counters)
-    int waves;                   // out: waves per plane
+    float* mean;                 // [n][cc] or [cc], or null
+    float* stddev;
+    int groups;                  // out: workgroups per plane
     bool used;                   // out
 };
 
@@ -357,8 +367,9 @@ int resize_impl(const vacv_image* src_d, const vacv_image* dst_d, int interpolat
             L.sum_partials = fs->partials;
             L.sum_out = fs->sums;
             L.sum_per_image = fs->per_image;
-            L.sum_count = fs->count;
-            fs->waves = cubic_direct_waves(L);
+            L.sum_mean = fs->mean;
+            L.sum_std = fs->stddev;
+            fs->groups = cubic_direct_groups(L);
             fs->used = true;
         }
         return hip_status(launch_cubic_direct(L, s));
@@ -879,36 +890,49 @@ int vacv_channel_sums(const vacv_image* src_d, double* sums, int per_image, void
     return channel_sums_into(src, sums, per_image ? 1 : 0, static_cast<double*>(ws), blocks, s);
 }
 
-int vacv_resize_channel_sums(const vacv_image* src_d, const vacv_image* dst_d, int interpolation, int mode,
-                             double* sums, int per_image, void* stream) {
+namespace {
+// vacv_resize_channel_sums with optional statistics: u8 -> fp32 cubic into a
+// dense NHWC output (cfg5) takes the gather kernel's per-workgroup sums
+// epilogue and one fixed-order reduction launch that also derives mean /
+// stddev -- the output is not read back (a separate vacv_channel_sums pass
+// re-read 77 MB per cfg5 batch).  Everything else: resize, then
+// vacv_channel_sums (and vacv_stats_from_sums).
+int resize_sums(const vacv_image* src_d, const vacv_image* dst_d, int interpolation, int mode, double* sums,
+                int per_image, float* mean, float* stddev, void* stream) {
     if (!sums) return VACV_ERR_INVALID_ARG;
     hipStream_t s = (hipStream_t)stream;
     Img src, dst;
     int st = load(src_d, src);
     if (st) return st;
     if ((st = load(dst_d, dst))) return st;
-    // u8 -> fp32 cubic into a dense NHWC output (cfg5): the gather kernel's
-    // per-wave sums epilogue, then only the fixed-order reduction -- the output
-    // is not read back (a separate vacv_channel_sums pass re-read 77 MB per
-    // cfg5 batch).  Everything else: resize, then vacv_channel_sums.
     if (interpolation == VACV_INTER_CUBIC && src.dtype == VACV_INT8 && dst.dtype == VACV_FP32 &&
         dst.layout == VACV_NHWC && dst.c <= 3 && dense(dst) && src.n == dst.n) {
         const int64_t P = (int64_t)dst.w * dst.h;
-        const int64_t waves = (P + 511) / 512 * 4;  // cubic_direct_waves() for this size
+        const int64_t groups = (P + 511) / 512;  // cubic_direct_groups() for this size
         void* ws = nullptr;
-        // the per-wave partials [c][2][n][waves], then 2 c x 16 split sums
-        if ((st = workspace(s, (size_t)(dst.n * waves * 2 * dst.c + 2 * dst.c * 16) * sizeof(double), &ws))) return st;
-        // the batch sum's second level: 2c ints of counters, left zeroed by
-        // every launch (k_cubic_direct.hip)
-        void* cnt = nullptr;
-        if ((st = workspace(s, 64 * sizeof(int), &cnt, 2, true))) return st;
-        FusedSums fs{static_cast<double*>(ws), sums, per_image ? 1 : 0, static_cast<int*>(cnt), 0, false};
+        if ((st = workspace(s, (size_t)(dst.n * groups * 2 * dst.c) * sizeof(double), &ws))) return st;
+        FusedSums fs{static_cast<double*>(ws), sums, per_image ? 1 : 0, mean, stddev, 0, false};
         if ((st = resize_impl(src_d, dst_d, interpolation, mode, kOutSame, nullptr, s, 0.0, 0.0, &fs))) return st;
-        if (fs.used) return fs.waves == waves ? VACV_OK : VACV_ERR_HIP;  // (a layout mismatch cannot happen)
-        return vacv_channel_sums(dst_d, sums, per_image, stream);
+        if (fs.used) return fs.groups == groups ? VACV_OK : VACV_ERR_HIP;  // (a layout mismatch cannot happen)
+    } else if ((st = resize_impl(src_d, dst_d, interpolation, mode, kOutSame, nullptr, s))) {
+        return st;
     }
-    if ((st = resize_impl(src_d, dst_d, interpolation, mode, kOutSame, nullptr, s))) return st;
-    return vacv_channel_sums(dst_d, sums, per_image, stream);
+    if ((st = vacv_channel_sums(dst_d, sums, per_image, stream))) return st;
+    if (!mean) return VACV_OK;
+    const double count = (double)dst.w * dst.h * (per_image ? 1 : dst.n);
+    return hip_status(launch_stats(sums, per_image ? dst.n : 1, dst.c, count, mean, stddev, s));
+}
+}  // namespace
+
+int vacv_resize_channel_sums(const vacv_image* src_d, const vacv_image* dst_d, int interpolation, int mode,
+                             double* sums, int per_image, void* stream) {
+    return resize_sums(src_d, dst_d, interpolation, mode, sums, per_image, nullptr, nullptr, stream);
+}
+
+int vacv_resize_mean_stddev(const vacv_image* src_d, const vacv_image* dst_d, int interpolation, int mode,
+                            double* sums, float* mean, float* stddev, int per_image, void* stream) {
+    if (!mean || !stddev) return VACV_ERR_INVALID_ARG;
+    return resize_sums(src_d, dst_d, interpolation, mode, sums, per_image, mean, stddev, stream);
 }
 
 int vacv_stats_from_sums(const double* sums, int groups, int c, double count, float* mean, float* stddev,

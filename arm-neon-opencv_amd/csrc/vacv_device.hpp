@@ -23,6 +23,9 @@ typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 #ifndef VACV_STORE_AUX
 #define VACV_STORE_AUX 2
 #endif
+#ifndef VACV_NO_F32_NORM
+#define VACV_NO_F32_NORM 0
+#endif
 
 // A raw buffer resource over [base16, base16 + bytes): loads past the end
 // return zeros instead of faulting, so a 16-byte staging load may overhang
@@ -106,20 +109,30 @@ __device__ __forceinline__ void norm_params(const NormSpec& ns, int img, int ch,
 struct ChanNorm {
     float mean, stdv;
     double inv;
-    bool mul;  // host-verified multiply is exact for u8-valued inputs
+    float hi, lo;
+    bool mul;  // host-verified fp64 multiply is exact for u8-valued inputs
+    bool f32;  // host-verified fp32 two-term multiply is exact (NormSpec.f32_ok)
 };
 
 __device__ __forceinline__ ChanNorm chan_norm(const NormSpec& ns, int img, int ch) {
     ChanNorm c;
     norm_params(ns, img, ch, c.mean, c.stdv);
     c.mul = ns.mode == 1 && ((ns.mul_ok >> ch) & 1u);
+    c.f32 = ns.mode == 1 && ((ns.f32_ok >> ch) & 1u);
     c.inv = c.mul ? ns.inv[ch] : 0.0;
+    c.hi = c.f32 ? ns.inv_hi[ch] : 0.f;
+    c.lo = c.f32 ? ns.inv_lo[ch] : 0.f;
     return c;
 }
 
-// normalize_naive.cpp:74-90 for a value known to be an integer in [0,255]
+// normalize_naive.cpp:74-90 for a value known to be an integer in [0,255]:
+// the host proved one of the two short forms equal to the reference's
+// (float)((double)d / ((double)std + 1e-6)) for all 256 values (norm_spec)
 __device__ __forceinline__ float normalize_u8v(const ChanNorm& c, int v) {
     const float d = (float)v - c.mean;
+#if !VACV_NO_F32_NORM
+    if (c.f32) return __builtin_fmaf(d, c.hi, d * c.lo);
+#endif
     if (c.mul) return (float)((double)d * c.inv);
     return (float)((double)d / ((double)c.stdv + 1e-6));
 }

@@ -52,6 +52,14 @@ struct NormSpec {
     // u8-valued inputs (an fp64 divide is ~10x the issue cost).
     double inv[kMaxC];
     uint32_t mul_ok;
+    // Bit k of f32_ok: the host verified, for all 256 u8 values v, that the
+    // fp32 form fmaf(d, inv_hi[k], d * inv_lo[k]) (d = (float)v - mean[k];
+    // inv_hi + inv_lo = inv[k] to ~48 bits) equals the reference's result;
+    // kernels then take it instead of the fp64 multiply (2 fp32 VALU
+    // instead of 3 fp64 ones).
+    float inv_hi[kMaxC];
+    float inv_lo[kMaxC];
+    uint32_t f32_ok;
 };
 
 enum SampleKind : int {
@@ -107,13 +115,15 @@ struct ResizeLaunch {
     ResizePlanDev plan;
     NormSpec norm;
     // cubic gather kernel only (or null): the output's per-channel
-    // (Sum x, Sum x^2) -- per-wave partials [cc][2][image][wave]
-    // (cubic_direct_waves() waves, a workspace), then sum_out = [n][cc][2]
-    // (sum_per_image) or [cc][2] in a fixed order
+    // (Sum x, Sum x^2) -- per-workgroup partials [cc][2][image][workgroup]
+    // (cubic_direct_groups() per image, a workspace), then sum_out =
+    // [n][cc][2] (sum_per_image) or [cc][2] in a fixed order; with sum_mean /
+    // sum_std (or null) also the population mean / stddev of each group
     double* sum_partials;
     double* sum_out;
     int sum_per_image;
-    int* sum_count;              // 2 cc zeroed ints, left zeroed (the batch sum)
+    float* sum_mean;
+    float* sum_std;
 };
 
 // Fills tiles, strips and the cached device plan of L (host).
@@ -165,7 +175,7 @@ int release_lanczos_tables();
 // u8 -> fp32 cubic as per-pixel gathers (k_cubic_direct.hip); needs no plan
 bool cubic_direct_applies(const ResizeLaunch& L);
 hipError_t launch_cubic_direct(const ResizeLaunch& L, hipStream_t s);
-int cubic_direct_waves(const ResizeLaunch& L);  // waves per output plane (the sum_partials layout)
+int cubic_direct_groups(const ResizeLaunch& L);  // workgroups per output plane (the sum_partials layout)
 
 struct WarpLaunch {
     PlaneGeom src;

@@ -82,6 +82,7 @@ SIGNATURES = {
     "vacv_channel_sums": ([_IMG, _P, _I, _P], _I),
     "vacv_stats_from_sums": ([_P, _I, _I, _D, _P, _P, _P], _I),
     "vacv_resize_channel_sums": ([_IMG, _IMG, _I, _I, _P, _I, _P], _I),
+    "vacv_resize_mean_stddev": ([_IMG, _IMG, _I, _I, _P, _P, _P, _I, _P], _I),
     "vacv_mean_stddev": ([_IMG, _P, _P, _P], _I),
     "vacv_resize_normalize": ([_IMG, _IMG, _I, _I, _FP, _FP, _P], _I),
     "vacv_warp_affine_normalize": ([_IMG, _IMG, _FP, _I, _I, _DP, _FP, _FP, _P], _I),
@@ -97,11 +98,10 @@ SIGNATURES = {
 }
 
 # kernel-variant knobs (VACV_TUNE_*, include/vacv_hip.h)
-TUNE = {"RESIZE_DIRECT": 0, "CUBIC_DIRECT": 1, "RESIZE_INTERLEAVE": 2, "RESIZE_ROWS": 3, "DIRECT_XCD": 4,
-        "WARP_PX": 5, "NEAREST_KERNEL": 6, "AREA_KERNEL": 7, "AREA_ROWS": 8, "COLOR_CHUNKS": 9,
-        "RESIZE_WGS": 10, "RESIZE_TILE_H": 11, "RESIZE_TILE_W": 12, "RESIZE_WORK": 13, "RESIZE_ROWS_BYTES": 14,
-        "WARP_KERNEL": 15, "RESIZE_STRIP": 16, "MATCH_KERNEL": 17,
-        "WARP_FRAMES": 18, "WARP_TILE_H": 19, "WARP_SLOTS": 20}
+TUNE = {"RESIZE_DIRECT": 0, "CUBIC_DIRECT": 1, "RESIZE_INTERLEAVE": 2, "DIRECT_XCD": 3, "WARP_PX": 4,
+        "NEAREST_KERNEL": 5, "AREA_KERNEL": 6, "AREA_ROWS": 7, "RESIZE_WGS": 8, "RESIZE_TILE_H": 9,
+        "RESIZE_TILE_W": 10, "RESIZE_WORK": 11, "WARP_KERNEL": 12, "RESIZE_STRIP": 13, "MATCH_KERNEL": 14,
+        "WARP_FRAMES": 15, "WARP_TILE_H": 16, "WARP_SLOTS": 17}
 
 _lib = None
 

@@ -248,19 +248,24 @@ def _yuv_desc(yuv: torch.Tensor) -> VacvImage:
 _DCN4 = (L.COLOR_YUV2RGBA_NV12, L.COLOR_YUV2BGRA_NV12, L.COLOR_YUV2RGBA_NV21, L.COLOR_YUV2BGRA_NV21)
 
 
-def cvt_color(yuv: torch.Tensor, code: int = L.COLOR_YUV2BGR_NV21, stream=None) -> torch.Tensor:
+def cvt_color(yuv: torch.Tensor, code: int = L.COLOR_YUV2BGR_NV21, out=None, stream=None) -> torch.Tensor:
     """va_cv::cvt_color (cv.h:95): (n, h*3/2, w) u8 -> (n, h, w, 3) u8 (4
     channels for the RGBA/BGRA codes; YV12 is Y then the V and U planes).
-    COLOR_GRAY2BGR: (n, h, w) u8/fp32 -> (n, h, w, 3) of the same dtype."""
+    COLOR_GRAY2BGR: (n, h, w) u8/fp32 -> (n, h, w, 3) of the same dtype.
+    `out` (optional): a preallocated output of that shape."""
     if code == L.COLOR_GRAY2BGR:
         g4 = yuv if yuv.dim() == 3 else yuv.unsqueeze(0)
-        out = torch.empty(tuple(g4.shape) + (3,), dtype=g4.dtype, device=yuv.device)
+        if out is None:
+            out = torch.empty(tuple(g4.shape) + (3,), dtype=g4.dtype, device=yuv.device)
+        out = out if out.dim() == 4 else out.unsqueeze(0)
         check("vacv_cvt_color", L.load().vacv_cvt_color(ctypes.byref(describe(g4.unsqueeze(-1), NHWC)),
                                                         ctypes.byref(describe(out, NHWC)), code, _stream(stream)))
         return out if yuv.dim() == 3 else out[0]
     y4 = yuv if yuv.dim() == 3 else yuv.unsqueeze(0)
     n, hh, w = y4.shape
-    out = torch.empty((n, hh // 3 * 2, w, 4 if code in _DCN4 else 3), dtype=torch.uint8, device=yuv.device)
+    if out is None:
+        out = torch.empty((n, hh // 3 * 2, w, 4 if code in _DCN4 else 3), dtype=torch.uint8, device=yuv.device)
+    out = out if out.dim() == 4 else out.unsqueeze(0)
     check("vacv_cvt_color", L.load().vacv_cvt_color(ctypes.byref(_yuv_desc(y4)), ctypes.byref(describe(out, NHWC)),
                                                     code, _stream(stream)))
     return out if yuv.dim() == 3 else out[0]
@@ -357,6 +362,30 @@ def resize_channel_sums(src: torch.Tensor, w: int, h: int, interpolation: int = 
           L.load().vacv_resize_channel_sums(ctypes.byref(describe(s4, layout)), ctypes.byref(describe(o4, layout)),
                                             interpolation, mode, sums.data_ptr(), int(per_image), _stream(stream)))
     return out, sums
+
+
+def resize_mean_stddev(src: torch.Tensor, w: int, h: int, interpolation: int = INTER_LINEAR,
+                       mode: int = LINEAR_REFERENCE, per_image: bool = True, layout: int = NHWC, out=None,
+                       stream=None) -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor, torch.Tensor]:
+    """resize() and the population mean / stddev of its output (per image, or
+    over the whole batch) in one call: the one-GPU form of cfg5 (resize, then
+    normalize_naive.cpp:7-48's mean_stddev).  Returns (resized, sums, mean,
+    stddev); sums is (groups, c, 2) fp64, mean / stddev (groups, c) fp32."""
+    s4 = _as4d(src, layout)
+    if out is None:
+        dt = torch.float32 if (interpolation == INTER_CUBIC or src.dtype == torch.float32) else src.dtype
+        out = _empty_like_shape(s4, layout, w, h, dt, False, src.dim())
+    o4 = _as4d(out, layout)
+    c = o4.shape[3] if layout == NHWC else o4.shape[1]
+    groups = o4.shape[0] if per_image else 1
+    sums = torch.empty((groups, c, 2), dtype=torch.float64, device=src.device)
+    mean = torch.empty((groups, c), dtype=torch.float32, device=src.device)
+    std = torch.empty((groups, c), dtype=torch.float32, device=src.device)
+    check("vacv_resize_mean_stddev",
+          L.load().vacv_resize_mean_stddev(ctypes.byref(describe(s4, layout)), ctypes.byref(describe(o4, layout)),
+                                           interpolation, mode, sums.data_ptr(), mean.data_ptr(), std.data_ptr(),
+                                           int(per_image), _stream(stream)))
+    return out, sums, mean, std
 
 
 def stats_from_sums(sums: torch.Tensor, count: float, stream=None) -> Tuple[torch.Tensor, torch.Tensor]:

@@ -241,6 +241,20 @@ def pmc_traffic(workload: str = "resize_normalize"):
         return None
 
 
+def global_sums(sums):
+    """All-reduce (SUM) of a rank's (groups, c, 2) fp64 channel sums over the
+    default process group: in place on the device under RCCL ("nccl"); gloo
+    reduces host tensors, so a device tensor goes through a host copy there."""
+    import torch.distributed as dist
+    if dist.get_backend() == "gloo" and sums.is_cuda:
+        host = sums.cpu()
+        dist.all_reduce(host, op=dist.ReduceOp.SUM)
+        sums.copy_(host)
+    else:
+        dist.all_reduce(sums, op=dist.ReduceOp.SUM)
+    return sums
+
+
 def make_workload(name: str, batch: int, dev, rank: int, world: int, ops) -> dict:
     """Inputs resident in HBM, the step's launches and the roofline terms of
     one BASELINE config.  b_alg = algorithmic bytes of the dominant kernel per
@@ -285,26 +299,32 @@ def make_workload(name: str, batch: int, dev, rank: int, world: int, ops) -> dic
         src = u8(B, 1440, 2560, 3)
         dst = torch.empty((B, 224, 224, 3), dtype=torch.float32, device=dev)
         stats = {}
+        count = float(B) * world * 224 * 224
 
-        def main(stream=None):
-            # the resize with the per-rank (Sum x, Sum x^2) fused into the
-            # cubic kernel (vacv_resize_channel_sums) and its fixed-order
-            # reduction
-            stats["sums"] = ops.resize_channel_sums(src, 224, 224, INTER_CUBIC, per_image=False, out=dst,
-                                                    stream=stream)[1]
+        if world == 1:
+            def main(stream=None):
+                # one GPU: the resize with the batch's (Sum x, Sum x^2) fused
+                # into the cubic kernel and one fixed-order reduction launch
+                # that also derives mean / stddev (vacv_resize_mean_stddev)
+                _, stats["sums"], stats["mean"], stats["std"] = ops.resize_mean_stddev(
+                    src, 224, 224, INTER_CUBIC, per_image=False, out=dst, stream=stream)
+            extra = None
+        else:
+            def main(stream=None):
+                # the per-rank sums (vacv_resize_channel_sums) ...
+                stats["sums"] = ops.resize_channel_sums(src, 224, 224, INTER_CUBIC, per_image=False, out=dst,
+                                                        stream=stream)[1]
 
-        def extra(stream=None):
-            # the global mean/stddev of the whole sharded batch: ONE all-reduce
-            # of the (c, 2) fp64 sums over RCCL, vacv_stats_from_sums --
-            # identical on every rank, no host sync
-            sums = stats["sums"]
-            if world > 1:
-                torch.distributed.all_reduce(sums, op=torch.distributed.ReduceOp.SUM)
-            stats["mean"], stats["std"] = ops.stats_from_sums(sums, float(B) * world * 224 * 224)
+            def extra(stream=None):
+                # ... then the global mean/stddev of the whole sharded batch:
+                # ONE all-reduce of the (c, 2) fp64 sums, vacv_stats_from_sums --
+                # identical on every rank
+                stats["sums"] = global_sums(stats["sums"])
+                stats["mean"], stats["std"] = ops.stats_from_sums(stats["sums"], count, stream=stream)
         return {"batch": B, "px": 2560 * 1440, "b_alg": B * resize_bytes(2560, 1440, 3, 224, 224, 1, 4, cubic=True),
                 "kernel": "cubic_direct_kernel", "frame": "2560x1440x3", "output": "224x224x3 fp32 + global mean/std",
                 "desc": "resize INTER_CUBIC 2560x1440x3 u8 -> 224x224x3 fp32 + global mean_stddev (RCCL all-reduce)",
-                "main": main, "extra": extra}
+                "main": main, "extra": extra, "stats": stats, "inputs": src}
     B = batch or 256
     src = u8(B, H_IN, W_IN, C)
     dst = torch.empty((B, H_OUT, W_OUT, C), dtype=torch.float32, device=dev)
@@ -417,9 +437,9 @@ def main():
         else:
             launch()
 
-    for _ in range(3):
-        step()
-    torch.cuda.synchronize(dev)
+    if graph is not None:
+        graph.replay()  # the instantiated graph's first replay, before the timed region
+        torch.cuda.synchronize(dev)
 
     # per-launch HIP events on the launch stream (kernel duration)
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]

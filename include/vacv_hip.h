@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define VACV_ABI_VERSION 1
+#define VACV_ABI_VERSION 2
 #define VACV_MAX_CHANNELS 16
 
 typedef enum vacv_status {
@@ -152,8 +152,11 @@ int vacv_resize_scaled(const vacv_image* src, const vacv_image* dst, int interpo
  *                  half to even), remap's nearest sampler; the border modes
  *                  below on the mapped pixel
  * INTER_LINEAR: a pixel whose top-left tap is
- * inside [0,w-2]x[0,h-2] is the reference's naive sampler bit for bit; the
- * others depend on border_mode:
+ * inside [0,w-2]x[0,h-2] is the reference's naive sampler bit for bit (with
+ * VACV_WARP_INVERSE_MAP too: the reference would hand that flag to
+ * cv::warpAffine, whose INTER_BITS = 5 remap tables round differently, so
+ * LINEAR | WARP_INVERSE_MAP keeps the naive arithmetic and does NOT
+ * reproduce OpenCV's); the others depend on border_mode:
  *   BORDER_CONSTANT     border_value (the reference leaves them untouched);
  *                       border_value may be NULL (zeros)
  *   BORDER_TRANSPARENT  left untouched (the reference's own behaviour); dst
@@ -212,6 +215,16 @@ int vacv_channel_sums(const vacv_image* src, double* sums, int per_image, void* 
  * merges.  dst must be dense. */
 int vacv_resize_channel_sums(const vacv_image* src, const vacv_image* dst, int interpolation, int mode,
                              double* sums, int per_image, void* stream);
+
+/* vacv_resize_channel_sums followed by vacv_stats_from_sums, for one GPU:
+ * the resize (cfg5: u8 -> fp32 INTER_CUBIC), the sums[groups][c][2] of its
+ * output and the population mean / stddev [groups][c] (groups = n per
+ * image, else 1) -- resize_naive.cpp:130-569, then NormalizeNaive::
+ * mean_stddev_naive_* (normalize_naive.cpp:7-48) over the image or the whole
+ * batch.  On several GPUs use vacv_resize_channel_sums, all-reduce the sums,
+ * then vacv_stats_from_sums.  dst must be dense. */
+int vacv_resize_mean_stddev(const vacv_image* src, const vacv_image* dst, int interpolation, int mode,
+                            double* sums, float* mean, float* stddev, int per_image, void* stream);
 
 /* mean = S1/count, stddev = sqrt(max(S2/count - mean^2, 0)) per group and
  * channel, on the device: sums[groups][c][2] -> mean/stddev[groups][c]. */
@@ -301,25 +314,22 @@ enum {
     VACV_TUNE_RESIZE_DIRECT = 0,     /* u8 bilinear: 0 staged, 1 gather kernel for one-tap rows, 2 gather always */
     VACV_TUNE_CUBIC_DIRECT = 1,      /* u8 cubic: 0 staged kernel, else the gather kernel */
     VACV_TUNE_RESIZE_INTERLEAVE = 2, /* staged kernel: 0 strip order, else address-ordered tasks */
-    VACV_TUNE_RESIZE_ROWS = 3,       /* retired (the whole-row staged kernel, never faster, was removed): no effect */
-    VACV_TUNE_DIRECT_XCD = 4,        /* gather kernel block order: 0 plain, 1 XCD-contiguous */
-    VACV_TUNE_WARP_PX = 5,           /* warp gather kernel: lane blocks per wave (4, 5, 8, 10) */
-    VACV_TUNE_NEAREST_KERNEL = 6,    /* INTER_NEAREST: 0 per-pixel kernel, 1 row per workgroup, else row per wave (when they apply) */
-    VACV_TUNE_AREA_KERNEL = 7,       /* u8 INTER_AREA: 1 per-pixel kernel, 2 dword column sums */
-    VACV_TUNE_AREA_ROWS = 8,         /* u8 INTER_AREA column sums: output rows per workgroup */
-    VACV_TUNE_COLOR_CHUNKS = 9,      /* 1: the chunked fp32 NV21 kernel */
-    VACV_TUNE_RESIZE_WGS = 10,       /* staged kernel: workgroups launched */
-    VACV_TUNE_RESIZE_TILE_H = 11,    /* staged kernel planner: tile height */
-    VACV_TUNE_RESIZE_TILE_W = 12,    /* staged kernel planner: tile width */
-    VACV_TUNE_RESIZE_WORK = 13,      /* staged kernel planner: work per thread */
-    VACV_TUNE_RESIZE_ROWS_BYTES = 14,/* retired with VACV_TUNE_RESIZE_ROWS: no effect */
-    VACV_TUNE_WARP_KERNEL = 15,      /* u8 CONSTANT warp: 0 per-pixel gathers, 2 batched gathers, 4 LDS-staged frames: an LDS-DMA ring of source boxes (k_warp_frames.hip) */
-    VACV_TUNE_RESIZE_STRIP = 16,     /* two-tap u8 bilinear: column strips with an LDS row ring, 1: 64 columns x 16-row batches, 2: 128 x 8; 0 staged kernel */
-    VACV_TUNE_MATCH_KERNEL = 17,     /* u8 match_template correlation: 0 v_dot4 kernel, else i8 MFMA where it fits */
-    VACV_TUNE_WARP_FRAMES = 18,      /* u8 CONSTANT warp, LDS-staged kernel: frames per workgroup */
-    VACV_TUNE_WARP_TILE_H = 19,      /* u8 CONSTANT warp, LDS-staged kernel: tile rows (16 or 32) */
-    VACV_TUNE_WARP_SLOTS = 20,       /* u8 CONSTANT warp, LDS-staged kernel: source boxes in the LDS ring (2-4) */
-    VACV_TUNE_COUNT = 21
+    VACV_TUNE_DIRECT_XCD = 3,        /* gather kernel block order: 0 plain, 1 XCD-contiguous */
+    VACV_TUNE_WARP_PX = 4,           /* warp gather kernel: lane blocks per wave (4, 5, 8, 10) */
+    VACV_TUNE_NEAREST_KERNEL = 5,    /* INTER_NEAREST: 0 per-pixel kernel, 1 row per workgroup, else row per wave (when they apply) */
+    VACV_TUNE_AREA_KERNEL = 6,       /* u8 INTER_AREA: 1 per-pixel kernel, 2 dword column sums */
+    VACV_TUNE_AREA_ROWS = 7,         /* u8 INTER_AREA column sums: output rows per workgroup */
+    VACV_TUNE_RESIZE_WGS = 8,        /* staged kernel: workgroups launched */
+    VACV_TUNE_RESIZE_TILE_H = 9,     /* staged kernel planner: tile height */
+    VACV_TUNE_RESIZE_TILE_W = 10,    /* staged kernel planner: tile width */
+    VACV_TUNE_RESIZE_WORK = 11,      /* staged kernel planner: work per thread */
+    VACV_TUNE_WARP_KERNEL = 12,      /* u8 CONSTANT warp: 0 per-pixel gathers, 2 batched gathers, 4 LDS-staged frames: an LDS-DMA ring of source boxes (k_warp_frames.hip) */
+    VACV_TUNE_RESIZE_STRIP = 13,     /* two-tap u8 bilinear: column strips with an LDS row ring, 1: 64 columns x 16-row batches, 2: 128 x 8; 0 staged kernel */
+    VACV_TUNE_MATCH_KERNEL = 14,     /* u8 match_template correlation: 0 v_dot4 kernel, else i8 MFMA where it fits */
+    VACV_TUNE_WARP_FRAMES = 15,      /* u8 CONSTANT warp, LDS-staged kernel: frames per workgroup */
+    VACV_TUNE_WARP_TILE_H = 16,      /* u8 CONSTANT warp, LDS-staged kernel: tile rows (16 or 32) */
+    VACV_TUNE_WARP_SLOTS = 17,       /* u8 CONSTANT warp, LDS-staged kernel: source boxes in the LDS ring (2-4) */
+    VACV_TUNE_COUNT = 18
 };
 /* value < 0 restores the built-in choice.  Returns VACV_OK or INVALID_ARG. */
 int vacv_set_tuning(int key, int value);

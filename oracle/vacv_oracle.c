@@ -1128,8 +1128,11 @@ void oracle_min_max_idx(const void* src, int w, int h, int esize, const uint8_t*
  * row is resized horizontally into a WT buffer (HResizeLanczos4: taps sx - 3
  * .. sx + 4, an out-of-range tap walks by cn to the nearest pixel of its
  * channel; columns outside [xmin, xmax) sum from 0, the others unrolled),
- * then output row dy combines rows clip(sy - 3 + k, 0, h) (VResizeLanczos4:
- * (b0 r0 + .. + b3 r3) + (b4 r4 + .. + b7 r7), u8 by FixedPtCast<int, uchar, 22>). */
+ * then output row dy combines rows clip(sy - 3 + k, 0, h) (VResizeLanczos4; u8
+ * in int, where the order is immaterial, rounded by FixedPtCast<int, uchar,
+ * 22>; fp32: elements x < (dst.w * cn & ~3) in the 4-wide NEON loop of
+ * VResizeLanczos4Vec_32f, (b0 r0 + .. + b3 r3) + (b4 r4 + .. + b7 r7), the
+ * rest in the scalar tail's left-to-right b0 r0 + b1 r1 + .. + b7 r7). */
 static void lz_coeffs(float x, float* coeffs) {
     static const double s45 = 0.70710678118654752440084436210485;
     static const double cs[8][2] = {{1, 0}, {-s45, -s45}, {0, 1}, {s45, -s45}, {-1, 0}, {s45, s45}, {0, -1}, {-s45, s45}};
@@ -1242,11 +1245,18 @@ void oracle_resize_lanczos4(const void* src, int w_in, int h_in, int cc, int esi
                 ((uint8_t*)dst)[(size_t)dy * dw + dx] = (uint8_t)(v < 0 ? 0 : v > 255 ? 255 : v);
             } else {
                 const float* b = ya + 8 * dy;
-                float s0 = bf[(size_t)rows[0] * dw + dx] * b[0] + bf[(size_t)rows[1] * dw + dx] * b[1] +
-                           bf[(size_t)rows[2] * dw + dx] * b[2] + bf[(size_t)rows[3] * dw + dx] * b[3];
-                float s1 = bf[(size_t)rows[4] * dw + dx] * b[4] + bf[(size_t)rows[5] * dw + dx] * b[5] +
-                           bf[(size_t)rows[6] * dw + dx] * b[6] + bf[(size_t)rows[7] * dw + dx] * b[7];
-                ((float*)dst)[(size_t)dy * dw + dx] = s0 + s1;
+                float v;
+                if (dx < (dw & ~3)) {
+                    float s0 = bf[(size_t)rows[0] * dw + dx] * b[0] + bf[(size_t)rows[1] * dw + dx] * b[1] +
+                               bf[(size_t)rows[2] * dw + dx] * b[2] + bf[(size_t)rows[3] * dw + dx] * b[3];
+                    float s1 = bf[(size_t)rows[4] * dw + dx] * b[4] + bf[(size_t)rows[5] * dw + dx] * b[5] +
+                               bf[(size_t)rows[6] * dw + dx] * b[6] + bf[(size_t)rows[7] * dw + dx] * b[7];
+                    v = s0 + s1;
+                } else {
+                    v = bf[(size_t)rows[0] * dw + dx] * b[0];
+                    for (k = 1; k < 8; k++) v = v + bf[(size_t)rows[k] * dw + dx] * b[k];
+                }
+                ((float*)dst)[(size_t)dy * dw + dx] = v;
             }
         }
     }

@@ -39,7 +39,7 @@ def test_header_matches_exports_and_binding(lib):
 
 
 def test_version_and_status(lib):
-    assert lib.vacv_abi_version() == 1
+    assert lib.vacv_abi_version() == 2
     assert lib.vacv_status_string(0) == b"ok"
     assert lib.vacv_status_string(-2) == b"unsupported"
 

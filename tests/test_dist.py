@@ -185,3 +185,71 @@ def test_global_stats_two_ranks_on_gpu():
         assert count == 7 * 90 * 160
         assert same_sums and same_stats, rank
         assert np.array_equal(m, want_m) and np.array_equal(s, want_s), rank
+
+
+def _bench_rank_worker(rank, world, port, batch, out_q):
+    """One rank of bench.py's cfg5 step on cuda:0 (gloo): make_workload's
+    main + extra exactly as bench.py runs them at world > 1 -- the fused
+    device sums of this rank's shard, the all-reduce, vacv_stats_from_sums."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    for p in (repo, os.path.join(repo, "arm-neon-opencv_amd")):
+        sys.path.insert(0, p)
+    try:
+        import torch.distributed as dist
+        import bench
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        dev = torch.device("cuda:0")  # both ranks on the one card of the box
+        torch.cuda.set_device(dev)
+        from vacv_amd import ops
+        wl = bench.make_workload("cubic_stats", batch, dev, rank, world, ops)
+        for _ in range(2):  # a repeated step gives the same answer
+            wl["main"]()
+            wl["extra"]()
+        torch.cuda.synchronize(dev)
+        st = wl["stats"]
+        out_q.put((rank, st["sums"].cpu().numpy(), st["mean"].cpu().numpy(), st["std"].cpu().numpy()))
+        dist.destroy_process_group()
+    except Exception as e:  # report, do not hang the parent on q.get
+        out_q.put(("error", repr(e)))
+        raise
+
+
+@pytest.mark.gpu
+def test_bench_cubic_stats_two_ranks(hip_device):
+    """bench.py --workload cubic_stats at world size 2, on real kernels: two
+    spawned gloo ranks on cuda:0 run make_workload's main + extra as the bench
+    does (fused cubic sums per rank, all-reduce of the device sums, stats).
+    Both ranks agree bit for bit, and their global mean / stddev equal one
+    process running the whole batch (vacv_resize_mean_stddev) within SURVEY
+    8(c)'s |d mean| <= 1e-3, |d std| / std <= 1e-4."""
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    from vacv_amd import INTER_CUBIC, ops
+    batch = 3
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_bench_rank_worker, args=(r, 2, port, batch, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=240) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+    assert all(r[0] != "error" for r in res), res
+    assert all(p.exitcode == 0 for p in procs)
+    res.sort(key=lambda r: r[0])
+    (_, s0, m0, d0), (_, s1, m1, d1) = res
+    assert np.array_equal(s0, s1) and np.array_equal(m0, m1) and np.array_equal(d0, d1), "ranks disagree"
+    # the whole batch in one process: both ranks' inputs, regenerated the way
+    # make_workload draws them (seed 1234 + rank on this device)
+    dev = hip_device
+    whole = torch.cat([bench.make_workload("cubic_stats", batch, dev, r, 2, ops)["inputs"] for r in range(2)])
+    _, sums, mean, std = ops.resize_mean_stddev(whole, 224, 224, INTER_CUBIC, per_image=False)
+    torch.cuda.synchronize(dev)
+    sums, mean, std = sums.cpu().numpy(), mean.cpu().numpy(), std.cpu().numpy()
+    assert np.abs(s0 - sums).max() / np.abs(sums).max() <= 1e-12
+    assert np.abs(m0 - mean).max() <= 1e-3
+    assert (np.abs(d0 - std) / std).max() <= 1e-4
+    del whole
+    torch.cuda.empty_cache()

@@ -175,10 +175,11 @@ def test_cubic_direct_and_staged_agree(ops, dev, oracle):
 
 
 def test_resize_channel_sums(ops, dev, oracle):
-    """vacv_resize_channel_sums: the resize output is unchanged and the sums
-    match vacv_channel_sums of that output.  u8 -> fp32 cubic (cfg5) fuses the
-    sums into the gather kernel (per-wave fp32 partials of 128 pixels, then a
-    fixed-order fp64 reduction): within 1e-6 relative of the fp64 sums, the
+    """vacv_resize_channel_sums / vacv_resize_mean_stddev: the resize output is
+    unchanged and the sums match vacv_channel_sums of that output.  u8 -> fp32
+    cubic (cfg5) fuses the sums into the gather kernel (fp32 over <= 2 pixels
+    per lane, then fp64 per wave and workgroup, then a fixed-order fp64
+    reduction launch): within 1e-6 relative of the fp64 sums, the
     derived mean / stddev within SURVEY 8(c)'s |d mean| <= 1e-3 and
     |d std| / std <= 1e-4 of the oracle's exact statistics, and bit-identical
     run to run.  The batch statistic of cfg5 (2560x1440 -> 224x224 cubic) at
@@ -204,21 +205,37 @@ def test_resize_channel_sums(ops, dev, oracle):
         em, es = exact.mean(axis=1), exact.std(axis=1)
         assert np.abs(host(mean) - em).max() <= 1e-3
         assert (np.abs(host(std) - es) / es).max() <= 1e-4
+        # vacv_resize_mean_stddev (the one-GPU cfg5 call): the same sums, and the
+        # statistics its reduction launch derives equal vacv_stats_from_sums'
+        out2, sums2, mean2, std2 = ops.resize_mean_stddev(src, 224, 224, INTER_CUBIC, per_image=per_image)
+        assert torch.equal(out2, ref) and torch.equal(sums2, sums)
+        assert torch.equal(mean2, mean) and torch.equal(std2, std)
     odd = to_dev(np.stack([synthetic_image(310 + k, 301, 257, 3) for k in range(3)]), dev)
     out, sums = ops.resize_channel_sums(odd, 61, 37, INTER_CUBIC, per_image=True)
     want = ops.channel_sums(out)
     torch.cuda.synchronize(dev)
     assert ((sums - want).abs() / want.abs().clamp(min=1.0)).max().item() <= 1e-6
+    for per_image in (True, False):  # partial workgroups (61 x 37 = 2,257 px: 5 workgroups, the last one partial)
+        _, s2, m2, d2 = ops.resize_mean_stddev(odd, 61, 37, INTER_CUBIC, per_image=per_image)
+        count = 61 * 37 * (1 if per_image else 3)
+        want = ops.channel_sums(out, per_image=per_image)
+        wm, wd = ops.stats_from_sums(want, count)
+        torch.cuda.synchronize(dev)
+        assert ((s2 - want).abs() / want.abs().clamp(min=1.0)).max().item() <= 1e-6
+        assert (m2 - wm).abs().max().item() <= 1e-3 and ((d2 - wd).abs() / wd).max().item() <= 1e-4
     # NCHW planes and odd sizes
     chw = ops.change_layout(src[:2, :301, :257].contiguous(), NCHW)
     out, sums = ops.resize_channel_sums(chw, 61, 37, INTER_CUBIC, layout=NCHW)
     want = ops.channel_sums(out, layout=NCHW)
     torch.cuda.synchronize(dev)
     assert ((sums - want).abs() / want.abs().clamp(min=1.0)).max().item() <= 1e-12
-    # u8 bilinear: identical to the two calls
+    # u8 bilinear: identical to the two calls (three with the statistics)
     out, sums = ops.resize_channel_sums(src, 640, 360)
     assert torch.equal(out, ops.resize(src, 640, 360))
     assert torch.equal(sums, ops.channel_sums(out))
+    _, s2, m2, d2 = ops.resize_mean_stddev(src, 640, 360, per_image=True)
+    wm, wd = ops.stats_from_sums(sums, 640 * 360)
+    assert torch.equal(s2, sums) and torch.equal(m2, wm) and torch.equal(d2, wd)
     del src
     torch.cuda.empty_cache()
 
@@ -1085,6 +1102,45 @@ def test_cvt_color_pipeline_digests(ops, dev, oracle, golden):
     assert sha(bgr) == d["cfg3_nv21_to_bgr_1080p"]["sha256"]
     out = host(ops.cvt_color_normalize(to_dev(nv, dev), mean=MEAN, std=STD))
     assert sha(out) == d["cfg3_nv21_bgr_normalize_1080p"]["sha256"]
+
+
+def test_cvt_color_cfg3_as_benchmarked(ops, dev, oracle, golden):
+    """BASELINE cfg3 exactly as bench.py --workload cvt_normalize runs it: 256
+    NV21 1080p frames (1920 x 1620 u8, drawn on the device as bench.py draws
+    them) -> cvt_color_normalize into a preallocated (256, 1080, 1920, 3) fp32
+    output of 6.37 GB, the only BASELINE output past 2^32 bytes.  Frame 0 is
+    the reference's 1080p test image (its NV21 must hash to the reference's
+    cfg3 digest); frames 127, 128, 200 and 255 -- 200 and 255 start beyond
+    the 4 GiB output offset -- must equal the oracle bit for bit.  The same
+    for cvt_color's u8 output (1.59 GB) once.
+    Reference: cvt_color.cpp:39-135, normalize_naive.cpp:74-90."""
+    import torch
+    meta, _ = golden
+    d = meta["digests"]
+    b = load_bgr("1920x1080.jpeg")
+    if sha(b) != d["input_1920x1080"]["sha256"]:
+        pytest.skip("PIL decodes differently here")
+    nv = oracle.bgr2nv21(b)
+    g = torch.Generator(device=dev)
+    g.manual_seed(1234)
+    yuv = torch.randint(0, 256, (256, 1620, 1920), dtype=torch.uint8, device=dev, generator=g)
+    yuv[0] = to_dev(nv, dev)
+    out = torch.empty((256, 1080, 1920, 3), dtype=torch.float32, device=dev)
+    assert out.numel() * 4 > 200 * 1080 * 1920 * 12 > 2 ** 32
+    ops.cvt_color_normalize(yuv, mean=MEAN, std=STD, out=out)
+    assert sha(host(out[0])) == d["cfg3_nv21_bgr_normalize_1080p"]["sha256"]
+    for k in (127, 128, 200, 255):
+        want = oracle.normalize(oracle.u8_to_f32(oracle.yuv420sp_to_bgr(host(yuv[k]))), MEAN, STD)
+        assert_same(host(out[k]), want, f"cfg3 frame {k}")
+    del out
+    torch.cuda.empty_cache()
+    bgr = torch.empty((256, 1080, 1920, 3), dtype=torch.uint8, device=dev)
+    ops.cvt_color(yuv, out=bgr)
+    assert sha(host(bgr[0])) == d["cfg3_nv21_to_bgr_1080p"]["sha256"]
+    for k in (128, 255):
+        assert_same(host(bgr[k]), oracle.yuv420sp_to_bgr(host(yuv[k])), f"cvt_color u8 frame {k}")
+    del bgr, yuv
+    torch.cuda.empty_cache()
 
 
 # ---------------------------------------------------------------------------

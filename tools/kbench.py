@@ -69,6 +69,19 @@ def main():
         cases["nearest_1080p_640x360_u8"] = (
             lambda src=src, o=o3: ops.resize(src, 640, 360, interpolation=vacv_amd.INTER_NEAREST, out=o),
             n * (360 * 1920 * 3 + 640 * 360 * 3), n * 1920 * 1080)
+    if a.op in ("lanczos", "all"):
+        # INTER_LANCZOS4: every source row is weighted (8 taps at a 3x downscale)
+        n = a.batch or 256
+        src = frames(n, 1080, 1920)
+        o3 = torch.empty((n, 360, 640, 3), dtype=torch.uint8, device=dev)
+        cases["lanczos_1080p_640x360_u8"] = (
+            lambda src=src, o=o3: ops.resize(src, 640, 360, interpolation=vacv_amd.INTER_LANCZOS4, out=o),
+            n * (1920 * 1080 * 3 + 640 * 360 * 3), n * 1920 * 1080)
+        of = torch.empty((n, 360, 640, 3), dtype=torch.float32, device=dev)
+        cases["lanczos_normalize_1080p_640x360"] = (
+            lambda src=src, o=of: ops.resize_normalize(src, 640, 360, MEAN, STD, interpolation=vacv_amd.INTER_LANCZOS4,
+                                                       out=o),
+            n * (1920 * 1080 * 3 + 640 * 360 * 12), n * 1920 * 1080)
     if a.op in ("warp", "all"):
         n = a.batch or 128
         src = frames(n, 720, 1280)
@@ -80,6 +93,10 @@ def main():
             mr = ops.rotation_matrix(0.9, rot, (640, 360, 640, 360))
             cases[f"warp_720p_rot{int(rot)}_u8"] = (lambda src=src, m=mr, o=o: ops.warp_affine(src, m, 1280, 720, out=o),
                                                    n * 2 * 1280 * 720 * 3, n * 1280 * 720)
+        # INTER_NEAREST (OpenCV's fixed-point map): the source pixels it reads, ~1/0.81 of a frame at scale 0.9
+        cases["warp_nearest_720p_rot15_u8"] = (
+            lambda src=src, m=m, o=o: ops.warp_affine(src, m, 1280, 720, flags=vacv_amd.INTER_NEAREST, out=o),
+            n * 2 * 1280 * 720 * 3, n * 1280 * 720)
         of = torch.empty((n, 720, 1280, 3), dtype=torch.float32, device=dev)
         cases["warp_normalize_720p_rot15"] = (lambda src=src, m=m, of=of: ops.warp_affine_normalize(src, m, 1280, 720, MEAN, STD, out=of),
                                               n * 5 * 1280 * 720 * 3, n * 1280 * 720)
@@ -89,6 +106,19 @@ def main():
         o = torch.empty((n, 1080, 1920, 3), dtype=torch.float32, device=dev)
         cases["nv21_bgr_normalize_1080p"] = (lambda yuv=yuv, o=o: ops.cvt_color_normalize(yuv, mean=MEAN, std=STD, out=o),
                                              n * (1920 * 1620 + 1920 * 1080 * 12), n * 1920 * 1080)
+    if a.op in ("cvt_cv", "all"):
+        # the OpenCV colour codes (k_color_cv.hip): YUV420 in, 3 or 4 channels out; gray -> BGR
+        n = a.batch or 256
+        yuv = torch.randint(0, 256, (n, 1620, 1920), dtype=torch.uint8, device=dev, generator=g)
+        o4 = torch.empty((n, 1080, 1920, 4), dtype=torch.uint8, device=dev)
+        o3 = torch.empty((n, 1080, 1920, 3), dtype=torch.uint8, device=dev)
+        cases["nv21_bgra_1080p"] = (lambda yuv=yuv, o=o4: ops.cvt_color(yuv, vacv_amd.COLOR_YUV2BGRA_NV21, out=o),
+                                    n * (1920 * 1620 + 1920 * 1080 * 4), n * 1920 * 1080)
+        cases["yv12_bgr_1080p"] = (lambda yuv=yuv, o=o3: ops.cvt_color(yuv, vacv_amd.COLOR_YUV2BGR_YV12, out=o),
+                                   n * (1920 * 1620 + 1920 * 1080 * 3), n * 1920 * 1080)
+        gray = yuv[:, :1080]
+        cases["gray_bgr_1080p"] = (lambda g_=gray, o=o3: ops.cvt_color(g_, vacv_amd.COLOR_GRAY2BGR, out=o),
+                                   n * 1920 * 1080 * 4, n * 1920 * 1080)
     if a.op in ("yuv_resize", "all"):
         from vacv_amd.roofline import yuv_resize_bytes
         n = a.batch or 256
