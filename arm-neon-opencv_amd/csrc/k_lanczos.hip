@@ -67,11 +67,66 @@ struct LanczosLaunch {
     LanczosTabsDev t;
 };
 
+// A lane's horizontal taps as an 8-pixel WINDOW of its source row, starting
+// at column wstart = clamp(sx - 3, 0, w - 8): tap j is window pixel
+// clamp(j + SH, 0, 7) with SH = (sx - 3) - wstart in [-4, 4] -- 0 for the
+// interior columns (OpenCV's unrolled loop), else the border clamp (its
+// `sxj += cn` walk).  Every lane's row data is then one window load, the
+// same shape for all lanes, which is what lets the loads run ahead.
+template <int SH>
+__device__ __forceinline__ constexpr int lz_pos(int j) {
+    return j + SH < 0 ? 0 : (j + SH > 7 ? 7 : j + SH);
+}
+
+// u8: the window's bytes (after the byte shift) in ND - 1 dwords
+template <int CC, int SH>
+__device__ __forceinline__ void lz_h_u8(const uint32_t* wv, const int (&c)[8], int (&hv)[CC]) {
+#pragma unroll
+    for (int k = 0; k < CC; ++k) {
+        int v = 0;  // int sums: the order is immaterial
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const int e = lz_pos<SH>(j) * CC + k;
+            v += (int)((wv[e >> 2] >> (8 * (e & 3))) & 0xFFu) * c[j];
+        }
+        hv[k] = v;
+    }
+}
+
+// fp32: the window's 8 CC floats; HResizeLanczos4's sum in tap order, from
+// 0 + in the border loop (SH != 0)
+template <int CC, int SH>
+__device__ __forceinline__ void lz_h_f32(const float* wf, const float (&c)[8], float (&hv)[CC]) {
+#pragma unroll
+    for (int k = 0; k < CC; ++k) {
+        float a[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) a[j] = wf[lz_pos<SH>(j) * CC + k] * c[j];
+        float v = SH == 0 ? a[0] : 0.f + a[0];
+#pragma unroll
+        for (int j = 1; j < 8; ++j) v = v + a[j];
+        hv[k] = v;
+    }
+}
+
+// The per-row tables are read through the constant address space: their
+// indices are wave-uniform, so these are scalar loads -- as vector loads they
+// would be counted behind the in-flight row windows and wait for all of them.
+template <typename T>
+__device__ __forceinline__ T lz_const(const T* p, int i) {
+    return ((const __attribute__((address_space(4))) T*)(uintptr_t)p)[i];
+}
+
 template <typename TIn, int OUT, int CC>
 __global__ void __launch_bounds__(kBlock) lanczos_kernel(LanczosLaunch L, int strips, int bands, int band_rows) {
     constexpr bool U8 = std::is_same<TIn, uint8_t>::value;
     using TW = typename std::conditional<U8, int, float>::type;
     using TOut = typename std::conditional<(OUT == kOutSame), TIn, float>::type;
+    // the row window in registers: u8 8 CC bytes at any byte offset, fp32 8 CC floats
+    constexpr int ND = U8 ? (8 * CC + 6) / 4 : 8 * CC;
+    // source rows in flight per wave (the loads of rows r + 1 .. r + D - 1
+    // run while row r is resized)
+    constexpr int D = U8 ? 4 : 2;
     __shared__ TW ring[4][8][64 * CC];  // per wave: 8 source rows x 64 columns x CC
 
     // wave-uniform, and said so: the plane's buffer resource stays in SGPRs
@@ -95,106 +150,88 @@ __global__ void __launch_bounds__(kBlock) lanczos_kernel(LanczosLaunch L, int st
     const uint32_t slimit = (uint32_t)L.src.plane_bytes + srs.delta;
     const uint32_t rp = (uint32_t)L.src.row_pitch;  // plane < 2^31 bytes (kMaxPlaneBytes)
 
-    // this column's taps: origin, coefficients, fast (unrolled, unclamped) or not
+    // this column's window and coefficients (the host guarantees w >= 8)
     const int sx = L.t.xofs[xc];
-    const bool fast = xc >= L.t.xmin && xc < L.t.xmax;
+    const int wstart = min(max(sx - 3, 0), w - 8);
+    const int shift = (sx - 3) - wstart;  // [-4, 4]; 0 <=> OpenCV's [xmin, xmax)
     TW c[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
         if constexpr (U8) c[j] = (int)L.t.xai[8 * xc + j];
         else c[j] = L.t.xaf[8 * xc + j];
     }
+    const uint32_t wbyte = (uint32_t)(wstart * CC * (int)sizeof(TIn)) + srs.delta;
+    const uint32_t wsh = wbyte & 3u;  // u8: the window's byte offset in its first dword
 
-    // HResizeLanczos4 of source row r for this lane's column -> ring slot
-    auto hrow = [&](int r, int slot) {
-        TW hv[CC];
-        const uint32_t row0 = (uint32_t)r * rp;
-        if constexpr (U8) {
-            constexpr int ND = (8 * CC + 6) / 4;  // dwords covering 8 CC bytes at any byte offset
-            const uint32_t off = row0 + (uint32_t)((sx - 3) * CC) + srs.delta;
-            const uint32_t a = off & ~3u, sh = off & 3u;
-            uint32_t d[ND];
-            if (fast && a + 4u * ND <= slimit) {
-                int q = 0;
+    // the window of source row r (issued; consumed by hrow).  SAFE: the
+    // window may reach past the plane's last byte (only in the waves holding
+    // the plane's last row and right-most columns), so those dwords are read
+    // bytewise -- an overhanging 16-byte load reads as zeros.
+    auto load = [&](auto safe_c, uint32_t (&d)[ND], int r) {
+        constexpr bool SAFE = decltype(safe_c)::value;
+        const uint32_t a = (uint32_t)r * rp + (wbyte & ~3u);
+        if (!SAFE || a + 4u * ND <= slimit) {
+            int q = 0;
 #pragma unroll
-                for (; q + 4 <= ND; q += 4) {
-                    const auto v = __builtin_amdgcn_raw_buffer_load_b128(srs.r, (int)(a + 4 * q), 0, 0);
-                    d[q] = v[0]; d[q + 1] = v[1]; d[q + 2] = v[2]; d[q + 3] = v[3];
-                }
-                if constexpr (ND % 4 == 3) {
-                    const auto v = __builtin_amdgcn_raw_buffer_load_b96(srs.r, (int)(a + 4 * q), 0, 0);
-                    d[q] = v[0]; d[q + 1] = v[1]; d[q + 2] = v[2];
-                } else if constexpr (ND % 4 == 2) {
-                    const auto v = __builtin_amdgcn_raw_buffer_load_b64(srs.r, (int)(a + 4 * q), 0, 0);
-                    d[q] = v[0]; d[q + 1] = v[1];
-                } else if constexpr (ND % 4 == 1) {
-                    d[q] = __builtin_amdgcn_raw_buffer_load_b32(srs.r, (int)(a + 4 * q), 0, 0);
-                }
-            } else {
-                // border columns (clamped taps) and the plane's last bytes: the
-                // 8 CC tap bytes one by one, placed where the window load puts them
-#pragma unroll
-                for (int q = 0; q < ND; ++q) d[q] = 0u;
-#pragma unroll
-                for (int j = 0; j < 8; ++j) {
-                    const int col = min(max(sx - 3 + j, 0), w - 1);
-#pragma unroll
-                    for (int k = 0; k < CC; ++k) {
-                        const uint32_t e = sh + (uint32_t)(j * CC + k);
-                        const uint32_t b = __builtin_amdgcn_raw_buffer_load_b8(
-                            srs.r, (int)(row0 + (uint32_t)(col * CC + k) + srs.delta), 0, 0);
-                        d[e >> 2] |= b << (8 * (e & 3));
-                    }
-                }
+            for (; q + 4 <= ND; q += 4) {
+                const auto v = __builtin_amdgcn_raw_buffer_load_b128(srs.r, (int)(a + 4 * q), 0, 0);
+                d[q] = v[0]; d[q + 1] = v[1]; d[q + 2] = v[2]; d[q + 3] = v[3];
             }
-            uint32_t wv[ND - 1];
-#pragma unroll
-            for (int q = 0; q < ND - 1; ++q) wv[q] = __builtin_amdgcn_alignbyte(d[q + 1], d[q], sh);
-#pragma unroll
-            for (int k = 0; k < CC; ++k) {
-                int v = 0;  // int sums: the order is immaterial
-#pragma unroll
-                for (int j = 0; j < 8; ++j) {
-                    const int e = j * CC + k;
-                    v += (int)((wv[e >> 2] >> (8 * (e & 3))) & 0xFFu) * c[j];
-                }
-                hv[k] = v;
+            if constexpr (ND % 4 == 3) {
+                const auto v = __builtin_amdgcn_raw_buffer_load_b96(srs.r, (int)(a + 4 * q), 0, 0);
+                d[q] = v[0]; d[q + 1] = v[1]; d[q + 2] = v[2];
+            } else if constexpr (ND % 4 == 2) {
+                const auto v = __builtin_amdgcn_raw_buffer_load_b64(srs.r, (int)(a + 4 * q), 0, 0);
+                d[q] = v[0]; d[q + 1] = v[1];
+            } else if constexpr (ND % 4 == 1) {
+                d[q] = __builtin_amdgcn_raw_buffer_load_b32(srs.r, (int)(a + 4 * q), 0, 0);
             }
         } else {
-            float t[8][CC];
-            const uint32_t off = row0 + (uint32_t)((sx - 3) * CC * 4) + srs.delta;
-            if (fast && off + 32u * CC <= slimit) {
 #pragma unroll
-                for (int q = 0; q < 2 * CC; ++q) {
-                    const auto v = __builtin_amdgcn_raw_buffer_load_b128(srs.r, (int)(off + 16 * q), 0, 0);
+            for (int q = 0; q < ND; ++q) {
+                uint32_t v = 0;
 #pragma unroll
-                    for (int i = 0; i < 4; ++i) {
-                        const int e = 4 * q + i;
-                        // (__builtin_bit_cast(float, v[i]) of a vector element reads
-                        // element 0 for every i with this compiler: ROCm 7.2 clang)
-                        t[e / CC][e % CC] = __uint_as_float(v[i]);
-                    }
-                }
-            } else {
-#pragma unroll
-                for (int j = 0; j < 8; ++j) {
-                    const int col = min(max(sx - 3 + j, 0), w - 1);
-#pragma unroll
-                    for (int k = 0; k < CC; ++k)
-                        t[j][k] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
-                                                                srs.r, (int)(row0 + (uint32_t)(col * CC + k) * 4 + srs.delta), 0, 0));
-                }
+                for (int e = 0; e < 4; ++e)
+                    if (a + 4u * q + e < slimit)
+                        v |= (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(srs.r, (int)(a + 4u * q + e), 0, 0) << (8 * e);
+                d[q] = v;
             }
+        }
+    };
+    // HResizeLanczos4 of the loaded window -> ring slot
+    auto hrow = [&](const uint32_t (&d)[ND], int slot) {
+        TW hv[CC];
+        if constexpr (U8) {
+            uint32_t wv[ND - 1];
 #pragma unroll
-            for (int k = 0; k < CC; ++k) {
-                float a[8];
+            for (int q = 0; q < ND - 1; ++q) wv[q] = __builtin_amdgcn_alignbyte(d[q + 1], d[q], wsh);
+            switch (shift) {  // divergent only in the strips at the image's edges
+                case -4: lz_h_u8<CC, -4>(wv, c, hv); break;
+                case -3: lz_h_u8<CC, -3>(wv, c, hv); break;
+                case -2: lz_h_u8<CC, -2>(wv, c, hv); break;
+                case -1: lz_h_u8<CC, -1>(wv, c, hv); break;
+                case 1: lz_h_u8<CC, 1>(wv, c, hv); break;
+                case 2: lz_h_u8<CC, 2>(wv, c, hv); break;
+                case 3: lz_h_u8<CC, 3>(wv, c, hv); break;
+                case 4: lz_h_u8<CC, 4>(wv, c, hv); break;
+                default: lz_h_u8<CC, 0>(wv, c, hv); break;
+            }
+        } else {
+            float wf[ND];
+            // (__builtin_bit_cast(float, v[i]) of a vector element read element 0
+            // for every i with this compiler, ROCm 7.2 clang: scalars only here)
 #pragma unroll
-                for (int j = 0; j < 8; ++j) a[j] = t[j][k] * c[j];
-                // HResizeLanczos4: the border loop starts from v = 0, the unrolled one does not
-                float v = fast ? a[0] : 0.f + a[0];
-#pragma unroll
-                for (int j = 1; j < 8; ++j) v = v + a[j];
-                hv[k] = v;
+            for (int q = 0; q < ND; ++q) wf[q] = __uint_as_float(d[q]);
+            switch (shift) {
+                case -4: lz_h_f32<CC, -4>(wf, c, hv); break;
+                case -3: lz_h_f32<CC, -3>(wf, c, hv); break;
+                case -2: lz_h_f32<CC, -2>(wf, c, hv); break;
+                case -1: lz_h_f32<CC, -1>(wf, c, hv); break;
+                case 1: lz_h_f32<CC, 1>(wf, c, hv); break;
+                case 2: lz_h_f32<CC, 2>(wf, c, hv); break;
+                case 3: lz_h_f32<CC, 3>(wf, c, hv); break;
+                case 4: lz_h_f32<CC, 4>(wf, c, hv); break;
+                default: lz_h_f32<CC, 0>(wf, c, hv); break;
             }
         }
 #pragma unroll
@@ -212,23 +249,27 @@ __global__ void __launch_bounds__(kBlock) lanczos_kernel(LanczosLaunch L, int st
         for (int k = 0; k < CC; ++k) cn[k] = chan_norm(L.norm, img, CC == 1 ? plane % L.norm.c_total : k);
     }
 
-    int next = INT_MIN;  // first source row (unclamped) not yet in the ring
-    for (int y = y0; y < y1; ++y) {
-        const int sy = L.t.yofs[y];  // uniform, non-decreasing in y
-        for (int r = max(next, sy - 3); r <= sy + 4; ++r) hrow(min(max(r, 0), h - 1), r & 7);
-        next = max(next, sy + 5);
+    // VResizeLanczos4 of output row y from the ring, and its store
+    auto emit = [&](int y) {
+        const int sy = lz_const(L.t.yofs, y);
         TW hs[8][CC];
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
+            const int slot = min(max(sy - 3 + k, 0), h - 1) & 7;
 #pragma unroll
-            for (int q = 0; q < CC; ++q) hs[k][q] = ring[wave][(sy - 3 + k) & 7][lane * CC + q];
+            for (int q = 0; q < CC; ++q) hs[k][q] = ring[wave][slot][lane * CC + q];
         }
         TOut o[CC];
         if constexpr (U8) {
-            const short* b = L.t.yai + 8 * y;
+            // the row's 8 shorts as 4 dwords (scalar loads are dword-granular)
             int bb[8];
+            const int* b32 = reinterpret_cast<const int*>(L.t.yai);
 #pragma unroll
-            for (int k = 0; k < 8; ++k) bb[k] = b[k];
+            for (int k = 0; k < 4; ++k) {
+                const int wd = lz_const(b32, 4 * y + k);
+                bb[2 * k] = (int)(short)(wd & 0xFFFF);
+                bb[2 * k + 1] = wd >> 16;
+            }
 #pragma unroll
             for (int q = 0; q < CC; ++q) {
                 const int s0 = hs[0][q] * bb[0] + hs[1][q] * bb[1] + hs[2][q] * bb[2] + hs[3][q] * bb[3];
@@ -239,10 +280,9 @@ __global__ void __launch_bounds__(kBlock) lanczos_kernel(LanczosLaunch L, int st
                 else o[q] = (TOut)normalize_u8v(cn[q], vi);
             }
         } else {
-            const float* b = L.t.yaf + 8 * y;
             float bb[8];
 #pragma unroll
-            for (int k = 0; k < 8; ++k) bb[k] = b[k];
+            for (int k = 0; k < 8; ++k) bb[k] = lz_const(L.t.yaf, 8 * y + k);
 #pragma unroll
             for (int q = 0; q < CC; ++q) {
                 float v;
@@ -281,31 +321,66 @@ __global__ void __launch_bounds__(kBlock) lanczos_kernel(LanczosLaunch L, int st
             }
         } else if (live) {
             const uint32_t off = orow + (uint32_t)(x * CC) * 4u;
-            TOut* dq = reinterpret_cast<TOut*>(dp + (off - drs.delta));
+            uint32_t ov[CC];
+#pragma unroll
+            for (int q = 0; q < CC; ++q) ov[q] = __float_as_uint(o[q]);
             if (dst_al) {
                 if constexpr (CC == 1) {
-                    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, o[0]), drs.r, (int)off, 0, 0);
+                    __builtin_amdgcn_raw_buffer_store_b32(ov[0], drs.r, (int)off, 0, 0);
                 } else if constexpr (CC == 2) {
                     typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
-                    __builtin_amdgcn_raw_buffer_store_b64(
-                        u32x2{__builtin_bit_cast(uint32_t, o[0]), __builtin_bit_cast(uint32_t, o[1])}, drs.r, (int)off, 0, 0);
+                    __builtin_amdgcn_raw_buffer_store_b64(u32x2{ov[0], ov[1]}, drs.r, (int)off, 0, 0);
                 } else if constexpr (CC == 3) {
                     typedef unsigned int u32x3 __attribute__((ext_vector_type(3)));
-                    __builtin_amdgcn_raw_buffer_store_b96(
-                        u32x3{__builtin_bit_cast(uint32_t, o[0]), __builtin_bit_cast(uint32_t, o[1]),
-                              __builtin_bit_cast(uint32_t, o[2])}, drs.r, (int)off, 0, 0);
+                    __builtin_amdgcn_raw_buffer_store_b96(u32x3{ov[0], ov[1], ov[2]}, drs.r, (int)off, 0, 0);
                 } else {
-                    __builtin_amdgcn_raw_buffer_store_b128(
-                        u32x4{__builtin_bit_cast(uint32_t, o[0]), __builtin_bit_cast(uint32_t, o[1]),
-                              __builtin_bit_cast(uint32_t, o[2]), __builtin_bit_cast(uint32_t, o[3])},
-                        drs.r, (int)off, 0, 0);
+                    __builtin_amdgcn_raw_buffer_store_b128(u32x4{ov[0], ov[1], ov[2], ov[3]}, drs.r, (int)off, 0, 0);
                 }
             } else {
+                TOut* dq = reinterpret_cast<TOut*>(dp + (off - drs.delta));
 #pragma unroll
                 for (int q = 0; q < CC; ++q) dq[q] = o[q];
             }
         }
-    }
+    };
+
+    // Walk the band's source rows in order, D windows in flight; after row rr
+    // is in the ring, emit every output row whose last tap row is rr.  Row rr
+    // overwrites slot rr mod 8, whose row rr - 8 no pending output reads (an
+    // output's 8 rows are consecutive rows, clamped).  Every step issues its
+    // load (past the band's last row: the last row again), so the compiler's
+    // wait for window u leaves the D - 1 later windows in flight.
+    const int rs = max(lz_const(L.t.yofs, y0) - 3, 0);
+    const int re = min(lz_const(L.t.yofs, y1 - 1) + 4, h - 1);
+    auto walk = [&](auto safe_c) {
+        int y = __builtin_amdgcn_readfirstlane(y0);
+        int need = min(lz_const(L.t.yofs, y) + 4, h - 1);  // the last row output y taps
+        uint32_t buf[D][ND];
+#pragma unroll
+        for (int u = 0; u < D; ++u) load(safe_c, buf[u], min(rs + u, re));
+        for (int r = rs; r <= re; r += D) {
+#pragma unroll
+            for (int u = 0; u < D; ++u) {
+                const int rr = r + u;
+                if (rr <= re) {  // uniform
+                    hrow(buf[u], rr & 7);
+                    while (y < y1 && need == rr) {
+                        // y is wave-uniform; said so, its table reads are scalar
+                        // loads (as vector loads they would wait behind the windows)
+                        y = __builtin_amdgcn_readfirstlane(y);
+                        emit(y);
+                        ++y;
+                        if (y < y1) need = min(lz_const(L.t.yofs, y) + 4, h - 1);
+                    }
+                }
+                load(safe_c, buf[u], min(rr + D, re));
+            }
+        }
+    };
+    // uniform: can any lane's window of the band's last row overhang the plane?
+    const bool over = (uint32_t)re * rp + (wbyte & ~3u) + 4u * ND > slimit;
+    if (__builtin_amdgcn_ballot_w64(over) != 0) walk(std::integral_constant<bool, true>());
+    else walk(std::integral_constant<bool, false>());
 }
 
 // interpolateLanczos4 (imgwarp.cpp): float x, double sin / cos, float sums
@@ -446,6 +521,8 @@ hipError_t launch_t(const LanczosLaunch& A, const LzGrid& g, hipStream_t s) {
 
 int launch_resize_lanczos(const ResizeLaunch& R, double inv_x, double inv_y, hipStream_t s) {
     if (R.src.cc > 4) return VACV_ERR_UNSUPPORTED;
+    // the kernel reads each tap row as an 8-pixel window (narrower sources: unsupported)
+    if (R.src.w < 8) return VACV_ERR_UNSUPPORTED;
     LanczosLaunch A{};
     A.src = R.src;
     A.dst = R.dst;

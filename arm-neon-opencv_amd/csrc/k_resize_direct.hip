@@ -49,6 +49,10 @@ constexpr int kGroupPx = 256;  // pixels per LDS exchange round (4 per lane)
 #ifndef VACV_DIRECT_LAUX
 #define VACV_DIRECT_LAUX 0
 #endif
+// column-stationary lanes (resize_cols_kernel) for one-tap-row geometries
+#ifndef VACV_DIRECT_COLS
+#define VACV_DIRECT_COLS 1
+#endif
 
 // Pixels per lane: 8 when one tap row is gathered and the kernel still fits
 // 64 VGPRs (8 waves per SIMD) at 8, else 4 (measured: spills otherwise).
@@ -224,8 +228,159 @@ resize_direct_kernel(ResizeLaunch L, int blocks_per_plane, int total, int xcd) {
     }
 }
 
+// ---------------------------------------------------------------------------
+// resize_cols_kernel: one-tap-row geometries with COLUMN-stationary lanes.  A
+// wave owns a block of 64 output columns x 8 output rows; lane l keeps column
+// x0 + l for all 8 rows, so its horizontal tap (index, weights) is computed
+// once instead of per pixel, and the rows' vertical taps are computed once
+// per wave by lanes 0..7 in parallel and broadcast (readlane).  Per pixel
+// what is left is one address add, the gather and the blend.  A gather
+// instruction still reads one contiguous run of a source row (64 columns),
+// and the 8 x 64 results leave through the wave's LDS buffer as 16-byte
+// non-temporal stores, 4 rows at a time.  Same arithmetic as above.
+constexpr int kColsRows = 8;  // output rows per wave task
+template <int CC, int OUT, int MODE>
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8)))
+resize_cols_kernel(ResizeLaunch L, int col_blocks, int row_groups, int tasks) {
+    using TOut = typename std::conditional<(OUT == kOutSame), uint8_t, float>::type;
+    constexpr int kOutPx = CC * (int)sizeof(TOut);
+    constexpr int kHalf = kColsRows / 2;          // rows per LDS exchange round
+    constexpr int kRowB = 64 * kOutPx;             // output bytes of one block row
+    constexpr int kLoadAux = OUT == kOutSame ? VACV_LOAD_AUX : VACV_DIRECT_LAUX;
+    constexpr int kStoreAux = OUT == kOutSame ? VACV_STORE_AUX : VACV_DIRECT_SAUX;
+    __shared__ __attribute__((aligned(16))) unsigned char xch[4][kHalf * kRowB];
+    const int lane = (int)threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
+    const int task = (int)blockIdx.x * 4 + wave;   // (plane, row group, column block), column block fastest
+    if (task >= tasks) return;                     // whole wave
+    const int per_plane = col_blocks * row_groups;
+    const int pidx = task / per_plane;
+    const int rem = task - pidx * per_plane;
+    const int rg = rem / col_blocks, cb = rem - rg * col_blocks;
+    const int img = pidx / L.src.planes, plane = pidx - img * L.src.planes;
+    const int W = L.dst.w, H = L.dst.h;
+    const int x0 = cb * 64, y0 = rg * kColsRows;
+    const int ncol = min(64, W - x0);              // uniform
+    const int nrow = min(kColsRows, H - y0);       // uniform
+    const bool col_ok = lane < ncol;
+    const int x = col_ok ? x0 + lane : W - 1;
+
+    const unsigned char* sp = L.src.base + (int64_t)img * L.src.img_pitch + (int64_t)plane * L.src.plane_pitch;
+    const Rsrc srs = make_rsrc(sp, L.src.plane_bytes);
+    const uint32_t slimit = (uint32_t)L.src.plane_bytes + srs.delta;
+    const uint32_t rp = (uint32_t)L.src.row_pitch;
+
+    // the column's tap (once), the rows' taps (lanes 0..7, then broadcast)
+    const FixedTap tx = tap_of<MODE>(x, L.src.w, W, L.scale_xf, L.scale_xd);
+    const us2 wx = __builtin_bit_cast(us2, (uint32_t)tx.w0 | ((uint32_t)tx.w1 << 16));
+    const uint32_t xoff = (uint32_t)(tx.i * CC) + srs.delta;
+    uint32_t my_row = 0, my_w = 0;
+    if (lane < kColsRows) {
+        FixedTap ty = tap_of<MODE>(min(y0 + lane, H - 1), L.src.h, H, L.scale_yf, L.scale_yd);
+        if (ty.w0 == 0) { ty.i += 1; ty.w0 = ty.w1; ty.w1 = 0; }  // the weighted row (ONE_ROW)
+        my_row = (uint32_t)ty.i * rp;
+        my_w = (uint32_t)ty.w0;
+    }
+    uint32_t tap[kColsRows][2];
+#pragma unroll
+    for (int r = 0; r < kColsRows; ++r) {
+        const uint32_t ro = (uint32_t)__builtin_amdgcn_readlane((int)my_row, r);
+        const uint32_t o = ro + xoff;
+        tap[r][0] = tap[r][1] = 0u;
+        if (r < nrow) {
+            if (o + 8u <= slimit) {
+                load_taps<CC, false, kLoadAux>(srs, o, tap[r][0], tap[r][1]);
+            } else {  // the plane's last pixels: bytewise (an overhanging load reads zeros)
+                const unsigned char* b = sp + (int64_t)(o - srs.delta);
+#pragma unroll
+                for (int e = 0; e < 2 * CC; ++e) tap[r][e >> 2] |= (uint32_t)b[e] << (8 * (e & 3));
+            }
+        }
+    }
+    ChanNorm cn[CC] = {};
+    if (OUT == kOutNorm) {
+#pragma unroll
+        for (int k = 0; k < CC; ++k) cn[k] = chan_norm(L.norm, img, CC == 1 ? plane % L.norm.c_total : k);
+    }
+    unsigned char* dp = const_cast<unsigned char*>(L.dst.base) + (int64_t)img * L.dst.img_pitch +
+                        (int64_t)plane * L.dst.plane_pitch;
+    const Rsrc rd = make_rsrc(dp, L.dst.plane_bytes);
+    const bool full = ncol == 64;  // 16-byte chunks (the host checked the alignment)
+    TOut* xo = reinterpret_cast<TOut*>(xch[wave]);
+    const unsigned char* xs = xch[wave];
+#pragma unroll
+    for (int g = 0; g < 2; ++g) {
+#pragma unroll
+        for (int j = 0; j < kHalf; ++j) {
+            const int r = g * kHalf + j;
+            const uint32_t wA = (uint32_t)__builtin_amdgcn_readlane((int)my_w, r);
+#pragma unroll
+            for (int k = 0; k < CC; ++k) {
+                const uint32_t sel = (uint32_t)k | (0x0Cu << 8) | ((uint32_t)(CC + k) << 16) | (0x0Cu << 24);
+                const int v = blend_fixed<MODE>(__builtin_amdgcn_perm(tap[r][1], tap[r][0], sel), 0u, wx, wA, 0u);
+                TOut ov;
+                if (OUT == kOutSame) ov = (TOut)v;
+                else if (OUT == kOutF32) ov = (TOut)(float)v;
+                else ov = (TOut)normalize_u8v(cn[k], v);
+                xo[(j * 64 + lane) * CC + k] = ov;
+            }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        const int rows = min(kHalf, nrow - g * kHalf);  // uniform
+        if (rows > 0) {
+            const uint32_t base = (uint32_t)(y0 + g * kHalf) * (uint32_t)L.dst.row_pitch + (uint32_t)(x0 * kOutPx) +
+                                  rd.delta;
+            if (full) {
+                constexpr int kCpr = kRowB / 16;  // 16-byte chunks per block row
+                for (int c = lane; c < rows * kCpr; c += 64) {
+                    const int rr = c / kCpr, cc = c - rr * kCpr;
+                    __builtin_amdgcn_raw_buffer_store_b128(*reinterpret_cast<const u32x4*>(xs + 16 * c), rd.r,
+                                                           (int)(base + (uint32_t)rr * (uint32_t)L.dst.row_pitch + 16u * cc),
+                                                           0, kStoreAux);
+                }
+            } else {  // the image's last column block: bytes
+                const int rb = ncol * kOutPx;
+                for (int e = lane; e < rows * rb; e += 64) {
+                    const int rr = e / rb, cc = e - rr * rb;
+                    __builtin_amdgcn_raw_buffer_store_b8(xs[rr * kRowB + cc], rd.r,
+                                                         (int)(base + (uint32_t)rr * (uint32_t)L.dst.row_pitch + cc), 0,
+                                                         kStoreAux);
+                }
+            }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+}
+
+// The column kernel's grid, or false where it does not apply (it needs
+// 16-byte aligned block rows in the destination).
+bool cols_plan(const ResizeLaunch& L, int out_px, int& col_blocks, int& row_groups, int64_t& tasks) {
+    if (!VACV_DIRECT_COLS) return false;
+    const uintptr_t dbits = reinterpret_cast<uintptr_t>(L.dst.base) | (uintptr_t)L.dst.row_pitch |
+                            (uintptr_t)L.dst.img_pitch | (uintptr_t)L.dst.plane_pitch;
+    if ((dbits & 15) || (64 * out_px) % 16) return false;
+    col_blocks = (L.dst.w + 63) / 64;
+    row_groups = (L.dst.h + kColsRows - 1) / kColsRows;
+    tasks = (int64_t)col_blocks * row_groups * L.n * L.src.planes;
+    return tasks < 0x7FFFFFF0LL;
+}
+
 template <int CC, int OUT, int MODE, bool ONE_ROW>
 hipError_t launch_one(const ResizeLaunch& L, hipStream_t s) {
+    if constexpr (ONE_ROW) {
+        constexpr int kOutPx = CC * (OUT == kOutSame ? 1 : 4);
+        int col_blocks = 0, row_groups = 0;
+        int64_t tasks = 0;
+        if (cols_plan(L, kOutPx, col_blocks, row_groups, tasks)) {
+            hipLaunchKernelGGL((resize_cols_kernel<CC, OUT, MODE>), dim3((unsigned)((tasks + 3) / 4)), dim3(kBlock), 0, s,
+                               L, col_blocks, row_groups, (int)tasks);
+            return hipGetLastError();
+        }
+    }
     constexpr int kBlockPx = 4 * 64 * direct_pxl(CC, OUT, ONE_ROW);
     const int64_t P = (int64_t)L.dst.w * L.dst.h;
     const int64_t per_plane = (P + kBlockPx - 1) / kBlockPx;

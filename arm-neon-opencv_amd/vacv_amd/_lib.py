@@ -15,7 +15,9 @@ from pathlib import Path
 PKG_ROOT = Path(__file__).resolve().parent.parent          # arm-neon-opencv_amd/
 REPO_ROOT = PKG_ROOT.parent
 LIB_DIR = PKG_ROOT / "lib"
-HIP_LIB = LIB_DIR / "libvacv_hip.so"
+# VACV_LIB_DIR: another in-tree build of the same library (A/B variant
+# builds, tools/variants.sh); the default is lib/
+HIP_LIB = (Path(os.environ["VACV_LIB_DIR"]).resolve() if os.environ.get("VACV_LIB_DIR") else LIB_DIR) / "libvacv_hip.so"
 API_LIB = LIB_DIR / "libvacv.so"
 HEADER = REPO_ROOT / "include" / "vacv_hip.h"
 
