@@ -78,16 +78,25 @@ __device__ __forceinline__ constexpr int lz_pos(int j) {
     return j + SH < 0 ? 0 : (j + SH > 7 ? 7 : j + SH);
 }
 
-// u8: the window's bytes (after the byte shift) in ND - 1 dwords
-template <int CC, int SH>
-__device__ __forceinline__ void lz_h_u8(const uint32_t* wv, const int (&c)[8], int (&hv)[CC]) {
+// u8: the window's bytes (after the byte shift) in NW dwords; the 8 taps of a
+// channel as 4 packed-u16 pairs (v_perm_b32) against the coefficient pairs
+// (v_dot2_i32_i16): int sums, the order is immaterial
+typedef short sh2 __attribute__((ext_vector_type(2)));
+template <int CC, int SH, int NW>
+__device__ __forceinline__ void lz_h_u8(const uint32_t* wv, const uint32_t (&cp)[4], int (&hv)[CC]) {
 #pragma unroll
     for (int k = 0; k < CC; ++k) {
-        int v = 0;  // int sums: the order is immaterial
+        int v = 0;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            const int e = lz_pos<SH>(j) * CC + k;
-            v += (int)((wv[e >> 2] >> (8 * (e & 3))) & 0xFFu) * c[j];
+        for (int m = 0; m < 4; ++m) {
+            constexpr int dummy = 0;
+            (void)dummy;
+            const int e0 = lz_pos<SH>(2 * m) * CC + k, e1 = lz_pos<SH>(2 * m + 1) * CC + k;
+            const int q0 = e0 >> 2;
+            const uint32_t lo = wv[q0], hi = q0 + 1 < NW ? wv[q0 + 1] : 0u;
+            const uint32_t sel = (uint32_t)(e0 - 4 * q0) | (0x0Cu << 8) | ((uint32_t)(e1 - 4 * q0) << 16) | (0x0Cu << 24);
+            const uint32_t pr = __builtin_amdgcn_perm(hi, lo, sel);
+            v = __builtin_amdgcn_sdot2(__builtin_bit_cast(sh2, pr), __builtin_bit_cast(sh2, cp[m]), v, false);
         }
         hv[k] = v;
     }
@@ -160,6 +169,9 @@ __global__ void __launch_bounds__(kBlock) lanczos_kernel(LanczosLaunch L, int st
         if constexpr (U8) c[j] = (int)L.t.xai[8 * xc + j];
         else c[j] = L.t.xaf[8 * xc + j];
     }
+    uint32_t cp[4];  // u8: the coefficients as (c[2m], c[2m + 1]) short pairs
+#pragma unroll
+    for (int m = 0; m < 4; ++m) cp[m] = ((uint32_t)c[2 * m] & 0xFFFFu) | ((uint32_t)c[2 * m + 1] << 16);
     const uint32_t wbyte = (uint32_t)(wstart * CC * (int)sizeof(TIn)) + srs.delta;
     const uint32_t wsh = wbyte & 3u;  // u8: the window's byte offset in its first dword
 
@@ -206,15 +218,15 @@ __global__ void __launch_bounds__(kBlock) lanczos_kernel(LanczosLaunch L, int st
 #pragma unroll
             for (int q = 0; q < ND - 1; ++q) wv[q] = __builtin_amdgcn_alignbyte(d[q + 1], d[q], wsh);
             switch (shift) {  // divergent only in the strips at the image's edges
-                case -4: lz_h_u8<CC, -4>(wv, c, hv); break;
-                case -3: lz_h_u8<CC, -3>(wv, c, hv); break;
-                case -2: lz_h_u8<CC, -2>(wv, c, hv); break;
-                case -1: lz_h_u8<CC, -1>(wv, c, hv); break;
-                case 1: lz_h_u8<CC, 1>(wv, c, hv); break;
-                case 2: lz_h_u8<CC, 2>(wv, c, hv); break;
-                case 3: lz_h_u8<CC, 3>(wv, c, hv); break;
-                case 4: lz_h_u8<CC, 4>(wv, c, hv); break;
-                default: lz_h_u8<CC, 0>(wv, c, hv); break;
+                case -4: lz_h_u8<CC, -4, ND - 1>(wv, cp, hv); break;
+                case -3: lz_h_u8<CC, -3, ND - 1>(wv, cp, hv); break;
+                case -2: lz_h_u8<CC, -2, ND - 1>(wv, cp, hv); break;
+                case -1: lz_h_u8<CC, -1, ND - 1>(wv, cp, hv); break;
+                case 1: lz_h_u8<CC, 1, ND - 1>(wv, cp, hv); break;
+                case 2: lz_h_u8<CC, 2, ND - 1>(wv, cp, hv); break;
+                case 3: lz_h_u8<CC, 3, ND - 1>(wv, cp, hv); break;
+                case 4: lz_h_u8<CC, 4, ND - 1>(wv, cp, hv); break;
+                default: lz_h_u8<CC, 0, ND - 1>(wv, cp, hv); break;
             }
         } else {
             float wf[ND];
@@ -272,8 +284,13 @@ __global__ void __launch_bounds__(kBlock) lanczos_kernel(LanczosLaunch L, int st
             }
 #pragma unroll
             for (int q = 0; q < CC; ++q) {
-                const int s0 = hs[0][q] * bb[0] + hs[1][q] * bb[1] + hs[2][q] * bb[2] + hs[3][q] * bb[3];
-                const int s1 = hs[4][q] * bb[4] + hs[5][q] * bb[5] + hs[6][q] * bb[6] + hs[7][q] * bb[7];
+                // |h| < 2^23 (255 x sum |coefficient| <= 255 x ~2,900) and |b| < 2^12:
+                // 24-bit multiplies, whose low 32 bits are the int product
+                // (wrapping as OpenCV's int arithmetic does)
+                const int s0 = __mul24(hs[0][q], bb[0]) + __mul24(hs[1][q], bb[1]) + __mul24(hs[2][q], bb[2]) +
+                               __mul24(hs[3][q], bb[3]);
+                const int s1 = __mul24(hs[4][q], bb[4]) + __mul24(hs[5][q], bb[5]) + __mul24(hs[6][q], bb[6]) +
+                               __mul24(hs[7][q], bb[7]);
                 const int vi = min(max((s0 + s1 + (1 << 21)) >> 22, 0), 255);  // FixedPtCast<int, uchar, 22>
                 if (OUT == kOutSame) o[q] = (TOut)vi;
                 else if (OUT == kOutF32) o[q] = (TOut)(float)vi;

@@ -238,13 +238,17 @@ resize_direct_kernel(ResizeLaunch L, int blocks_per_plane, int total, int xcd) {
 // instruction still reads one contiguous run of a source row (64 columns),
 // and the 8 x 64 results leave through the wave's LDS buffer as 16-byte
 // non-temporal stores, 4 rows at a time.  Same arithmetic as above.
-constexpr int kColsRows = 8;  // output rows per wave task
-template <int CC, int OUT, int MODE>
+#ifndef VACV_COLS_ROWS
+#define VACV_COLS_ROWS 8
+#endif
+constexpr int kColsRows = VACV_COLS_ROWS;  // output rows per wave task (a multiple of 8)
+template <int CC, int OUT, int MODE, bool ONE_ROW>
 __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8)))
 resize_cols_kernel(ResizeLaunch L, int col_blocks, int row_groups, int tasks) {
+    constexpr int NR = ONE_ROW ? 1 : 2;           // gathered source rows per output row
     using TOut = typename std::conditional<(OUT == kOutSame), uint8_t, float>::type;
     constexpr int kOutPx = CC * (int)sizeof(TOut);
-    constexpr int kHalf = kColsRows / 2;          // rows per LDS exchange round
+    constexpr int kHalf = 4;                       // rows per LDS exchange round
     constexpr int kRowB = 64 * kOutPx;             // output bytes of one block row
     constexpr int kLoadAux = OUT == kOutSame ? VACV_LOAD_AUX : VACV_DIRECT_LAUX;
     constexpr int kStoreAux = OUT == kOutSame ? VACV_STORE_AUX : VACV_DIRECT_SAUX;
@@ -274,26 +278,31 @@ resize_cols_kernel(ResizeLaunch L, int col_blocks, int row_groups, int tasks) {
     const FixedTap tx = tap_of<MODE>(x, L.src.w, W, L.scale_xf, L.scale_xd);
     const us2 wx = __builtin_bit_cast(us2, (uint32_t)tx.w0 | ((uint32_t)tx.w1 << 16));
     const uint32_t xoff = (uint32_t)(tx.i * CC) + srs.delta;
-    uint32_t my_row = 0, my_w = 0;
+    uint32_t my_row = 0, my_w = 0;  // lane r < kColsRows: row r's first source row offset, weights (w0 | w1 << 16)
     if (lane < kColsRows) {
         FixedTap ty = tap_of<MODE>(min(y0 + lane, H - 1), L.src.h, H, L.scale_yf, L.scale_yd);
-        if (ty.w0 == 0) { ty.i += 1; ty.w0 = ty.w1; ty.w1 = 0; }  // the weighted row (ONE_ROW)
+        if (ONE_ROW && ty.w0 == 0) { ty.i += 1; ty.w0 = ty.w1; ty.w1 = 0; }  // the weighted row
         my_row = (uint32_t)ty.i * rp;
-        my_w = (uint32_t)ty.w0;
+        my_w = (uint32_t)ty.w0 | ((uint32_t)ty.w1 << 16);
     }
-    uint32_t tap[kColsRows][2];
+    uint32_t tap[kColsRows][NR][2];
 #pragma unroll
     for (int r = 0; r < kColsRows; ++r) {
         const uint32_t ro = (uint32_t)__builtin_amdgcn_readlane((int)my_row, r);
-        const uint32_t o = ro + xoff;
-        tap[r][0] = tap[r][1] = 0u;
-        if (r < nrow) {
-            if (o + 8u <= slimit) {
-                load_taps<CC, false, kLoadAux>(srs, o, tap[r][0], tap[r][1]);
-            } else {  // the plane's last pixels: bytewise (an overhanging load reads zeros)
-                const unsigned char* b = sp + (int64_t)(o - srs.delta);
+        const uint32_t wr = (uint32_t)__builtin_amdgcn_readlane((int)my_w, r);
 #pragma unroll
-                for (int e = 0; e < 2 * CC; ++e) tap[r][e >> 2] |= (uint32_t)b[e] << (8 * (e & 3));
+        for (int n = 0; n < NR; ++n) {
+            const uint32_t o = ro + (uint32_t)n * rp + xoff;
+            tap[r][n][0] = tap[r][n][1] = 0u;
+            // a row of zero weight is not read (its product is 0 either way)
+            if (r < nrow && (n == 0 ? (ONE_ROW || (wr & 0xFFFFu)) : (wr >> 16))) {
+                if (o + 8u <= slimit) {
+                    load_taps<CC, false, kLoadAux>(srs, o, tap[r][n][0], tap[r][n][1]);
+                } else {  // the plane's last pixels: bytewise (an overhanging load reads zeros)
+                    const unsigned char* b = sp + (int64_t)(o - srs.delta);
+#pragma unroll
+                    for (int e = 0; e < 2 * CC; ++e) tap[r][n][e >> 2] |= (uint32_t)b[e] << (8 * (e & 3));
+                }
             }
         }
     }
@@ -309,15 +318,18 @@ resize_cols_kernel(ResizeLaunch L, int col_blocks, int row_groups, int tasks) {
     TOut* xo = reinterpret_cast<TOut*>(xch[wave]);
     const unsigned char* xs = xch[wave];
 #pragma unroll
-    for (int g = 0; g < 2; ++g) {
+    for (int g = 0; g < kColsRows / kHalf; ++g) {
 #pragma unroll
         for (int j = 0; j < kHalf; ++j) {
             const int r = g * kHalf + j;
-            const uint32_t wA = (uint32_t)__builtin_amdgcn_readlane((int)my_w, r);
+            const uint32_t wr = (uint32_t)__builtin_amdgcn_readlane((int)my_w, r);
+            const uint32_t wA = wr & 0xFFFFu, wB = ONE_ROW ? 0u : wr >> 16;
 #pragma unroll
             for (int k = 0; k < CC; ++k) {
                 const uint32_t sel = (uint32_t)k | (0x0Cu << 8) | ((uint32_t)(CC + k) << 16) | (0x0Cu << 24);
-                const int v = blend_fixed<MODE>(__builtin_amdgcn_perm(tap[r][1], tap[r][0], sel), 0u, wx, wA, 0u);
+                const uint32_t top = __builtin_amdgcn_perm(tap[r][0][1], tap[r][0][0], sel);
+                const uint32_t bot = ONE_ROW ? 0u : __builtin_amdgcn_perm(tap[r][NR - 1][1], tap[r][NR - 1][0], sel);
+                const int v = blend_fixed<MODE>(top, bot, wx, wA, wB);
                 TOut ov;
                 if (OUT == kOutSame) ov = (TOut)v;
                 else if (OUT == kOutF32) ov = (TOut)(float)v;
@@ -371,13 +383,13 @@ bool cols_plan(const ResizeLaunch& L, int out_px, int& col_blocks, int& row_grou
 
 template <int CC, int OUT, int MODE, bool ONE_ROW>
 hipError_t launch_one(const ResizeLaunch& L, hipStream_t s) {
-    if constexpr (ONE_ROW) {
+    {
         constexpr int kOutPx = CC * (OUT == kOutSame ? 1 : 4);
         int col_blocks = 0, row_groups = 0;
         int64_t tasks = 0;
         if (cols_plan(L, kOutPx, col_blocks, row_groups, tasks)) {
-            hipLaunchKernelGGL((resize_cols_kernel<CC, OUT, MODE>), dim3((unsigned)((tasks + 3) / 4)), dim3(kBlock), 0, s,
-                               L, col_blocks, row_groups, (int)tasks);
+            hipLaunchKernelGGL((resize_cols_kernel<CC, OUT, MODE, ONE_ROW>), dim3((unsigned)((tasks + 3) / 4)), dim3(kBlock),
+                               0, s, L, col_blocks, row_groups, (int)tasks);
             return hipGetLastError();
         }
     }

@@ -197,10 +197,9 @@ hipError_t launch_warp_nearest(const WarpLaunch& L, hipStream_t s);
 // workgroup (k_warp_frames.hip)
 struct WarpFramesPlan {
     int th;                      // tile rows (16 or 32; 64 columns)
-    int S;                       // LDS bytes per staged source row (raw pixel bytes, a multiple of 16)
-    int rows_max;                // staged rows per LDS slot
+    int rows_max;                // largest tile source box (rows) of the geometry
     int ns;                      // LDS slots of the ring (boxes: one being sampled, ns - 1 in flight)
-    int slot;                    // bytes per slot (a 16-byte border head, rows in whole 1 KiB DMA units)
+    int slot;                    // bytes per slot (a 16-byte border head, compact row spans in whole 1 KiB DMA units)
     int lds;                     // dynamic LDS per workgroup
     int kf;                      // frames per workgroup (<= 0: chosen at launch)
     int dst_al;                  // destination dword-aligned (u8 quad stores)

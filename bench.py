@@ -6,7 +6,7 @@ resize_normalize, 1920x1080x3 u8 NHWC -> 640x360x3 fp32, INTER_LINEAR with
 the reference's arithmetic, mean (103.94,116.78,123.68) / std
 (57.375,57.12,58.395), a batch of --batch images per GPU resident in HBM.
 One step = one vacv_resize_normalize call over the whole per-GPU batch (one
-kernel launch: resize_direct_kernel, k_resize_direct.hip).  Metric = input-frame Mpixels/s over all GPUs ("at 1080p").
+kernel launch: resize_cols_kernel, k_resize_direct.hip).  Metric = input-frame Mpixels/s over all GPUs ("at 1080p").
 
 Other BASELINE configs (--workload; the default is the headline above):
   warp          cfg4: warp_affine INTER_LINEAR 1280x720x3 u8, scale 0.9, rot 15,
@@ -329,7 +329,7 @@ def make_workload(name: str, batch: int, dev, rank: int, world: int, ops) -> dic
     src = u8(B, H_IN, W_IN, C)
     dst = torch.empty((B, H_OUT, W_OUT, C), dtype=torch.float32, device=dev)
     return {"batch": B, "px": W_IN * H_IN, "b_alg": resize_bytes(W_IN, H_IN, C, W_OUT, H_OUT, 1, 4) * B,
-            "kernel": "resize_direct_kernel", "frame": "1920x1080x3", "output": "640x360x3 fp32",
+            "kernel": "resize_cols_kernel", "frame": "1920x1080x3", "output": "640x360x3 fp32",
             "desc": "resize_normalize INTER_LINEAR 1920x1080x3 u8 NHWC -> 640x360x3 fp32 "
                     "(reference arithmetic) + per-channel normalize",
             "main": lambda stream=None: ops.resize_normalize(src, W_OUT, H_OUT, MEAN, STD, out=dst, stream=stream)}
