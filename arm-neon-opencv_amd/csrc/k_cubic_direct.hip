@@ -263,58 +263,257 @@ cubic_direct_kernel(ResizeLaunch L, int blocks_per_plane) {
     }
 }
 
+// ---------------------------------------------------------------------------
+// cubic_cols_kernel: the same arithmetic with COLUMN-stationary lanes (as
+// resize_cols_kernel, k_resize_direct.hip).  A wave owns 64 output columns x
+// kCcRows output rows of one plane; lane l keeps column x0 + l, so its
+// horizontal tap (index and 4 coefficients) is computed once instead of per
+// pixel, and lanes 0..kCcRows-1 compute the rows' vertical taps in parallel
+// (broadcast by readlane: scalar weights, a scalar skip of zero-weight rows).
+// Per pixel and tap row one dword-aligned 16-byte load, as above; a load
+// instruction reads one contiguous run of a source row.  The 4 waves of a
+// workgroup are the column blocks of the same rows, in order (224 columns: one
+// workgroup = 4 full output rows); workgroups never straddle planes, so the
+// SUMS partials stay per workgroup and per image.  SUMS adds each value and
+// its square in fp64 per lane (exact squares), then as the kernel above.
+#ifndef VACV_CUBIC_COLS
+#define VACV_CUBIC_COLS 1
+#endif
+constexpr int kCcRows = 4;
+constexpr int cubic_cols_waves(int cc) { return cc == 1 ? 8 : 5; }
+template <int CC, int OUT, bool SUMS>
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(cubic_cols_waves(CC))))
+cubic_cols_kernel(ResizeLaunch L, int col_blocks, int plane_tasks, int blocks_per_plane) {
+    constexpr int kRowB = 64 * CC * 4;  // LDS bytes of one block row
+    __shared__ __attribute__((aligned(16))) float xch[4][kCcRows * 64 * CC];
+    __shared__ double wsum[SUMS ? 4 : 1][2 * CC];
+    const int lane = (int)threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
+    const int pidx = (int)blockIdx.x / blocks_per_plane;  // image * planes + plane
+    const int t = ((int)blockIdx.x - pidx * blocks_per_plane) * 4 + wave;
+    double d[2 * CC];
+#pragma unroll
+    for (int v = 0; v < 2 * CC; ++v) d[v] = 0.0;
+    if (t < plane_tasks) {  // uniform
+        const int rg = t / col_blocks, cb = t - rg * col_blocks;
+        const int img = pidx / L.src.planes, plane = pidx - img * L.src.planes;
+        const int W = L.dst.w, H = L.dst.h;
+        const int x0 = cb * 64, y0 = rg * kCcRows;
+        const int ncol = min(64, W - x0), nrow = min(kCcRows, H - y0);  // uniform
+        const bool col_ok = lane < ncol;
+        const int x = col_ok ? x0 + lane : W - 1;  // idle lanes repeat the last column
+
+        const unsigned char* sp = L.src.base + (int64_t)img * L.src.img_pitch + (int64_t)plane * L.src.plane_pitch;
+        const Rsrc srs = make_rsrc(sp, L.src.plane_bytes);
+        const uint32_t slimit = (uint32_t)L.src.plane_bytes + srs.delta;
+        const uint32_t rp = (uint32_t)L.src.row_pitch;  // plane < 2^31 bytes (kMaxPlaneBytes)
+        const uint32_t xoff = (uint32_t)((cubic_tap(x, L.src.w, L.scale_xd).i - 1) * CC) + srs.delta;
+        int my_i = 0;
+        float my_c[4] = {0.f, 0.f, 0.f, 0.f};
+        if (lane < kCcRows) {
+            const CubicTap ty = cubic_tap(min(y0 + lane, H - 1), L.src.h, L.scale_yd);
+            my_i = ty.i;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) my_c[q] = ty.c[q];
+        }
+
+        // ---- gathers: the 16 bytes at (row ty.i - 1 + q, column tx.i - 1) ----
+        uint32_t ch[kCcRows][4][4];
+#pragma unroll
+        for (int r = 0; r < kCcRows; ++r) {
+            const uint32_t ro = (uint32_t)(__builtin_amdgcn_readlane(my_i, r) - 1) * rp + xoff;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                ch[r][q][0] = ch[r][q][1] = ch[r][q][2] = ch[r][q][3] = 0u;
+                // a tap row of weight 0 is not read (as above: its term is 0)
+                const float cq = __uint_as_float((uint32_t)__builtin_amdgcn_readlane((int)__float_as_uint(my_c[q]), r));
+                if (r >= nrow || cq == 0.f) continue;  // uniform
+                const uint32_t a4 = (ro + (uint32_t)q * rp) & ~3u;
+                if (a4 + 16u <= slimit) {
+                    const auto v = __builtin_amdgcn_raw_buffer_load_b128(srs.r, (int)a4, 0, VACV_LOAD_AUX);
+                    ch[r][q][0] = v[0];
+                    ch[r][q][1] = v[1];
+                    ch[r][q][2] = v[2];
+                    ch[r][q][3] = v[3];
+                } else {  // the plane's last bytes: an overhanging load would read zeros
+                    const unsigned char* b = sp + ((int64_t)a4 - (int64_t)srs.delta);
+#pragma unroll
+                    for (int e = 0; e < 16; ++e)
+                        if (a4 + (uint32_t)e < slimit) ch[r][q][e >> 2] |= (uint32_t)b[e] << (8 * (e & 3));
+                }
+            }
+        }
+
+        ChanNorm cn[CC] = {};
+        if (OUT == kOutNorm) {
+#pragma unroll
+            for (int k = 0; k < CC; ++k) cn[k] = chan_norm(L.norm, img, CC == 1 ? plane % L.norm.c_total : k);
+        }
+        // the column's coefficients, recomputed after the loads (registers)
+        const CubicTap tx = cubic_tap(x, L.src.w, L.scale_xd);
+        float* xo = xch[wave];
+#pragma unroll
+        for (int r = 0; r < kCcRows; ++r) {
+            float cy[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+                cy[q] = __uint_as_float((uint32_t)__builtin_amdgcn_readlane((int)__float_as_uint(my_c[q]), r));
+            const uint32_t ro = (uint32_t)(__builtin_amdgcn_readlane(my_i, r) - 1) * rp + xoff;
+            float h[4][CC];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const uint32_t sh = (ro + (uint32_t)q * rp) & 3u;
+                const uint32_t wv[3] = {__builtin_amdgcn_alignbyte(ch[r][q][1], ch[r][q][0], sh),
+                                        __builtin_amdgcn_alignbyte(ch[r][q][2], ch[r][q][1], sh),
+                                        __builtin_amdgcn_alignbyte(ch[r][q][3], ch[r][q][2], sh)};
+#pragma unroll
+                for (int k = 0; k < CC; ++k) {
+                    float sv[4];
+#pragma unroll
+                    for (int m = 0; m < 4; ++m) {
+                        const int e = m * CC + k;
+                        sv[m] = (float)((wv[e >> 2] >> (8 * (e & 3))) & 0xFFu);
+                    }
+                    // resize_naive.cpp:325-328
+                    h[q][k] = sv[0] * tx.c[0] + sv[1] * tx.c[1] + sv[2] * tx.c[2] + sv[3] * tx.c[3];
+                }
+            }
+#pragma unroll
+            for (int k = 0; k < CC; ++k) {
+                // resize_naive.cpp:349-351
+                float v = h[0][k] * cy[0] + h[1][k] * cy[1] + h[2][k] * cy[2] + h[3][k] * cy[3];
+                if (OUT == kOutNorm) v = normalize_f(cn[k], v);
+                xo[(r * 64 + lane) * CC + k] = v;
+                if (SUMS && col_ok && r < nrow) {
+                    const double dv = (double)v;
+                    d[2 * k] += dv;
+                    d[2 * k + 1] += dv * dv;
+                }
+            }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        // ---- LDS -> HBM: nrow rows of ncol * CC floats (the host checked the
+        // destination's 16-byte alignment) ----------------------------------------
+        unsigned char* dp = const_cast<unsigned char*>(L.dst.base) + (int64_t)img * L.dst.img_pitch +
+                            (int64_t)plane * L.dst.plane_pitch;
+        const Rsrc rd = make_rsrc(dp, L.dst.plane_bytes);
+        const uint32_t rowp = (uint32_t)L.dst.row_pitch;
+        const uint32_t base = (uint32_t)y0 * rowp + (uint32_t)(x0 * CC * 4) + rd.delta;
+        const unsigned char* xs = reinterpret_cast<const unsigned char*>(xch[wave]);
+        const int rb = ncol * CC * 4;  // bytes of one block row
+        if ((rb & 15) == 0) {
+            const int cpr = rb >> 4;
+            for (int c = lane; c < nrow * cpr; c += 64) {
+                const int rr = c / cpr, cc = c - rr * cpr;
+                __builtin_amdgcn_raw_buffer_store_b128(*reinterpret_cast<const u32x4*>(xs + rr * kRowB + 16 * cc), rd.r,
+                                                       (int)(base + (uint32_t)rr * rowp + 16u * (uint32_t)cc), 0,
+                                                       VACV_STORE_AUX);
+            }
+        } else {
+            for (int e = lane; e < nrow * rb; e += 64) {
+                const int rr = e / rb, cc = e - rr * rb;
+                __builtin_amdgcn_raw_buffer_store_b8(xs[rr * kRowB + cc], rd.r, (int)(base + (uint32_t)rr * rowp + cc), 0,
+                                                     VACV_STORE_AUX);
+            }
+        }
+    }
+    if (SUMS) {
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+#pragma unroll
+            for (int v = 0; v < 2 * CC; ++v) d[v] += __shfl_xor(d[v], o, 64);
+        }
+        if (lane == 0) {
+#pragma unroll
+            for (int v = 0; v < 2 * CC; ++v) wsum[wave][v] = d[v];
+        }
+        __syncthreads();
+        if (wave == 0 && lane < 2 * CC) {
+            // value-major [CC][2][image][workgroup], as above
+            const int64_t groups = (int64_t)L.n * blocks_per_plane;
+            double a = 0.0;
+#pragma unroll
+            for (int w = 0; w < 4; ++w) a += wsum[w][lane];
+            L.sum_partials[lane * groups + blockIdx.x] = a;
+        }
+    }
+}
+
+// The column kernel's grid, or false where it does not apply (16-byte aligned
+// destination rows, the tuning knob).
+bool cubic_cols_plan(const ResizeLaunch& L, int& col_blocks, int& plane_tasks, int& blocks_per_plane) {
+    if (!VACV_CUBIC_COLS || tune(VACV_TUNE_CUBIC_DIRECT) == 2) return false;  // 2: the gather kernel (A/B)
+    const uintptr_t dbits = reinterpret_cast<uintptr_t>(L.dst.base) | (uintptr_t)L.dst.row_pitch |
+                            (uintptr_t)L.dst.img_pitch | (uintptr_t)L.dst.plane_pitch;
+    if (dbits & 15) return false;
+    const int64_t cbk = (L.dst.w + 63) / 64;
+    const int64_t tasks = cbk * ((L.dst.h + kCcRows - 1) / kCcRows);
+    const int64_t bpp = (tasks + 3) / 4;
+    if (tasks > 0x7FFFFFF0LL || bpp * L.n * L.src.planes > 0x7FFFFFF0LL) return false;
+    col_blocks = (int)cbk;
+    plane_tasks = (int)tasks;
+    blocks_per_plane = (int)bpp;
+    return true;
+}
+
 // The fixed-order sum of the per-workgroup partials and, optionally, the
 // population mean / stddev (stats_kernel's formula, k_pixel.hip): one
 // 1024-thread workgroup per (group, channel) sums both of the channel's
-// values -- thread t adds terms t, t + 1024, ... in order (8 loads issued
-// ahead of their adds), then a fixed LDS tree -- so the statistics need no
-// communication between workgroups (cfg5: 12,544 terms per value, 3
-// workgroups; round 3's per-wave partials took 16 split workgroups per value,
+// values.  Thread t adds terms t, t + 1024, ... in order, issuing a batch of
+// kSumDepth loads (clamped to the run, zeroed past it) before any add, so a
+// batch costs one memory latency (cfg5: 12,544 terms per value = one batch);
+// then each wave reduces in a fixed xor-shuffle order and thread 0 adds the
+// 16 wave sums in order: deterministic run to run, no communication between
+// workgroups (round 3's per-wave partials took 16 split workgroups per value,
 // an agent-scope counter and a separate stats launch).
 constexpr int kSumThreads = 1024;
+constexpr int kSumDepth = 16;
 __global__ void __launch_bounds__(kSumThreads) group_sums_kernel(const double* partials, int groups, int n, int cc,
                                                                 int per_image, double count, double* sums,
                                                                 float* mean, float* stddev) {
-    __shared__ double red[2][kSumThreads];
+    __shared__ double red[2][kSumThreads / 64];
     const int g = blockIdx.x / cc;  // output group (image, or 0)
     const int k = blockIdx.x - g * cc;
-    const int64_t run = per_image ? groups : (int64_t)n * groups;  // terms of this (group, value)
+    const int64_t run = per_image ? groups : (int64_t)n * groups;  // terms of this (group, value), >= 1
     const int64_t vstride = (int64_t)n * groups;
     const double* p1 = partials + (int64_t)(2 * k) * vstride + (per_image ? (int64_t)g * groups : 0);
     const double* p2 = p1 + vstride;
-    constexpr int kDepth = 8;
     double a1 = 0.0, a2 = 0.0;
-    int64_t t = threadIdx.x;
-    for (; t + (kDepth - 1) * kSumThreads < run; t += kDepth * kSumThreads) {
-        double x[kDepth], y[kDepth];
+    for (int64_t b = threadIdx.x; b < run; b += (int64_t)kSumDepth * kSumThreads) {
+        double x[kSumDepth], y[kSumDepth];
 #pragma unroll
-        for (int q = 0; q < kDepth; ++q) {
-            x[q] = p1[t + (int64_t)q * kSumThreads];
-            y[q] = p2[t + (int64_t)q * kSumThreads];
+        for (int q = 0; q < kSumDepth; ++q) {
+            const int64_t t = min(b + (int64_t)q * kSumThreads, run - 1);
+            x[q] = p1[t];
+            y[q] = p2[t];
         }
 #pragma unroll
-        for (int q = 0; q < kDepth; ++q) {
-            a1 += x[q];
-            a2 += y[q];
+        for (int q = 0; q < kSumDepth; ++q) {
+            const bool ok = b + (int64_t)q * kSumThreads < run;
+            a1 += ok ? x[q] : 0.0;
+            a2 += ok ? y[q] : 0.0;
         }
     }
-    for (; t < run; t += kSumThreads) {
-        a1 += p1[t];
-        a2 += p2[t];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        a1 += __shfl_xor(a1, o, 64);
+        a2 += __shfl_xor(a2, o, 64);
     }
-    red[0][threadIdx.x] = a1;
-    red[1][threadIdx.x] = a2;
+    const int wave = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) {
+        red[0][wave] = a1;
+        red[1][wave] = a2;
+    }
     __syncthreads();
-    for (int h = kSumThreads / 2; h > 0; h >>= 1) {
-        if ((int)threadIdx.x < h) {
-            red[0][threadIdx.x] += red[0][threadIdx.x + h];
-            red[1][threadIdx.x] += red[1][threadIdx.x + h];
-        }
-        __syncthreads();
-    }
     if (threadIdx.x == 0) {
+        double s1 = 0.0, s2 = 0.0;
+        for (int w = 0; w < kSumThreads / 64; ++w) {
+            s1 += red[0][w];
+            s2 += red[1][w];
+        }
         const int idx = g * cc + k;
-        const double s1 = red[0][0], s2 = red[1][0];
         sums[2 * idx] = s1;
         sums[2 * idx + 1] = s2;
         if (mean) {
@@ -329,28 +528,45 @@ __global__ void __launch_bounds__(kSumThreads) group_sums_kernel(const double* p
 
 template <int CC>
 hipError_t launch_cc(const ResizeLaunch& L, hipStream_t s) {
-    constexpr int kBlockPx = 4 * kWavePx;
-    const int64_t P = (int64_t)L.dst.w * L.dst.h;
-    const int64_t per_plane = (P + kBlockPx - 1) / kBlockPx;
-    const int64_t total = per_plane * L.n * L.src.planes;
-    if (P >= 0x7FFFFFFF - kBlockPx || total > 0x7FFFFFF0LL) return hipErrorInvalidValue;
-    if (L.out == kOutNorm)
-        hipLaunchKernelGGL((cubic_direct_kernel<CC, kOutNorm, false>), dim3((unsigned)total), dim3(64, 4), 0, s, L,
-                           (int)per_plane);
-    else if (L.sum_partials) {
-        hipLaunchKernelGGL((cubic_direct_kernel<CC, kOutF32, true>), dim3((unsigned)total), dim3(64, 4), 0, s, L,
-                           (int)per_plane);
-        const hipError_t e = hipGetLastError();
-        if (e != hipSuccess) return e;
-        const int blocks = (L.sum_per_image ? L.n : 1) * CC;
-        const double count = (double)P * (L.sum_per_image ? 1 : L.n);
-        hipLaunchKernelGGL(group_sums_kernel, dim3((unsigned)blocks), dim3(kSumThreads), 0, s,
-                           (const double*)L.sum_partials, (int)per_plane, L.n, CC, L.sum_per_image, count,
-                           L.sum_out, L.sum_mean, L.sum_std);
+    const bool sums = L.out == kOutF32 && L.sum_partials;
+    int groups = 0;  // workgroups per plane
+    int col_blocks = 0, plane_tasks = 0;
+    if (cubic_cols_plan(L, col_blocks, plane_tasks, groups)) {
+        const dim3 grid((unsigned)((int64_t)groups * L.n * L.src.planes));
+        if (L.out == kOutNorm)
+            hipLaunchKernelGGL((cubic_cols_kernel<CC, kOutNorm, false>), grid, dim3(kBlock), 0, s, L, col_blocks,
+                               plane_tasks, groups);
+        else if (sums)
+            hipLaunchKernelGGL((cubic_cols_kernel<CC, kOutF32, true>), grid, dim3(kBlock), 0, s, L, col_blocks,
+                               plane_tasks, groups);
+        else
+            hipLaunchKernelGGL((cubic_cols_kernel<CC, kOutF32, false>), grid, dim3(kBlock), 0, s, L, col_blocks,
+                               plane_tasks, groups);
+    } else {
+        constexpr int kBlockPx = 4 * kWavePx;
+        const int64_t P = (int64_t)L.dst.w * L.dst.h;
+        const int64_t per_plane = (P + kBlockPx - 1) / kBlockPx;
+        const int64_t total = per_plane * L.n * L.src.planes;
+        if (P >= 0x7FFFFFFF - kBlockPx || total > 0x7FFFFFF0LL) return hipErrorInvalidValue;
+        groups = (int)per_plane;
+        if (L.out == kOutNorm)
+            hipLaunchKernelGGL((cubic_direct_kernel<CC, kOutNorm, false>), dim3((unsigned)total), dim3(64, 4), 0, s, L,
+                               groups);
+        else if (sums)
+            hipLaunchKernelGGL((cubic_direct_kernel<CC, kOutF32, true>), dim3((unsigned)total), dim3(64, 4), 0, s, L,
+                               groups);
+        else
+            hipLaunchKernelGGL((cubic_direct_kernel<CC, kOutF32, false>), dim3((unsigned)total), dim3(64, 4), 0, s, L,
+                               groups);
     }
-    else
-        hipLaunchKernelGGL((cubic_direct_kernel<CC, kOutF32, false>), dim3((unsigned)total), dim3(64, 4), 0, s, L,
-                           (int)per_plane);
+    if (!sums) return hipGetLastError();
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    const int blocks = (L.sum_per_image ? L.n : 1) * CC;
+    const double count = (double)L.dst.w * L.dst.h * (L.sum_per_image ? 1 : L.n);
+    hipLaunchKernelGGL(group_sums_kernel, dim3((unsigned)blocks), dim3(kSumThreads), 0, s,
+                       (const double*)L.sum_partials, groups, L.n, CC, L.sum_per_image, count, L.sum_out, L.sum_mean,
+                       L.sum_std);
     return hipGetLastError();
 }
 
@@ -362,9 +578,17 @@ bool cubic_direct_applies(const ResizeLaunch& L) {
 }
 
 int cubic_direct_groups(const ResizeLaunch& L) {
+    int col_blocks = 0, plane_tasks = 0, groups = 0;
+    if (cubic_cols_plan(L, col_blocks, plane_tasks, groups)) return groups;
     constexpr int kBlockPx = 4 * kWavePx;
     const int64_t P = (int64_t)L.dst.w * L.dst.h;
     return (int)((P + kBlockPx - 1) / kBlockPx);
+}
+
+int64_t cubic_sums_groups_bound(int w, int h) {
+    const int64_t gather = ((int64_t)w * h + 4 * kWavePx - 1) / (4 * kWavePx);
+    const int64_t cols = (((int64_t)(w + 63) / 64) * ((h + kCcRows - 1) / kCcRows) + 3) / 4;
+    return gather > cols ? gather : cols;
 }
 
 hipError_t launch_cubic_direct(const ResizeLaunch& L, hipStream_t s) {

@@ -314,7 +314,8 @@ warp_ring_kernel(WarpLaunch L, int gx, int gy, int kf, int ns, int slot, int dst
             const uint32_t bot = 16u + 16u * (uint32_t)(tab_pre[r + 1] + ch - tab_lo[r + 1]) + (uint32_t)(byte & 15);
             rw[j] = top | (bot << 16);
         }
-        wxp[j] = ok ? vwa[j] : (2048u | (8192u << 16));  // outside: (2048, 0) x (8192, 0)
+        // weights for every pixel with taps (the unstaged path samples from memory)
+        wxp[j] = ((okm >> j) & 1u) ? vwa[j] : (2048u | (8192u << 16));  // outside: (2048, 0) x (8192, 0)
     }
 
     // this lane's DMA source offsets (frame-relative), frame-independent:
@@ -395,8 +396,9 @@ warp_ring_kernel(WarpLaunch L, int gx, int gy, int kf, int ns, int slot, int dst
         const bool inside = FULL || (x < L.dst.w && y < L.dst.h);
         unsigned char* dbase = const_cast<unsigned char*>(L.dst.base) + frame_off(f, L.dst);
         const Rsrc drs = make_rsrc(dbase, L.dst.plane_bytes);
-        const us2 wx = __builtin_bit_cast(us2, wxp[j]);
-        const uint32_t wA = rw[j] >> 16, wB = 8192u - (rw[j] >> 16);
+        const uint32_t v0 = wxp[j] & 0xFFFFu;  // (v0, 2048 - v0) x (wA, 8192 - wA)
+        const us2 wx = __builtin_bit_cast(us2, v0 | ((2048u - v0) << 16));
+        const uint32_t wA = wxp[j] >> 16, wB = 8192u - wA;
         uint32_t vv[CC];
 #pragma unroll
         for (int k = 0; k < CC; ++k) {
@@ -407,6 +409,8 @@ warp_ring_kernel(WarpLaunch L, int gx, int gy, int kf, int ns, int slot, int dst
             const uint32_t ht = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, top), wx, 0u, false);
             const uint32_t hb = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, bot), wx, 0u, false);
             vv[k] = __umul24(ht, wA) + __umul24(hb, wB);  // warp_affine_naive.cpp:50-54, x4
+            if (VACV_RING_DBG & 8) vv[k] = ((tlo >> (8 * k)) & 0xFFu) << 24;  // diagnosis: the top-left tap itself
+            if (VACV_RING_DBG & 16) vv[k] = ((blo >> (8 * k)) & 0xFFu) << 24;  // diagnosis: the bottom-left tap
         }
         const uint32_t drow = (uint32_t)y * dpitch + drs.delta;
         if constexpr (OUT == kOutSame) {

@@ -907,13 +907,12 @@ int resize_sums(const vacv_image* src_d, const vacv_image* dst_d, int interpolat
     if ((st = load(dst_d, dst))) return st;
     if (interpolation == VACV_INTER_CUBIC && src.dtype == VACV_INT8 && dst.dtype == VACV_FP32 &&
         dst.layout == VACV_NHWC && dst.c <= 3 && dense(dst) && src.n == dst.n) {
-        const int64_t P = (int64_t)dst.w * dst.h;
-        const int64_t groups = (P + 511) / 512;  // cubic_direct_groups() for this size
+        const int64_t groups = cubic_sums_groups_bound(dst.w, dst.h);  // the workspace's bound
         void* ws = nullptr;
         if ((st = workspace(s, (size_t)(dst.n * groups * 2 * dst.c) * sizeof(double), &ws))) return st;
         FusedSums fs{static_cast<double*>(ws), sums, per_image ? 1 : 0, mean, stddev, 0, false};
         if ((st = resize_impl(src_d, dst_d, interpolation, mode, kOutSame, nullptr, s, 0.0, 0.0, &fs))) return st;
-        if (fs.used) return fs.groups == groups ? VACV_OK : VACV_ERR_HIP;  // (a layout mismatch cannot happen)
+        if (fs.used) return fs.groups <= groups ? VACV_OK : VACV_ERR_HIP;  // (a layout mismatch cannot happen)
     } else if ((st = resize_impl(src_d, dst_d, interpolation, mode, kOutSame, nullptr, s))) {
         return st;
     }

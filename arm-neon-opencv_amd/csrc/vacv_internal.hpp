@@ -176,6 +176,7 @@ int release_lanczos_tables();
 bool cubic_direct_applies(const ResizeLaunch& L);
 hipError_t launch_cubic_direct(const ResizeLaunch& L, hipStream_t s);
 int cubic_direct_groups(const ResizeLaunch& L);  // workgroups per output plane (the sum_partials layout)
+int64_t cubic_sums_groups_bound(int w, int h);  // >= cubic_direct_groups() for any w x h output
 
 struct WarpLaunch {
     PlaneGeom src;

@@ -322,7 +322,7 @@ def make_workload(name: str, batch: int, dev, rank: int, world: int, ops) -> dic
                 stats["sums"] = global_sums(stats["sums"])
                 stats["mean"], stats["std"] = ops.stats_from_sums(stats["sums"], count, stream=stream)
         return {"batch": B, "px": 2560 * 1440, "b_alg": B * resize_bytes(2560, 1440, 3, 224, 224, 1, 4, cubic=True),
-                "kernel": "cubic_direct_kernel", "frame": "2560x1440x3", "output": "224x224x3 fp32 + global mean/std",
+                "kernel": "cubic_cols_kernel", "frame": "2560x1440x3", "output": "224x224x3 fp32 + global mean/std",
                 "desc": "resize INTER_CUBIC 2560x1440x3 u8 -> 224x224x3 fp32 + global mean_stddev (RCCL all-reduce)",
                 "main": main, "extra": extra, "stats": stats, "inputs": src}
     B = batch or 256

@@ -145,6 +145,10 @@ def main():
         o = torch.empty((n, 224, 224, 3), dtype=torch.float32, device=dev)
         cases["cubic_1440p_224_u8_f32"] = (lambda src=src, o=o: ops.resize(src, 224, 224, interpolation=vacv_amd.INTER_CUBIC, out=o),
                                            n * resize_bytes(2560, 1440, 3, 224, 224, 1, 4, cubic=True), n * 2560 * 1440)
+        cases["cubic_stats_1440p_224"] = (
+            lambda src=src, o=o: ops.resize_mean_stddev(src, 224, 224, interpolation=vacv_amd.INTER_CUBIC,
+                                                        per_image=False, out=o),
+            n * resize_bytes(2560, 1440, 3, 224, 224, 1, 4, cubic=True), n * 2560 * 1440)
     if a.op in ("match", "all"):
         # correlation MACs: (W-w+1)(H-h+1) * w*h*c; bytes: image + result
         n = a.batch or 8
