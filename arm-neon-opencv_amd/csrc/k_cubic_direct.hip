@@ -263,6 +263,28 @@ cubic_direct_kernel(ResizeLaunch L, int blocks_per_plane) {
     }
 }
 
+// ---- the column kernel's statistics: fixed-point integer sums -----------------
+// Each workgroup rounds its fp64 (Sum x, Sum x^2) to integers in units of
+// 2^-q1 / 2^-q2 and adds them to its image's int64 accumulators with
+// fire-and-forget agent-scope atomics: integer addition is associative, so
+// the totals are the same bits whatever the order the workgroups finish in
+// (deterministic without a fixed reduction order, no partials buffer, no
+// waiting).  q1 / q2 leave 2 bits of headroom over the largest possible total
+// (|v| < 2^10: a u8 source through Keys cubic weights, fixed_shifts()), so the
+// integers never overflow; each workgroup's rounding is <= 2^-(q + 1), e.g.
+// cfg5: q1 = 29, q2 = 19, i.e. <= 7e-6 and <= 7e-3 absolute over the batch's
+// 7,168 workgroups on totals of ~1e9 and ~1e11.  fixed_sums_kernel (one
+// workgroup) then converts, derives mean / stddev and zeroes the accumulators.
+// (Finishing inside the cubic launch instead -- write-through partials, an
+// arrival counter, the last workgroup reducing -- measured +10 us of kernel
+// time: every workgroup's wave 0 waited out a store drain and an atomic's
+// round trip.)
+__device__ __forceinline__ void acc_add(int64_t* p, double v, int q) {
+    const long long x = __double2ll_rn(ldexp(v, q));
+    __hip_atomic_fetch_add((__attribute__((address_space(1))) unsigned long long*)p, (unsigned long long)x,
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // ---------------------------------------------------------------------------
 // cubic_cols_kernel: the same arithmetic with COLUMN-stationary lanes (as
 // resize_cols_kernel, k_resize_direct.hip).  A wave owns 64 output columns x
@@ -279,7 +301,13 @@ cubic_direct_kernel(ResizeLaunch L, int blocks_per_plane) {
 #ifndef VACV_CUBIC_COLS
 #define VACV_CUBIC_COLS 1
 #endif
-constexpr int kCcRows = 4;
+#ifndef VACV_CUBIC_ROWS
+#define VACV_CUBIC_ROWS 4
+#endif
+#ifndef VACV_CUBIC_SAUX
+#define VACV_CUBIC_SAUX VACV_STORE_AUX
+#endif
+constexpr int kCcRows = VACV_CUBIC_ROWS;  // output rows per wave task
 constexpr int cubic_cols_waves(int cc) { return cc == 1 ? 8 : 5; }
 template <int CC, int OUT, bool SUMS>
 __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(cubic_cols_waves(CC))))
@@ -409,13 +437,13 @@ cubic_cols_kernel(ResizeLaunch L, int col_blocks, int plane_tasks, int blocks_pe
                 const int rr = c / cpr, cc = c - rr * cpr;
                 __builtin_amdgcn_raw_buffer_store_b128(*reinterpret_cast<const u32x4*>(xs + rr * kRowB + 16 * cc), rd.r,
                                                        (int)(base + (uint32_t)rr * rowp + 16u * (uint32_t)cc), 0,
-                                                       VACV_STORE_AUX);
+                                                       VACV_CUBIC_SAUX);
             }
         } else {
             for (int e = lane; e < nrow * rb; e += 64) {
                 const int rr = e / rb, cc = e - rr * rb;
                 __builtin_amdgcn_raw_buffer_store_b8(xs[rr * kRowB + cc], rd.r, (int)(base + (uint32_t)rr * rowp + cc), 0,
-                                                     VACV_STORE_AUX);
+                                                     VACV_CUBIC_SAUX);
             }
         }
     }
@@ -430,13 +458,18 @@ cubic_cols_kernel(ResizeLaunch L, int col_blocks, int plane_tasks, int blocks_pe
             for (int v = 0; v < 2 * CC; ++v) wsum[wave][v] = d[v];
         }
         __syncthreads();
-        if (wave == 0 && lane < 2 * CC) {
-            // value-major [CC][2][image][workgroup], as above
-            const int64_t groups = (int64_t)L.n * blocks_per_plane;
+        if (wave == 0) {
             double a = 0.0;
+            if (lane < 2 * CC) {
 #pragma unroll
-            for (int w = 0; w < 4; ++w) a += wsum[w][lane];
-            L.sum_partials[lane * groups + blockIdx.x] = a;
+                for (int w = 0; w < 4; ++w) a += wsum[w][lane];
+            }
+            if (L.sum_acc) {
+                if (lane < 2 * CC) acc_add(L.sum_acc + (int64_t)pidx * 2 * CC + lane, a, (lane & 1) ? L.sum_q2 : L.sum_q1);
+            } else if (lane < 2 * CC) {
+                // value-major [CC][2][image][workgroup], as above (group_sums_kernel)
+                L.sum_partials[lane * (int64_t)L.n * blocks_per_plane + blockIdx.x] = a;
+            }
         }
     }
 }
@@ -526,21 +559,89 @@ __global__ void __launch_bounds__(kSumThreads) group_sums_kernel(const double* p
     }
 }
 
+// The accumulators -> sums (fp64), optionally mean / stddev (stats_kernel's
+// formula); zeroes the accumulators for the next call.  One workgroup: wave w
+// takes values w, w + 4, ... of the n x 2cc; per_image: one value per lane.
+// Batch totals: a wave sums one value's n images (integers: any order).
+__global__ void __launch_bounds__(kBlock) fixed_sums_kernel(int64_t* acc, int n, int cc, int per_image, int q1,
+                                                            int q2, double count, double* sums, float* mean,
+                                                            float* stddev) {
+    const int lane = (int)threadIdx.x & 63, wave = (int)threadIdx.x >> 6;
+    const int nv = 2 * cc;
+    if (per_image) {
+        for (int i = (int)threadIdx.x; i < n * nv; i += kBlock) {
+            const int64_t x = acc[i];
+            acc[i] = 0;
+            sums[i] = ldexp((double)x, -((i & 1) ? q2 : q1));
+        }
+        __syncthreads();
+        if (mean) {
+            for (int i = (int)threadIdx.x; i < n * cc; i += kBlock) {
+                const double m = sums[2 * i] / count;
+                double var = sums[2 * i + 1] / count - m * m;
+                if (var < 0) var = 0;
+                mean[i] = (float)m;
+                stddev[i] = (float)sqrt(var);
+            }
+        }
+        return;
+    }
+    __shared__ double tot[2 * kMaxC];
+    for (int v = wave; v < nv; v += kBlock / 64) {
+        int64_t a = 0;
+        for (int g = lane; g < n; g += 64) {
+            a += acc[(int64_t)g * nv + v];
+            acc[(int64_t)g * nv + v] = 0;
+        }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) a += __shfl_xor(a, o, 64);
+        if (lane == 0) {
+            tot[v] = ldexp((double)a, -((v & 1) ? q2 : q1));
+            sums[v] = tot[v];
+        }
+    }
+    __syncthreads();
+    if (mean && (int)threadIdx.x < cc) {
+        const int k = (int)threadIdx.x;
+        const double m = tot[2 * k] / count;
+        double var = tot[2 * k + 1] / count - m * m;
+        if (var < 0) var = 0;
+        mean[k] = (float)m;
+        stddev[k] = (float)sqrt(var);
+    }
+}
+
+// The fixed-point units (fixed_sums_kernel): the batch's total of |v| < 2^10
+// (Sum x) or v^2 < 2^20 (Sum x^2) over n * P values stays below 2^61.
+void fixed_shifts(int64_t values, int& q1, int& q2) {
+    int lg = 0;
+    while (lg < 62 && (int64_t(1) << lg) < values) ++lg;
+    q1 = 61 - 10 - lg;
+    q2 = 61 - 20 - lg;
+}
+
 template <int CC>
 hipError_t launch_cc(const ResizeLaunch& L, hipStream_t s) {
     const bool sums = L.out == kOutF32 && L.sum_partials;
     int groups = 0;  // workgroups per plane
     int col_blocks = 0, plane_tasks = 0;
-    if (cubic_cols_plan(L, col_blocks, plane_tasks, groups)) {
+    const bool cols = cubic_cols_plan(L, col_blocks, plane_tasks, groups);
+    ResizeLaunch La = L;
+    if (!cols || !sums) La.sum_acc = nullptr;
+    if (La.sum_acc) {
+        fixed_shifts((int64_t)L.n * L.dst.w * L.dst.h, La.sum_q1, La.sum_q2);
+        if (La.sum_q2 < 0) La.sum_acc = nullptr;  // enormous batches: partials and group_sums
+    }
+    if (cols) {
         const dim3 grid((unsigned)((int64_t)groups * L.n * L.src.planes));
         if (L.out == kOutNorm)
-            hipLaunchKernelGGL((cubic_cols_kernel<CC, kOutNorm, false>), grid, dim3(kBlock), 0, s, L, col_blocks,
+            hipLaunchKernelGGL((cubic_cols_kernel<CC, kOutNorm, false>), grid, dim3(kBlock), 0, s, La, col_blocks,
                                plane_tasks, groups);
         else if (sums)
-            hipLaunchKernelGGL((cubic_cols_kernel<CC, kOutF32, true>), grid, dim3(kBlock), 0, s, L, col_blocks,
+            hipLaunchKernelGGL((cubic_cols_kernel<CC, kOutF32, true>), grid, dim3(kBlock), 0, s, La, col_blocks,
                                plane_tasks, groups);
         else
-            hipLaunchKernelGGL((cubic_cols_kernel<CC, kOutF32, false>), grid, dim3(kBlock), 0, s, L, col_blocks,
+            hipLaunchKernelGGL((cubic_cols_kernel<CC, kOutF32, false>), grid, dim3(kBlock), 0, s, La, col_blocks,
                                plane_tasks, groups);
     } else {
         constexpr int kBlockPx = 4 * kWavePx;
@@ -562,6 +663,12 @@ hipError_t launch_cc(const ResizeLaunch& L, hipStream_t s) {
     if (!sums) return hipGetLastError();
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
+    if (La.sum_acc) {
+        const double cnt = (double)L.dst.w * L.dst.h * (L.sum_per_image ? 1 : L.n);
+        hipLaunchKernelGGL(fixed_sums_kernel, dim3(1), dim3(kBlock), 0, s, La.sum_acc, L.n, CC, L.sum_per_image,
+                           La.sum_q1, La.sum_q2, cnt, L.sum_out, L.sum_mean, L.sum_std);
+        return hipGetLastError();
+    }
     const int blocks = (L.sum_per_image ? L.n : 1) * CC;
     const double count = (double)L.dst.w * L.dst.h * (L.sum_per_image ? 1 : L.n);
     hipLaunchKernelGGL(group_sums_kernel, dim3((unsigned)blocks), dim3(kSumThreads), 0, s,

@@ -73,48 +73,6 @@ __device__ __forceinline__ void direct_taps(const WarpLaunch& L, const unsigned 
     }
 }
 
-// The 16-byte chunk columns [glo, ghi] (box-relative, chunks of the box row
-// from column bx0) of source row r that a 64 x TH output tile taps: the tile's
-// parallelogram (its corners through the matrix) clipped to the band of
-// source rows whose pixels tap row r (fy in [r - 1, r + 1), widened by 0.05 px
-// for the float rounding of the reference's coordinates), columns floor(x) ..
-// floor(x) + 1.  Returns glo | ghi << 16, or 1 (lo > hi) when empty.  Host and
-// device run this same code (the host bounds the slot size with it).
-VACV_HD uint32_t ring_row_span(const float* M, int bx, int by, int th, int dst_w, int dst_h, int r, int bx0, int G,
-                               int cc) {
-    const float X0 = (float)(bx * kFrTileW), X1 = (float)(min(bx * kFrTileW + kFrTileW, dst_w) - 1);
-    const float Y0 = (float)(by * th), Y1 = (float)(min(by * th + th, dst_h) - 1);
-    float cx[4], cy[4];
-    const float px[4] = {X0, X1, X1, X0}, py[4] = {Y0, Y0, Y1, Y1};
-    for (int i = 0; i < 4; ++i) {
-        cx[i] = (M[0] * px[i] + M[1] * py[i]) + M[2];
-        cy[i] = (M[3] * px[i] + M[4] * py[i]) + M[5];
-    }
-    const float rf = (float)r, ya = rf - 1.05f, yb = rf + 1.05f;
-    float lo = 3.0e38f, hi = -3.0e38f;
-    for (int i = 0; i < 4; ++i) {
-        const int i2 = (i + 1) & 3;
-        if (cy[i] >= ya && cy[i] <= yb) { lo = fminf(lo, cx[i]); hi = fmaxf(hi, cx[i]); }
-        for (int e = 0; e < 2; ++e) {
-            const float yl = e ? yb : ya;
-            if ((cy[i] - yl) * (cy[i2] - yl) < 0.f) {
-                const float xc = cx[i] + (yl - cy[i]) / (cy[i2] - cy[i]) * (cx[i2] - cx[i]);
-                lo = fminf(lo, xc);
-                hi = fmaxf(hi, xc);
-            }
-        }
-    }
-    if (lo <= hi) {
-        const int clo = (int)floorf(fmaxf(lo - 0.05f, -1.0e9f)) - bx0;     // left tap column
-        const int chi = (int)floorf(fminf(hi + 0.05f, 1.0e9f)) + 1 - bx0;  // right tap column
-        if (chi >= 0 && clo * cc <= 16 * G - 1) {
-            const int glo = (max(clo, 0) * cc) >> 4, ghi = min(((chi + 1) * cc - 1) >> 4, G - 1);
-            return (uint32_t)glo | ((uint32_t)ghi << 16);
-        }
-    }
-    return 1u;
-}
-
 // ---------------------------------------------------------------------------
 // warp_ring_kernel: the frames kernel with its staging moved off the
 // registers.  Boxes are copied HBM -> LDS by LDS-DMA (buffer_load_dwordx4 ...
@@ -143,17 +101,17 @@ constexpr int kRingMaxIt = 6;  // DMA instructions per wave and frame, at most (
 #endif
 
 
-// L: launch block; gx, gy: tiles per frame; kf: frames per workgroup; ns,
-// slot: LDS slots and their bytes (ring_layout_th); dst_al: the destination
-// allows dword (u8 out) stores.
+// L: launch block; gx, gy: tiles per frame; kf: frames per workgroup; S: LDS
+// bytes per staged row (a multiple of 16); rows_max: staged rows per slot;
+// ns, slot: LDS slots and their bytes; dst_al: the destination allows dword
+// (u8 out) stores; ginv = ceil(2^20 / (S / 16)) (row of chunk c = c ginv >> 20,
+// exact for c < 4096 and S / 16 <= 256).
 // cache policy of the ring kernel's output stores (A/B builds: EXTRA=-DVACV_RING_SAUX=n)
 #ifndef VACV_RING_SAUX
 #define VACV_RING_SAUX VACV_STORE_AUX
 #endif
-// waves per SIMD the register allocation must allow: byte output fits 5
-// (96 VGPRs, no spills); the fp32 outputs take what they need
 #ifndef VACV_RING_WPE
-#define VACV_RING_WPE (OUT == kOutSame ? 5 : 1)
+#define VACV_RING_WPE 1
 #endif
 #ifndef VACV_RING_GRP
 // pixels whose taps are read before their blends: 2 keeps the kernel at 95
@@ -162,7 +120,8 @@ constexpr int kRingMaxIt = 6;  // DMA instructions per wave and frame, at most (
 #endif
 template <int CC, int OUT, int NP, bool PLANAR>
 __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(VACV_RING_WPE)))
-warp_ring_kernel(WarpLaunch L, int gx, int gy, int kf, int ns, int slot, int dst_al) {
+warp_ring_kernel(WarpLaunch L, int gx, int gy, int kf, int S, int rows_max, int ns, int slot, int dst_al,
+                 uint32_t ginv) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     constexpr int TH = 4 * NP;
     // staging loads: sc0 for byte output (neighbouring tiles' boxes share
@@ -263,83 +222,90 @@ warp_ring_kernel(WarpLaunch L, int gx, int gy, int kf, int ns, int slot, int dst
     const int bx0 = any ? (xmin & ~3) : 0;                         // first staged column (bx0 * CC dword-aligned)
     const int G = any ? ((xmax + 2 - bx0) * CC + 15) >> 4 : 0;     // 16-byte chunks per staged row
     const int R = any ? ymax + 2 - ymin : 0;                       // staged rows ymin .. ymax + 1
-    // Compact row spans (round 4).  The box's rows near its top and bottom
-    // need only part of its width (a rotated tile's source footprint is a
-    // parallelogram: ~0.6 of its bounding box at 15 degrees), and only those
-    // chunks are copied -- stored back to back, row after row, so a slot holds
-    // the spans, not the box: row t's chunks start at chunk pre[t] of the
-    // slot.  Lanes t < R of wave 0 compute the spans and their prefix sum into
-    // tables kept in the last slot, which no DMA writes before frame f0's
-    // barrier.
-    constexpr int kMaxRows = 64;
-    int* tab_lo = reinterpret_cast<int*>(lds + (ns - 1) * slot + 16);  // after that slot's border head
-    int* tab_pre = tab_lo + kMaxRows;                                  // kMaxRows + 1 entries
-    const bool fits = any && R <= kMaxRows;                           // uniform
-    if (fits && wave == 0) {
-        int cnt = 0, glo = 0;
-        if (lane < R) {
-            const uint32_t sp = ring_row_span(M, bx, by, TH, L.dst.w, L.dst.h, ymin + lane, bx0, G, CC);
-            glo = (int)(sp & 0xFFFFu);
-            cnt = max((int)(sp >> 16) - glo + 1, 0);
-        }
-        int inc = cnt;  // inclusive prefix sum over the wave
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const int t = __shfl_up(inc, o, 64);
-            if (lane >= o) inc += t;
-        }
-        if (lane < R) {
-            tab_lo[lane] = glo;
-            tab_pre[lane] = inc - cnt;
-        }
-        if (lane == R - 1) tab_pre[R] = inc;
-    }
-    __syncthreads();
-    const int nch = fits ? __builtin_amdgcn_readfirstlane(tab_pre[R]) : 0;  // chunks per frame
-    const int n_inst = (nch + 63) >> 6;                                         // 1 KiB DMA instructions per frame
-    const bool staged = fits && n_inst <= min(4 * kRingMaxIt, (slot - 16) >> 10);  // uniform
+    const int Gs = S >> 4;                                         // chunks per LDS row
+    const int n_inst = (R * Gs + 63) >> 6;                         // 1 KiB DMA instructions per frame
+    const bool staged = any && G <= Gs && R <= rows_max && n_inst <= 4 * kRingMaxIt;  // uniform
     // this wave's DMA instructions per frame: i = wave, wave + 4, ...
     const int n_w = staged && n_inst > wave ? (n_inst - wave + 3) >> 2 : 0;
-    // per pixel: the LDS offsets of its top and bottom tap rows (16 bits each;
-    // outside the source both are the border head) and its weights (v0, 4 w0)
     uint32_t rw[NP], wxp[NP];
 #pragma unroll
     for (int j = 0; j < NP; ++j) {
-        const bool ok = staged && ((okm >> j) & 1u);
+        const bool ok = (okm >> j) & 1u;
         const int sx = (int)(sxy[j] & 0xFFFFu), sy = (int)(sxy[j] >> 16);
-        rw[j] = 0u;
-        if (ok) {
-            const int r = sy - ymin, byte = (sx - bx0) * CC, ch = byte >> 4;
-            const uint32_t top = 16u + 16u * (uint32_t)(tab_pre[r] + ch - tab_lo[r]) + (uint32_t)(byte & 15);
-            const uint32_t bot = 16u + 16u * (uint32_t)(tab_pre[r + 1] + ch - tab_lo[r + 1]) + (uint32_t)(byte & 15);
-            rw[j] = top | (bot << 16);
-        }
-        // weights for every pixel with taps (the unstaged path samples from memory)
-        wxp[j] = ((okm >> j) & 1u) ? vwa[j] : (2048u | (8192u << 16));  // outside: (2048, 0) x (8192, 0)
+        rw[j] = (ok ? (uint32_t)(16 + (sy - ymin) * S + (sx - bx0) * CC) : 0u) | (vwa[j] & 0xFFFF0000u);
+        const uint32_t v0 = vwa[j] & 0xFFFFu;  // outside: (2048, 0)
+        wxp[j] = ok ? (v0 | ((2048u - v0) << 16)) : 2048u;
     }
 
+    // Row spans.  The box's rows near its top and bottom need only part of
+    // its width (a rotated tile's source footprint is a parallelogram: ~0.6
+    // of its bounding box at 15 degrees).  Thread t < R clips the
+    // parallelogram of the tile's corners to the band of source rows whose
+    // pixels tap row ymin + t (fy in [r - 1, r + 1), widened by 0.05 px for
+    // the float rounding of the reference's coordinates) and records the
+    // 16-byte chunks it needs, columns floor(x) .. floor(x) + 1.
+    // The table lives in the last slot's data, which no DMA writes before
+    // frame f0's barrier.
+    uint32_t* spans = reinterpret_cast<uint32_t*>(lds + (ns - 1) * slot + 16);  // after that slot's border head
+    if (staged && tid < R) {
+        const float X0 = (float)(bx * kFrTileW), X1 = (float)(min(bx * kFrTileW + kFrTileW, L.dst.w) - 1);
+        const float Y0 = (float)(by * TH), Y1 = (float)(min(by * TH + TH, L.dst.h) - 1);
+        float cx[4], cy[4];
+        const float px[4] = {X0, X1, X1, X0}, py[4] = {Y0, Y0, Y1, Y1};
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            cx[i] = (M[0] * px[i] + M[1] * py[i]) + M[2];
+            cy[i] = (M[3] * px[i] + M[4] * py[i]) + M[5];
+        }
+        const float r = (float)(ymin + tid), ya = r - 1.05f, yb = r + 1.05f;
+        float lo = 3.0e38f, hi = -3.0e38f;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int i2 = (i + 1) & 3;
+            if (cy[i] >= ya && cy[i] <= yb) { lo = fminf(lo, cx[i]); hi = fmaxf(hi, cx[i]); }
+#pragma unroll
+            for (int e = 0; e < 2; ++e) {
+                const float yl = e ? yb : ya;
+                if ((cy[i] - yl) * (cy[i2] - yl) < 0.f) {
+                    const float xc = cx[i] + (yl - cy[i]) / (cy[i2] - cy[i]) * (cx[i2] - cx[i]);
+                    lo = fminf(lo, xc);
+                    hi = fmaxf(hi, xc);
+                }
+            }
+        }
+        uint32_t sp = 1u;  // empty: lo = 1 > hi = 0
+        if (lo <= hi) {
+            const int clo = (int)floorf(fmaxf(lo - 0.05f, -1.0e9f)) - bx0;       // left tap column
+            const int chi = (int)floorf(fminf(hi + 0.05f, 1.0e9f)) + 1 - bx0;    // right tap column
+            if (chi >= 0 && clo * CC <= 16 * G - 1) {
+                const int glo = (max(clo, 0) * CC) >> 4, ghi = min(((chi + 1) * CC - 1) >> 4, G - 1);
+                sp = (uint32_t)glo | ((uint32_t)ghi << 16);
+            }
+        }
+        spans[tid] = sp;
+    }
+    __syncthreads();
+
     // this lane's DMA source offsets (frame-relative), frame-independent:
-    // instruction u of this wave covers the slot's chunks 64 (wave + 4u) + lane,
-    // chunk c of row t where pre[t] <= c < pre[t + 1] (a binary search).
-    // vm: chunks to copy; tailm: those reaching past the plane's last byte
-    // (loaded bytewise after the DMA instead)
+    // instruction u of this wave covers the slot's chunks 64 (wave + 4u) + lane.
+    // vm: chunks inside their row's span; tailm: those reaching past the
+    // plane's last byte (loaded bytewise after the DMA instead)
     uint32_t goff[kRingMaxIt];
     uint32_t vm = 0, tailm = 0;
 #pragma unroll
     for (int u = 0; u < kRingMaxIt; ++u) {
         goff[u] = 0;
-        const int c = 64 * (wave + 4 * u) + lane;
-        if (u < n_w && c < nch) {
-            int lo = 0, hi = R - 1;  // the last row t with pre[t] <= c
-            while (lo < hi) {
-                const int mid = (lo + hi + 1) >> 1;
-                if (tab_pre[mid] <= c) lo = mid;
-                else hi = mid - 1;
+        if (u < n_w) {
+            const int c = 64 * (wave + 4 * u) + lane;
+            const int row = (int)(__umul24((uint32_t)c, ginv) >> 20), col = c - row * Gs;  // c / Gs
+            if (row < R && col < G) {
+                const uint32_t sp = spans[row];
+                if ((int)(sp & 0xFFFFu) <= col && col <= (int)(sp >> 16)) {
+                    goff[u] = (uint32_t)(ymin + row) * rp + (uint32_t)(bx0 * CC + 16 * col);
+                    if ((int64_t)goff[u] + 16 > L.src.plane_bytes) tailm |= 1u << u;
+                    else vm |= 1u << u;
+                }
             }
-            const int col = tab_lo[lo] + (c - tab_pre[lo]);
-            goff[u] = (uint32_t)(ymin + lo) * rp + (uint32_t)(bx0 * CC + 16 * col);
-            if ((int64_t)goff[u] + 16 > L.src.plane_bytes) tailm |= 1u << u;
-            else vm |= 1u << u;
         }
     }
     // frame f's box -> slot s: n_w instructions, idle lanes out of range
@@ -396,9 +362,8 @@ warp_ring_kernel(WarpLaunch L, int gx, int gy, int kf, int ns, int slot, int dst
         const bool inside = FULL || (x < L.dst.w && y < L.dst.h);
         unsigned char* dbase = const_cast<unsigned char*>(L.dst.base) + frame_off(f, L.dst);
         const Rsrc drs = make_rsrc(dbase, L.dst.plane_bytes);
-        const uint32_t v0 = wxp[j] & 0xFFFFu;  // (v0, 2048 - v0) x (wA, 8192 - wA)
-        const us2 wx = __builtin_bit_cast(us2, v0 | ((2048u - v0) << 16));
-        const uint32_t wA = wxp[j] >> 16, wB = 8192u - wA;
+        const us2 wx = __builtin_bit_cast(us2, wxp[j]);
+        const uint32_t wA = rw[j] >> 16, wB = 8192u - (rw[j] >> 16);
         uint32_t vv[CC];
 #pragma unroll
         for (int k = 0; k < CC; ++k) {
@@ -409,8 +374,6 @@ warp_ring_kernel(WarpLaunch L, int gx, int gy, int kf, int ns, int slot, int dst
             const uint32_t ht = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, top), wx, 0u, false);
             const uint32_t hb = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, bot), wx, 0u, false);
             vv[k] = __umul24(ht, wA) + __umul24(hb, wB);  // warp_affine_naive.cpp:50-54, x4
-            if (VACV_RING_DBG & 8) vv[k] = ((tlo >> (8 * k)) & 0xFFu) << 24;  // diagnosis: the top-left tap itself
-            if (VACV_RING_DBG & 16) vv[k] = ((blo >> (8 * k)) & 0xFFu) << 24;  // diagnosis: the bottom-left tap
         }
         const uint32_t drow = (uint32_t)y * dpitch + drs.delta;
         if constexpr (OUT == kOutSame) {
@@ -579,11 +542,10 @@ warp_ring_kernel(WarpLaunch L, int gx, int gy, int kf, int ns, int slot, int dst
             uint32_t tp[kGrp][4];
 #pragma unroll
             for (int j = 0; j < kGrp; ++j) {
-                // top and bottom tap rows share their byte offset within a chunk
                 const uint32_t ra = (VACV_RING_DBG & 4) ? 16u : rw[j0 + j] & 0xFFFFu;
-                const uint32_t rb = (VACV_RING_DBG & 4) ? 16u : rw[j0 + j] >> 16;
-                taps_at(lds + sbase + (ra & ~3u), ra & 3u, tp[j][0], tp[j][1]);
-                taps_at(lds + sbase + (rb & ~3u), ra & 3u, tp[j][2], tp[j][3]);
+                const unsigned char* a = lds + sbase + (ra & ~3u);
+                taps_at(a, ra & 3u, tp[j][0], tp[j][1]);
+                taps_at(a + S, ra & 3u, tp[j][2], tp[j][3]);
             }
 #pragma unroll
             for (int j = 0; j < kGrp; ++j) emit(full_c, f, j0 + j, tp[j][0], tp[j][1], tp[j][2], tp[j][3]);
@@ -648,8 +610,9 @@ hipError_t launch_frames(const WarpLaunch& L, const WarpFramesPlan& P, hipStream
     const int64_t total = (int64_t)gx * gy * ((L.n * L.src.planes + kf - 1) / kf);
     if (total >= 0x7FFFFFF0LL) return hipErrorInvalidValue;
     const int64_t blocks = (total + 7) / 8 * 8;
-    hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(kBlock), (size_t)P.lds, s, L, gx, gy, kf, P.ns, P.slot,
-                       P.dst_al);
+    const uint32_t gs = (uint32_t)(P.S / 16), ginv = ((1u << 20) + gs - 1) / gs;
+    hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(kBlock), (size_t)P.lds, s, L, gx, gy, kf, P.S, P.rows_max,
+                       P.ns, P.slot, P.dst_al, ginv);
     return hipGetLastError();
 }
 
@@ -672,55 +635,94 @@ hipError_t launch_frames_cc(const WarpLaunch& L, const WarpFramesPlan& P, hipStr
 
 }  // namespace
 
-// The LDS layout of one geometry (pointer-independent): ns slots, each a
-// 16-byte border head and whole 1 KiB DMA instructions holding the tile's
-// compact row spans (ring_row_span) back to back.  The slot is sized by the
-// largest span total over the geometry's tiles, bounded on the host with the
-// kernel's own span code: each tile's source box from its corners (+- 1 px
-// for the rounding of the pixels between them, clamped to the source), per
-// box row its span plus one chunk (the kernel's box, and so its chunk
-// alignment, may be smaller).  The kernel re-checks its real total and takes
-// its taps from memory if it is over (never, for the planned geometry).
-// ns (2-4, VACV_TUNE_WARP_SLOTS) defaults to 3 -- the compact spans (~0.6 of
-// the box at 15 degrees) fit a third slot where two box slots used to fit --
-// so two frames' copies are in flight while one is sampled.
+// The LDS row stride (bytes, a multiple of 16, >= 16 G) with the fewest LDS
+// bank conflicts for the tap reads.  A wave's 64 lanes read the taps of 64
+// consecutive output pixels of one row; rotated, they fall on several staged
+// rows, and the stride decides whether those rows' dwords land on distinct
+// banks.  Per tap row a pixel reads the 2 (3 for CC = 3) dwords from byte
+// address 16 + row S + col CC rounded down, each a ds_read_b32 (bank = dword
+// mod 32 within each half-wave; distinct dwords on one bank serialise).
+// Counted on a few sample rows of the output for the 8 strides 16 G ..
+// 16 G + 112 (those <= s_max); ties go to the smaller stride.
+int ring_stride(const WarpLaunch& L, int G, int s_max) {
+    const float* M = L.inv;
+    const int CC = L.src.cc;
+    int best_s = 16 * G;
+    long best_cost = -1;
+    for (int k = 0; k < 8; ++k) {
+        const int S = 16 * (G + k);
+        if (k > 0 && S > s_max) break;
+        long cost = 0;
+        for (int yi = 1; yi <= 3; ++yi) {
+            const int y = L.dst.h * yi / 4;
+            for (int xi = 0; xi < 3; ++xi) {
+                const int x0 = std::max(0, std::min(L.dst.w - 64, (L.dst.w - 64) * xi / 2));
+                for (int half = 0; half < 2; ++half) {
+                    long a0[32];
+                    for (int l = 0; l < 32; ++l) {
+                        const int x = x0 + 32 * half + l;
+                        const float fx = (M[0] * (float)x + M[1] * (float)y) + M[2];
+                        const float fy = (M[3] * (float)x + M[4] * (float)y) + M[5];
+                        long a = 0;  // outside: the slot's border head
+                        if (fx >= 0.f && fx < (float)(L.src.w - 1) && fy >= 0.f && fy < (float)(L.src.h - 1))
+                            a = 16 + (long)(int)fy * S + (long)(int)fx * CC;
+                        a0[l] = a >> 2;
+                    }
+                    for (int q = 0; q < (CC == 3 ? 3 : 2); ++q) {  // one ds_read_b32 per covering dword
+                        int worst = 1;
+                        for (int l = 0; l < 32; ++l) {  // distinct dwords on lane l's bank
+                            int n = 0;
+                            for (int m = 0; m < 32; ++m) {
+                                if (((a0[m] - a0[l]) & 31) != 0) continue;
+                                bool first = true;
+                                for (int t = 0; t < m; ++t) first = first && a0[t] != a0[m];
+                                n += first;
+                            }
+                            worst = std::max(worst, n);
+                        }
+                        cost += worst;
+                    }
+                }
+            }
+        }
+        if (best_cost < 0 || cost < best_cost) {
+            best_cost = cost;
+            best_s = S;
+        }
+    }
+    return best_s;
+}
+
+// The LDS layout of one geometry (pointer-independent).  The box bound is the
+// tile's coordinate span (|m0|*63 + |m1|*(TH-1) columns, |m3|*63 +
+// |m4|*(TH-1) rows) plus floor, the second tap, 4-alignment and slack; the
+// kernel re-checks the real box and reads memory if it is larger.  Raw pixel
+// rows of G 16-byte chunks; ns slots, each a 16-byte border head and whole
+// 1 KiB DMA instructions.  ns (2-4, VACV_TUNE_WARP_SLOTS) defaults to 2:
+// occupancy beats depth (720p rot15: 2 / 3 / 4 slots 0.159 / 0.183 / 0.29 ms,
+// 5 / 3 / 2 workgroups per CU).
 bool ring_layout_th(const WarpLaunch& L, WarpFramesPlan& P, int th) {
     P.th = th;
     const int CC = L.src.cc;
-    const float* M = L.inv;
-    const int gx = (L.dst.w + kFrTileW - 1) / kFrTileW, gy = (L.dst.h + th - 1) / th;
-    int cap = 0, rows = 0;
-    for (int by = 0; by < gy; ++by) {
-        for (int bx = 0; bx < gx; ++bx) {
-            const float X0 = (float)(bx * kFrTileW), X1 = (float)(std::min(bx * kFrTileW + kFrTileW, L.dst.w) - 1);
-            const float Y0 = (float)(by * th), Y1 = (float)(std::min(by * th + th, L.dst.h) - 1);
-            float fx0 = 3e38f, fx1 = -3e38f, fy0 = 3e38f, fy1 = -3e38f;
-            for (int i = 0; i < 4; ++i) {
-                const float px = (i == 1 || i == 2) ? X1 : X0, py = i >= 2 ? Y1 : Y0;
-                const float fx = (M[0] * px + M[1] * py) + M[2], fy = (M[3] * px + M[4] * py) + M[5];
-                fx0 = std::min(fx0, fx); fx1 = std::max(fx1, fx);
-                fy0 = std::min(fy0, fy); fy1 = std::max(fy1, fy);
-            }
-            if (!(fx1 >= -1.f && fy1 >= -1.f && fx0 < (float)L.src.w && fy0 < (float)L.src.h)) continue;  // border only
-            const int xmin = std::max(0, (int)std::floor(fx0) - 1), xmax = std::min(L.src.w - 2, (int)std::floor(fx1) + 1);
-            const int ymin = std::max(0, (int)std::floor(fy0) - 1), ymax = std::min(L.src.h - 2, (int)std::floor(fy1) + 1);
-            if (xmax < xmin || ymax < ymin) continue;
-            const int bx0 = xmin & ~3, G = ((xmax + 2 - bx0) * CC + 15) >> 4, R = ymax + 2 - ymin;
-            int total = 0;
-            for (int t = 0; t < R; ++t) {
-                const uint32_t sp = ring_row_span(M, bx, by, th, L.dst.w, L.dst.h, ymin + t, bx0, G, CC);
-                total += std::max((int)(sp >> 16) - (int)(sp & 0xFFFFu) + 1, 0) + 1;
-            }
-            cap = std::max(cap, total);
-            rows = std::max(rows, R);
-        }
-    }
-    if (rows > 64 || (cap + 63) / 64 > 4 * kRingMaxIt) return false;  // the kernel's span tables / DMA budget
-    P.rows_max = rows;
-    P.slot = 16 + std::max((cap + 63) / 64, 1) * 1024;
-    const int knob = tune(VACV_TUNE_WARP_SLOTS);
-    P.ns = knob >= 2 && knob <= 4 ? knob : 3;
+    const double sx = std::fabs(L.inv[0]) * (kFrTileW - 1) + std::fabs(L.inv[1]) * (P.th - 1);
+    const double sy = std::fabs(L.inv[3]) * (kFrTileW - 1) + std::fabs(L.inv[4]) * (P.th - 1);
+    const int W = (int)std::ceil(sx * (1 + 1e-5) + 1e-3) + 6;  // + floor spread, right tap, 4-alignment
+    const int G = (W * CC + 15) / 16;
+    P.rows_max = (int)std::ceil(sy * (1 + 1e-5) + 1e-3) + 3;
     const int extra = 64 + (L.out == kOutSame ? 4 * 2 * 64 * CC : 0);
+    auto slot_of = [&](int S) { return 16 + (P.rows_max * (S / 16) + 63) / 64 * 1024; };
+    if ((P.rows_max * G + 63) / 64 > 4 * kRingMaxIt) return false;
+    const int knob = tune(VACV_TUNE_WARP_SLOTS);
+    P.ns = knob >= 2 && knob <= 4 ? knob : 2;
+    if (P.ns * slot_of(16 * G) + extra > 64 * 1024) return false;
+    // strides that keep the same resident workgroups per CU
+    const int per_cu = 160 * 1024 / (P.ns * slot_of(16 * G) + extra);
+    int s_max = 16 * G;
+    for (int S = 16 * G; S <= 16 * (G + 7); S += 16)
+        if (160 * 1024 / (P.ns * slot_of(S) + extra) >= per_cu && (P.rows_max * (S / 16) + 63) / 64 <= 4 * kRingMaxIt)
+            s_max = S;
+    P.S = ring_stride(L, G, s_max);
+    P.slot = slot_of(P.S);
     P.lds = P.ns * P.slot + extra;
     return P.lds <= 64 * 1024;
 }

@@ -247,6 +247,7 @@ struct FusedSums {
     float* stddev;
     int groups;                  // out: workgroups per plane
     bool used;                   // out
+    int64_t* acc;                // [n][cc][2], zero between calls (the column kernel's fixed-point sums)
 };
 
 int resize_impl(const vacv_image* src_d, const vacv_image* dst_d, int interpolation, int mode, int out_kind,
@@ -369,6 +370,7 @@ int resize_impl(const vacv_image* src_d, const vacv_image* dst_d, int interpolat
             L.sum_per_image = fs->per_image;
             L.sum_mean = fs->mean;
             L.sum_std = fs->stddev;
+            L.sum_acc = fs->acc;
             fs->groups = cubic_direct_groups(L);
             fs->used = true;
         }
@@ -892,11 +894,12 @@ int vacv_channel_sums(const vacv_image* src_d, double* sums, int per_image, void
 
 namespace {
 // vacv_resize_channel_sums with optional statistics: u8 -> fp32 cubic into a
-// dense NHWC output (cfg5) takes the gather kernel's per-workgroup sums
-// epilogue and one fixed-order reduction launch that also derives mean /
-// stddev -- the output is not read back (a separate vacv_channel_sums pass
-// re-read 77 MB per cfg5 batch).  Everything else: resize, then
-// vacv_channel_sums (and vacv_stats_from_sums).
+// dense NHWC output (cfg5) takes the cubic kernel's sums epilogue (the column
+// kernel: per-image fixed-point integer accumulators, then one tiny launch
+// for the sums and mean / stddev; the gather kernel: per-workgroup partials
+// and a fixed-order reduction launch) -- the output is not read back (a
+// separate vacv_channel_sums pass re-read 77 MB per cfg5 batch).  Everything
+// else: resize, then vacv_channel_sums (and vacv_stats_from_sums).
 int resize_sums(const vacv_image* src_d, const vacv_image* dst_d, int interpolation, int mode, double* sums,
                 int per_image, float* mean, float* stddev, void* stream) {
     if (!sums) return VACV_ERR_INVALID_ARG;
@@ -909,8 +912,12 @@ int resize_sums(const vacv_image* src_d, const vacv_image* dst_d, int interpolat
         dst.layout == VACV_NHWC && dst.c <= 3 && dense(dst) && src.n == dst.n) {
         const int64_t groups = cubic_sums_groups_bound(dst.w, dst.h);  // the workspace's bound
         void* ws = nullptr;
+        void* acc = nullptr;
         if ((st = workspace(s, (size_t)(dst.n * groups * 2 * dst.c) * sizeof(double), &ws))) return st;
-        FusedSums fs{static_cast<double*>(ws), sums, per_image ? 1 : 0, mean, stddev, 0, false};
+        // fixed-point accumulators: zeroed when allocated, and every call leaves them zero
+        if ((st = workspace(s, (size_t)dst.n * 2 * dst.c * sizeof(int64_t), &acc, 4, true))) return st;
+        FusedSums fs{static_cast<double*>(ws), sums, per_image ? 1 : 0, mean, stddev, 0, false,
+                     static_cast<int64_t*>(acc)};
         if ((st = resize_impl(src_d, dst_d, interpolation, mode, kOutSame, nullptr, s, 0.0, 0.0, &fs))) return st;
         if (fs.used) return fs.groups <= groups ? VACV_OK : VACV_ERR_HIP;  // (a layout mismatch cannot happen)
     } else if ((st = resize_impl(src_d, dst_d, interpolation, mode, kOutSame, nullptr, s))) {

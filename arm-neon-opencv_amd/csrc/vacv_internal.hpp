@@ -124,6 +124,12 @@ struct ResizeLaunch {
     int sum_per_image;
     float* sum_mean;
     float* sum_std;
+    // the column kernel's fixed-point accumulators (or null: per-workgroup
+    // partials and group_sums_kernel): [n][cc][2] int64, zero on entry and
+    // left zero; Sum x in units of 2^-sum_q1, Sum x^2 in units of 2^-sum_q2
+    // (set by the launcher)
+    int64_t* sum_acc;
+    int sum_q1, sum_q2;
 };
 
 // Fills tiles, strips and the cached device plan of L (host).
@@ -198,9 +204,10 @@ hipError_t launch_warp_nearest(const WarpLaunch& L, hipStream_t s);
 // workgroup (k_warp_frames.hip)
 struct WarpFramesPlan {
     int th;                      // tile rows (16 or 32; 64 columns)
-    int rows_max;                // largest tile source box (rows) of the geometry
+    int S;                       // LDS bytes per staged source row (raw pixel bytes, a multiple of 16)
+    int rows_max;                // staged rows per LDS slot
     int ns;                      // LDS slots of the ring (boxes: one being sampled, ns - 1 in flight)
-    int slot;                    // bytes per slot (a 16-byte border head, compact row spans in whole 1 KiB DMA units)
+    int slot;                    // bytes per slot (a 16-byte border head, rows in whole 1 KiB DMA units)
     int lds;                     // dynamic LDS per workgroup
     int kf;                      // frames per workgroup (<= 0: chosen at launch)
     int dst_al;                  // destination dword-aligned (u8 quad stores)

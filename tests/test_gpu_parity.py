@@ -177,13 +177,16 @@ def test_cubic_direct_and_staged_agree(ops, dev, oracle):
 def test_resize_channel_sums(ops, dev, oracle):
     """vacv_resize_channel_sums / vacv_resize_mean_stddev: the resize output is
     unchanged and the sums match vacv_channel_sums of that output.  u8 -> fp32
-    cubic (cfg5) fuses the sums into the gather kernel (fp32 over <= 2 pixels
-    per lane, then fp64 per wave and workgroup, then a fixed-order fp64
-    reduction launch): within 1e-6 relative of the fp64 sums, the
-    derived mean / stddev within SURVEY 8(c)'s |d mean| <= 1e-3 and
-    |d std| / std <= 1e-4 of the oracle's exact statistics, and bit-identical
-    run to run.  The batch statistic of cfg5 (2560x1440 -> 224x224 cubic) at
-    full size, plus an odd size whose last wave is partial."""
+    cubic (cfg5) fuses the sums into the cubic kernel: the column kernel adds
+    fp64 per lane, wave and workgroup, then into per-image fixed-point int64
+    accumulators (atomics: integer sums, order-free) that one small launch
+    converts; the gather kernel (16-byte unaligned destination rows) adds fp32
+    over <= 2 pixels per lane and reduces the per-workgroup partials in a
+    fixed order.  Within 1e-6 relative of the fp64 sums, the derived mean /
+    stddev within SURVEY 8(c)'s |d mean| <= 1e-3 and |d std| / std <= 1e-4 of
+    the oracle's exact statistics, and bit-identical run to run (whatever
+    order the workgroups finish in).  The batch statistic of cfg5 (2560x1440 -> 224x224 cubic) at full
+    size, plus odd sizes with partial column blocks / row groups / waves."""
     import torch
     from vacv_amd import INTER_CUBIC, NCHW
     imgs = np.stack([synthetic_image(300 + k, 1440, 2560, 3) for k in range(4)])
@@ -210,19 +213,27 @@ def test_resize_channel_sums(ops, dev, oracle):
         out2, sums2, mean2, std2 = ops.resize_mean_stddev(src, 224, 224, INTER_CUBIC, per_image=per_image)
         assert torch.equal(out2, ref) and torch.equal(sums2, sums)
         assert torch.equal(mean2, mean) and torch.equal(std2, std)
+        for _ in range(8):  # the atomic accumulation: same bits whatever the finishing order
+            _, s3, m3, d3 = ops.resize_mean_stddev(src, 224, 224, INTER_CUBIC, per_image=per_image)
+            assert torch.equal(s3, sums) and torch.equal(m3, mean) and torch.equal(d3, std)
     odd = to_dev(np.stack([synthetic_image(310 + k, 301, 257, 3) for k in range(3)]), dev)
-    out, sums = ops.resize_channel_sums(odd, 61, 37, INTER_CUBIC, per_image=True)
-    want = ops.channel_sums(out)
-    torch.cuda.synchronize(dev)
-    assert ((sums - want).abs() / want.abs().clamp(min=1.0)).max().item() <= 1e-6
-    for per_image in (True, False):  # partial workgroups (61 x 37 = 2,257 px: 5 workgroups, the last one partial)
-        _, s2, m2, d2 = ops.resize_mean_stddev(odd, 61, 37, INTER_CUBIC, per_image=per_image)
-        count = 61 * 37 * (1 if per_image else 3)
-        want = ops.channel_sums(out, per_image=per_image)
-        wm, wd = ops.stats_from_sums(want, count)
+    # 61 x 37: 732-byte output rows -> the gather kernel (5 workgroups, the
+    # last one partial); 68 x 37: 816-byte rows -> the column kernel (a
+    # 4-column last block, a 1-row last row group)
+    for ow, oh in ((61, 37), (68, 37)):
+        out, sums = ops.resize_channel_sums(odd, ow, oh, INTER_CUBIC, per_image=True)
+        assert torch.equal(out, ops.resize(odd, ow, oh, interpolation=INTER_CUBIC))
+        want = ops.channel_sums(out)
         torch.cuda.synchronize(dev)
-        assert ((s2 - want).abs() / want.abs().clamp(min=1.0)).max().item() <= 1e-6
-        assert (m2 - wm).abs().max().item() <= 1e-3 and ((d2 - wd).abs() / wd).max().item() <= 1e-4
+        assert ((sums - want).abs() / want.abs().clamp(min=1.0)).max().item() <= 1e-6
+        for per_image in (True, False):
+            _, s2, m2, d2 = ops.resize_mean_stddev(odd, ow, oh, INTER_CUBIC, per_image=per_image)
+            count = ow * oh * (1 if per_image else 3)
+            want = ops.channel_sums(out, per_image=per_image)
+            wm, wd = ops.stats_from_sums(want, count)
+            torch.cuda.synchronize(dev)
+            assert ((s2 - want).abs() / want.abs().clamp(min=1.0)).max().item() <= 1e-6
+            assert (m2 - wm).abs().max().item() <= 1e-3 and ((d2 - wd).abs() / wd).max().item() <= 1e-4
     # NCHW planes and odd sizes
     chw = ops.change_layout(src[:2, :301, :257].contiguous(), NCHW)
     out, sums = ops.resize_channel_sums(chw, 61, 37, INTER_CUBIC, layout=NCHW)
