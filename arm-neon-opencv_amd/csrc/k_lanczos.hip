@@ -55,6 +55,7 @@ struct LanczosTabsDev {
     const float* xaf;    // [dst.w][8] fp32 coefficients
     const int* yofs;     // [dst.h]
     const short* yai;    // [dst.h][8]
+    const int* yrot;     // [dst.h][4] u8: the 8 coefficients per ring SLOT (row mod 8) as short pairs
     const float* yaf;    // [dst.h][8]
     int xmin, xmax;      // output columns [xmin, xmax) take the unrolled horizontal sum
 };
@@ -126,6 +127,9 @@ __device__ __forceinline__ T lz_const(const T* p, int i) {
     return ((const __attribute__((address_space(4))) T*)(uintptr_t)p)[i];
 }
 
+#ifndef VACV_LZ_SLOTS
+#define VACV_LZ_SLOTS 1
+#endif
 template <typename TIn, int OUT, int CC>
 __global__ void __launch_bounds__(kBlock) lanczos_kernel(LanczosLaunch L, int strips, int bands, int band_rows) {
     constexpr bool U8 = std::is_same<TIn, uint8_t>::value;
@@ -136,7 +140,11 @@ __global__ void __launch_bounds__(kBlock) lanczos_kernel(LanczosLaunch L, int st
     // source rows in flight per wave (the loads of rows r + 1 .. r + D - 1
     // run while row r is resized)
     constexpr int D = U8 ? 4 : 2;
-    __shared__ TW ring[4][8][64 * CC];  // per wave: 8 source rows x 64 columns x CC
+    // per wave: 8 source rows x 64 columns x RS (padding c = 3 to 4, for one
+    // 16-byte LDS access per lane and row, cost a workgroup per CU of LDS:
+    // 0.589 vs 0.530 ms)
+    constexpr int RS = CC;
+    __shared__ __attribute__((aligned(16))) TW ring[4][8][64 * RS];
 
     // wave-uniform, and said so: the plane's buffer resource stays in SGPRs
     // (derived from a per-lane value it would be waterfalled at every load)
@@ -174,6 +182,11 @@ __global__ void __launch_bounds__(kBlock) lanczos_kernel(LanczosLaunch L, int st
     for (int m = 0; m < 4; ++m) cp[m] = ((uint32_t)c[2 * m] & 0xFFFFu) | ((uint32_t)c[2 * m + 1] << 16);
     const uint32_t wbyte = (uint32_t)(wstart * CC * (int)sizeof(TIn)) + srs.delta;
     const uint32_t wsh = wbyte & 3u;  // u8: the window's byte offset in its first dword
+    // uniform: every lane of the strip takes the unrolled sum (shift 0) -- all
+    // strips but the image's first and last.  The per-lane switch below would
+    // otherwise run its 9-way exec-mask chain for every source row (PMC: the
+    // kernel issued more scalar than vector instructions).
+    const bool interior = __builtin_amdgcn_ballot_w64(shift != 0) == 0;
 
     // the window of source row r (issued; consumed by hrow).  SAFE: the
     // window may reach past the plane's last byte (only in the waves holding
@@ -217,7 +230,8 @@ __global__ void __launch_bounds__(kBlock) lanczos_kernel(LanczosLaunch L, int st
             uint32_t wv[ND - 1];
 #pragma unroll
             for (int q = 0; q < ND - 1; ++q) wv[q] = __builtin_amdgcn_alignbyte(d[q + 1], d[q], wsh);
-            switch (shift) {  // divergent only in the strips at the image's edges
+            if (interior) lz_h_u8<CC, 0, ND - 1>(wv, cp, hv);
+            else switch (shift) {  // divergent: the strips at the image's edges
                 case -4: lz_h_u8<CC, -4, ND - 1>(wv, cp, hv); break;
                 case -3: lz_h_u8<CC, -3, ND - 1>(wv, cp, hv); break;
                 case -2: lz_h_u8<CC, -2, ND - 1>(wv, cp, hv); break;
@@ -234,7 +248,8 @@ __global__ void __launch_bounds__(kBlock) lanczos_kernel(LanczosLaunch L, int st
             // for every i with this compiler, ROCm 7.2 clang: scalars only here)
 #pragma unroll
             for (int q = 0; q < ND; ++q) wf[q] = __uint_as_float(d[q]);
-            switch (shift) {
+            if (interior) lz_h_f32<CC, 0>(wf, c, hv);
+            else switch (shift) {
                 case -4: lz_h_f32<CC, -4>(wf, c, hv); break;
                 case -3: lz_h_f32<CC, -3>(wf, c, hv); break;
                 case -2: lz_h_f32<CC, -2>(wf, c, hv); break;
@@ -247,7 +262,8 @@ __global__ void __launch_bounds__(kBlock) lanczos_kernel(LanczosLaunch L, int st
             }
         }
 #pragma unroll
-        for (int k = 0; k < CC; ++k) ring[wave][slot][lane * CC + k] = hv[k];
+        for (int k = 0; k < CC; ++k) ring[wave][slot][lane * RS + k] = hv[k];
+        if constexpr (RS > CC) ring[wave][slot][lane * RS + CC] = 0;
     };
 
     const int dw = L.dst.w * CC;
@@ -255,6 +271,7 @@ __global__ void __launch_bounds__(kBlock) lanczos_kernel(LanczosLaunch L, int st
                         (int64_t)plane * L.dst.plane_pitch;
     const Rsrc drs = make_rsrc(dp, L.dst.plane_bytes);
     const bool dst_al = ((reinterpret_cast<uintptr_t>(dp) | (uintptr_t)L.dst.row_pitch) & 3) == 0;
+    const bool full = strip * 64 + 64 <= L.dst.w;  // uniform: every lane of the strip is live
     ChanNorm cn[CC] = {};
     if (OUT == kOutNorm) {
 #pragma unroll
@@ -263,30 +280,49 @@ __global__ void __launch_bounds__(kBlock) lanczos_kernel(LanczosLaunch L, int st
 
     // VResizeLanczos4 of output row y from the ring, and its store
     auto emit = [&](int y) {
-        const int sy = lz_const(L.t.yofs, y);
-        TW hs[8][CC];
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-            const int slot = min(max(sy - 3 + k, 0), h - 1) & 7;
-#pragma unroll
-            for (int q = 0; q < CC; ++q) hs[k][q] = ring[wave][slot][lane * CC + q];
-        }
         TOut o[CC];
         if constexpr (U8) {
-            // the row's 8 shorts as 4 dwords (scalar loads are dword-granular)
+            // The u8 sum is int arithmetic (wrapping, order immaterial), so it
+            // is taken per ring SLOT: all 8 slots in a fixed order, from one
+            // base address with immediate offsets, against the row's
+            // coefficients regrouped by slot on the host (yrot: a clamped
+            // border tap adds its coefficient to its row's slot; a slot no tap
+            // reads gets 0).  No per-row slot arithmetic on the scalar unit.
+            int hs[8][CC];
             int bb[8];
-            const int* b32 = reinterpret_cast<const int*>(L.t.yai);
+            if constexpr (VACV_LZ_SLOTS && OUT != kOutNorm) {  // (normalising: 0.647 vs 0.599 ms, registers)
 #pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                const int wd = lz_const(b32, 4 * y + k);
-                bb[2 * k] = (int)(short)(wd & 0xFFFF);
-                bb[2 * k + 1] = wd >> 16;
+                for (int j = 0; j < 8; ++j) {
+#pragma unroll
+                    for (int q = 0; q < CC; ++q) hs[j][q] = ring[wave][j][lane * RS + q];
+                }
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    const int wd = lz_const(L.t.yrot, 4 * y + k);
+                    bb[2 * k] = (int)(short)(wd & 0xFFFF);
+                    bb[2 * k + 1] = wd >> 16;
+                }
+            } else {  // A/B: the taps in tap order, slots clamped per row
+                const int sy = lz_const(L.t.yofs, y);
+#pragma unroll
+                for (int k = 0; k < 8; ++k) {
+                    const int slot = min(max(sy - 3 + k, 0), h - 1) & 7;
+#pragma unroll
+                    for (int q = 0; q < CC; ++q) hs[k][q] = ring[wave][slot][lane * RS + q];
+                }
+                const int* b32 = reinterpret_cast<const int*>(L.t.yai);
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    const int wd = lz_const(b32, 4 * y + k);
+                    bb[2 * k] = (int)(short)(wd & 0xFFFF);
+                    bb[2 * k + 1] = wd >> 16;
+                }
             }
 #pragma unroll
             for (int q = 0; q < CC; ++q) {
-                // |h| < 2^23 (255 x sum |coefficient| <= 255 x ~2,900) and |b| < 2^12:
-                // 24-bit multiplies, whose low 32 bits are the int product
-                // (wrapping as OpenCV's int arithmetic does)
+                // |h| < 2^23 (255 x sum |coefficient| <= 255 x ~2,900) and |b| < 2^12
+                // (a slot's summed coefficients too): 24-bit multiplies, whose low
+                // 32 bits are the int product (wrapping as OpenCV's int arithmetic does)
                 const int s0 = __mul24(hs[0][q], bb[0]) + __mul24(hs[1][q], bb[1]) + __mul24(hs[2][q], bb[2]) +
                                __mul24(hs[3][q], bb[3]);
                 const int s1 = __mul24(hs[4][q], bb[4]) + __mul24(hs[5][q], bb[5]) + __mul24(hs[6][q], bb[6]) +
@@ -297,6 +333,14 @@ __global__ void __launch_bounds__(kBlock) lanczos_kernel(LanczosLaunch L, int st
                 else o[q] = (TOut)normalize_u8v(cn[q], vi);
             }
         } else {
+            const int sy = lz_const(L.t.yofs, y);
+            TW hs[8][CC];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                const int slot = min(max(sy - 3 + k, 0), h - 1) & 7;
+#pragma unroll
+                for (int q = 0; q < CC; ++q) hs[k][q] = ring[wave][slot][lane * RS + q];
+            }
             float bb[8];
 #pragma unroll
             for (int k = 0; k < 8; ++k) bb[k] = lz_const(L.t.yaf, 8 * y + k);
@@ -324,9 +368,13 @@ __global__ void __launch_bounds__(kBlock) lanczos_kernel(LanczosLaunch L, int st
 #pragma unroll
             for (int q = 0; q < CC; ++q) own |= (uint32_t)(uint8_t)o[q] << (8 * q);
             const int xq = x & ~3;
-            const bool quad = dst_al && xq + 4 <= L.dst.w;  // uniform per quad
+            const bool quad = dst_al && (full || xq + 4 <= L.dst.w);  // uniform per quad; per wave where full
             const uint32_t word = quad_pack<CC>(own, lane & 3);
-            if (quad) {
+            if (dst_al && full) {
+                if ((lane & 3) < CC)
+                    __builtin_amdgcn_raw_buffer_store_b32(word, drs.r, (int)(orow + (uint32_t)(xq * CC + 4 * (lane & 3))),
+                                                          0, 0);
+            } else if (quad) {
                 if ((lane & 3) < CC)
                     __builtin_amdgcn_raw_buffer_store_b32(word, drs.r, (int)(orow + (uint32_t)(xq * CC + 4 * (lane & 3))),
                                                           0, 0);
@@ -481,9 +529,20 @@ int lanczos_tables(const ResizeLaunch& R, double inv_x, double inv_y, hipStream_
             if (b) std::memcpy(img.data() + o, p, b);
             return o;
         };
+        // u8 vertical coefficients regrouped by ring slot: tap k of row y reads
+        // source row clip(sy - 3 + k, 0, h - 1), held in slot (row & 7)
+        std::vector<int> yr(4 * (size_t)R.dst.h);
+        for (int y = 0; y < R.dst.h; ++y) {
+            int b[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+            for (int k = 0; k < 8; ++k)
+                b[std::min(std::max(yo[y] - 3 + k, 0), R.src.h - 1) & 7] += yi[8 * (size_t)y + k];
+            for (int m = 0; m < 4; ++m)
+                yr[4 * (size_t)y + m] = (int)(((uint32_t)b[2 * m] & 0xFFFFu) | ((uint32_t)b[2 * m + 1] << 16));
+        }
         const size_t o0 = put(xo.data(), xo.size() * 4), o1 = put(xi.data(), xi.size() * 2),
                      o2 = put(xf.data(), xf.size() * 4), o3 = put(yo.data(), yo.size() * 4),
-                     o4 = put(yi.data(), yi.size() * 2), o5 = put(yf.data(), yf.size() * 4);
+                     o4 = put(yi.data(), yi.size() * 2), o5 = put(yf.data(), yf.size() * 4),
+                     o6 = put(yr.data(), yr.size() * 4);
         if (g_lz_tabs.size() > 64)  // bounded cache
             (void)evict_device_cache(g_lz_tabs, free_lz);
         CachedLanczos c;
@@ -502,6 +561,7 @@ int lanczos_tables(const ResizeLaunch& R, double inv_x, double inv_y, hipStream_
         c.t.yofs = reinterpret_cast<const int*>(b + o3);
         c.t.yai = reinterpret_cast<const short*>(b + o4);
         c.t.yaf = reinterpret_cast<const float*>(b + o5);
+        c.t.yrot = reinterpret_cast<const int*>(b + o6);
         c.t.xmin = xmin;
         c.t.xmax = xmax;
         it = g_lz_tabs.emplace(key, c).first;

@@ -34,6 +34,7 @@ namespace vacv {
 namespace {
 
 constexpr int kFetchIters = 3;    // 16-byte chunks per thread and batch
+constexpr int kOobOff = (int)0x80000000;  // a buffer offset past every plane: loads read 0, stores drop
 constexpr int kMaxLds = 64 * 1024;
 // cache policy of the strip loads: the default (0), not non-temporal.  The
 // 16-byte chunks at a strip's edges share 128-byte lines with the
@@ -49,31 +50,39 @@ constexpr int kMaxLds = 64 * 1024;
 #define VACV_STRIP_SAUX VACV_STORE_AUX
 #endif
 
-// one output pixel (lane-quad packed for u8) at row byte offset row_off
+// one output pixel (lane-quad packed for u8) at row byte offset row_off.
+// Every store is issued (an offset past the plane where a lane has nothing to
+// write: the store is dropped), so each path through a batch issues a fixed
+// number of stores and the compiler's wait for the next batch's loads (park)
+// is a counted vmcnt that leaves them in flight.  u8: the lane quad's dword
+// store always; the CC byte stores of partial quads only in strips that have
+// them (a uniform branch: every path still holds the dword stores).
+constexpr uint32_t kOobStore = 0x80000000u;
 template <int CC, int OUT>
 __device__ __forceinline__ void store_pixel(const int (&v)[CC], const ChanNorm (&cn)[CC], const Rsrc& drs, uint32_t row_off,
-                                            int ox, int qx, int W, bool quad_full, int lane) {
+                                            int ox, int qx, int W, bool quad_full, bool strip_full, int lane) {
     if constexpr (OUT == kOutSame) {
         uint32_t own = 0;
 #pragma unroll
         for (int k = 0; k < CC; ++k) own |= (uint32_t)v[k] << (8 * k);
         const uint32_t word = quad_pack<CC>(own, lane & 3);
-        if (quad_full) {
-            if ((lane & 3) < CC)
-                __builtin_amdgcn_raw_buffer_store_b32(word, drs.r, (int)(row_off + (uint32_t)(qx * CC + 4 * (lane & 3))), 0,
-                                                      VACV_STRIP_SAUX);
-        } else if (ox < W) {
+        const bool wq = quad_full && (lane & 3) < CC;
+        __builtin_amdgcn_raw_buffer_store_b32(word, drs.r, (int)(wq ? row_off + (uint32_t)(qx * CC + 4 * (lane & 3)) : kOobStore),
+                                              0, VACV_STRIP_SAUX);
+        if (!strip_full) {  // uniform: the partial quads' bytes
+            const bool wb = !quad_full && ox < W;
 #pragma unroll
             for (int k = 0; k < CC; ++k)
-                __builtin_amdgcn_raw_buffer_store_b8((unsigned char)v[k], drs.r, (int)(row_off + (uint32_t)(ox * CC + k)), 0,
+                __builtin_amdgcn_raw_buffer_store_b8((unsigned char)v[k], drs.r,
+                                                     (int)(wb ? row_off + (uint32_t)(ox * CC + k) : kOobStore), 0,
                                                      VACV_STRIP_SAUX);
         }
-    } else if (ox < W) {
+    } else {
         uint32_t f[CC];
 #pragma unroll
         for (int k = 0; k < CC; ++k)
             f[k] = __builtin_bit_cast(uint32_t, OUT == kOutF32 ? (float)v[k] : normalize_u8v(cn[k], v[k]));
-        const int off = (int)(row_off + (uint32_t)(ox * CC * 4));
+        const int off = (int)(ox < W ? row_off + (uint32_t)(ox * CC * 4) : kOobStore);
         if constexpr (CC == 1) {
             __builtin_amdgcn_raw_buffer_store_b32(f[0], drs.r, off, 0, VACV_STRIP_SAUX);
         } else if constexpr (CC == 2) {
@@ -161,32 +170,56 @@ resize_strip_kernel(ResizeLaunch L, int strips_x, int groups, int rows_per_group
         }
     }
     uint4 pre[kFetchIters];
-    uint32_t dst_off[kFetchIters];
+    uint32_t dst_off[kFetchIters], tail_o[kFetchIters];
+    uint32_t tailm = 0;
+    // every fetch issues all kFetchIters loads (chunks beyond the rows being
+    // added read out of range: zeros, no fault; a chunk straddling the plane's
+    // end likewise, assembled bytewise in park()), so the loads are
+    // unconditional and the compiler can count them: park() then waits for
+    // the loads only, not for the blend's stores issued after them.
+    // per thread and chunk u, what no fill changes: the chunk's byte offset
+    // from its row's strip start (rp % 16 == 0: (r rp + col0) & ~15 =
+    // r rp + (col0 & ~15)), its row within the fill, its column in a ring row
+    uint32_t koff[kFetchIters];
+#pragma unroll
+    for (int u = 0; u < kFetchIters; ++u)
+        koff[u] = (rcu[u] >> 16) * rp + (col0 & ~15u) + 16u * (rcu[u] & 0xFFFFu);
     auto fetch = [&](int r_first, int r_last) {
         const uint32_t nrows = (uint32_t)max(r_last - r_first + 1, 0);
+        const uint32_t obase = (uint32_t)r_first * rp;  // uniform
+        const uint32_t s0 = slot((uint32_t)r_first);    // uniform
+        tailm = 0;
 #pragma unroll
         for (int u = 0; u < kFetchIters; ++u) {
             const uint32_t rr = rcu[u] >> 16, c = rcu[u] & 0xFFFFu;
-            dst_off[u] = 0xFFFFFFFFu;
-            if (rr < nrows) {
-                const uint32_t r = (uint32_t)r_first + rr;
-                const uint32_t o = ((r * rp + col0) & ~15u) + 16u * c;
-                if (o + 16u <= lim) {
-                    const auto v = __builtin_amdgcn_raw_buffer_load_b128(srs.r, (int)o, 0, VACV_STRIP_AUX);
-                    pre[u] = *reinterpret_cast<const uint4*>(&v);
-                } else {  // the plane's last chunk: a straddling 16-byte load reads as zeros
-                    uint32_t d[4] = {0u, 0u, 0u, 0u};
-#pragma unroll 1
-                    for (uint32_t e = 0; e < 16u; ++e)
-                        if (o + e < lim)
-                            d[e >> 2] |= (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(srs.r, (int)(o + e), 0, 0) << (8 * (e & 3));
-                    pre[u] = make_uint4(d[0], d[1], d[2], d[3]);
-                }
-                dst_off[u] = slot(r) * (uint32_t)stride + 16u * c;
-            }
+            const uint32_t o = obase + koff[u];
+            const bool live = rr < nrows;
+            const bool tail = live && o + 16u > lim;
+            uint32_t sl = s0 + rr;  // (r_first + rr) mod ring: rr < ring
+            sl = sl >= (uint32_t)ring ? sl - (uint32_t)ring : sl;
+            dst_off[u] = live ? sl * (uint32_t)stride + 16u * c : 0xFFFFFFFFu;
+            tail_o[u] = o;
+            tailm |= tail ? 1u << u : 0u;
+            const auto v = __builtin_amdgcn_raw_buffer_load_b128(srs.r, (int)(live && !tail ? o : kOobOff), 0,
+                                                                 VACV_STRIP_AUX);
+            pre[u] = *reinterpret_cast<const uint4*>(&v);
         }
     };
     auto park = [&]() {
+        if (tailm) {  // the plane's last chunk: a straddling 16-byte load reads as zeros
+#pragma unroll
+            for (int u = 0; u < kFetchIters; ++u) {
+                if ((tailm >> u) & 1u) {
+                    uint32_t d[4] = {0u, 0u, 0u, 0u};
+#pragma unroll 1
+                    for (uint32_t e = 0; e < 16u; ++e)
+                        if (tail_o[u] + e < lim)
+                            d[e >> 2] |= (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(srs.r, (int)(tail_o[u] + e), 0, 0)
+                                         << (8 * (e & 3));
+                    pre[u] = make_uint4(d[0], d[1], d[2], d[3]);
+                }
+            }
+        }
 #pragma unroll
         for (int u = 0; u < kFetchIters; ++u)
             if (dst_off[u] != 0xFFFFFFFFu) *reinterpret_cast<uint4*>(lds + dst_off[u]) = pre[u];
@@ -212,17 +245,24 @@ resize_strip_kernel(ResizeLaunch L, int strips_x, int groups, int rows_per_group
         }
     };
 
+    // uniform: every lane quad of the strip whole, the destination dword-aligned
+    const bool strip_full = ox0 + SW <= W && dst_al;
     const int batches = (oy_end - oy_begin + BR - 1) / BR;
     if (batches <= 0) return;  // uniform
     int lo_row, hi_row;
     rows_of(0, lo_row, hi_row);
     fetch(lo_row, hi_row);
     put_rows(0);
+    park();
     int loaded = hi_row;
+    // park() of batch b + 1 sits at the END of iteration b, after its blend:
+    // on every path into it the blend's stores follow the loads, so its wait
+    // leaves them in flight (at the top of the loop, the path from the
+    // prologue -- no stores -- made it a vmcnt(0) for every batch)
     for (int b = 0; b < batches; ++b) {
-        park();
         __syncthreads();  // batch b's rows and taps are in LDS; batch b - 1's reads are done
-        if (b + 1 < batches) {  // the next batch's new rows, in flight while this one blends
+        const bool more = b + 1 < batches;  // uniform
+        if (more) {  // the next batch's new rows, in flight while this one blends
             int l1, h1;
             rows_of(b + 1, l1, h1);
             fetch(max(l1, loaded + 1), h1);
@@ -271,12 +311,13 @@ resize_strip_kernel(ResizeLaunch L, int strips_x, int groups, int rows_per_group
                         const uint32_t sel = (uint32_t)k | (0x0Cu << 8) | ((uint32_t)(CC + k) << 16) | (0x0Cu << 24);
                         v[k] = blend_fixed<MODE>(__builtin_amdgcn_perm(a1, a0, sel), __builtin_amdgcn_perm(c1, c0, sel), wx, wA, wB);
                     }
-                    if (oy >= oy_end) continue;  // wave-uniform
-                    const uint32_t row_off = (uint32_t)oy * (uint32_t)L.dst.row_pitch + drs.delta;
-                    store_pixel<CC, OUT>(v, cn, drs, row_off, ox, qx, W, quad_full, lane);
+                    // rows past the group: stores dropped (issued all the same)
+                    const uint32_t row_off = oy < oy_end ? (uint32_t)oy * (uint32_t)L.dst.row_pitch + drs.delta : kOobStore;
+                    store_pixel<CC, OUT>(v, cn, drs, row_off, ox, qx, W, quad_full, strip_full, lane);
                 }
             }
         }
+        if (more) park();
     }
 }
 

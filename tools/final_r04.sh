@@ -24,7 +24,7 @@ timeout -k 10 900 python3 -u -m pytest tests -m gpu -x -v --timeout 200 --timeou
 tail -2 gpurun_out/${T}_gpu_tests.log
 step smoke
 timeout -k 10 200 python3 -c "import __graft_entry__ as g; g.smoke()" || exit 1
-for W in resize_normalize:resize_cols warp:warp_ring cvt_normalize:color_kernel cubic_stats:cubic_direct yuv_resize:yuv_resize; do
+for W in resize_normalize:resize_cols warp:warp_ring cvt_normalize:color_kernel cubic_stats:cubic_cols yuv_resize:yuv_resize; do
   wl=${W%%:*}; key=${W##*:}
   step "pmc $wl"
   timeout -k 10 400 rocprofv3 -i "$R/tools/pmc_bench.txt" -d "$R/gpurun_out/pmc_$wl" -o pmc --output-format csv \
@@ -57,7 +57,7 @@ step kbench_stats
 timeout -k 10 500 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/prof_kbench" -o kbench --output-format csv \
     -- python3 "$R/tools/kbench.py" --op all --iters 30 > gpurun_out/prof_kbench.log 2>&1 || exit $?
 find gpurun_out/prof_kbench -name "*kernel_stats.csv" -exec cp {} "gpurun_out/${T}_kbench_kernel_stats.csv" \;
-for W in "resize:1280x720:resize_cols" "resize_other:area_1080p_960:area_u8_unit" "lanczos:lanczos_1080p_640x360_u8:lanczos"; do
+for W in "resize:1280x720:resize_strip" "resize_other:area_1080p_960:area_u8_unit" "lanczos:lanczos_1080p_640x360_u8:lanczos"; do
   op=${W%%:*}; rest=${W#*:}; only=${rest%%:*}; key=${rest#*:}
   step "pmc $key"
   timeout -s KILL 300 rocprofv3 -i "$R/tools/pmc_bench.txt" -d "$R/gpurun_out/pmc_k_$key" -o pmc --output-format csv \
