@@ -347,6 +347,12 @@ cubic_cols_kernel(ResizeLaunch L, int col_blocks, int plane_tasks, int blocks_pe
 
         // ---- gathers: the 16 bytes at (row ty.i - 1 + q, column tx.i - 1) ----
         uint32_t ch[kCcRows][4][4];
+        // uniform: can any gather of the task reach past the plane's last
+        // byte?  If not, no per-lane range check (no exec-mask branch per load)
+        const uint32_t last_a = (uint32_t)(__builtin_amdgcn_readlane(my_i, nrow - 1) + 2) * rp + xoff;
+        const bool safe = __builtin_amdgcn_ballot_w64(last_a + 16u > slimit) == 0;
+        auto gather = [&](auto safe_c) {
+        constexpr bool SAFE = decltype(safe_c)::value;
 #pragma unroll
         for (int r = 0; r < kCcRows; ++r) {
             const uint32_t ro = (uint32_t)(__builtin_amdgcn_readlane(my_i, r) - 1) * rp + xoff;
@@ -357,7 +363,7 @@ cubic_cols_kernel(ResizeLaunch L, int col_blocks, int plane_tasks, int blocks_pe
                 const float cq = __uint_as_float((uint32_t)__builtin_amdgcn_readlane((int)__float_as_uint(my_c[q]), r));
                 if (r >= nrow || cq == 0.f) continue;  // uniform
                 const uint32_t a4 = (ro + (uint32_t)q * rp) & ~3u;
-                if (a4 + 16u <= slimit) {
+                if (SAFE || a4 + 16u <= slimit) {
                     const auto v = __builtin_amdgcn_raw_buffer_load_b128(srs.r, (int)a4, 0, VACV_LOAD_AUX);
                     ch[r][q][0] = v[0];
                     ch[r][q][1] = v[1];
@@ -371,6 +377,9 @@ cubic_cols_kernel(ResizeLaunch L, int col_blocks, int plane_tasks, int blocks_pe
                 }
             }
         }
+        };
+        if (safe) gather(std::true_type());
+        else gather(std::false_type());
 
         ChanNorm cn[CC] = {};
         if (OUT == kOutNorm) {

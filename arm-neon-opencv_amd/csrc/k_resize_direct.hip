@@ -286,26 +286,36 @@ resize_cols_kernel(ResizeLaunch L, int col_blocks, int row_groups, int tasks) {
         my_w = (uint32_t)ty.w0 | ((uint32_t)ty.w1 << 16);
     }
     uint32_t tap[kColsRows][NR][2];
+    // uniform: can any gather of the task reach past the plane's last byte
+    // (only tasks holding the plane's last source row)?  If not, the gathers
+    // are issued without a per-lane range check (no exec-mask branch per load)
+    const uint32_t last_ro = (uint32_t)__builtin_amdgcn_readlane((int)my_row, nrow - 1) + (uint32_t)(NR - 1) * rp;
+    const bool safe = __builtin_amdgcn_ballot_w64(last_ro + xoff + 8u > slimit) == 0;
+    auto gather = [&](auto safe_c) {
+        constexpr bool SAFE = decltype(safe_c)::value;
 #pragma unroll
-    for (int r = 0; r < kColsRows; ++r) {
-        const uint32_t ro = (uint32_t)__builtin_amdgcn_readlane((int)my_row, r);
-        const uint32_t wr = (uint32_t)__builtin_amdgcn_readlane((int)my_w, r);
+        for (int r = 0; r < kColsRows; ++r) {
+            const uint32_t ro = (uint32_t)__builtin_amdgcn_readlane((int)my_row, r);
+            const uint32_t wr = (uint32_t)__builtin_amdgcn_readlane((int)my_w, r);
 #pragma unroll
-        for (int n = 0; n < NR; ++n) {
-            const uint32_t o = ro + (uint32_t)n * rp + xoff;
-            tap[r][n][0] = tap[r][n][1] = 0u;
-            // a row of zero weight is not read (its product is 0 either way)
-            if (r < nrow && (n == 0 ? (ONE_ROW || (wr & 0xFFFFu)) : (wr >> 16))) {
-                if (o + 8u <= slimit) {
-                    load_taps<CC, false, kLoadAux>(srs, o, tap[r][n][0], tap[r][n][1]);
-                } else {  // the plane's last pixels: bytewise (an overhanging load reads zeros)
-                    const unsigned char* b = sp + (int64_t)(o - srs.delta);
+            for (int n = 0; n < NR; ++n) {
+                const uint32_t o = ro + (uint32_t)n * rp + xoff;
+                tap[r][n][0] = tap[r][n][1] = 0u;
+                // a row of zero weight is not read (its product is 0 either way)
+                if (r < nrow && (n == 0 ? (ONE_ROW || (wr & 0xFFFFu)) : (wr >> 16))) {
+                    if (SAFE || o + 8u <= slimit) {
+                        load_taps<CC, false, kLoadAux>(srs, o, tap[r][n][0], tap[r][n][1]);
+                    } else {  // the plane's last pixels: bytewise (an overhanging load reads zeros)
+                        const unsigned char* b = sp + (int64_t)(o - srs.delta);
 #pragma unroll
-                    for (int e = 0; e < 2 * CC; ++e) tap[r][n][e >> 2] |= (uint32_t)b[e] << (8 * (e & 3));
+                        for (int e = 0; e < 2 * CC; ++e) tap[r][n][e >> 2] |= (uint32_t)b[e] << (8 * (e & 3));
+                    }
                 }
             }
         }
-    }
+    };
+    if (safe) gather(std::true_type());
+    else gather(std::false_type());
     ChanNorm cn[CC] = {};
     if (OUT == kOutNorm) {
 #pragma unroll
