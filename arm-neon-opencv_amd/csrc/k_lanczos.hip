@@ -127,6 +127,9 @@ __device__ __forceinline__ T lz_const(const T* p, int i) {
     return ((const __attribute__((address_space(4))) T*)(uintptr_t)p)[i];
 }
 
+#ifndef VACV_LZ_D
+#define VACV_LZ_D 3  // u8 source rows in flight per wave (1 / 2 / 3 / 4 / 6 / 8: 0.580 / 0.522 / 0.495 / 0.525 / 0.534 / 0.565 ms)
+#endif
 #ifndef VACV_LZ_SLOTS
 #define VACV_LZ_SLOTS 1
 #endif
@@ -139,7 +142,7 @@ __global__ void __launch_bounds__(kBlock) lanczos_kernel(LanczosLaunch L, int st
     constexpr int ND = U8 ? (8 * CC + 6) / 4 : 8 * CC;
     // source rows in flight per wave (the loads of rows r + 1 .. r + D - 1
     // run while row r is resized)
-    constexpr int D = U8 ? 4 : 2;
+    constexpr int D = U8 ? VACV_LZ_D : 2;
     // per wave: 8 source rows x 64 columns x RS (padding c = 3 to 4, for one
     // 16-byte LDS access per lane and row, cost a workgroup per CU of LDS:
     // 0.589 vs 0.530 ms)

@@ -244,7 +244,7 @@ resize_direct_kernel(ResizeLaunch L, int blocks_per_plane, int total, int xcd) {
 constexpr int kColsRows = VACV_COLS_ROWS;  // output rows per wave task (a multiple of 8)
 template <int CC, int OUT, int MODE, bool ONE_ROW>
 __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8)))
-resize_cols_kernel(ResizeLaunch L, int col_blocks, int row_groups, int tasks) {
+resize_cols_kernel(ResizeLaunch L, int col_blocks, int row_groups, int tasks, int xcd_groups) {
     constexpr int NR = ONE_ROW ? 1 : 2;           // gathered source rows per output row
     using TOut = typename std::conditional<(OUT == kOutSame), uint8_t, float>::type;
     constexpr int kOutPx = CC * (int)sizeof(TOut);
@@ -255,7 +255,13 @@ resize_cols_kernel(ResizeLaunch L, int col_blocks, int row_groups, int tasks) {
     __shared__ __attribute__((aligned(16))) unsigned char xch[4][kHalf * kRowB];
     const int lane = (int)threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
-    const int task = (int)blockIdx.x * 4 + wave;   // (plane, row group, column block), column block fastest
+    // (plane, row group, column block), column block fastest.  xcd_groups > 0:
+    // XCD-contiguous order -- workgroup b runs on XCD b % 8, and the 8 XCDs
+    // take consecutive runs of xcd_groups workgroups (neighbouring column
+    // blocks share the 128-byte source lines at their edges, which then come
+    // from one L2)
+    const int blk = xcd_groups > 0 ? (int)(blockIdx.x % 8) * xcd_groups + (int)(blockIdx.x / 8) : (int)blockIdx.x;
+    const int task = blk * 4 + wave;
     if (task >= tasks) return;                     // whole wave
     const int per_plane = col_blocks * row_groups;
     const int pidx = task / per_plane;
@@ -398,8 +404,11 @@ hipError_t launch_one(const ResizeLaunch& L, hipStream_t s) {
         int col_blocks = 0, row_groups = 0;
         int64_t tasks = 0;
         if (cols_plan(L, kOutPx, col_blocks, row_groups, tasks)) {
-            hipLaunchKernelGGL((resize_cols_kernel<CC, OUT, MODE, ONE_ROW>), dim3((unsigned)((tasks + 3) / 4)), dim3(kBlock),
-                               0, s, L, col_blocks, row_groups, (int)tasks);
+            const int64_t groups = (tasks + 3) / 4;
+            const int xcd = tune_or(VACV_TUNE_DIRECT_XCD, 0) ? (int)((groups + 7) / 8) : 0;
+            const int64_t grid = xcd ? (int64_t)xcd * 8 : groups;
+            hipLaunchKernelGGL((resize_cols_kernel<CC, OUT, MODE, ONE_ROW>), dim3((unsigned)grid), dim3(kBlock), 0, s, L,
+                               col_blocks, row_groups, (int)tasks, xcd);
             return hipGetLastError();
         }
     }
