@@ -114,9 +114,11 @@ constexpr int kRingMaxIt = 6;  // DMA instructions per wave and frame, at most (
 #define VACV_RING_WPE 1
 #endif
 #ifndef VACV_RING_GRP
-// pixels whose taps are read before their blends: 2 keeps the kernel at 95
-// VGPRs, 5 waves per SIMD (4 pixels: 103, 4 waves; 720p rot15 0.159 vs 0.169 ms)
-#define VACV_RING_GRP 2
+// u8 output: pixels whose taps are read before their blends.  4: 103 VGPRs, 4
+// waves per SIMD; 2: 95, 5 waves (round 4, one box, 720p rot15: 0.1761 /
+// 0.1776 vs 0.1807 / 0.1812 ms; round 2's register-staged kernel preferred 2).
+// Other outputs keep 2.
+#define VACV_RING_GRP 4
 #endif
 template <int CC, int OUT, int NP, bool PLANAR>
 __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(VACV_RING_WPE)))
@@ -536,7 +538,7 @@ warp_ring_kernel(WarpLaunch L, int gx, int gy, int kf, int S, int rows_max, int 
         }
     };
     auto sample = [&](auto full_c, int f, uint32_t sbase) {
-        constexpr int kGrp = VACV_RING_GRP;
+        constexpr int kGrp = OUT == kOutSame ? VACV_RING_GRP : 2;
 #pragma unroll
         for (int j0 = 0; j0 < NP; j0 += kGrp) {
             uint32_t tp[kGrp][4];
