@@ -281,6 +281,7 @@ __global__ void __launch_bounds__(kBlock) lanczos_kernel(LanczosLaunch L, int st
         for (int k = 0; k < CC; ++k) cn[k] = chan_norm(L.norm, img, CC == 1 ? plane % L.norm.c_total : k);
     }
 
+    constexpr uint32_t kOobStore = 0x80000000u;  // a store offset past every plane: dropped
     // VResizeLanczos4 of output row y from the ring, and its store
     auto emit = [&](int y) {
         TOut o[CC];
@@ -426,20 +427,36 @@ __global__ void __launch_bounds__(kBlock) lanczos_kernel(LanczosLaunch L, int st
         uint32_t buf[D][ND];
 #pragma unroll
         for (int u = 0; u < D; ++u) load(safe_c, buf[u], min(rs + u, re));
+        // D - 1 dropped stores after the prologue's windows: the path into
+        // the loop then has the steady state's shape (a store per step after
+        // each window), and the compiler's wait for a window is not the
+        // vmcnt(0) the prologue path alone would need
+#pragma unroll
+        for (int u = 0; u + 1 < D; ++u) __builtin_amdgcn_raw_buffer_store_b32(0u, drs.r, (int)kOobStore, 0, 0);
         for (int r = rs; r <= re; r += D) {
 #pragma unroll
             for (int u = 0; u < D; ++u) {
+                // Every step runs, also the up to D - 1 past the band's last row
+                // (their windows are the last row again; they only write ring
+                // slots no pending output reads), and every step issues at
+                // least one store: a row's, or a dropped one (an offset past
+                // the plane).  The compiler's wait for a window then counts the
+                // stores issued after it and leaves them in flight; with steps
+                // of no store (or skipped) on some path, its waits drained the
+                // stores too (vmcnt(0) at every loop iteration's first window).
                 const int rr = r + u;
-                if (rr <= re) {  // uniform
-                    hrow(buf[u], rr & 7);
-                    while (y < y1 && need == rr) {
+                hrow(buf[u], rr & 7);
+                if (y < y1 && need == rr) {  // uniform
+                    do {
                         // y is wave-uniform; said so, its table reads are scalar
                         // loads (as vector loads they would wait behind the windows)
                         y = __builtin_amdgcn_readfirstlane(y);
                         emit(y);
                         ++y;
                         if (y < y1) need = min(lz_const(L.t.yofs, y) + 4, h - 1);
-                    }
+                    } while (y < y1 && need == rr);
+                } else {
+                    __builtin_amdgcn_raw_buffer_store_b32(0u, drs.r, (int)kOobStore, 0, 0);
                 }
                 load(safe_c, buf[u], min(rr + D, re));
             }
