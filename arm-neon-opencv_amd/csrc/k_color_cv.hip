@@ -85,36 +85,175 @@ __global__ void __launch_bounds__(256) yuv420_cv_kernel(CvColorLaunch L) {
     }
 }
 
-template <int DCN, typename T>
-__global__ void __launch_bounds__(256) gray_kernel(CvColorLaunch L) {
+// GRAY2BGR(A): a thread takes a unit of PX pixels of one row (u8: 16, one
+// 16-byte load and 3 or 4 16-byte stores; fp32: 4, the same in floats) where
+// the unit is whole and the host found every base and pitch 16-byte aligned;
+// elementwise otherwise (a row's last partial unit, unaligned images).  Round
+// 3's one-pixel-per-thread kernel (byte loads, 3 byte stores) ran at 0.21 of
+// 8 TB/s; 4-pixel u8 units (a dword in, dwordx3 out) 0.56.
+// The same decode with a thread per 8 x 2 pixels (4 chroma samples), for
+// images whose width is a multiple of 8 with every base and pitch aligned
+// (host-checked): Y as two 8-byte loads, the chroma as one 8-byte (NV12/21)
+// or two 4-byte (planar) loads, each output row segment as 16-byte (BGRA: 32
+// bytes) or 8-byte (BGR: 24 bytes) stores.  The 2 x 2 kernel above issued
+// byte loads and 2-byte stores (nv21 -> BGRA 0.48, YV12 -> BGR 0.35 of 8 TB/s).
+template <int DCN>
+__global__ void __launch_bounds__(256) yuv420_cv8_kernel(CvColorLaunch L, int upr) {
     const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int img = blockIdx.y;
-    if (t >= (int64_t)L.w * L.h) return;
-    const int y = (int)(t / L.w), x = (int)(t - (int64_t)y * L.w);
-    const T v = *reinterpret_cast<const T*>(L.src + (int64_t)img * L.src_img + (int64_t)y * L.src_row +
-                                            (int64_t)x * sizeof(T));
-    T* o = reinterpret_cast<T*>(L.dst + (int64_t)img * L.dst_img + (int64_t)y * L.dst_row) + (int64_t)x * DCN;
-    o[0] = v;
-    o[1] = v;
-    o[2] = v;
-    if (DCN == 4) o[3] = sizeof(T) == 1 ? (T)255 : (T)1;
+    const int bh = L.h >> 1;
+    if (t >= (int64_t)upr * bh) return;
+    const int by = (int)(t / upr), u = (int)(t - (int64_t)by * upr);
+    const int x0 = 8 * u;
+    const unsigned char* s = L.src + (int64_t)img * L.src_img;
+    uint32_t cu, cv;  // 4 U and 4 V bytes
+    if (L.layout <= 1) {
+        typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+        const u32x2 c = *reinterpret_cast<const u32x2*>(s + (int64_t)(L.h + by) * L.src_row + x0);
+        // bytes u0 v0 u1 v1 | u2 v2 u3 v3 (NV12); V first for NV21
+        const uint32_t ev = __builtin_amdgcn_perm(c[1], c[0], 0x06040200u);  // bytes 0 2 4 6
+        const uint32_t od = __builtin_amdgcn_perm(c[1], c[0], 0x07050301u);  // bytes 1 3 5 7
+        cu = L.layout == 0 ? ev : od;
+        cv = L.layout == 0 ? od : ev;
+    } else {
+        const unsigned char* c0 = s + (int64_t)L.h * L.src_row;
+        const int64_t q = (int64_t)(L.w >> 1) * bh, k = (int64_t)by * (L.w >> 1) + (x0 >> 1);
+        const uint32_t p0 = *reinterpret_cast<const uint32_t*>(c0 + k);
+        const uint32_t p1 = *reinterpret_cast<const uint32_t*>(c0 + q + k);
+        cu = L.layout == 2 ? p1 : p0;
+        cv = L.layout == 2 ? p0 : p1;
+    }
+    int ruv[4], guv[4], buv[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int uu = (int)((cu >> (8 * i)) & 0xFFu) - 128, vv = (int)((cv >> (8 * i)) & 0xFFu) - 128;
+        ruv[i] = (1 << 19) + 1673527 * vv;
+        guv[i] = (1 << 19) - 852492 * vv - 409993 * uu;
+        buv[i] = (1 << 19) + 2116026 * uu;
+    }
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+        typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+        const u32x2 yv = *reinterpret_cast<const u32x2*>(s + (int64_t)(2 * by + r) * L.src_row + x0);
+        uint32_t px[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const int Y = (int)((yv[j >> 2] >> (8 * (j & 3))) & 0xFFu);
+            px[j] = bt601(Y, ruv[j >> 1], guv[j >> 1], buv[j >> 1], L.bidx);
+        }
+        unsigned char* o = L.dst + (int64_t)img * L.dst_img + (int64_t)(2 * by + r) * L.dst_row + (int64_t)x0 * DCN;
+        if constexpr (DCN == 4) {
+            reinterpret_cast<u32x4*>(o)[0] = u32x4{px[0], px[1], px[2], px[3]};
+            reinterpret_cast<u32x4*>(o)[1] = u32x4{px[4], px[5], px[6], px[7]};
+        } else {
+            // 8 pixels' 24 bytes: drop each pixel's alpha byte
+            uint32_t w[6];
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                const uint32_t a = px[4 * i], b = px[4 * i + 1], c = px[4 * i + 2], d = px[4 * i + 3];
+                w[3 * i] = __builtin_amdgcn_perm(b, a, 0x04020100u);      // a0 a1 a2 b0
+                w[3 * i + 1] = __builtin_amdgcn_perm(c, b, 0x05040201u);  // b1 b2 c0 c1
+                w[3 * i + 2] = __builtin_amdgcn_perm(d, c, 0x06050402u);  // c2 d0 d1 d2
+            }
+            typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+#pragma unroll
+            for (int k = 0; k < 3; ++k) reinterpret_cast<u32x2*>(o)[k] = u32x2{w[2 * k], w[2 * k + 1]};
+        }
+    }
+}
+
+template <typename T>
+constexpr int gray_px() { return sizeof(T) == 1 ? 16 : 4; }
+template <int DCN, typename T>
+__global__ void __launch_bounds__(256) gray_kernel(CvColorLaunch L, int upr) {
+    constexpr int PX = gray_px<T>();
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int img = blockIdx.y;
+    if (t >= (int64_t)upr * L.h) return;
+    const int y = (int)(t / upr), u = (int)(t - (int64_t)y * upr);
+    const int x0 = PX * u;
+    const unsigned char* srow = L.src + (int64_t)img * L.src_img + (int64_t)y * L.src_row;
+    unsigned char* drow = L.dst + (int64_t)img * L.dst_img + (int64_t)y * L.dst_row;
+    constexpr T alpha = sizeof(T) == 1 ? (T)255 : (T)1;
+    if (L.aligned && x0 + PX <= L.w) {
+        if constexpr (sizeof(T) == 1) {
+            const u32x4 v = *reinterpret_cast<const u32x4*>(srow + x0);
+            u32x4* o = reinterpret_cast<u32x4*>(drow + DCN * x0);
+            if constexpr (DCN == 3) {
+                // per source dword: bytes v0 v0 v0 v1 | v1 v1 v2 v2 | v2 v3 v3 v3
+                uint32_t w[12];
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    w[3 * i] = __builtin_amdgcn_perm(v[i], v[i], 0x01000000u);
+                    w[3 * i + 1] = __builtin_amdgcn_perm(v[i], v[i], 0x02020101u);
+                    w[3 * i + 2] = __builtin_amdgcn_perm(v[i], v[i], 0x03030302u);
+                }
+#pragma unroll
+                for (int k = 0; k < 3; ++k) o[k] = u32x4{w[4 * k], w[4 * k + 1], w[4 * k + 2], w[4 * k + 3]};
+            } else {
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const uint32_t a = 0xFF000000u, d = v[i];
+                    o[i] = u32x4{(d & 0xFFu) * 0x010101u | a, ((d >> 8) & 0xFFu) * 0x010101u | a,
+                                 ((d >> 16) & 0xFFu) * 0x010101u | a, (d >> 24) * 0x010101u | a};
+                }
+            }
+        } else {
+            const float4 v = *reinterpret_cast<const float4*>(srow + 4 * x0);
+            float4* o = reinterpret_cast<float4*>(drow + 4 * DCN * x0);
+            if constexpr (DCN == 3) {
+                o[0] = make_float4(v.x, v.x, v.x, v.y);
+                o[1] = make_float4(v.y, v.y, v.z, v.z);
+                o[2] = make_float4(v.z, v.w, v.w, v.w);
+            } else {
+                o[0] = make_float4(v.x, v.x, v.x, alpha);
+                o[1] = make_float4(v.y, v.y, v.y, alpha);
+                o[2] = make_float4(v.z, v.z, v.z, alpha);
+                o[3] = make_float4(v.w, v.w, v.w, alpha);
+            }
+        }
+        return;
+    }
+    for (int x = x0; x < min(x0 + PX, L.w); ++x) {
+        const T v = *reinterpret_cast<const T*>(srow + (int64_t)x * sizeof(T));
+        T* o = reinterpret_cast<T*>(drow) + (int64_t)x * DCN;
+        o[0] = v;
+        o[1] = v;
+        o[2] = v;
+        if (DCN == 4) o[3] = alpha;
+    }
 }
 
 }  // namespace
 
 hipError_t launch_color_cv(const CvColorLaunch& L, hipStream_t s) {
-    const int64_t units = L.gray ? (int64_t)L.w * L.h : (int64_t)(L.w / 2) * (L.h / 2);
+    const int upr = L.esize == 4 ? (L.w + 3) / 4 : (L.w + 15) / 16;  // gray: units per row (gray_px)
+    const int64_t units = L.gray ? (int64_t)upr * L.h : (int64_t)(L.w / 2) * (L.h / 2);
     const int64_t grid = (units + 255) / 256;
     if (grid > 0x7FFFFFFF || L.n > 65535) return hipErrorInvalidValue;
     const dim3 g((unsigned)grid, (unsigned)L.n);
     if (L.gray) {
+        CvColorLaunch G = L;
+        // the vector path: every base and pitch 16-byte aligned
+        const uintptr_t bits = reinterpret_cast<uintptr_t>(L.src) | reinterpret_cast<uintptr_t>(L.dst) |
+                               (uintptr_t)L.src_img | (uintptr_t)L.src_row | (uintptr_t)L.dst_img | (uintptr_t)L.dst_row;
+        G.aligned = (bits & 15) == 0;
         if (L.esize == 4) {
-            if (L.dcn == 4) hipLaunchKernelGGL((gray_kernel<4, float>), g, dim3(256), 0, s, L);
-            else hipLaunchKernelGGL((gray_kernel<3, float>), g, dim3(256), 0, s, L);
+            if (L.dcn == 4) hipLaunchKernelGGL((gray_kernel<4, float>), g, dim3(256), 0, s, G, upr);
+            else hipLaunchKernelGGL((gray_kernel<3, float>), g, dim3(256), 0, s, G, upr);
         } else {
-            if (L.dcn == 4) hipLaunchKernelGGL((gray_kernel<4, unsigned char>), g, dim3(256), 0, s, L);
-            else hipLaunchKernelGGL((gray_kernel<3, unsigned char>), g, dim3(256), 0, s, L);
+            if (L.dcn == 4) hipLaunchKernelGGL((gray_kernel<4, unsigned char>), g, dim3(256), 0, s, G, upr);
+            else hipLaunchKernelGGL((gray_kernel<3, unsigned char>), g, dim3(256), 0, s, G, upr);
         }
+    } else if ((L.w & 7) == 0 &&
+               ((reinterpret_cast<uintptr_t>(L.src) | (uintptr_t)L.src_img | (uintptr_t)L.src_row) & 7) == 0 &&
+               ((reinterpret_cast<uintptr_t>(L.dst) | (uintptr_t)L.dst_img | (uintptr_t)L.dst_row) & (L.dcn == 4 ? 15 : 7)) == 0) {
+        // 8 x 2 pixels per thread (the planar chroma rows are w / 2 bytes: 4-byte aligned as w % 8 == 0)
+        const int upr8 = L.w >> 3;
+        const int64_t g8 = ((int64_t)upr8 * (L.h >> 1) + 255) / 256;
+        const dim3 gg((unsigned)g8, (unsigned)L.n);
+        if (L.dcn == 4) hipLaunchKernelGGL(yuv420_cv8_kernel<4>, gg, dim3(256), 0, s, L, upr8);
+        else hipLaunchKernelGGL(yuv420_cv8_kernel<3>, gg, dim3(256), 0, s, L, upr8);
     } else if (L.dcn == 4) {
         hipLaunchKernelGGL(yuv420_cv_kernel<4>, g, dim3(256), 0, s, L);
     } else {

@@ -1374,11 +1374,15 @@ def test_cvt_color_opencv_codes(ops, dev, oracle):
         assert_same(g[k, :, 1:27], oracle.yuv420_cv(yuv[k], COLOR_YUV2BGRA_NV21), "pitched rgba")
     g[:, :, 1:27] = 0
     assert not g.any(), "cvt_color wrote outside the window"
+    # 53 wide: elementwise (unaligned rows); 64 / 1920 wide: 4-pixel units
+    # with vector loads and stores; a pitched source (a 61-wide slice of 64)
     for dt in (np.uint8, np.float32):
-        gray = (rng.integers(0, 256, (2, 37, 53)).astype(dt) * (dt(0.5) if dt == np.float32 else 1)).astype(dt)
-        got = host(ops.cvt_color(to_dev(gray, dev), COLOR_GRAY2BGR))
-        for k in range(2):
-            assert_same(got[k], oracle.gray_to_bgr(gray[k]), f"gray2bgr {dt}")
+        for shape, crop in (((2, 37, 53), 53), ((2, 36, 64), 64), ((2, 8, 1920), 1920), ((2, 9, 64), 61)):
+            full = (rng.integers(0, 256, shape).astype(dt) * (dt(0.5) if dt == np.float32 else 1)).astype(dt)
+            gray = full[:, :, :crop]
+            got = host(ops.cvt_color(to_dev(full, dev)[:, :, :crop], COLOR_GRAY2BGR))
+            for k in range(2):
+                assert_same(got[k], oracle.gray_to_bgr(np.ascontiguousarray(gray[k])), f"gray2bgr {dt} {shape} {crop}")
 
 
 def test_warp_flags_nearest_and_inverse_map(ops, dev, oracle):
