@@ -513,6 +513,61 @@ __global__ void __launch_bounds__(kBlock) warp_nearest_kernel(WarpLaunch L) {
     }
 }
 
+// u8 -> u8 nearest (all border modes but TRANSPARENT, 4-byte aligned
+// destination): one pixel per lane as above (consecutive lanes gather
+// neighbouring source pixels, so a load instruction touches few lines), but
+// the pixel's CC bytes by ONE unaligned dword gather (bytewise only where that
+// dword would reach past the plane), and each lane quad's 4 CC output bytes
+// packed across the quad (quad_pack, DPP) into CC dword stores instead of
+// CC byte stores per lane.
+template <int CC>
+__global__ void __launch_bounds__(kBlock) warp_nearest4_kernel(WarpLaunch L) {
+    const int x = blockIdx.x * kBlock + threadIdx.x, y = blockIdx.y, pidx = blockIdx.z;
+    const int xq = x & ~3;
+    if (xq >= L.dst.w) return;  // whole quads leave together (the DPP reads quad neighbours)
+    const int lane = (int)threadIdx.x & 63;
+    const int img = pidx / L.src.planes, pl = pidx - img * L.src.planes;
+    const double* M = L.invd;
+    const int xc = min(x, L.dst.w - 1);
+    const int X0 = (int)rint((M[1] * y + M[2]) * 1024.0) + 512;
+    const int Y0 = (int)rint((M[4] * y + M[5]) * 1024.0) + 512;
+    int X = (int)((uint32_t)X0 + (uint32_t)(int)rint(M[0] * xc * 1024.0)) >> 10;
+    int Y = (int)((uint32_t)Y0 + (uint32_t)(int)rint(M[3] * xc * 1024.0)) >> 10;
+    X = min(max(X, -32768), 32767);  // remap's short map (saturate_cast<short>)
+    Y = min(max(Y, -32768), 32767);
+    const bool inside = (unsigned)X < (unsigned)L.src.w && (unsigned)Y < (unsigned)L.src.h;
+    const unsigned char* sp = L.src.base + (int64_t)img * L.src.img_pitch + (int64_t)pl * L.src.plane_pitch;
+    const Rsrc srs = make_rsrc(sp, L.src.plane_bytes);
+    const uint32_t lim = (uint32_t)L.src.plane_bytes + srs.delta;
+    uint32_t own = 0;
+#pragma unroll
+    for (int k = 0; k < CC; ++k) own |= (uint32_t)(int)L.border[L.src.planes > 1 ? pl : k] << (8 * k);
+    if (inside || L.border_mode != kBorderConstant) {
+        const int sx = inside ? X : border_index(X, L.src.w, L.border_mode);
+        const int sy = inside ? Y : border_index(Y, L.src.h, L.border_mode);
+        const uint32_t o = (uint32_t)sy * (uint32_t)L.src.row_pitch + (uint32_t)(sx * CC) + srs.delta;
+        if (o + 4u <= lim) {
+            own = __builtin_amdgcn_raw_buffer_load_b32(srs.r, (int)o, 0, 0);
+        } else {  // the plane's last pixel: bytewise (an overhanging load reads zeros)
+            uint32_t v = 0;
+#pragma unroll
+            for (int k = 0; k < CC; ++k)
+                v |= (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(srs.r, (int)(o + k), 0, 0) << (8 * k);
+            own = v;
+        }
+    }
+    if constexpr (CC < 4) own &= (1u << (8 * CC)) - 1u;  // the gathered dword's other bytes (quad_pack ORs bytes)
+    const uint32_t word = quad_pack<CC>(own, lane & 3);
+    unsigned char* d = const_cast<unsigned char*>(L.dst.base) + (int64_t)img * L.dst.img_pitch +
+                       (int64_t)pl * L.dst.plane_pitch + (int64_t)y * L.dst.row_pitch;
+    if (xq + 4 <= L.dst.w) {
+        if ((lane & 3) < CC) *reinterpret_cast<uint32_t*>(d + xq * CC + 4 * (lane & 3)) = word;
+    } else if (x < L.dst.w) {  // the row's last partial quad: bytes
+#pragma unroll
+        for (int k = 0; k < CC; ++k) d[x * CC + k] = (unsigned char)(own >> (8 * k));
+    }
+}
+
 template <typename TIn, int OUT>
 hipError_t launch_nearest_t(const WarpLaunch& L, hipStream_t s) {
     const dim3 grid((unsigned)((L.dst.w + kBlock - 1) / kBlock), (unsigned)L.dst.h, (unsigned)(L.n * L.src.planes));
@@ -530,6 +585,21 @@ hipError_t launch_nearest_t(const WarpLaunch& L, hipStream_t s) {
 }  // namespace
 
 hipError_t launch_warp_nearest(const WarpLaunch& L, hipStream_t s) {
+    const bool al4 = ((reinterpret_cast<uintptr_t>(L.dst.base) | (uintptr_t)L.dst.row_pitch | (uintptr_t)L.dst.img_pitch |
+                       (uintptr_t)L.dst.plane_pitch) & 3) == 0;
+    if (L.src.esize == 1 && L.out == kOutSame && L.border_mode != kBorderTransparent && al4 &&
+        L.src.plane_bytes <= kMaxPlaneBytes && tune(VACV_TUNE_WARP_KERNEL) != 5) {
+        const dim3 grid((unsigned)((L.dst.w + kBlock - 1) / kBlock), (unsigned)L.dst.h, (unsigned)(L.n * L.src.planes));
+        if ((int64_t)L.n * L.src.planes > 65535 || L.dst.h > 65535) return hipErrorInvalidValue;
+        switch (L.src.cc) {
+            case 1: hipLaunchKernelGGL((warp_nearest4_kernel<1>), grid, dim3(kBlock), 0, s, L); break;
+            case 2: hipLaunchKernelGGL((warp_nearest4_kernel<2>), grid, dim3(kBlock), 0, s, L); break;
+            case 3: hipLaunchKernelGGL((warp_nearest4_kernel<3>), grid, dim3(kBlock), 0, s, L); break;
+            case 4: hipLaunchKernelGGL((warp_nearest4_kernel<4>), grid, dim3(kBlock), 0, s, L); break;
+            default: return hipErrorInvalidValue;
+        }
+        return hipGetLastError();
+    }
     if (L.src.esize == 1) {
         if (L.out == kOutSame) return launch_nearest_t<uint8_t, kOutSame>(L, s);
         if (L.out == kOutF32) return launch_nearest_t<uint8_t, kOutF32>(L, s);

@@ -1406,12 +1406,15 @@ def test_warp_flags_nearest_and_inverse_map(ops, dev, oracle):
             for inv in (False, True):
                 mm = oracle.invert_affine(m) if inv else m
                 fl = INTER_NEAREST | (WARP_INVERSE_MAP if inv else 0)
+                # 97 wide: byte-aligned rows for c = 1, 3 (the per-pixel kernel);
+                # 96 wide (and c = 4): 4-pixel units with packed stores
                 for mode in (0, 1, 2, 3, 4):
-                    got = host(ops.warp_affine(to_dev(img[None], dev), mm, 97, 71, flags=fl, border_mode=mode,
-                                               border_value=bv))[0].reshape(71, 97, c)
-                    want = oracle.warp_affine_nn(img, mm, 97, 71, inverse_map=inv, border_mode=mode,
-                                                 border=bv).reshape(71, 97, c)
-                    assert_same(got, want, f"nearest c{c} inv={inv} mode {mode}")
+                    for dw, dh in ((97, 71), (96, 70)):
+                        got = host(ops.warp_affine(to_dev(img[None], dev), mm, dw, dh, flags=fl, border_mode=mode,
+                                                   border_value=bv))[0].reshape(dh, dw, c)
+                        want = oracle.warp_affine_nn(img, mm, dw, dh, inverse_map=inv, border_mode=mode,
+                                                     border=bv).reshape(dh, dw, c)
+                        assert_same(got, want, f"nearest c{c} {dw}x{dh} inv={inv} mode {mode}")
                 gotf = host(ops.warp_affine(to_dev(f[None], dev), mm, 97, 71, flags=fl, border_mode=1))[0]
                 wantf = oracle.warp_affine_nn(f, mm, 97, 71, inverse_map=inv, border_mode=1)
                 assert_same(gotf.reshape(71, 97, c), wantf.reshape(71, 97, c), f"nearest f32 c{c}")
