@@ -676,7 +676,11 @@ hipError_t launch_cc(const ResizeLaunch& L, hipStream_t s) {
         const double cnt = (double)L.dst.w * L.dst.h * (L.sum_per_image ? 1 : L.n);
         hipLaunchKernelGGL(fixed_sums_kernel, dim3(1), dim3(kBlock), 0, s, La.sum_acc, L.n, CC, L.sum_per_image,
                            La.sum_q1, La.sum_q2, cnt, L.sum_out, L.sum_mean, L.sum_std);
-        return hipGetLastError();
+        const hipError_t e2 = hipGetLastError();
+        // the accumulators must be zero for the next call: if the finishing
+        // launch did not go in, clear them here (the error is still returned)
+        if (e2 != hipSuccess) (void)hipMemsetAsync(La.sum_acc, 0, (size_t)L.n * 2 * CC * sizeof(int64_t), s);
+        return e2;
     }
     const int blocks = (L.sum_per_image ? L.n : 1) * CC;
     const double count = (double)L.dst.w * L.dst.h * (L.sum_per_image ? 1 : L.n);
