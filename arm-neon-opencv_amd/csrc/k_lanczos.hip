@@ -127,6 +127,10 @@ __device__ __forceinline__ T lz_const(const T* p, int i) {
     return ((const __attribute__((address_space(4))) T*)(uintptr_t)p)[i];
 }
 
+#ifndef VACV_LZ_WAVES
+#define VACV_LZ_WAVES 4
+#endif
+constexpr int kLzWaves = VACV_LZ_WAVES;  // waves (strip tasks) per workgroup; each owns its own ring
 #ifndef VACV_LZ_D
 #define VACV_LZ_D 3  // u8 source rows in flight per wave (1 / 2 / 3 / 4 / 6 / 8: 0.580 / 0.522 / 0.495 / 0.525 / 0.534 / 0.565 ms)
 #endif
@@ -134,7 +138,7 @@ __device__ __forceinline__ T lz_const(const T* p, int i) {
 #define VACV_LZ_SLOTS 1
 #endif
 template <typename TIn, int OUT, int CC>
-__global__ void __launch_bounds__(kBlock) lanczos_kernel(LanczosLaunch L, int strips, int bands, int band_rows) {
+__global__ void __launch_bounds__(64 * kLzWaves) lanczos_kernel(LanczosLaunch L, int strips, int bands, int band_rows) {
     constexpr bool U8 = std::is_same<TIn, uint8_t>::value;
     using TW = typename std::conditional<U8, int, float>::type;
     using TOut = typename std::conditional<(OUT == kOutSame), TIn, float>::type;
@@ -147,12 +151,12 @@ __global__ void __launch_bounds__(kBlock) lanczos_kernel(LanczosLaunch L, int st
     // 16-byte LDS access per lane and row, cost a workgroup per CU of LDS:
     // 0.589 vs 0.530 ms)
     constexpr int RS = CC;
-    __shared__ __attribute__((aligned(16))) TW ring[4][8][64 * RS];
+    __shared__ __attribute__((aligned(16))) TW ring[kLzWaves][8][64 * RS];
 
     // wave-uniform, and said so: the plane's buffer resource stays in SGPRs
     // (derived from a per-lane value it would be waterfalled at every load)
     const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)), lane = (int)(threadIdx.x & 63);
-    const int task = (int)blockIdx.x * 4 + wave;  // (plane, band, strip), strip fastest
+    const int task = (int)blockIdx.x * kLzWaves + wave;  // (plane, band, strip), strip fastest
     const int strip = task % strips;
     const int rest = task / strips;
     const int band = rest % bands;
@@ -596,7 +600,7 @@ struct LzGrid {
 
 template <typename TIn, int OUT>
 hipError_t launch_out(const LanczosLaunch& A, const LzGrid& g, hipStream_t s) {
-    const dim3 grid((unsigned)g.blocks), block(kBlock);
+    const dim3 grid((unsigned)g.blocks), block(64 * kLzWaves);
     switch (A.src.cc) {
         case 1: hipLaunchKernelGGL((lanczos_kernel<TIn, OUT, 1>), grid, block, 0, s, A, g.strips, g.bands, g.band_rows); break;
         case 2: hipLaunchKernelGGL((lanczos_kernel<TIn, OUT, 2>), grid, block, 0, s, A, g.strips, g.bands, g.band_rows); break;
@@ -639,8 +643,8 @@ int launch_resize_lanczos(const ResizeLaunch& R, double inv_x, double inv_y, hip
     g.band_rows = (R.dst.h + g.bands - 1) / g.bands;
     g.bands = (R.dst.h + g.band_rows - 1) / g.band_rows;
     const int64_t tasks = (int64_t)g.strips * g.bands * planes;
-    if ((tasks + 3) / 4 > 0x7FFFFFF0LL) return VACV_ERR_UNSUPPORTED;
-    g.blocks = (int)((tasks + 3) / 4);
+    if ((tasks + kLzWaves - 1) / kLzWaves > 0x7FFFFFF0LL) return VACV_ERR_UNSUPPORTED;
+    g.blocks = (int)((tasks + kLzWaves - 1) / kLzWaves);
     const hipError_t e = R.src.esize == 1 ? launch_t<uint8_t>(A, g, s) : launch_t<float>(A, g, s);
     return e == hipSuccess ? VACV_OK : VACV_ERR_HIP;
 }
