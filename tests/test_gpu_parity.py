@@ -646,6 +646,31 @@ def test_resize_normalize(ops, dev, oracle):
         assert_same(out[k], oracle.normalize(oracle.u8_to_f32(r), m, s), "resize_normalize auto")
 
 
+def test_resize_normalize_random_geometry(ops, dev, oracle):
+    """Seeded random geometries for the headline op (u8 HWC -> fp32
+    normalised, resize_naive.cpp:10-68 then the normalize): down- and
+    up-scales, 1-4 channels, widths that are not multiples of the column
+    blocks, batches of 3 -- whichever kernel the dispatcher picks matches the
+    oracle bit for bit; the plain u8 resize of the same batch too."""
+    rng = np.random.default_rng(20260419)
+    for t in range(16):
+        c = 1 + t % 4
+        h, w = int(rng.integers(9, 700)), int(rng.integers(9, 1300))
+        f = rng.uniform(0.2, 1.6, 2)
+        ho, wo = max(1, int(h * f[0])), max(1, int(w * f[1]))
+        mu = np.concatenate([MEAN, [1.0]]).astype(np.float32)[:c]
+        sd = np.concatenate([STD, [2.0]]).astype(np.float32)[:c]
+        imgs = [synthetic_image(7000 + 3 * t + k, h, w, c).reshape(h, w, c) for k in range(3)]
+        src = to_dev(np.stack(imgs), dev)
+        out = host(ops.resize_normalize(src, wo, ho, mu, sd))
+        out8 = host(ops.resize(src, wo, ho))
+        for k in range(3):
+            r = oracle.resize_linear(imgs[k] if c > 1 else imgs[k][..., 0], wo, ho).reshape(ho, wo, c)
+            assert_same(out8[k], r, f"u8 {w}x{h}x{c} -> {wo}x{ho}")
+            want = oracle.normalize(oracle.u8_to_f32(r), mu, sd).reshape(ho, wo, c)
+            assert_same(out[k], want, f"normalize {w}x{h}x{c} -> {wo}x{ho}")
+
+
 def test_resize_normalize_bench_batch(ops, dev, oracle):
     """The bench workload at its full size (256 x 1080p, one launch): images
     spread over the batch match the oracle bit for bit, every image equals the
@@ -1019,6 +1044,44 @@ def test_warp_frames_kernel(ops, dev, oracle, variant):
             assert_same(got[k, ch], want.reshape(83, 121), f"frames chw {k} {ch}")
             wn = oracle.normalize(oracle.u8_to_f32(want.reshape(83, 121, 1)), MEAN[ch:ch + 1], STD[ch:ch + 1])
             assert_same(gotn[k, ch], wn.reshape(83, 121), f"frames chw norm {k} {ch}")
+
+def test_warp_random_matrices(ops, dev, oracle):
+    """Seeded random affine maps (any rotation, anisotropic scale 0.4-2.5,
+    shear, the source centre jittered by up to half a frame), odd sizes, 1-4
+    channels, u8 and fp32 sources, all five sampling border modes, batches of
+    2: whichever kernel the planner picks (the LDS ring for u8 CONSTANT, the
+    gather kernels for boxes over its LDS plan, fp32 and the other borders)
+    is bit-exact against the oracle (warp_affine_naive.cpp:9-62, inverse as
+    warp_affine.cpp:121-133), and so is the normalize epilogue."""
+    rng = np.random.default_rng(20260418)
+    for t in range(40):
+        c = 1 + t % 4
+        h, w = int(rng.integers(13, 150)), int(rng.integers(13, 190))
+        ho, wo = int(rng.integers(7, 140)), int(rng.integers(7, 180))
+        a = np.deg2rad(rng.uniform(-180.0, 180.0))
+        sx, sy = rng.uniform(0.4, 2.5, 2)
+        A = np.array([[np.cos(a), -np.sin(a)], [np.sin(a), np.cos(a)]]) @ np.array([[sx, rng.uniform(-0.6, 0.6)],
+                                                                                   [0.0, sy]])
+        tv = np.array([wo / 2, ho / 2]) - A @ np.array([w / 2, h / 2]) + rng.uniform(-0.5, 0.5, 2) * (wo, ho)
+        m = np.concatenate([A, tv[:, None]], 1).astype(np.float32).reshape(6)
+        mode = 0 if (t // 4) % 2 == 0 else int(rng.integers(1, 5))  # half on the LDS ring's CONSTANT path
+        ims = np.stack([synthetic_image(9000 + 2 * t + k, h, w, c).reshape(h, w, c) for k in range(2)])
+        fl = ims.astype(np.float32) * np.float32(0.75) + np.float32(0.125)
+        mu = np.concatenate([MEAN, [1.0]]).astype(np.float32)[:c]
+        sd = np.concatenate([STD, [2.0]]).astype(np.float32)[:c]
+        got = host(ops.warp_affine(to_dev(ims, dev), m, wo, ho, border_mode=mode))
+        gotf = host(ops.warp_affine(to_dev(fl, dev), m, wo, ho, border_mode=mode))
+        gotn = host(ops.warp_affine_normalize(to_dev(ims, dev), m, wo, ho, mu, sd, border_mode=mode))
+        what = f"case {t}: {w}x{h}x{c} -> {wo}x{ho} border {mode} m={m.tolist()}"
+        for k in range(2):
+            src = ims[k] if c > 1 else ims[k, ..., 0]
+            want = oracle.warp_affine(src, m, wo, ho, border_mode=mode).reshape(ho, wo, c)
+            assert_same(got[k].reshape(ho, wo, c), want, what)
+            wantf = oracle.warp_affine(fl[k] if c > 1 else fl[k, ..., 0], m, wo, ho, border_mode=mode)
+            assert_same(gotf[k].reshape(ho, wo, c), wantf.reshape(ho, wo, c), what + " f32")
+            wantn = oracle.normalize(oracle.u8_to_f32(want), mu, sd)
+            assert_same(gotn[k].reshape(ho, wo, c), wantn.reshape(ho, wo, c), what + " normalize")
+
 
 def test_warp_kernels_agree(ops, dev, oracle):
     """u8 BORDER_CONSTANT warps run on the LDS-staged frames kernel
