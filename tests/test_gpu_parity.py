@@ -671,6 +671,40 @@ def test_resize_normalize_random_geometry(ops, dev, oracle):
             assert_same(out[k], want, f"normalize {w}x{h}x{c} -> {wo}x{ho}")
 
 
+def test_resize_random_geometry_interpolations(ops, dev, oracle):
+    """Seeded random geometries (scale 0.15-3 per axis, 1-4 channels, batches
+    of 2) for INTER_NEAREST, INTER_AREA, INTER_CUBIC (u8 in, fp32 out) and
+    INTER_LANCZOS4, u8 and fp32 sources: the dispatcher's pick is bit-exact
+    against the oracle's OpenCV 2.4 restatements (parity unpinned, as in the
+    per-mode tests above)."""
+    from vacv_amd import INTER_AREA, INTER_CUBIC, INTER_LANCZOS4, INTER_NEAREST
+    rng = np.random.default_rng(20260420)
+    for t in range(24):
+        interp = (INTER_NEAREST, INTER_AREA, INTER_CUBIC, INTER_LANCZOS4)[t % 4]
+        c = 1 + (t // 4) % 4
+        h, w = int(rng.integers(4, 300)), int(rng.integers(4, 500))
+        f = rng.uniform(0.15, 3.0, 2)
+        ho, wo = max(1, int(h * f[0])), max(1, int(w * f[1]))
+        imgs = np.stack([synthetic_image(8000 + 2 * t + k, h, w, c).reshape(h, w, c) for k in range(2)])
+        fl = imgs.astype(np.float32) * np.float32(0.75) + np.float32(0.125)
+        got = host(ops.resize(to_dev(imgs, dev), wo, ho, interpolation=interp))
+        gotf = host(ops.resize(to_dev(fl, dev), wo, ho, interpolation=interp))
+        what = f"interp {interp} {w}x{h}x{c} -> {wo}x{ho}"
+        for k in range(2):
+            sq = (lambda a: a) if c > 1 else (lambda a: a[..., 0])
+            if interp == INTER_NEAREST:
+                want, wantf = oracle.resize_nearest(sq(imgs[k]), wo, ho), oracle.resize_nearest(sq(fl[k]), wo, ho)
+            elif interp == INTER_AREA:
+                want, wantf = oracle.resize_area_any(sq(imgs[k]), wo, ho), oracle.resize_area_any(sq(fl[k]), wo, ho)
+            elif interp == INTER_CUBIC:
+                want = oracle.resize_cubic(oracle.u8_to_f32(sq(imgs[k])), wo, ho)
+                wantf = oracle.resize_cubic(sq(fl[k]), wo, ho)
+            else:
+                want, wantf = oracle.resize_lanczos4(sq(imgs[k]), wo, ho), oracle.resize_lanczos4(sq(fl[k]), wo, ho)
+            assert_same(got[k].reshape(ho, wo, c), want.reshape(ho, wo, c), what + " u8")
+            assert_same(gotf[k].reshape(ho, wo, c), wantf.reshape(ho, wo, c), what + " f32")
+
+
 def test_resize_normalize_bench_batch(ops, dev, oracle):
     """The bench workload at its full size (256 x 1080p, one launch): images
     spread over the batch match the oracle bit for bit, every image equals the
@@ -1229,6 +1263,37 @@ def _yuv_chain(oracle, yuv, w, h, v_first, rgb, mode, mean=None, std=None, chw=F
         if mean is not None:
             r = oracle.normalize(r, mean, std)
     return oracle.hwc_to_chw(r) if chw else r
+
+
+def test_cvt_color_resize_random_geometry(ops, dev, oracle):
+    """Seeded random even frame sizes and output sizes (scale 0.1-2.5) for the
+    four semi-planar codes: cvt_color, cvt_color_normalize and the fused
+    cvt_color_resize_normalize (NHWC / NCHW) match the reference's step-by-step
+    chain on the oracle bit for bit (cvt_color.cpp:39-135, resize_naive.cpp,
+    normalize_naive.cpp:74-90)."""
+    import vacv_amd as V
+    codes = [(V.COLOR_YUV2BGR_NV21, True, False), (V.COLOR_YUV2BGR_NV12, False, False),
+             (V.COLOR_YUV2RGB_NV21, True, True), (V.COLOR_YUV2RGB_NV12, False, True)]
+    rng = np.random.default_rng(20260421)
+    for t in range(16):
+        code, v_first, rgb = codes[t % 4]
+        h, w = 2 * int(rng.integers(1, 300)), 2 * int(rng.integers(1, 500))
+        f = rng.uniform(0.1, 2.5, 2)
+        ho, wo = max(1, int(h * f[0])), max(1, int(w * f[1]))
+        yuv = np.stack([rng.integers(0, 256, (h * 3 // 2, w), dtype=np.uint8) for _ in range(2)])
+        ydev = to_dev(yuv, dev)
+        bgr = host(ops.cvt_color(ydev, code))
+        bgrn = host(ops.cvt_color_normalize(ydev, code, MEAN, STD))
+        what = f"code {code} {w}x{h} -> {wo}x{ho}"
+        for k in range(2):
+            want = oracle.yuv420sp_to_bgr(yuv[k], v_first=v_first, rgb=rgb)
+            assert_same(bgr[k], want, what + " cvt")
+            assert_same(bgrn[k], oracle.normalize(oracle.u8_to_f32(want), MEAN, STD), what + " cvt normalize")
+        for layout, chw in ((V.NHWC, False), (V.NCHW, True)):
+            got = host(ops.cvt_color_resize_normalize(ydev, wo, ho, MEAN, STD, code, layout=layout))
+            for k in range(2):
+                assert_same(got[k], _yuv_chain(oracle, yuv[k], wo, ho, v_first, rgb, 0, MEAN, STD, chw=chw),
+                            what + f" resize normalize chw={chw}")
 
 
 @pytest.mark.parametrize("v_first,rgb", [(True, False), (False, True)])
