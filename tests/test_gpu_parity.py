@@ -1115,6 +1115,18 @@ def test_warp_random_matrices(ops, dev, oracle):
             assert_same(gotf[k].reshape(ho, wo, c), wantf.reshape(ho, wo, c), what + " f32")
             wantn = oracle.normalize(oracle.u8_to_f32(want), mu, sd)
             assert_same(gotn[k].reshape(ho, wo, c), wantn.reshape(ho, wo, c), what + " normalize")
+        # INTER_NEAREST on the same map (every other case through WARP_INVERSE_MAP
+        # with the host-inverted matrix), a non-zero border value
+        from vacv_amd import INTER_NEAREST, WARP_INVERSE_MAP
+        inv = t % 2 == 1
+        mm = oracle.invert_affine(m) if inv else m
+        bv = (7, 200, 31, 99)
+        gotnn = host(ops.warp_affine(to_dev(ims, dev), mm, wo, ho, flags=INTER_NEAREST | (WARP_INVERSE_MAP if inv else 0),
+                                     border_mode=mode, border_value=bv))
+        for k in range(2):
+            src = ims[k] if c > 1 else ims[k, ..., 0]
+            want = oracle.warp_affine_nn(src, mm, wo, ho, inverse_map=inv, border_mode=mode, border=bv)
+            assert_same(gotnn[k].reshape(ho, wo, c), want.reshape(ho, wo, c), what + f" nearest inv={inv}")
 
 
 def test_warp_kernels_agree(ops, dev, oracle):
