@@ -251,6 +251,41 @@ def test_resize_channel_sums(ops, dev, oracle):
     torch.cuda.empty_cache()
 
 
+def test_resize_mean_stddev_random_geometry(ops, dev, oracle):
+    """cfg5's fused call at seeded random geometries (u8 -> fp32 cubic, 1-4
+    channels, batches of 3, per-image and batch statistics): the image equals
+    the oracle's cubic resize bit for bit, the fused sums are within 1e-6
+    relative of vacv_channel_sums of that output, the statistics within
+    SURVEY 8(c)'s bounds of the exact fp64 ones, and a repeat gives the same
+    bits (fixed-point accumulators)."""
+    import torch
+    from vacv_amd import INTER_CUBIC
+    rng = np.random.default_rng(20260422)
+    for t in range(12):
+        c = 1 + t % 4
+        h, w = int(rng.integers(8, 900)), int(rng.integers(8, 1500))
+        ho, wo = int(rng.integers(4, 300)), int(rng.integers(4, 300))
+        per_image = t % 3 != 2
+        imgs = np.stack([synthetic_image(6000 + 3 * t + k, h, w, c).reshape(h, w, c) for k in range(3)])
+        src = to_dev(imgs, dev)
+        out, sums, mean, std = ops.resize_mean_stddev(src, wo, ho, INTER_CUBIC, per_image=per_image)
+        _, s2, m2, d2 = ops.resize_mean_stddev(src, wo, ho, INTER_CUBIC, per_image=per_image)
+        want = ops.channel_sums(out, per_image=per_image)
+        torch.cuda.synchronize(dev)
+        what = f"{w}x{h}x{c} -> {wo}x{ho} per_image={per_image}"
+        assert torch.equal(s2, sums) and torch.equal(m2, mean) and torch.equal(d2, std), what + " repeat"
+        assert ((sums - want).abs() / want.abs().clamp(min=1.0)).max().item() <= 1e-6, what
+        ho_ = host(out)
+        for k in range(3):
+            r = oracle.resize_cubic(oracle.u8_to_f32(imgs[k] if c > 1 else imgs[k][..., 0]), wo, ho)
+            assert_same(ho_[k].reshape(ho, wo, c), r.reshape(ho, wo, c), what + " image")
+        ex = ho_.astype(np.float64).reshape(3, -1, c)
+        ex = ex if per_image else ex.reshape(1, -1, c)
+        em, es = ex.mean(axis=1), ex.std(axis=1)
+        assert np.abs(host(mean).reshape(em.shape) - em).max() <= 1e-3, what
+        assert (np.abs(host(std).reshape(es.shape) - es) / np.maximum(es, 1e-6)).max() <= 1e-4, what
+
+
 def test_resize_nearest(ops, dev, oracle):
     """INTER_NEAREST (OpenCV 2.4 resizeNN semantics, parity unpinned -- see
     oracle/vacv_oracle.c): u8 and fp32, NHWC c = 1..4 and NCHW, down- and
