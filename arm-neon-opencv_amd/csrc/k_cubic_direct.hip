@@ -225,6 +225,13 @@ cubic_direct_kernel(ResizeLaunch L, int blocks_per_plane) {
     }
     // ---- LDS -> HBM: dense byte b of the plane's output lives at row
     // b / out_row, column byte b % out_row --------------------------------------
+    // Lanes read bytes other lanes of the wave wrote to xch: order those
+    // writes before the reads (the SUMS instance's __syncthreads already did).
+    if (!SUMS) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
     unsigned char* dp = const_cast<unsigned char*>(L.dst.base) + (int64_t)img * L.dst.img_pitch +
                         (int64_t)plane * L.dst.plane_pitch;
     const uint32_t out_row = (uint32_t)W * CC * 4u;

@@ -472,6 +472,69 @@ __global__ void __launch_bounds__(64 * kLzWaves) lanczos_kernel(LanczosLaunch L,
     else walk(std::integral_constant<bool, false>());
 }
 
+// Sources narrower than the 8-pixel window (w < 8): every column is a border
+// column of HResizeLanczos4 (no output column has all 8 taps inside), so each
+// tap is clamped to [0, w - 1] and the horizontal sum starts from 0 +.  One
+// thread per output pixel, the same tables and the same vertical arithmetic
+// as lanczos_kernel; these images are tiny, so no staging.
+template <typename TIn, int OUT>
+__global__ void __launch_bounds__(256) lanczos_small_kernel(LanczosLaunch L) {
+    constexpr bool U8 = std::is_same<TIn, uint8_t>::value;
+    using TOut = typename std::conditional<(OUT == kOutSame), TIn, float>::type;
+    const int64_t per_plane = (int64_t)L.dst.w * L.dst.h;
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= per_plane * L.n * L.src.planes) return;
+    const int pidx = (int)(i / per_plane);
+    const int rem = (int)(i - (int64_t)pidx * per_plane);
+    const int y = rem / L.dst.w, x = rem - y * L.dst.w;
+    const int img = pidx / L.src.planes, plane = pidx - img * L.src.planes;
+    const int CC = L.src.cc, w = L.src.w, h = L.src.h;
+    const unsigned char* sp = L.src.base + (int64_t)img * L.src.img_pitch + (int64_t)plane * L.src.plane_pitch;
+    unsigned char* dp = const_cast<unsigned char*>(L.dst.base) + (int64_t)img * L.dst.img_pitch +
+                        (int64_t)plane * L.dst.plane_pitch + (int64_t)y * L.dst.row_pitch;
+    const int sx = L.t.xofs[x], sy = L.t.yofs[y];
+    const int dw = L.dst.w * CC;
+    for (int q = 0; q < CC; ++q) {
+        TOut o;
+        if constexpr (U8) {
+            uint32_t acc = 0;  // int arithmetic, wrapping as OpenCV's
+            for (int k = 0; k < 8; ++k) {
+                const unsigned char* row = sp + (int64_t)min(max(sy - 3 + k, 0), h - 1) * L.src.row_pitch;
+                uint32_t hv = 0;
+                for (int j = 0; j < 8; ++j)
+                    hv += (uint32_t)row[min(max(sx - 3 + j, 0), w - 1) * CC + q] * (uint32_t)(int)L.t.xai[8 * x + j];
+                acc += hv * (uint32_t)(int)L.t.yai[8 * y + k];
+            }
+            const int vi = min(max(((int)acc + (1 << 21)) >> 22, 0), 255);  // FixedPtCast<int, uchar, 22>
+            if (OUT == kOutSame) o = (TOut)vi;
+            else if (OUT == kOutF32) o = (TOut)(float)vi;
+            else o = (TOut)normalize_u8v(chan_norm(L.norm, img, CC == 1 ? plane % L.norm.c_total : q), vi);
+        } else {
+            float hs[8];
+            for (int k = 0; k < 8; ++k) {
+                const float* row = reinterpret_cast<const float*>(sp + (int64_t)min(max(sy - 3 + k, 0), h - 1) *
+                                                                         L.src.row_pitch);
+                float v = 0.f + row[min(max(sx - 3, 0), w - 1) * CC + q] * L.t.xaf[8 * x];
+                for (int j = 1; j < 8; ++j) v = v + row[min(max(sx - 3 + j, 0), w - 1) * CC + q] * L.t.xaf[8 * x + j];
+                hs[k] = v;
+            }
+            const float* bb = L.t.yaf + 8 * y;
+            float v;
+            if (x * CC + q < (dw & ~3)) {  // VResizeLanczos4Vec_32f's 4-wide loop
+                const float s0 = ((hs[0] * bb[0] + hs[1] * bb[1]) + hs[2] * bb[2]) + hs[3] * bb[3];
+                const float s1 = ((hs[4] * bb[4] + hs[5] * bb[5]) + hs[6] * bb[6]) + hs[7] * bb[7];
+                v = s0 + s1;
+            } else {  // the scalar tail
+                v = hs[0] * bb[0];
+                for (int k = 1; k < 8; ++k) v = v + hs[k] * bb[k];
+            }
+            if (OUT == kOutNorm) v = normalize_f(chan_norm(L.norm, img, CC == 1 ? plane % L.norm.c_total : q), v);
+            o = (TOut)v;
+        }
+        reinterpret_cast<TOut*>(dp)[x * CC + q] = o;
+    }
+}
+
 // interpolateLanczos4 (imgwarp.cpp): float x, double sin / cos, float sums
 void lanczos4_coeffs(float x, float* c) {
     static const double s45 = 0.70710678118654752440084436210485;
@@ -622,8 +685,6 @@ hipError_t launch_t(const LanczosLaunch& A, const LzGrid& g, hipStream_t s) {
 
 int launch_resize_lanczos(const ResizeLaunch& R, double inv_x, double inv_y, hipStream_t s) {
     if (R.src.cc > 4) return VACV_ERR_UNSUPPORTED;
-    // the kernel reads each tap row as an 8-pixel window (narrower sources: unsupported)
-    if (R.src.w < 8) return VACV_ERR_UNSUPPORTED;
     LanczosLaunch A{};
     A.src = R.src;
     A.dst = R.dst;
@@ -632,6 +693,23 @@ int launch_resize_lanczos(const ResizeLaunch& R, double inv_x, double inv_y, hip
     A.norm = R.norm;
     const int st = lanczos_tables(R, inv_x, inv_y, s, A.t);
     if (st) return st;
+    if (R.src.w < 8) {
+        // narrower than lanczos_kernel's 8-pixel row window: per-pixel kernel
+        const int64_t total = (int64_t)R.dst.w * R.dst.h * R.n * R.src.planes;
+        const int64_t blocks = (total + 255) / 256;
+        if (blocks > 0x7FFFFFF0LL) return VACV_ERR_UNSUPPORTED;
+        const dim3 grid((unsigned)blocks), block(256);
+        if (R.src.esize == 1) {
+            if (A.out == kOutSame) hipLaunchKernelGGL((lanczos_small_kernel<uint8_t, kOutSame>), grid, block, 0, s, A);
+            else if (A.out == kOutF32) hipLaunchKernelGGL((lanczos_small_kernel<uint8_t, kOutF32>), grid, block, 0, s, A);
+            else hipLaunchKernelGGL((lanczos_small_kernel<uint8_t, kOutNorm>), grid, block, 0, s, A);
+        } else {
+            if (A.out == kOutSame) hipLaunchKernelGGL((lanczos_small_kernel<float, kOutSame>), grid, block, 0, s, A);
+            else if (A.out == kOutF32) hipLaunchKernelGGL((lanczos_small_kernel<float, kOutF32>), grid, block, 0, s, A);
+            else hipLaunchKernelGGL((lanczos_small_kernel<float, kOutNorm>), grid, block, 0, s, A);
+        }
+        return hipGetLastError() == hipSuccess ? VACV_OK : VACV_ERR_HIP;
+    }
     // wave tasks: 64-column strips x bands of output rows x planes; bands
     // shrink until there are ~16K tasks (a band's first row resizes all 8 of
     // its source rows, later rows only the new ones)

@@ -105,6 +105,10 @@ TUNE = {"RESIZE_DIRECT": 0, "CUBIC_DIRECT": 1, "RESIZE_INTERLEAVE": 2, "DIRECT_X
         "RESIZE_TILE_W": 10, "RESIZE_WORK": 11, "WARP_KERNEL": 12, "RESIZE_STRIP": 13, "MATCH_KERNEL": 14,
         "WARP_FRAMES": 15, "WARP_TILE_H": 16, "WARP_SLOTS": 17}
 
+# include/vacv_hip.h VACV_ABI_VERSION: the tuning enum above and every
+# signature here are laid out for it (tests/test_abi.py checks the header)
+ABI_VERSION = 2
+
 _lib = None
 
 
@@ -131,6 +135,11 @@ def load() -> ctypes.CDLL:
         fn = getattr(lib, name)
         fn.argtypes = args
         fn.restype = res
+    got = lib.vacv_abi_version()
+    if got != ABI_VERSION:
+        # e.g. a stale variant build under VACV_LIB_DIR: its tuning knobs and
+        # entry points would not mean what this binding passes
+        raise ImportError(f"{path} implements C ABI version {got}, this binding expects {ABI_VERSION}: rebuild it")
     _lib = lib
     return lib
 

@@ -393,10 +393,28 @@ def main():
 
     import torch
     import torch.distributed as dist
+    # VACV_BENCH_BACKEND=gloo runs the world > 1 protocol (barriers, the
+    # MAX-over-ranks merge, cfg5's all-reduce) without RCCL, so it can be
+    # exercised with several ranks on ONE GPU (ranks share the devices
+    # round-robin); the driver's multi-GPU runs use the default, nccl = RCCL.
+    backend = os.environ.get("VACV_BENCH_BACKEND", "nccl")
+    if backend not in ("nccl", "gloo"):
+        print(f"bench: VACV_BENCH_BACKEND={backend}: nccl or gloo", file=sys.stderr)
+        sys.exit(2)
     if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-        world = dist.get_world_size()  # what RCCL agreed on, reported as n_gpus
+        ndev = torch.cuda.device_count()  # (counting does not initialise the GPU)
+        if backend == "nccl":
+            if local >= ndev:
+                print(f"bench: rank {local} has no GPU ({ndev} visible); RCCL needs one GPU per rank",
+                      file=sys.stderr)
+                sys.exit(2)
+            torch.cuda.set_device(local)
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            local = local % max(ndev, 1)
+            torch.cuda.set_device(local)
+            dist.init_process_group("gloo")
+        world = dist.get_world_size()  # what the process group agreed on, reported as n_gpus
     dev = torch.device("cuda", local if world > 1 else 0)
     torch.cuda.set_device(dev)
 
@@ -406,6 +424,13 @@ def main():
 
     wl = make_workload(args.workload, args.batch, dev, rank, world, ops)
     B = wl["batch"]
+    if world > 1:
+        # value = B * world * px and cfg5's global count assume equal shards
+        sizes = [None] * world
+        dist.all_gather_object(sizes, B)
+        if len(set(sizes)) != 1:
+            print(f"bench: unequal per-rank batches {sizes}", file=sys.stderr)
+            sys.exit(2)
     stream = torch.cuda.current_stream(dev)
     launch = wl["main"]       # the dominant kernel (timed alone for the roofline)
     extra = wl.get("extra")   # the rest of the step (e.g. cfg5's stats + all-reduce)
@@ -422,9 +447,17 @@ def main():
     graph = None
     if args.graph and not extra:
         try:
+            # capture on a stream of our own, warmed first: the library keys its
+            # per-stream workspaces (cfg5's fixed-point accumulators) by stream,
+            # so their one-time allocation and zeroing happen before the capture
+            # instead of being recorded into it
+            cap = torch.cuda.Stream(dev)
+            cap.wait_stream(torch.cuda.current_stream(dev))
+            wl["main"](stream=cap)
+            cap.synchronize()
             g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g):
-                wl["main"](stream=torch.cuda.current_stream(dev))
+            with torch.cuda.graph(g, stream=cap):
+                wl["main"](stream=cap)
             graph = g
             stream = torch.cuda.current_stream(dev)
         except Exception as e:  # capture unsupported: eager launches
@@ -479,7 +512,25 @@ def main():
         torch.cuda.synchronize(dev)
         kern_ms = sum(a.elapsed_time(b) for a, b in ev) / args.steps
 
-    t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=dev)
+    # cfg5 across ranks: the step's statistics must be the GLOBAL ones -- the
+    # all-reduced sums equal the sum of every rank's own shard sums (recomputed
+    # here, gathered to the host, added in rank order)
+    stats_check = None
+    if world > 1 and "stats" in wl:
+        import numpy as np
+        from vacv_amd import INTER_CUBIC
+        mine = ops.resize_channel_sums(wl["inputs"], 224, 224, INTER_CUBIC, per_image=False)[1].cpu().numpy()
+        every = [None] * world
+        dist.all_gather_object(every, mine)
+        want = np.sum(np.stack(every), axis=0)
+        got = wl["stats"]["sums"].cpu().numpy()
+        rel = float(np.max(np.abs(got - want) / np.maximum(np.abs(want), 1.0)))
+        stats_check = {"max_rel_diff": rel, "ok": bool(rel <= 1e-9)}
+        if not stats_check["ok"]:
+            print(f"bench: global statistics differ from the ranks' sums (rel {rel:g})", file=sys.stderr)
+            sys.exit(3)
+
+    t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed, kern_ms = float(t[0]), float(t[1])
@@ -509,13 +560,16 @@ def main():
             "dtype": "u8",
             "data": "synthetic (torch.randint u8 frames resident in HBM)",
             "config": {"workload": wl["desc"], "global_batch": n_img, "batch_per_gpu": B,
-                       "parallelism": f"dp{world}", "frame": wl["frame"], "output": wl["output"]},
+                       "parallelism": f"dp{world}", "frame": wl["frame"], "output": wl["output"],
+                       "graph": graph is not None, "backend": backend if world > 1 else None},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                          "kernel": wl["kernel"], "kernel_ms": round(kern_ms, 4), "alg_bytes_per_launch": b_alg,
                          "gpu_ms_per_step": round(gpu_step_ms, 4)},
             "cpu_baseline": cpu,
         }
+        if stats_check is not None:
+            out["global_stats_check"] = stats_check
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.barrier()

@@ -39,7 +39,11 @@ def test_header_matches_exports_and_binding(lib):
 
 
 def test_version_and_status(lib):
-    assert lib.vacv_abi_version() == 2
+    import vacv_amd
+    hdr = vacv_amd._lib.HEADER.read_text()
+    declared = int(re.search(r"#define VACV_ABI_VERSION (\d+)", hdr).group(1))
+    assert vacv_amd._lib.ABI_VERSION == declared, "binding and header disagree on the ABI version"
+    assert lib.vacv_abi_version() == declared
     assert lib.vacv_status_string(0) == b"ok"
     assert lib.vacv_status_string(-2) == b"unsupported"
 

@@ -69,3 +69,28 @@ def test_gpus_flag_must_match_world_size():
     rc, lines, err = _run_bench(["--gpus", "4", "--dry-run", "--steps", "1", "--warmup", "0"],
                                 {"WORLD_SIZE": "1", "RANK": "0", "LOCAL_RANK": "0"})
     assert rc != 0 and not lines and "WORLD_SIZE" in err
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("workload", ["cubic_stats", "warp"])
+def test_bench_main_two_ranks_on_one_gpu(workload):
+    """bench.py's real world > 1 path -- main() with the kernels, the barriers,
+    the shard-size check, cfg5's all-reduce and the MAX-over-ranks merge --
+    with two ranks on the box's one GPU: VACV_BENCH_BACKEND=gloo replaces RCCL
+    (which needs a GPU per rank).  The parent spawns the ranks before anything
+    touches the GPU.  One JSON line, n_gpus 2, dp2, a roofline and a finite
+    step time; cfg5's statistics are global (the count covers both shards)."""
+    import math
+    rc, lines, err = _run_bench(["--gpus", "2", "--workload", workload, "--steps", "3", "--warmup", "1",
+                                 "--no-cpu-baseline"], {"VACV_BENCH_BACKEND": "gloo"}, timeout=300)
+    assert rc == 0, err[-3000:]
+    assert len(lines) == 1, lines
+    out = lines[0]
+    assert out["n_gpus"] == 2 and out["config"]["parallelism"] == "dp2"
+    assert out["config"]["backend"] == "gloo" and out["config"]["global_batch"] == 2 * out["config"]["batch_per_gpu"]
+    assert math.isfinite(out["ms_per_step"]) and out["ms_per_step"] > 0
+    r = out["roofline"]
+    assert r["bound"] == "hbm" and r["kernel_ms"] > 0 and 0 < r["frac"] < 1.2
+    assert out["value"] > 0 and out["cpu_baseline"] is None
+    if workload == "cubic_stats":
+        assert out["global_stats_check"]["ok"], out["global_stats_check"]

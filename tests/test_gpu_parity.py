@@ -159,12 +159,16 @@ def test_cubic_direct_and_staged_agree(ops, dev, oracle):
              lambda: ops.resize(src[:1, :100, :90], 250, 333, interpolation=INTER_CUBIC),
              lambda: ops.resize(ops.change_layout(src[:2], NCHW), 97, 61, interpolation=INTER_CUBIC, layout=NCHW)]
     for i, fn in enumerate(cases):
-        with ops.tuning(CUBIC_DIRECT=1):
-            a = fn()
         with ops.tuning(CUBIC_DIRECT=0):
             b = fn()
-        torch.cuda.synchronize(dev)
-        assert torch.equal(a.view(torch.int32), b.view(torch.int32)), f"case {i}: {(a != b).sum().item()} values differ"
+        # 1: the column kernel where it applies; 2: the row-major gather kernel
+        # (its non-SUMS instances, kOutNorm included, exchange through LDS)
+        for knob in (1, 2):
+            with ops.tuning(CUBIC_DIRECT=knob):
+                a = fn()
+            torch.cuda.synchronize(dev)
+            assert torch.equal(a.view(torch.int32), b.view(torch.int32)), \
+                f"case {i}, CUBIC_DIRECT={knob}: {(a != b).sum().item()} values differ"
     got = host(ops.resize(src[:1], 224, 224, interpolation=INTER_CUBIC))[0]
     assert_same(got, oracle.resize_cubic(oracle.u8_to_f32(imgs[0]), 224, 224), "cfg5 image 0 vs oracle")
     got = host(ops.resize(sdev[:1], 224, 224, interpolation=INTER_CUBIC))[0]
@@ -492,6 +496,22 @@ def test_resize_lanczos4(ops, dev, oracle):
             got = host(ops.resize(to_dev(img[None], dev), 0, 0, interpolation=INTER_LANCZOS4, fx=0.7, fy=0.45))[0]
             wo, ho = int(round(w * 0.7)), int(round(h * 0.45))
             assert_same(got, oracle.resize_lanczos4(img, wo, ho, 0.7, 0.45), "lanczos fx/fy")
+    # sources narrower than the 8-pixel row window (lanczos_small_kernel):
+    # every column is a border column of HResizeLanczos4
+    for i, (h, w, c) in enumerate([(20, 5, 3), (9, 7, 1), (13, 4, 4), (6, 6, 2)]):
+        img = synthetic_image(840 + i, h, w, c)
+        img = img if c > 1 else img[..., None]
+        f = (img.astype(np.float32) + rng.standard_normal(img.shape).astype(np.float32)).astype(np.float32)
+        sq = (lambda a: a) if c > 1 else (lambda a: a[..., 0])
+        for wo, ho in [(3, 11), (17, 5), (w + 1, h - 1)]:
+            got = host(ops.resize(to_dev(img[None], dev), wo, ho, interpolation=INTER_LANCZOS4))[0]
+            assert_same(sq(got), oracle.resize_lanczos4(sq(img), wo, ho), f"lanczos u8 narrow {h}x{w}x{c}->{ho}x{wo}")
+            gotf = host(ops.resize(to_dev(f[None], dev), wo, ho, interpolation=INTER_LANCZOS4))[0]
+            assert_same(sq(gotf), oracle.resize_lanczos4(sq(f), wo, ho), f"lanczos f32 narrow {h}x{w}x{c}->{ho}x{wo}")
+        if c == 3:
+            got = host(ops.resize_normalize(to_dev(img[None], dev), 9, 14, MEAN, STD, interpolation=INTER_LANCZOS4))[0]
+            want = oracle.normalize(oracle.u8_to_f32(oracle.resize_lanczos4(img, 9, 14)), MEAN, STD)
+            assert_same(got, want, "lanczos normalize narrow")
     big = np.stack([synthetic_image(830 + k, 1080, 1920, 3) for k in range(2)])
     got = host(ops.resize(to_dev(big, dev), 640, 360, interpolation=INTER_LANCZOS4))
     assert_same(got[1], oracle.resize_lanczos4(big[1], 640, 360), "lanczos 1080p -> 640x360")
