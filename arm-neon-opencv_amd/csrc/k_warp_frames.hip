@@ -95,7 +95,8 @@ __device__ __forceinline__ void direct_taps(const WarpLaunch& L, const unsigned 
 constexpr int kRingMaxIt = 6;  // DMA instructions per wave and frame, at most (a box of 24 KiB)
 // Diagnosis builds (make EXTRA=-DVACV_RING_DBG=n LIB=... OBJ=...; tools/kbench_lib.py):
 // bit 0 no sampling and stores, bit 1 no DMA, bit 2 every lane reads its taps at
-// one LDS address (no bank conflicts).  Results are wrong in those builds.
+// one LDS address (no bank conflicts), bit 3 (warp_exp_kernel, u8) every output
+// store dropped (offset past the plane).  Results are wrong in those builds.
 #ifndef VACV_RING_DBG
 #define VACV_RING_DBG 0
 #endif
@@ -577,6 +578,554 @@ warp_ring_kernel(WarpLaunch L, int gx, int gy, int kf, int S, int rows_max, int 
     wait_vm(0);  // no LDS-DMA may outlive the workgroup's LDS
 }
 
+// ---------------------------------------------------------------------------
+// warp_exp_kernel (round 5): 3-channel u8 warps.  Two changes against the
+// ring kernel, both per workgroup and frame-independent (once per tile):
+//
+// 1. Compact staging, two frames in flight.  The ring kernel's slots held the
+//    box's bounding rectangle (rows_max x G chunks, ~14 KiB at cfg4) although
+//    the DMA only fills each row's span of the tile's source parallelogram,
+//    so a slot per frame in flight cost the LDS of ~1.6 frames and four
+//    workgroups per CU kept only ~36 KiB of HBM reads in flight -- about half
+//    of what hides an HBM miss (MI355X_MICROARCH.md: ~72 KiB per CU).  Here a
+//    slot holds the spans back to back (row r's chunks glo_r .. ghi_r at
+//    chunk RB_r = the prefix of the rows above), ~9 KiB at cfg4, and there
+//    are two: frames f + 1 and f + 2 are in flight while f is sampled.
+// 2. A 4-byte-pixel image.  Each frame's spans are re-laid once into an LDS
+//    image of [b g r x] pixels, again only the spans (16-pixel units of each
+//    row, back to back): the re-lay is 3 VALU per 4 source pixels (the first
+//    dword as it is, one v_alignbyte / shift for each other); a thread takes
+//    4 pixels (a quarter unit) per step, 3 dwords in and one ds_write_b128
+//    out, so a wave's writes are 1 KiB contiguous (whole units per lane
+//    wrote 64 bytes apart: 4-way LDS bank conflicts, ~290 LDS cycles per
+//    tile and frame).  A pixel's taps are then two ds_read2_b32
+//    (offsets 0 and 1) at two frame-independent addresses, one per tap row --
+//    no per-pixel alignment fix-up (the ring kernel: 6 ds_read_b32 and 4
+//    v_alignbyte per pixel); the blend is unchanged (v_perm to the (tl_k,
+//    tr_k) u16 pair, v_dot2_u32_u16 per row, 24-bit row multiplies).
+//
+// The chunk -> row and unit -> row maps are byte tables built once per tile,
+// so every lane's DMA source offsets and re-lay offsets are registers.  u8
+// output leaves through a 4-row LDS exchange per wave as 12-byte stores (all
+// 64 lanes, 192 contiguous bytes per row); fp32 as 16-byte stores per row.
+// Per frame: wait for the own DMA of frame f, barrier, re-lay, barrier,
+// issue frame f + 2's DMA into the slot just re-laid, sample.
+constexpr int kExpQ = 4;         // re-lay quarter units (4 pixels of one box row) per thread and frame, at most
+constexpr int kExpUnits = kExpQ * kBlock / 4;  // image units (16 pixels) per tile, at most
+constexpr int kExpRows = 128;    // staged rows per tile, at most (the setup tables)
+constexpr int kExpTab = 16 + 12 * kExpRows + 64 * 4 * kRingMaxIt + kExpUnits + 16;  // setup tables, bytes
+#ifndef VACV_EXP_GRP
+#define VACV_EXP_GRP 2  // pixels whose taps are read before their blends (4: spills at <= 128 VGPRs)
+#endif
+#ifndef VACV_EXP_XCH
+#define VACV_EXP_XCH 1  // u8 output: 1 a 4-row LDS exchange + 12-byte stores; 0 DPP quad packing + dword stores per row
+#endif
+#ifndef VACV_EXP_WPE
+#define VACV_EXP_WPE 4  // 4 waves per SIMD: <= 128 VGPRs (4 workgroups per CU, as the LDS plan)
+#endif
+template <int OUT, int NP>
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(VACV_EXP_WPE)))
+warp_exp_kernel(WarpLaunch L, int gx, int gy, int kf, int slot_bytes, int exp_units, int dst_al) {
+    constexpr int CC = 3;
+    constexpr int TH = 4 * NP;
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+    // [48 B pad][slot 0][slot 1][64 B pad] (the re-lay reads up to 45 B before
+    // and 47 B after a row's chunks: bytes of no tapped pixel)
+    // [image: 16 B border pixel head, then exp_units x 16 pixels; the setup
+    //  tables live here until the first re-lay] [exchange: 4 waves x kXB]
+    constexpr int kXB = OUT == kOutSame ? (VACV_EXP_XCH ? 4 * 64 * 4 : 16) : 64 * CC * 4;
+    const uint32_t ebase = 48u + 2u * (uint32_t)slot_bytes + 64u;
+    const uint32_t xbase = ebase + 16u + 64u * (uint32_t)max(exp_units, (kExpTab + 63) / 64);
+#ifdef VACV_RING_AUX
+    constexpr int kAux = VACV_RING_AUX;
+#else
+    constexpr int kAux = OUT == kOutSame ? 1 : VACV_LOAD_AUX;
+#endif
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    int* red = reinterpret_cast<int*>(lds + xbase);  // 4 waves x 4 ints, setup only
+    unsigned char* xch = lds + xbase + wave * kXB;
+    // setup tables (image region): per row span glo | ghi << 16, prefix
+    // RB | UP << 16 (chunks, units), first unit | units << 16; chunk -> row and
+    // unit -> row bytes; totals
+    uint32_t* t_sp = reinterpret_cast<uint32_t*>(lds + ebase + 16);
+    uint32_t* t_pre = t_sp + kExpRows;
+    uint32_t* t_un = t_pre + kExpRows;
+    unsigned char* t_crow = reinterpret_cast<unsigned char*>(t_un + kExpRows);
+    unsigned char* t_urow = t_crow + 64 * 4 * kRingMaxIt;
+    uint32_t* t_tot = reinterpret_cast<uint32_t*>(t_urow + kExpUnits);
+
+    const int tiles = gx * gy;
+    const int nfr = L.n;
+    const int total = tiles * ((nfr + kf - 1) / kf);
+    const int per_xcd = (total + 7) / 8;
+    const int id = (int)(blockIdx.x % 8) * per_xcd + (int)(blockIdx.x / 8);
+    if (id >= total) return;  // uniform
+    const int fg = id / tiles, tile = id - fg * tiles;
+    const int by = tile / gx, bx = tile - by * gx;
+    const int f0 = fg * kf, f1 = min(f0 + kf, nfr);
+    const float* M = L.inv;
+    const float wlim = (float)(L.src.w - 1), hlim = (float)(L.src.h - 1);
+    const int x = bx * kFrTileW + lane;
+    const int yw = by * TH + wave * NP;
+    const uint32_t rp = (uint32_t)L.src.row_pitch;
+
+    // ---- 1. per-pixel taps, once for every frame (warp_affine_naive.cpp:23-42)
+    const float axm = M[0] * (float)x, aym = M[3] * (float)x;
+    uint32_t sxy[NP], vwa[NP], okm = 0;
+    int xmin = INT_MAX, xmax = INT_MIN, ymin = INT_MAX, ymax = INT_MIN;
+#pragma unroll
+    for (int j = 0; j < NP; ++j) {
+        const int y = yw + j;
+        const float fx = (axm + M[1] * (float)y) + M[2];
+        const float fy = (aym + M[4] * (float)y) + M[5];
+        const bool ok = (x < L.dst.w) & (y < L.dst.h) & (fx >= 0.f) & (fx < wlim) & (fy >= 0.f) & (fy < hlim);
+        const int sx = ok ? (int)fx : 0, sy = ok ? (int)fy : 0;
+        const float ax = fx - (float)sx, ay = fy - (float)sy;
+        const uint32_t w0 = (uint32_t)(int)((1.f - ay) * 2048.f + 0.5f);
+        const uint32_t v0 = (uint32_t)(int)((1.f - ax) * 2048.f + 0.5f);
+        sxy[j] = (uint32_t)sx | ((uint32_t)sy << 16);
+        vwa[j] = ok ? (v0 | ((4u * w0) << 16)) : (2048u | (8192u << 16));
+        okm |= (uint32_t)ok << j;
+        if (ok) {
+            xmin = min(xmin, sx);
+            xmax = max(xmax, sx);
+            ymin = min(ymin, sy);
+            ymax = max(ymax, sy);
+        }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        xmin = min(xmin, __shfl_xor(xmin, o, 64));
+        xmax = max(xmax, __shfl_xor(xmax, o, 64));
+        ymin = min(ymin, __shfl_xor(ymin, o, 64));
+        ymax = max(ymax, __shfl_xor(ymax, o, 64));
+    }
+    if (lane == 0) {
+        red[4 * wave + 0] = xmin;
+        red[4 * wave + 1] = xmax;
+        red[4 * wave + 2] = ymin;
+        red[4 * wave + 3] = ymax;
+    }
+    // the image's 16-byte head: the border pixel (a pixel outside the source
+    // reads its taps there, with weights (2048, 0) x (2048, 0))
+    if (tid < 4) {
+        uint32_t bp = 0;
+#pragma unroll
+        for (int e = 0; e < CC; ++e) bp |= (uint32_t)(int)L.border[e] << (8 * e);
+        *reinterpret_cast<uint32_t*>(lds + ebase + 4 * tid) = bp;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+        xmin = min(xmin, red[4 * w + 0]);
+        xmax = max(xmax, red[4 * w + 1]);
+        ymin = min(ymin, red[4 * w + 2]);
+        ymax = max(ymax, red[4 * w + 3]);
+    }
+    xmin = __builtin_amdgcn_readfirstlane(xmin);
+    xmax = __builtin_amdgcn_readfirstlane(xmax);
+    ymin = __builtin_amdgcn_readfirstlane(ymin);
+    ymax = __builtin_amdgcn_readfirstlane(ymax);
+    const bool any = xmax >= 0;
+    const int bx0 = any ? (xmin & ~3) : 0;                         // first staged column (bx0 * CC dword-aligned)
+    const int wpx = any ? xmax + 2 - bx0 : 0;                      // pixels of a box row
+    const int G = (wpx * CC + 15) >> 4;                            // 16-byte chunks of a box row
+    const int R = any ? ymax + 2 - ymin : 0;                       // staged rows ymin .. ymax + 1
+    const bool fits = any && R <= kExpRows;                        // uniform
+
+    // ---- 2. row spans: row ymin + t needs the columns its band of the tile's
+    // source parallelogram taps (fy in [r - 1, r + 1), widened by 0.05 px for
+    // the float rounding of the reference's coordinates): pixels plo .. phi
+    // (relative to bx0), raw chunks glo .. ghi, image units plo/16 .. phi/16
+    if (fits && tid < R) {
+        const float X0 = (float)(bx * kFrTileW), X1 = (float)(min(bx * kFrTileW + kFrTileW, L.dst.w) - 1);
+        const float Y0 = (float)(by * TH), Y1 = (float)(min(by * TH + TH, L.dst.h) - 1);
+        float cx[4], cy[4];
+        const float px[4] = {X0, X1, X1, X0}, py[4] = {Y0, Y0, Y1, Y1};
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            cx[i] = (M[0] * px[i] + M[1] * py[i]) + M[2];
+            cy[i] = (M[3] * px[i] + M[4] * py[i]) + M[5];
+        }
+        const float r = (float)(ymin + tid), ya = r - 1.05f, yb = r + 1.05f;
+        float lo = 3.0e38f, hi = -3.0e38f;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int i2 = (i + 1) & 3;
+            if (cy[i] >= ya && cy[i] <= yb) { lo = fminf(lo, cx[i]); hi = fmaxf(hi, cx[i]); }
+#pragma unroll
+            for (int e = 0; e < 2; ++e) {
+                const float yl = e ? yb : ya;
+                if ((cy[i] - yl) * (cy[i2] - yl) < 0.f) {
+                    const float xc = cx[i] + (yl - cy[i]) / (cy[i2] - cy[i]) * (cx[i2] - cx[i]);
+                    lo = fminf(lo, xc);
+                    hi = fmaxf(hi, xc);
+                }
+            }
+        }
+        uint32_t sp = 0, un = 0, cnt = 0;
+        if (lo <= hi) {
+            const int clo = (int)floorf(fmaxf(lo - 0.05f, -1.0e9f)) - bx0;       // left tap column
+            const int chi = (int)floorf(fminf(hi + 0.05f, 1.0e9f)) + 1 - bx0;    // right tap column
+            const int plo = max(clo, 0), phi = min(chi, wpx - 1);
+            if (plo <= phi) {
+                const int glo = (plo * CC) >> 4, ghi = ((phi + 1) * CC - 1) >> 4;
+                sp = (uint32_t)glo | ((uint32_t)ghi << 16);
+                cnt = (uint32_t)(ghi - glo + 1);
+                un = (uint32_t)(plo >> 4) | ((uint32_t)((phi >> 4) - (plo >> 4) + 1) << 16);
+            }
+        }
+        t_sp[tid] = sp;
+        t_un[tid] = un;
+        t_pre[tid] = cnt | (un & 0xFFFF0000u);  // counts, until the scan
+    }
+    __syncthreads();
+    // prefix over the rows (wave 0, two rows per lane): chunk offsets RB and
+    // unit offsets UP, both < 2^16 (packed and added together)
+    if (fits && wave == 0) {
+        const uint32_t a = lane < R ? t_pre[lane] : 0u, b = lane + 64 < R ? t_pre[lane + 64] : 0u;
+        uint32_t ia = a, ib = b;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t va = __shfl_up(ia, o, 64), vb = __shfl_up(ib, o, 64);
+            if (lane >= o) { ia += va; ib += vb; }
+        }
+        const uint32_t ta = __shfl(ia, 63, 64), tb = __shfl(ib, 63, 64);
+        if (lane < R) t_pre[lane] = ia - a;
+        if (lane + 64 < R) t_pre[lane + 64] = ta + ib - b;
+        if (lane == 0) *t_tot = ta + tb;
+    }
+    __syncthreads();
+    // the chunk -> row and unit -> row bytes
+    const uint32_t tot = fits ? *t_tot : 0u;
+    const int C = (int)(tot & 0xFFFFu), NU = (int)(tot >> 16);
+    const int n_inst = (C + 63) >> 6;
+    const bool staged = fits && n_inst <= 4 * kRingMaxIt && (n_inst << 10) <= slot_bytes && NU <= exp_units &&
+                        NU <= kExpUnits;  // uniform
+    if (staged && tid < R) {
+        const uint32_t pre = t_pre[tid], un = t_un[tid];
+        const int rb = (int)(pre & 0xFFFFu), up = (int)(pre >> 16);
+        const int cnt = (tid + 1 < R ? (int)(t_pre[tid + 1] & 0xFFFFu) : C) - rb;
+        for (int i = 0; i < cnt; ++i) t_crow[rb + i] = (unsigned char)tid;
+        for (int i = 0; i < (int)(un >> 16); ++i) t_urow[up + i] = (unsigned char)tid;
+    }
+    __syncthreads();
+    const int n_w = staged && n_inst > wave ? (n_inst - wave + 3) >> 2 : 0;
+
+    // per pixel, for every frame: the LDS byte addresses of its top and
+    // bottom tap pairs in the image (or the border head), the x-weight pair
+    // and the row weight
+    // (the two addresses as 16-bit halves of one register: LDS offsets are
+    // < 64 KiB, and 8 registers fewer keep the kernel at 4 waves per SIMD)
+    uint32_t eaTB[NP], wxp[NP], wa[NP];
+#pragma unroll
+    for (int j = 0; j < NP; ++j) {
+        const bool ok = staged && ((okm >> j) & 1u);
+        eaTB[j] = ebase | (ebase << 16);
+        if (ok) {
+            const int sx = (int)(sxy[j] & 0xFFFFu), r = (int)(sxy[j] >> 16) - ymin;
+            const int p = sx - bx0;
+            const uint32_t pt = t_pre[r], pb = t_pre[r + 1];
+            const uint32_t ut = t_un[r], ub = t_un[r + 1];
+            const uint32_t at = ebase + 4u * (uint32_t)(4 + 16 * ((int)(pt >> 16) - (int)(ut & 0xFFFFu)) + p);
+            const uint32_t ab = ebase + 4u * (uint32_t)(4 + 16 * ((int)(pb >> 16) - (int)(ub & 0xFFFFu)) + p);
+            eaTB[j] = at | (ab << 16);
+        }
+        const uint32_t v0 = vwa[j] & 0xFFFFu;
+        wxp[j] = ((okm >> j) & 1u) ? (v0 | ((2048u - v0) << 16)) : 2048u;
+        wa[j] = vwa[j] >> 16;
+    }
+    // this lane's DMA source offsets (frame-relative): instruction u of this
+    // wave covers slot chunks 64 (wave + 4u) + lane.  vm: chunks to load;
+    // tailm: those reaching past the plane's last byte (bytewise after the DMA)
+    uint32_t goff[kRingMaxIt];
+    uint32_t vm = 0, tailm = 0;
+#pragma unroll
+    for (int u = 0; u < kRingMaxIt; ++u) {
+        goff[u] = 0;
+        if (u < n_w) {
+            const int c = 64 * (wave + 4 * u) + lane;
+            if (c < C) {
+                const int r = t_crow[c];
+                const int col = (int)(t_sp[r] & 0xFFFFu) + c - (int)(t_pre[r] & 0xFFFFu);
+                goff[u] = (uint32_t)(ymin + r) * rp + (uint32_t)(bx0 * CC + 16 * col);
+                if ((int64_t)goff[u] + 16 > L.src.plane_bytes) tailm |= 1u << u;
+                else vm |= 1u << u;
+            }
+        }
+    }
+    // this thread's re-lay quarter units c = tid + 256 q: the raw byte offset
+    // of their 4 pixels in a slot (+ 48); their image bytes are 16 + 16 c
+    uint32_t rl[kExpQ];
+    int n_rl = 0;
+#pragma unroll
+    for (int q = 0; q < kExpQ; ++q) {
+        const int c = tid + kBlock * q;
+        rl[q] = 0;
+        if (staged && c < 4 * NU) {
+            const int r = t_urow[c >> 2];
+            const uint32_t pre = t_pre[r];
+            const int p = 16 * (int)(t_un[r] & 0xFFFFu) + 4 * (c - 4 * (int)(pre >> 16));  // first pixel
+            rl[q] = (uint32_t)(48 + 16 * (int)(pre & 0xFFFFu) + 3 * p - 16 * (int)(t_sp[r] & 0xFFFFu));
+            n_rl = q + 1;
+        }
+    }
+    auto dma = [&](int f, int s) {
+        if (VACV_RING_DBG & 2) return;
+        const Rsrc rs = make_rsrc(L.src.base + (int64_t)f * L.src.img_pitch, L.src.plane_bytes);
+        unsigned char* base = lds + 48 + s * slot_bytes + 1024 * wave;
+#pragma unroll
+        for (int u = 0; u < kRingMaxIt; ++u) {
+            if (u < n_w) {
+                const int off = ((vm >> u) & 1u) ? (int)(goff[u] + rs.delta) : (int)0x80000000;
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(rs.r, (lds_void*)(base + 4096 * u), 16, off, 0, 0, kAux);
+            }
+        }
+    };
+    auto fix_tail = [&](int f, int s) {
+        const Rsrc rs = make_rsrc(L.src.base + (int64_t)f * L.src.img_pitch, L.src.plane_bytes);
+#pragma unroll
+        for (int u = 0; u < kRingMaxIt; ++u) {
+            if ((tailm >> u) & 1u) {
+                uint32_t d[4];
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    uint32_t w = 0;
+#pragma unroll
+                    for (int e = 0; e < 4; ++e)
+                        w |= (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(rs.r, (int)(goff[u] + rs.delta) + 4 * q + e,
+                                                                           0, 0) << (8 * e);
+                    d[q] = w;
+                }
+                const int c = 64 * (wave + 4 * u) + lane;
+                *reinterpret_cast<u32x4*>(lds + 48 + s * slot_bytes + 16 * c) = u32x4{d[0], d[1], d[2], d[3]};
+            }
+        }
+    };
+    // slot s's raw 3-byte pixels -> the 4-byte image, 4 pixels (12 raw
+    // bytes, dword-aligned: 3 p with p a multiple of 4) a quarter unit
+    // All of a thread's reads are issued before its first write (one LDS
+    // round trip per frame, not one per quarter unit: the per-unit branch
+    // serialised them, ~800 of the wave's ~5,800 cycles per frame); a
+    // quarter unit past the thread's count reads and rewrites the image's
+    // border head (its own bytes, unchanged).
+    auto relay = [&](int s) {
+        const uint32_t sb = (uint32_t)(s * slot_bytes);
+        uint32_t d[kExpQ][3];
+#pragma unroll
+        for (int q = 0; q < kExpQ; ++q) {
+            const uint32_t* p = reinterpret_cast<const uint32_t*>(lds + (q < n_rl ? rl[q] + sb : ebase));
+            d[q][0] = p[0];
+            d[q][1] = p[1];
+            d[q][2] = p[2];
+        }
+#pragma unroll
+        for (int q = 0; q < kExpQ; ++q) {
+            if (q < n_rl)
+                *reinterpret_cast<u32x4*>(lds + ebase + 16u + 16u * (uint32_t)(tid + kBlock * q)) =
+                    u32x4{d[q][0], __builtin_amdgcn_alignbyte(d[q][1], d[q][0], 3),
+                          __builtin_amdgcn_alignbyte(d[q][2], d[q][1], 2), d[q][2] >> 8};
+        }
+    };
+
+    const uint32_t dpitch = (uint32_t)L.dst.row_pitch;
+    const bool tile_full = bx * kFrTileW + kFrTileW <= L.dst.w && by * TH + TH <= L.dst.h && dst_al;
+    constexpr uint32_t kOob = 0x80000000u;
+    // vector-memory stores per sampled frame (the wait counts; every one is
+    // issued): full tiles one 12-byte store per 4 rows (u8) or one 16-byte
+    // store per row (fp32); edge tiles count 0, so their waits also drain
+    // the stores of the frames before (conservative)
+    const int n_st = (VACV_RING_DBG & 1) || !tile_full ? 0 : (OUT != kOutSame || !VACV_EXP_XCH) ? NP : NP / 4;
+    const uint32_t qsel = (lane & 3) == 0 ? 0x04020100u : (lane & 3) == 1 ? 0x05040201u : 0x06050402u;
+
+    // one pixel's channels from its 4 taps ([b g r x] each): the sum << 2, the
+    // result in bits 24..31 (warp_affine_naive.cpp:50-54)
+    auto blend3 = [&](int j, uint32_t tl, uint32_t tr, uint32_t bl, uint32_t br, uint32_t (&vv)[CC]) {
+        const us2 wx = __builtin_bit_cast(us2, wxp[j]);
+        const uint32_t wA = wa[j], wB = 8192u - wa[j];
+#pragma unroll
+        for (int k = 0; k < CC; ++k) {
+            const uint32_t sel = (uint32_t)k | (0x0Cu << 8) | ((uint32_t)(4 + k) << 16) | (0x0Cu << 24);
+            const uint32_t top = __builtin_amdgcn_perm(tr, tl, sel);
+            const uint32_t bot = __builtin_amdgcn_perm(br, bl, sel);
+            const uint32_t ht = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, top), wx, 0u, false);
+            const uint32_t hb = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, bot), wx, 0u, false);
+            vv[k] = __umul24(ht, wA) + __umul24(hb, wB);
+        }
+    };
+    ChanNorm cn[CC];
+    auto emit = [&](auto full_c, int f, int j, const uint32_t (&vv)[CC]) {
+        constexpr bool FULL = decltype(full_c)::value;
+        const int y = yw + j;
+        const bool inside = FULL || (x < L.dst.w && y < L.dst.h);
+        unsigned char* dbase = const_cast<unsigned char*>(L.dst.base) + (int64_t)f * L.dst.img_pitch;
+        const Rsrc drs = make_rsrc(dbase, L.dst.plane_bytes);
+        if constexpr (OUT == kOutSame) {
+            const uint32_t own = __builtin_amdgcn_perm(vv[2], __builtin_amdgcn_perm(vv[1], vv[0], 0x0C0C0703u), 0x0C070100u);
+            if constexpr (FULL && !VACV_EXP_XCH) {
+                // the quad's 4 pixels as 3 dwords in its lanes 0..2 (DPP), one
+                // dword store per row: 48 lanes, 192 contiguous bytes
+                const uint32_t nxt = (uint32_t)__builtin_amdgcn_mov_dpp((int)own, 0xF9, 0xF, 0xF, false);  // [1,2,3,3]
+                const uint32_t word = __builtin_amdgcn_perm(nxt, own, qsel);
+                const uint32_t off = (VACV_RING_DBG & 8) || (lane & 3) == 3
+                                         ? kOob
+                                         : (uint32_t)y * dpitch + drs.delta +
+                                               (uint32_t)(bx * kFrTileW * CC + 12 * (lane >> 2) + 4 * (lane & 3));
+                __builtin_amdgcn_raw_buffer_store_b32(word, drs.r, (int)off, 0, VACV_RING_SAUX);
+            } else if constexpr (FULL) {
+                *reinterpret_cast<uint32_t*>(xch + 256 * (j & 3) + 4 * lane) = own;
+                if ((j & 3) == 3) {
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                    __builtin_amdgcn_wave_barrier();
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                    const int r = lane >> 4, q = lane & 15;
+                    const u32x4 p = *reinterpret_cast<const u32x4*>(xch + 256 * r + 16 * q);
+                    typedef unsigned int u32x3 __attribute__((ext_vector_type(3)));
+                    const u32x3 o = {__builtin_amdgcn_perm(p[1], p[0], 0x04020100u),
+                                     __builtin_amdgcn_perm(p[2], p[1], 0x05040201u),
+                                     __builtin_amdgcn_perm(p[3], p[2], 0x06050402u)};
+                    const uint32_t off = (VACV_RING_DBG & 8) ? kOob : (uint32_t)(y - 3 + r) * dpitch + drs.delta + (uint32_t)(bx * kFrTileW * CC + 12 * q);
+                    __builtin_amdgcn_raw_buffer_store_b96(o, drs.r, (int)off, 0, VACV_RING_SAUX);
+                }
+            } else {
+                const uint32_t off = (uint32_t)y * dpitch + drs.delta + (uint32_t)(x * CC);
+#pragma unroll
+                for (int k = 0; k < CC; ++k)
+                    __builtin_amdgcn_raw_buffer_store_b8((unsigned char)(own >> (8 * k)), drs.r,
+                                                         (int)(inside ? off + k : kOob), 0, VACV_RING_SAUX);
+            }
+        } else {
+            uint32_t o[CC];
+#pragma unroll
+            for (int k = 0; k < CC; ++k) {
+                const int v = (int)(vv[k] >> 24);
+                const float fv = OUT == kOutF32 ? (float)v : normalize_u8v(cn[k], v);
+                o[k] = __builtin_bit_cast(uint32_t, fv);
+            }
+            if constexpr (FULL) {
+#pragma unroll
+                for (int k = 0; k < CC; ++k) *reinterpret_cast<uint32_t*>(xch + 12 * lane + 4 * k) = o[k];
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                const u32x4 p = *reinterpret_cast<const u32x4*>(xch + 16 * (lane % (3 * 16)));
+                const uint32_t off = lane < 3 * 16 ? (uint32_t)y * dpitch + drs.delta +
+                                                         (uint32_t)(bx * kFrTileW * CC * 4 + 16 * lane)
+                                                   : kOob;
+                __builtin_amdgcn_raw_buffer_store_b128(p, drs.r, (int)off, 0, VACV_RING_SAUX);
+            } else {
+                typedef unsigned int u32x3 __attribute__((ext_vector_type(3)));
+                const uint32_t off = inside ? (uint32_t)y * dpitch + drs.delta + (uint32_t)(x * CC * 4) : kOob;
+                __builtin_amdgcn_raw_buffer_store_b96(u32x3{o[0], o[1], o[2]}, drs.r, (int)off, 0, VACV_RING_SAUX);
+            }
+        }
+    };
+    // frame f from the image
+    auto sample = [&](auto full_c, int fv) {
+        const int f = __builtin_amdgcn_readfirstlane(fv);
+        if constexpr (OUT != kOutSame) {
+#pragma unroll
+            for (int k = 0; k < CC; ++k) cn[k] = chan_norm(L.norm, f, k);
+        }
+        constexpr int kGrp = VACV_EXP_GRP;
+#pragma unroll
+        for (int j0 = 0; j0 < NP; j0 += kGrp) {
+            uint32_t tp[kGrp][4];
+#pragma unroll
+            for (int j = 0; j < kGrp; ++j) {
+                const uint32_t e = eaTB[j0 + j];
+                const uint32_t* pt = reinterpret_cast<const uint32_t*>(lds + ((VACV_RING_DBG & 4) ? ebase : e & 0xFFFFu));
+                const uint32_t* pb = reinterpret_cast<const uint32_t*>(lds + ((VACV_RING_DBG & 4) ? ebase : e >> 16));
+                tp[j][0] = pt[0];
+                tp[j][1] = pt[1];
+                tp[j][2] = pb[0];
+                tp[j][3] = pb[1];
+            }
+#pragma unroll
+            for (int j = 0; j < kGrp; ++j) {
+                uint32_t vv[CC];
+                blend3(j0 + j, tp[j][0], tp[j][1], tp[j][2], tp[j][3], vv);
+                emit(full_c, f, j0 + j, vv);
+            }
+        }
+    };
+
+    using full_t = std::integral_constant<bool, true>;
+    using edge_t = std::integral_constant<bool, false>;
+    if (!staged) {
+        // no staging: a tile no pixel of which taps the source reads the
+        // border head for every pixel (both addresses the head); a box over the
+        // plan (never for a planned geometry: the host sized the slots for
+        // every tile) takes its taps from memory
+        for (int f = f0; f < f1; ++f) {
+            if (!any) {
+                if (tile_full) sample(full_t(), f);
+                else sample(edge_t(), f);
+                continue;
+            }
+            const unsigned char* sp = L.src.base + (int64_t)f * L.src.img_pitch;
+            if constexpr (OUT != kOutSame) {
+#pragma unroll
+                for (int k = 0; k < CC; ++k) cn[k] = chan_norm(L.norm, f, k);
+            }
+            for (int j = 0; j < NP; ++j) {
+                uint32_t tl, tr, bl, br, vv[CC];
+                direct_taps<CC>(L, sp, x, yw + j, tl, tr, bl, br);
+                blend3(j, tl, tr, bl, br, vv);
+                emit(edge_t(), f, j, vv);
+            }
+        }
+        return;
+    }
+    // prologue: frames f0 and f0 + 1 in flight
+    dma(f0, 0);
+    if (f0 + 1 < f1) dma(f0 + 1, 1);
+#if VACV_RING_DBG & 16
+    // diagnosis build: per-phase shader-clock totals of a few waves (printf)
+    uint64_t tph[6] = {0, 0, 0, 0, 0, 0};
+    uint64_t t_ = __builtin_amdgcn_s_memtime();
+#define EXP_STAMP(i) do { const uint64_t n_ = __builtin_amdgcn_s_memtime(); tph[i] += n_ - t_; t_ = n_; } while (0)
+#else
+#define EXP_STAMP(i) do {} while (0)
+#endif
+    for (int f = f0; f < f1; ++f) {
+        const int s = (f - f0) & 1;
+        // this wave's DMA of frame f has landed; issued after it and possibly
+        // still in flight: frame f + 1's DMA and the stores of the (up to 2)
+        // frames sampled since
+        wait_vm((f + 1 < f1 ? n_w : 0) + min(f - f0, 2) * n_st);
+        EXP_STAMP(0);
+        if (tailm) {
+            fix_tail(f, s);
+            wait_lgkm();  // its LDS stores land before the barrier (s_barrier does not wait for them)
+        }
+        __builtin_amdgcn_s_barrier();  // every wave's part of frame f is in; frame f - 1's image reads are done
+        EXP_STAMP(1);
+        if (!(VACV_RING_DBG & 1)) relay(s);
+        wait_lgkm();
+        EXP_STAMP(2);
+        __builtin_amdgcn_s_barrier();  // the image holds frame f; slot s is free
+        EXP_STAMP(3);
+        if (f + 2 < f1) dma(f + 2, s);
+        EXP_STAMP(4);
+        if (!(VACV_RING_DBG & 1)) {
+            if (tile_full) sample(full_t(), f);
+            else sample(edge_t(), f);
+        }
+        EXP_STAMP(5);
+    }
+    wait_vm(0);  // no LDS-DMA may outlive the workgroup's LDS
+#if VACV_RING_DBG & 16
+    if (lane == 0 && (blockIdx.x % 911) == 7)
+        printf("expprof blk %u wave %d frames %d full %d: dmawait %llu b1 %llu relay %llu b2 %llu dmaissue %llu sample %llu\n",
+               blockIdx.x, wave, f1 - f0, (int)tile_full, (unsigned long long)tph[0], (unsigned long long)tph[1],
+               (unsigned long long)tph[2], (unsigned long long)tph[3], (unsigned long long)tph[4],
+               (unsigned long long)tph[5]);
+#endif
+#undef EXP_STAMP
+}
+
 template <typename K>
 int64_t frames_resident(K kernel, size_t lds) {
     static std::mutex mu;
@@ -593,6 +1142,25 @@ int64_t frames_resident(K kernel, size_t lds) {
     const int64_t r = (int64_t)std::max(per_cu, 1) * std::max(cus, 1);
     cache.emplace(key, r);
     return r;
+}
+
+template <int OUT, int NP>
+hipError_t launch_exp(const WarpLaunch& L, const WarpFramesPlan& P, hipStream_t s) {
+    constexpr int TH = 4 * NP;
+    const int gx = (L.dst.w + kFrTileW - 1) / kFrTileW, gy = (L.dst.h + TH - 1) / TH;
+    auto kern = warp_exp_kernel<OUT, NP>;
+    int kf = P.kf;
+    if (kf <= 0) {
+        const int64_t res = std::max<int64_t>(frames_resident(kern, (size_t)P.lds), 256);
+        const int64_t tiles = (int64_t)gx * gy;
+        kf = (int)std::max<int64_t>(1, std::min<int64_t>(16, tiles * L.n / (3 * res)));
+    }
+    const int64_t total = (int64_t)gx * gy * ((L.n + kf - 1) / kf);
+    if (total >= 0x7FFFFFF0LL) return hipErrorInvalidValue;
+    const int64_t blocks = (total + 7) / 8 * 8;
+    hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(kBlock), (size_t)P.lds, s, L, gx, gy, kf, P.raw_bytes,
+                       P.exp_units, P.dst_al);
+    return hipGetLastError();
 }
 
 template <int CC, int OUT, int NP, bool PLANAR>
@@ -627,6 +1195,7 @@ hipError_t launch_frames_np(const WarpLaunch& L, const WarpFramesPlan& P, hipStr
 
 template <int OUT>
 hipError_t launch_frames_cc(const WarpLaunch& L, const WarpFramesPlan& P, hipStream_t s) {
+    if (P.se > 0) return P.th == 16 ? launch_exp<OUT, 4>(L, P, s) : launch_exp<OUT, 8>(L, P, s);
     switch (L.src.cc) {
         case 1: return launch_frames_np<1, OUT>(L, P, s);
         case 2: return launch_frames_np<2, OUT>(L, P, s);
@@ -729,10 +1298,119 @@ bool ring_layout_th(const WarpLaunch& L, WarpFramesPlan& P, int th) {
     return P.lds <= 64 * 1024;
 }
 
+// warp_exp_kernel's staging, mirrored on the host with the kernel's float
+// arithmetic for EVERY tile of the output (the box from the pixels' taps, the
+// spans from the tile's corners): the most span chunks, image units and box
+// rows any tile needs.  The slots and the image are sized for that, so no
+// tile of the planned geometry takes the kernel's unstaged path.
+struct ExpNeeds {
+    int rows = 0, chunks = 0, units = 0;
+};
+ExpNeeds exp_needs(const WarpLaunch& L, int th) {
+    constexpr int CC = 3;
+    const float* M = L.inv;
+    const float wlim = (float)(L.src.w - 1), hlim = (float)(L.src.h - 1);
+    const int gx = (L.dst.w + kFrTileW - 1) / kFrTileW, gy = (L.dst.h + th - 1) / th;
+    ExpNeeds n;
+    for (int by = 0; by < gy; ++by) {
+        for (int bx = 0; bx < gx; ++bx) {
+            int xmin = INT_MAX, xmax = INT_MIN, ymin = INT_MAX, ymax = INT_MIN;
+            for (int y = by * th; y < by * th + th; ++y) {
+                for (int x = bx * kFrTileW; x < bx * kFrTileW + kFrTileW; ++x) {
+                    const float axm = M[0] * (float)x, aym = M[3] * (float)x;
+                    const float fx = (axm + M[1] * (float)y) + M[2];
+                    const float fy = (aym + M[4] * (float)y) + M[5];
+                    if (x < L.dst.w && y < L.dst.h && fx >= 0.f && fx < wlim && fy >= 0.f && fy < hlim) {
+                        xmin = std::min(xmin, (int)fx);
+                        xmax = std::max(xmax, (int)fx);
+                        ymin = std::min(ymin, (int)fy);
+                        ymax = std::max(ymax, (int)fy);
+                    }
+                }
+            }
+            if (xmax < 0) continue;
+            const int bx0 = xmin & ~3, wpx = xmax + 2 - bx0, R = ymax + 2 - ymin;
+            const float X0 = (float)(bx * kFrTileW), X1 = (float)(std::min(bx * kFrTileW + kFrTileW, L.dst.w) - 1);
+            const float Y0 = (float)(by * th), Y1 = (float)(std::min(by * th + th, L.dst.h) - 1);
+            float cx[4], cy[4];
+            const float px[4] = {X0, X1, X1, X0}, py[4] = {Y0, Y0, Y1, Y1};
+            for (int i = 0; i < 4; ++i) {
+                cx[i] = (M[0] * px[i] + M[1] * py[i]) + M[2];
+                cy[i] = (M[3] * px[i] + M[4] * py[i]) + M[5];
+            }
+            int chunks = 0, units = 0;
+            for (int t = 0; t < R; ++t) {
+                const float r = (float)(ymin + t), ya = r - 1.05f, yb = r + 1.05f;
+                float lo = 3.0e38f, hi = -3.0e38f;
+                for (int i = 0; i < 4; ++i) {
+                    const int i2 = (i + 1) & 3;
+                    if (cy[i] >= ya && cy[i] <= yb) { lo = std::fmin(lo, cx[i]); hi = std::fmax(hi, cx[i]); }
+                    for (int e = 0; e < 2; ++e) {
+                        const float yl = e ? yb : ya;
+                        if ((cy[i] - yl) * (cy[i2] - yl) < 0.f) {
+                            const float xc = cx[i] + (yl - cy[i]) / (cy[i2] - cy[i]) * (cx[i2] - cx[i]);
+                            lo = std::fmin(lo, xc);
+                            hi = std::fmax(hi, xc);
+                        }
+                    }
+                }
+                if (!(lo <= hi)) continue;
+                const int clo = (int)std::floor(std::fmax(lo - 0.05f, -1.0e9f)) - bx0;
+                const int chi = (int)std::floor(std::fmin(hi + 0.05f, 1.0e9f)) + 1 - bx0;
+                const int plo = std::max(clo, 0), phi = std::min(chi, wpx - 1);
+                if (plo > phi) continue;
+                chunks += (((phi + 1) * CC - 1) >> 4) - ((plo * CC) >> 4) + 1;
+                units += (phi >> 4) - (plo >> 4) + 1;
+            }
+            n.rows = std::max(n.rows, R);
+            n.chunks = std::max(n.chunks, chunks);
+            n.units = std::max(n.units, units);
+        }
+    }
+    return n;
+}
+
+// warp_exp_kernel's LDS: two compact raw slots, the image (at least the setup
+// tables), the output exchange; <= 40 KiB keeps 4 workgroups per CU
+bool exp_layout_th(const WarpLaunch& L, WarpFramesPlan& P, int th) {
+    const ExpNeeds n = exp_needs(L, th);
+    const int n_inst = (n.chunks + 63) / 64;
+    if (n.rows > kExpRows || n_inst > 4 * kRingMaxIt || n.units > kExpUnits) return false;
+    P.th = th;
+    P.se = 1;
+    P.raw_bytes = std::max(n_inst, 1) * 1024;
+    P.exp_units = n.units;
+    P.rows_max = n.rows;
+    P.S = 0;
+    P.ns = 2;
+    P.slot = P.raw_bytes;
+    const int xb = 4 * (L.out == kOutSame ? (VACV_EXP_XCH ? 4 * 64 * 4 : 16) : 64 * 3 * 4);
+    P.lds = 48 + 2 * P.raw_bytes + 64 + 16 + 64 * std::max(n.units, (kExpTab + 63) / 64) + xb;
+    return P.lds <= 64 * 1024;
+}
+
 // 32-row tiles (measured faster: 0.171 vs 0.182 ms at 720p rot15) unless
-// their box is over the staging budget, then 16
+// their box is over the staging budget, then 16.  Interleaved 3-channel u8
+// takes warp_exp_kernel where its image fits (VACV_TUNE_WARP_KERNEL = 6:
+// the ring kernel instead).
 bool frames_layout(const WarpLaunch& L, WarpFramesPlan& P) {
     const int th_knob = tune(VACV_TUNE_WARP_TILE_H);
+    P.se = 0;
+    P.raw_bytes = 0;
+    if (L.src.cc == 3 && L.src.planes == 1 && tune(VACV_TUNE_WARP_KERNEL) != 6) {
+        WarpFramesPlan Q = P;
+        // fp32 output: 16-row tiles by default (the 32-row instance spills at
+        // the 128 VGPRs of 4 waves per SIMD)
+        const int th0 = L.out == kOutSame ? 32 : 16;
+        if (th_knob == 16 || th_knob == 32) {
+            if (exp_layout_th(L, Q, th_knob)) { P = Q; return true; }
+        } else if (exp_layout_th(L, Q, th0) || exp_layout_th(L, Q, 48 - th0)) {
+            P = Q;
+            return true;
+        }
+        P.se = 0;
+        P.raw_bytes = 0;
+    }
     if (th_knob == 16 || th_knob == 32) return ring_layout_th(L, P, th_knob);
     return ring_layout_th(L, P, 32) || ring_layout_th(L, P, 16);
 }
@@ -742,7 +1420,7 @@ bool frames_layout(const WarpLaunch& L, WarpFramesPlan& P) {
 // time); the alignment checks are per call.
 bool warp_frames_plan(const WarpLaunch& L, WarpFramesPlan& P) {
     const int knob = tune(VACV_TUNE_WARP_KERNEL);
-    if (knob >= 0 && knob != 4) return false;
+    if (knob >= 0 && knob != 4 && knob != 6) return false;
     if (L.src.esize != 1 || L.border_mode != kBorderConstant) return false;
     if (L.src.planes > 1 && L.src.cc != 1) return false;
     if (L.src.cc < 1 || L.src.cc > 4) return false;
@@ -759,7 +1437,7 @@ bool warp_frames_plan(const WarpLaunch& L, WarpFramesPlan& P) {
     // layout of byte output carries the store exchange)
     struct Key {
         float inv[6];
-        int sw, sh, dw, dh, th, cc, bytes_out, slots;
+        int sw, sh, dw, dh, th, cc, bytes_out, slots, kernel;
         bool operator<(const Key& o) const { return std::memcmp(this, &o, sizeof(Key)) < 0; }
     };
     Key k;
@@ -769,6 +1447,7 @@ bool warp_frames_plan(const WarpLaunch& L, WarpFramesPlan& P) {
     k.cc = L.src.cc;
     k.bytes_out = L.out == kOutSame ? 1 : 0;
     k.slots = tune(VACV_TUNE_WARP_SLOTS);
+    k.kernel = knob;
     static std::mutex mu;
     static std::map<Key, std::pair<bool, WarpFramesPlan>> cache;
     bool ok;

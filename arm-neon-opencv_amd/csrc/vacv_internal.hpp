@@ -211,6 +211,9 @@ struct WarpFramesPlan {
     int lds;                     // dynamic LDS per workgroup
     int kf;                      // frames per workgroup (<= 0: chosen at launch)
     int dst_al;                  // destination dword-aligned (u8 quad stores)
+    int se;                      // 1: warp_exp_kernel (3 channels, compact spans, a 4-byte-pixel image); 0: warp_ring_kernel
+    int raw_bytes;               // warp_exp_kernel: bytes of each of its two raw DMA slots
+    int exp_units;               // warp_exp_kernel: 16-pixel units of its image
 };
 bool warp_frames_plan(const WarpLaunch& L, WarpFramesPlan& P);
 hipError_t launch_warp_frames(const WarpLaunch& L, const WarpFramesPlan& P, hipStream_t s);
