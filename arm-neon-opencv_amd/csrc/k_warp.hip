@@ -585,6 +585,11 @@ hipError_t launch_nearest_t(const WarpLaunch& L, hipStream_t s) {
 }  // namespace
 
 hipError_t launch_warp_nearest(const WarpLaunch& L, hipStream_t s) {
+    {
+        // 3-channel u8 CONSTANT: the LDS-staged kernel (k_warp_frames.hip)
+        WarpFramesPlan P;
+        if (warp_exp_nn_plan(L, P)) return launch_warp_exp_nn(L, P, s);
+    }
     const bool al4 = ((reinterpret_cast<uintptr_t>(L.dst.base) | (uintptr_t)L.dst.row_pitch | (uintptr_t)L.dst.img_pitch |
                        (uintptr_t)L.dst.plane_pitch) & 3) == 0;
     if (L.src.esize == 1 && L.out == kOutSame && L.border_mode != kBorderTransparent && al4 &&

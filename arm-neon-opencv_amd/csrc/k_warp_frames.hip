@@ -35,6 +35,7 @@
 #include <cmath>
 #include <map>
 #include <mutex>
+#include <vector>
 
 #include "vacv_device.hpp"
 
@@ -623,7 +624,9 @@ constexpr int kExpTab = 16 + 12 * kExpRows + 64 * 4 * kRingMaxIt + kExpUnits + 1
 #ifndef VACV_EXP_WPE
 #define VACV_EXP_WPE 4  // 4 waves per SIMD: <= 128 VGPRs (4 workgroups per CU, as the LDS plan)
 #endif
-template <int OUT, int NP>
+// NN: INTER_NEAREST (OpenCV 2.4's warpAffine map, see warp_nearest_kernel in
+// k_warp.hip): the same staging, one tap per pixel, no blend.
+template <int OUT, int NP, bool NN>
 __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(VACV_EXP_WPE)))
 warp_exp_kernel(WarpLaunch L, int gx, int gy, int kf, int slot_bytes, int exp_units, int dst_al) {
     constexpr int CC = 3;
@@ -654,6 +657,8 @@ warp_exp_kernel(WarpLaunch L, int gx, int gy, int kf, int slot_bytes, int exp_un
     unsigned char* t_crow = reinterpret_cast<unsigned char*>(t_un + kExpRows);
     unsigned char* t_urow = t_crow + 64 * 4 * kRingMaxIt;
     uint32_t* t_tot = reinterpret_cast<uint32_t*>(t_urow + kExpUnits);
+    int* t_min = reinterpret_cast<int*>(t_crow);  // per-row tapped columns (until the chunk map is built)
+    int* t_max = t_min + kExpRows;
 
     const int tiles = gx * gy;
     const int nfr = L.n;
@@ -677,15 +682,33 @@ warp_exp_kernel(WarpLaunch L, int gx, int gy, int kf, int slot_bytes, int exp_un
 #pragma unroll
     for (int j = 0; j < NP; ++j) {
         const int y = yw + j;
-        const float fx = (axm + M[1] * (float)y) + M[2];
-        const float fy = (aym + M[4] * (float)y) + M[5];
-        const bool ok = (x < L.dst.w) & (y < L.dst.h) & (fx >= 0.f) & (fx < wlim) & (fy >= 0.f) & (fy < hlim);
-        const int sx = ok ? (int)fx : 0, sy = ok ? (int)fy : 0;
-        const float ax = fx - (float)sx, ay = fy - (float)sy;
-        const uint32_t w0 = (uint32_t)(int)((1.f - ay) * 2048.f + 0.5f);
-        const uint32_t v0 = (uint32_t)(int)((1.f - ax) * 2048.f + 0.5f);
+        bool ok;
+        int sx, sy;
+        if constexpr (NN) {
+            // warpAffine's AB_BITS = 10 fixed point, remap's short map (k_warp.hip)
+            const double* Md = L.invd;
+            const int X0 = (int)rint((Md[1] * y + Md[2]) * 1024.0) + 512;
+            const int Y0 = (int)rint((Md[4] * y + Md[5]) * 1024.0) + 512;
+            int X = (int)((uint32_t)X0 + (uint32_t)(int)rint(Md[0] * x * 1024.0)) >> 10;
+            int Y = (int)((uint32_t)Y0 + (uint32_t)(int)rint(Md[3] * x * 1024.0)) >> 10;
+            X = min(max(X, -32768), 32767);
+            Y = min(max(Y, -32768), 32767);
+            ok = (x < L.dst.w) & (y < L.dst.h) & ((unsigned)X < (unsigned)L.src.w) & ((unsigned)Y < (unsigned)L.src.h);
+            sx = ok ? X : 0;
+            sy = ok ? Y : 0;
+            vwa[j] = 0;
+        } else {
+            const float fx = (axm + M[1] * (float)y) + M[2];
+            const float fy = (aym + M[4] * (float)y) + M[5];
+            ok = (x < L.dst.w) & (y < L.dst.h) & (fx >= 0.f) & (fx < wlim) & (fy >= 0.f) & (fy < hlim);
+            sx = ok ? (int)fx : 0;
+            sy = ok ? (int)fy : 0;
+            const float ax = fx - (float)sx, ay = fy - (float)sy;
+            const uint32_t w0 = (uint32_t)(int)((1.f - ay) * 2048.f + 0.5f);
+            const uint32_t v0 = (uint32_t)(int)((1.f - ax) * 2048.f + 0.5f);
+            vwa[j] = ok ? (v0 | ((4u * w0) << 16)) : (2048u | (8192u << 16));
+        }
         sxy[j] = (uint32_t)sx | ((uint32_t)sy << 16);
-        vwa[j] = ok ? (v0 | ((4u * w0) << 16)) : (2048u | (8192u << 16));
         okm |= (uint32_t)ok << j;
         if (ok) {
             xmin = min(xmin, sx);
@@ -715,6 +738,10 @@ warp_exp_kernel(WarpLaunch L, int gx, int gy, int kf, int slot_bytes, int exp_un
         for (int e = 0; e < CC; ++e) bp |= (uint32_t)(int)L.border[e] << (8 * e);
         *reinterpret_cast<uint32_t*>(lds + ebase + 4 * tid) = bp;
     }
+    if (tid < kExpRows) {
+        t_min[tid] = INT_MAX;
+        t_max[tid] = -1;
+    }
     __syncthreads();
 #pragma unroll
     for (int w = 0; w < 4; ++w) {
@@ -734,47 +761,40 @@ warp_exp_kernel(WarpLaunch L, int gx, int gy, int kf, int slot_bytes, int exp_un
     const int R = any ? ymax + 2 - ymin : 0;                       // staged rows ymin .. ymax + 1
     const bool fits = any && R <= kExpRows;                        // uniform
 
-    // ---- 2. row spans: row ymin + t needs the columns its band of the tile's
-    // source parallelogram taps (fy in [r - 1, r + 1), widened by 0.05 px for
-    // the float rounding of the reference's coordinates): pixels plo .. phi
-    // (relative to bx0), raw chunks glo .. ghi, image units plo/16 .. phi/16
-    if (fits && tid < R) {
-        const float X0 = (float)(bx * kFrTileW), X1 = (float)(min(bx * kFrTileW + kFrTileW, L.dst.w) - 1);
-        const float Y0 = (float)(by * TH), Y1 = (float)(min(by * TH + TH, L.dst.h) - 1);
-        float cx[4], cy[4];
-        const float px[4] = {X0, X1, X1, X0}, py[4] = {Y0, Y0, Y1, Y1};
+    // ---- 2. row spans: the columns each staged row is tapped at, exactly --
+    // an LDS min / max over the tile's pixels (bilinear: columns p, p + 1 of
+    // rows r, r + 1; nearest: column p of row r); pixels plo .. phi (relative
+    // to bx0), raw chunks glo .. ghi, image units plo/16 .. phi/16
+    // Along an output row the taps are monotone in x (an affine map, floored
+    // or OpenCV-rounded), so of each run of lanes tapping the same source row
+    // only the run's two end lanes can hold its min and max: only they update
+    // the table (every lane would serialise 64-way on one address at 0 deg).
+    if (fits) {
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            cx[i] = (M[0] * px[i] + M[1] * py[i]) + M[2];
-            cy[i] = (M[3] * px[i] + M[4] * py[i]) + M[5];
-        }
-        const float r = (float)(ymin + tid), ya = r - 1.05f, yb = r + 1.05f;
-        float lo = 3.0e38f, hi = -3.0e38f;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const int i2 = (i + 1) & 3;
-            if (cy[i] >= ya && cy[i] <= yb) { lo = fminf(lo, cx[i]); hi = fmaxf(hi, cx[i]); }
-#pragma unroll
-            for (int e = 0; e < 2; ++e) {
-                const float yl = e ? yb : ya;
-                if ((cy[i] - yl) * (cy[i2] - yl) < 0.f) {
-                    const float xc = cx[i] + (yl - cy[i]) / (cy[i2] - cy[i]) * (cx[i2] - cx[i]);
-                    lo = fminf(lo, xc);
-                    hi = fmaxf(hi, xc);
+        for (int j = 0; j < NP; ++j) {
+            const bool ok = (okm >> j) & 1u;
+            const uint32_t key = ok ? (sxy[j] >> 16) : 0xFFFFFFFFu;
+            const uint32_t kl = (uint32_t)__shfl_up((int)key, 1, 64), kr = (uint32_t)__shfl_down((int)key, 1, 64);
+            if (ok && (lane == 0 || lane == 63 || kl != key || kr != key)) {
+                const int p = (int)(sxy[j] & 0xFFFFu) - bx0, r = (int)(sxy[j] >> 16) - ymin;
+                atomicMin(&t_min[r], p);
+                atomicMax(&t_max[r], NN ? p : p + 1);
+                if constexpr (!NN) {
+                    atomicMin(&t_min[r + 1], p);
+                    atomicMax(&t_max[r + 1], p + 1);
                 }
             }
         }
+    }
+    __syncthreads();
+    if (fits && tid < R) {
+        const int plo = t_min[tid], phi = t_max[tid];
         uint32_t sp = 0, un = 0, cnt = 0;
-        if (lo <= hi) {
-            const int clo = (int)floorf(fmaxf(lo - 0.05f, -1.0e9f)) - bx0;       // left tap column
-            const int chi = (int)floorf(fminf(hi + 0.05f, 1.0e9f)) + 1 - bx0;    // right tap column
-            const int plo = max(clo, 0), phi = min(chi, wpx - 1);
-            if (plo <= phi) {
-                const int glo = (plo * CC) >> 4, ghi = ((phi + 1) * CC - 1) >> 4;
-                sp = (uint32_t)glo | ((uint32_t)ghi << 16);
-                cnt = (uint32_t)(ghi - glo + 1);
-                un = (uint32_t)(plo >> 4) | ((uint32_t)((phi >> 4) - (plo >> 4) + 1) << 16);
-            }
+        if (plo <= phi) {
+            const int glo = (plo * CC) >> 4, ghi = ((phi + 1) * CC - 1) >> 4;
+            sp = (uint32_t)glo | ((uint32_t)ghi << 16);
+            cnt = (uint32_t)(ghi - glo + 1);
+            un = (uint32_t)(plo >> 4) | ((uint32_t)((phi >> 4) - (plo >> 4) + 1) << 16);
         }
         t_sp[tid] = sp;
         t_un[tid] = un;
@@ -1038,14 +1058,22 @@ warp_exp_kernel(WarpLaunch L, int gx, int gy, int kf, int slot_bytes, int exp_un
                 const uint32_t* pt = reinterpret_cast<const uint32_t*>(lds + ((VACV_RING_DBG & 4) ? ebase : e & 0xFFFFu));
                 const uint32_t* pb = reinterpret_cast<const uint32_t*>(lds + ((VACV_RING_DBG & 4) ? ebase : e >> 16));
                 tp[j][0] = pt[0];
-                tp[j][1] = pt[1];
-                tp[j][2] = pb[0];
-                tp[j][3] = pb[1];
+                if constexpr (!NN) {
+                    tp[j][1] = pt[1];
+                    tp[j][2] = pb[0];
+                    tp[j][3] = pb[1];
+                }
             }
 #pragma unroll
             for (int j = 0; j < kGrp; ++j) {
                 uint32_t vv[CC];
-                blend3(j0 + j, tp[j][0], tp[j][1], tp[j][2], tp[j][3], vv);
+                if constexpr (NN) {
+                    // the tap's channel k in bits 24..31, as the blend leaves it
+#pragma unroll
+                    for (int q = 0; q < CC; ++q) vv[q] = tp[j][0] << (24 - 8 * q);
+                } else {
+                    blend3(j0 + j, tp[j][0], tp[j][1], tp[j][2], tp[j][3], vv);
+                }
                 emit(full_c, f, j0 + j, vv);
             }
         }
@@ -1070,9 +1098,22 @@ warp_exp_kernel(WarpLaunch L, int gx, int gy, int kf, int slot_bytes, int exp_un
                 for (int k = 0; k < CC; ++k) cn[k] = chan_norm(L.norm, f, k);
             }
             for (int j = 0; j < NP; ++j) {
-                uint32_t tl, tr, bl, br, vv[CC];
-                direct_taps<CC>(L, sp, x, yw + j, tl, tr, bl, br);
-                blend3(j, tl, tr, bl, br, vv);
+                uint32_t vv[CC];
+                if constexpr (NN) {
+                    uint32_t tl = 0;
+#pragma unroll
+                    for (int q = 0; q < CC; ++q) tl |= (uint32_t)(int)L.border[q] << (8 * q);
+                    if ((okm >> j) & 1u) {
+                        const int sx = (int)(sxy[j] & 0xFFFFu), sy = (int)(sxy[j] >> 16);
+                        tl = pack_bytes<CC>(sp + (int64_t)sy * L.src.row_pitch + (int64_t)sx * CC);
+                    }
+#pragma unroll
+                    for (int q = 0; q < CC; ++q) vv[q] = tl << (24 - 8 * q);
+                } else {
+                    uint32_t tl, tr, bl, br;
+                    direct_taps<CC>(L, sp, x, yw + j, tl, tr, bl, br);
+                    blend3(j, tl, tr, bl, br, vv);
+                }
                 emit(edge_t(), f, j, vv);
             }
         }
@@ -1144,11 +1185,11 @@ int64_t frames_resident(K kernel, size_t lds) {
     return r;
 }
 
-template <int OUT, int NP>
+template <int OUT, int NP, bool NN = false>
 hipError_t launch_exp(const WarpLaunch& L, const WarpFramesPlan& P, hipStream_t s) {
     constexpr int TH = 4 * NP;
     const int gx = (L.dst.w + kFrTileW - 1) / kFrTileW, gy = (L.dst.h + TH - 1) / TH;
-    auto kern = warp_exp_kernel<OUT, NP>;
+    auto kern = warp_exp_kernel<OUT, NP, NN>;
     int kf = P.kf;
     if (kf <= 0) {
         const int64_t res = std::max<int64_t>(frames_resident(kern, (size_t)P.lds), 256);
@@ -1298,69 +1339,73 @@ bool ring_layout_th(const WarpLaunch& L, WarpFramesPlan& P, int th) {
     return P.lds <= 64 * 1024;
 }
 
-// warp_exp_kernel's staging, mirrored on the host with the kernel's float
-// arithmetic for EVERY tile of the output (the box from the pixels' taps, the
-// spans from the tile's corners): the most span chunks, image units and box
+// warp_exp_kernel's staging, mirrored on the host with the kernel's
+// arithmetic for EVERY tile of the output (the box and the per-row tapped
+// columns from the pixels' taps): the most span chunks, image units and box
 // rows any tile needs.  The slots and the image are sized for that, so no
 // tile of the planned geometry takes the kernel's unstaged path.
 struct ExpNeeds {
     int rows = 0, chunks = 0, units = 0;
 };
-ExpNeeds exp_needs(const WarpLaunch& L, int th) {
+ExpNeeds exp_needs(const WarpLaunch& L, int th, bool nn) {
     constexpr int CC = 3;
     const float* M = L.inv;
+    const double* Md = L.invd;
     const float wlim = (float)(L.src.w - 1), hlim = (float)(L.src.h - 1);
     const int gx = (L.dst.w + kFrTileW - 1) / kFrTileW, gy = (L.dst.h + th - 1) / th;
+    // the kernel's tap of pixel (x, y): (sx, sy) or false outside
+    auto tap = [&](int x, int y, int& sx, int& sy) {
+        if (x >= L.dst.w || y >= L.dst.h) return false;
+        if (nn) {
+            const int X0 = (int)std::rint((Md[1] * y + Md[2]) * 1024.0) + 512;
+            const int Y0 = (int)std::rint((Md[4] * y + Md[5]) * 1024.0) + 512;
+            int X = (int)((uint32_t)X0 + (uint32_t)(int)std::rint(Md[0] * x * 1024.0)) >> 10;
+            int Y = (int)((uint32_t)Y0 + (uint32_t)(int)std::rint(Md[3] * x * 1024.0)) >> 10;
+            sx = std::min(std::max(X, -32768), 32767);
+            sy = std::min(std::max(Y, -32768), 32767);
+            return (unsigned)sx < (unsigned)L.src.w && (unsigned)sy < (unsigned)L.src.h;
+        }
+        const float axm = M[0] * (float)x, aym = M[3] * (float)x;
+        const float fx = (axm + M[1] * (float)y) + M[2];
+        const float fy = (aym + M[4] * (float)y) + M[5];
+        if (!(fx >= 0.f && fx < wlim && fy >= 0.f && fy < hlim)) return false;
+        sx = (int)fx;
+        sy = (int)fy;
+        return true;
+    };
     ExpNeeds n;
+    std::vector<int> rmin, rmax;
     for (int by = 0; by < gy; ++by) {
         for (int bx = 0; bx < gx; ++bx) {
-            int xmin = INT_MAX, xmax = INT_MIN, ymin = INT_MAX, ymax = INT_MIN;
-            for (int y = by * th; y < by * th + th; ++y) {
-                for (int x = bx * kFrTileW; x < bx * kFrTileW + kFrTileW; ++x) {
-                    const float axm = M[0] * (float)x, aym = M[3] * (float)x;
-                    const float fx = (axm + M[1] * (float)y) + M[2];
-                    const float fy = (aym + M[4] * (float)y) + M[5];
-                    if (x < L.dst.w && y < L.dst.h && fx >= 0.f && fx < wlim && fy >= 0.f && fy < hlim) {
-                        xmin = std::min(xmin, (int)fx);
-                        xmax = std::max(xmax, (int)fx);
-                        ymin = std::min(ymin, (int)fy);
-                        ymax = std::max(ymax, (int)fy);
+            int xmin = INT_MAX, xmax = INT_MIN, ymin = INT_MAX, ymax = INT_MIN, sx, sy;
+            for (int y = by * th; y < by * th + th; ++y)
+                for (int x = bx * kFrTileW; x < bx * kFrTileW + kFrTileW; ++x)
+                    if (tap(x, y, sx, sy)) {
+                        xmin = std::min(xmin, sx);
+                        xmax = std::max(xmax, sx);
+                        ymin = std::min(ymin, sy);
+                        ymax = std::max(ymax, sy);
                     }
-                }
-            }
             if (xmax < 0) continue;
-            const int bx0 = xmin & ~3, wpx = xmax + 2 - bx0, R = ymax + 2 - ymin;
-            const float X0 = (float)(bx * kFrTileW), X1 = (float)(std::min(bx * kFrTileW + kFrTileW, L.dst.w) - 1);
-            const float Y0 = (float)(by * th), Y1 = (float)(std::min(by * th + th, L.dst.h) - 1);
-            float cx[4], cy[4];
-            const float px[4] = {X0, X1, X1, X0}, py[4] = {Y0, Y0, Y1, Y1};
-            for (int i = 0; i < 4; ++i) {
-                cx[i] = (M[0] * px[i] + M[1] * py[i]) + M[2];
-                cy[i] = (M[3] * px[i] + M[4] * py[i]) + M[5];
-            }
-            int chunks = 0, units = 0;
-            for (int t = 0; t < R; ++t) {
-                const float r = (float)(ymin + t), ya = r - 1.05f, yb = r + 1.05f;
-                float lo = 3.0e38f, hi = -3.0e38f;
-                for (int i = 0; i < 4; ++i) {
-                    const int i2 = (i + 1) & 3;
-                    if (cy[i] >= ya && cy[i] <= yb) { lo = std::fmin(lo, cx[i]); hi = std::fmax(hi, cx[i]); }
-                    for (int e = 0; e < 2; ++e) {
-                        const float yl = e ? yb : ya;
-                        if ((cy[i] - yl) * (cy[i2] - yl) < 0.f) {
-                            const float xc = cx[i] + (yl - cy[i]) / (cy[i2] - cy[i]) * (cx[i2] - cx[i]);
-                            lo = std::fmin(lo, xc);
-                            hi = std::fmax(hi, xc);
+            const int bx0 = xmin & ~3, R = ymax + 2 - ymin;
+            rmin.assign(R + 1, INT_MAX);
+            rmax.assign(R + 1, -1);
+            for (int y = by * th; y < by * th + th; ++y)
+                for (int x = bx * kFrTileW; x < bx * kFrTileW + kFrTileW; ++x)
+                    if (tap(x, y, sx, sy)) {
+                        const int p = sx - bx0, r = sy - ymin;
+                        rmin[r] = std::min(rmin[r], p);
+                        rmax[r] = std::max(rmax[r], nn ? p : p + 1);
+                        if (!nn) {
+                            rmin[r + 1] = std::min(rmin[r + 1], p);
+                            rmax[r + 1] = std::max(rmax[r + 1], p + 1);
                         }
                     }
-                }
-                if (!(lo <= hi)) continue;
-                const int clo = (int)std::floor(std::fmax(lo - 0.05f, -1.0e9f)) - bx0;
-                const int chi = (int)std::floor(std::fmin(hi + 0.05f, 1.0e9f)) + 1 - bx0;
-                const int plo = std::max(clo, 0), phi = std::min(chi, wpx - 1);
-                if (plo > phi) continue;
-                chunks += (((phi + 1) * CC - 1) >> 4) - ((plo * CC) >> 4) + 1;
-                units += (phi >> 4) - (plo >> 4) + 1;
+            int chunks = 0, units = 0;
+            for (int t = 0; t < R; ++t) {
+                if (rmin[t] > rmax[t]) continue;
+                chunks += (((rmax[t] + 1) * CC - 1) >> 4) - ((rmin[t] * CC) >> 4) + 1;
+                units += (rmax[t] >> 4) - (rmin[t] >> 4) + 1;
             }
             n.rows = std::max(n.rows, R);
             n.chunks = std::max(n.chunks, chunks);
@@ -1372,8 +1417,8 @@ ExpNeeds exp_needs(const WarpLaunch& L, int th) {
 
 // warp_exp_kernel's LDS: two compact raw slots, the image (at least the setup
 // tables), the output exchange; <= 40 KiB keeps 4 workgroups per CU
-bool exp_layout_th(const WarpLaunch& L, WarpFramesPlan& P, int th) {
-    const ExpNeeds n = exp_needs(L, th);
+bool exp_layout_th(const WarpLaunch& L, WarpFramesPlan& P, int th, bool nn = false) {
+    const ExpNeeds n = exp_needs(L, th, nn);
     const int n_inst = (n.chunks + 63) / 64;
     if (n.rows > kExpRows || n_inst > 4 * kRingMaxIt || n.units > kExpUnits) return false;
     P.th = th;
@@ -1466,6 +1511,59 @@ bool warp_frames_plan(const WarpLaunch& L, WarpFramesPlan& P) {
     P.dst_al = al4(L.dst) ? 1 : 0;
     P.kf = tune(VACV_TUNE_WARP_FRAMES);
     return ok;
+}
+
+// INTER_NEAREST on warp_exp_kernel: 3-channel u8 NHWC, BORDER_CONSTANT,
+// 4-byte aligned destination rows (VACV_TUNE_WARP_KERNEL = 5 keeps the
+// gather kernels).  Layouts cached per geometry, as warp_frames_plan.
+bool warp_exp_nn_plan(const WarpLaunch& L, WarpFramesPlan& P) {
+    if (tune(VACV_TUNE_WARP_KERNEL) == 5) return false;
+    if (L.src.esize != 1 || L.src.cc != 3 || L.src.planes != 1 || L.border_mode != kBorderConstant) return false;
+    if (L.src.plane_bytes > kMaxPlaneBytes || L.dst.plane_bytes > kMaxPlaneBytes) return false;
+    const auto al4 = [](const PlaneGeom& g) {
+        return !(g.row_pitch % 4 || g.img_pitch % 4 || g.plane_pitch % 4 || reinterpret_cast<uintptr_t>(g.base) % 4);
+    };
+    if (!al4(L.src) || !al4(L.dst)) return false;
+    for (int i = 0; i < 6; ++i)
+        if (!std::isfinite(L.inv[i]) || !std::isfinite(L.invd[i])) return false;
+    struct Key {
+        double invd[6];
+        float inv[6];
+        int sw, sh, dw, dh, th, bytes_out;
+        bool operator<(const Key& o) const { return std::memcmp(this, &o, sizeof(Key)) < 0; }
+    };
+    Key k;
+    std::memset(&k, 0, sizeof(k));
+    std::memcpy(k.invd, L.invd, sizeof(k.invd));
+    std::memcpy(k.inv, L.inv, sizeof(k.inv));
+    k.sw = L.src.w; k.sh = L.src.h; k.dw = L.dst.w; k.dh = L.dst.h; k.th = tune(VACV_TUNE_WARP_TILE_H);
+    k.bytes_out = L.out == kOutSame ? 1 : 0;
+    static std::mutex mu;
+    static std::map<Key, std::pair<bool, WarpFramesPlan>> cache;
+    bool ok;
+    {
+        std::lock_guard<std::mutex> lk(mu);
+        auto it = cache.find(k);
+        if (it == cache.end()) {
+            WarpFramesPlan Q{};
+            const int th0 = L.out == kOutSame ? 32 : 16;
+            const bool r = (k.th == 16 || k.th == 32) ? exp_layout_th(L, Q, k.th, true)
+                                                      : exp_layout_th(L, Q, th0, true) || exp_layout_th(L, Q, 48 - th0, true);
+            if (cache.size() > 256) cache.clear();
+            it = cache.emplace(k, std::make_pair(r, Q)).first;
+        }
+        ok = it->second.first;
+        P = it->second.second;
+    }
+    P.dst_al = 1;
+    P.kf = tune(VACV_TUNE_WARP_FRAMES);
+    return ok;
+}
+
+hipError_t launch_warp_exp_nn(const WarpLaunch& L, const WarpFramesPlan& P, hipStream_t s) {
+    if (L.out == kOutSame) return P.th == 16 ? launch_exp<kOutSame, 4, true>(L, P, s) : launch_exp<kOutSame, 8, true>(L, P, s);
+    if (L.out == kOutF32) return P.th == 16 ? launch_exp<kOutF32, 4, true>(L, P, s) : launch_exp<kOutF32, 8, true>(L, P, s);
+    return P.th == 16 ? launch_exp<kOutNorm, 4, true>(L, P, s) : launch_exp<kOutNorm, 8, true>(L, P, s);
 }
 
 hipError_t launch_warp_frames(const WarpLaunch& L, const WarpFramesPlan& P, hipStream_t s) {

@@ -217,6 +217,9 @@ struct WarpFramesPlan {
 };
 bool warp_frames_plan(const WarpLaunch& L, WarpFramesPlan& P);
 hipError_t launch_warp_frames(const WarpLaunch& L, const WarpFramesPlan& P, hipStream_t s);
+// INTER_NEAREST with the same staging (3-channel u8, BORDER_CONSTANT)
+bool warp_exp_nn_plan(const WarpLaunch& L, WarpFramesPlan& P);
+hipError_t launch_warp_exp_nn(const WarpLaunch& L, const WarpFramesPlan& P, hipStream_t s);
 
 struct CopyLaunch {                // crop / clone: row copies
     PlaneGeom src;                 // base already offset to the crop origin

@@ -1184,6 +1184,53 @@ def test_warp_random_matrices(ops, dev, oracle):
             assert_same(gotnn[k].reshape(ho, wo, c), want.reshape(ho, wo, c), what + f" nearest inv={inv}")
 
 
+def test_warp_nearest_staged(ops, dev, oracle):
+    """INTER_NEAREST on the LDS-staged kernel (warp_exp_kernel<..., NN>: 3-channel
+    u8, BORDER_CONSTANT, dword-aligned rows): seeded random maps on 4-aligned
+    widths, u8 and normalised fp32 output, through WARP_INVERSE_MAP every other
+    case, against the oracle's OpenCV restatement (parity unpinned); and cfg4's
+    720p rot-15 map on 6 frames, bit-identical to the gather kernel
+    (VACV_TUNE_WARP_KERNEL = 5) and to the oracle on frames 0 and 5."""
+    import torch
+    from vacv_amd import INTER_NEAREST, WARP_INVERSE_MAP
+    rng = np.random.default_rng(20261018)
+    bv = (7, 200, 31, 99)
+    for t in range(16):
+        h, w = int(rng.integers(20, 160)), 4 * int(rng.integers(5, 48))
+        ho, wo = int(rng.integers(9, 140)), 4 * int(rng.integers(3, 45))
+        a = np.deg2rad(rng.uniform(-180.0, 180.0))
+        sx, sy = rng.uniform(0.5, 1.8, 2)
+        A = np.array([[np.cos(a), -np.sin(a)], [np.sin(a), np.cos(a)]]) @ np.array([[sx, rng.uniform(-0.4, 0.4)],
+                                                                                   [0.0, sy]])
+        tv = np.array([wo / 2, ho / 2]) - A @ np.array([w / 2, h / 2]) + rng.uniform(-0.5, 0.5, 2) * (wo, ho)
+        m = np.concatenate([A, tv[:, None]], 1).astype(np.float32).reshape(6)
+        inv = t % 2 == 1
+        mm = oracle.invert_affine(m) if inv else m
+        fl = INTER_NEAREST | (WARP_INVERSE_MAP if inv else 0)
+        ims = np.stack([synthetic_image(9500 + 2 * t + k, h, w, 3) for k in range(2)])
+        got = host(ops.warp_affine(to_dev(ims, dev), mm, wo, ho, flags=fl, border_value=bv))
+        gotn = host(ops.warp_affine_normalize(to_dev(ims, dev), mm, wo, ho, MEAN, STD, flags=fl, border_value=bv))
+        what = f"case {t}: {w}x{h} -> {wo}x{ho} inv={inv} m={m.tolist()}"
+        for k in range(2):
+            want = oracle.warp_affine_nn(ims[k], mm, wo, ho, inverse_map=inv, border=bv).reshape(ho, wo, 3)
+            assert_same(got[k].reshape(ho, wo, 3), want, what)
+            assert_same(gotn[k].reshape(ho, wo, 3), oracle.normalize(oracle.u8_to_f32(want), MEAN, STD),
+                        what + " normalize")
+    m = ops.rotation_matrix(0.9, 15.0, (640, 360, 640, 360))
+    src = torch.randint(0, 256, (6, 720, 1280, 3), dtype=torch.uint8, device=dev,
+                        generator=torch.Generator(device=dev).manual_seed(5))
+    a = ops.warp_affine(src, m, 1280, 720, flags=INTER_NEAREST)
+    with ops.tuning(WARP_KERNEL=5):
+        b = ops.warp_affine(src, m, 1280, 720, flags=INTER_NEAREST)
+    torch.cuda.synchronize(dev)
+    assert torch.equal(a, b), f"{(a != b).sum().item()} bytes differ from the gather kernel"
+    for k in (0, 5):
+        want = oracle.warp_affine_nn(host(src[k]), m, 1280, 720)
+        assert_same(host(a[k]), want.reshape(720, 1280, 3), f"cfg4 nearest frame {k}")
+    del src, a, b
+    torch.cuda.empty_cache()
+
+
 def test_warp_kernels_agree(ops, dev, oracle):
     """u8 BORDER_CONSTANT warps run on the LDS-staged frames kernel
     (k_warp_frames.hip) unless its box plan does not fit (e.g. a 4x
