@@ -621,6 +621,9 @@ constexpr int kExpTab = 16 + 12 * kExpRows + 64 * 4 * kRingMaxIt + kExpUnits + 1
 #ifndef VACV_EXP_XCH
 #define VACV_EXP_XCH 1  // u8 output: 1 a 4-row LDS exchange + 12-byte stores; 0 DPP quad packing + dword stores per row
 #endif
+#ifndef VACV_EXP_F32XCH
+#define VACV_EXP_F32XCH 1  // fp32 output: 1 through the LDS exchange as 16-byte stores; 0 one 12-byte store per pixel (lanes contiguous)
+#endif
 #ifndef VACV_EXP_WPE
 #define VACV_EXP_WPE 4  // 4 waves per SIMD: <= 128 VGPRs (4 workgroups per CU, as the LDS plan)
 #endif
@@ -636,7 +639,7 @@ warp_exp_kernel(WarpLaunch L, int gx, int gy, int kf, int slot_bytes, int exp_un
     // and 47 B after a row's chunks: bytes of no tapped pixel)
     // [image: 16 B border pixel head, then exp_units x 16 pixels; the setup
     //  tables live here until the first re-lay] [exchange: 4 waves x kXB]
-    constexpr int kXB = OUT == kOutSame ? (VACV_EXP_XCH ? 4 * 64 * 4 : 16) : 64 * CC * 4;
+    constexpr int kXB = OUT == kOutSame ? (VACV_EXP_XCH ? 4 * 64 * 4 : 16) : (VACV_EXP_F32XCH ? 64 * CC * 4 : 16);
     const uint32_t ebase = 48u + 2u * (uint32_t)slot_bytes + 64u;
     const uint32_t xbase = ebase + 16u + 64u * (uint32_t)max(exp_units, (kExpTab + 63) / 64);
 #ifdef VACV_RING_AUX
@@ -1023,7 +1026,7 @@ warp_exp_kernel(WarpLaunch L, int gx, int gy, int kf, int slot_bytes, int exp_un
                 const float fv = OUT == kOutF32 ? (float)v : normalize_u8v(cn[k], v);
                 o[k] = __builtin_bit_cast(uint32_t, fv);
             }
-            if constexpr (FULL) {
+            if constexpr (FULL && VACV_EXP_F32XCH) {
 #pragma unroll
                 for (int k = 0; k < CC; ++k) *reinterpret_cast<uint32_t*>(xch + 12 * lane + 4 * k) = o[k];
                 __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -1429,7 +1432,7 @@ bool exp_layout_th(const WarpLaunch& L, WarpFramesPlan& P, int th, bool nn = fal
     P.S = 0;
     P.ns = 2;
     P.slot = P.raw_bytes;
-    const int xb = 4 * (L.out == kOutSame ? (VACV_EXP_XCH ? 4 * 64 * 4 : 16) : 64 * 3 * 4);
+    const int xb = 4 * (L.out == kOutSame ? (VACV_EXP_XCH ? 4 * 64 * 4 : 16) : (VACV_EXP_F32XCH ? 64 * 3 * 4 : 16));
     P.lds = 48 + 2 * P.raw_bytes + 64 + 16 + 64 * std::max(n.units, (kExpTab + 63) / 64) + xb;
     return P.lds <= 64 * 1024;
 }
@@ -1444,9 +1447,9 @@ bool frames_layout(const WarpLaunch& L, WarpFramesPlan& P) {
     P.raw_bytes = 0;
     if (L.src.cc == 3 && L.src.planes == 1 && tune(VACV_TUNE_WARP_KERNEL) != 6) {
         WarpFramesPlan Q = P;
-        // fp32 output: 16-row tiles by default (the 32-row instance spills at
-        // the 128 VGPRs of 4 waves per SIMD)
-        const int th0 = L.out == kOutSame ? 32 : 16;
+        // 32-row tiles (fp32 output too: 0.4155 vs 0.4398 ms normalised at
+        // 720p rot15 x128, although its instance spills a few registers)
+        const int th0 = 32;
         if (th_knob == 16 || th_knob == 32) {
             if (exp_layout_th(L, Q, th_knob)) { P = Q; return true; }
         } else if (exp_layout_th(L, Q, th0) || exp_layout_th(L, Q, 48 - th0)) {
@@ -1546,7 +1549,7 @@ bool warp_exp_nn_plan(const WarpLaunch& L, WarpFramesPlan& P) {
         auto it = cache.find(k);
         if (it == cache.end()) {
             WarpFramesPlan Q{};
-            const int th0 = L.out == kOutSame ? 32 : 16;
+            const int th0 = 32;
             const bool r = (k.th == 16 || k.th == 32) ? exp_layout_th(L, Q, k.th, true)
                                                       : exp_layout_th(L, Q, th0, true) || exp_layout_th(L, Q, 48 - th0, true);
             if (cache.size() > 256) cache.clear();

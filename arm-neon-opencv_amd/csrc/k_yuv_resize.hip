@@ -298,6 +298,162 @@ yuv_resize_kernel(YuvResizeLaunch L) {
     }
 }
 
+// ---------------------------------------------------------------------------
+// yuv_cols_kernel (round 5): the same arithmetic with COLUMN-stationary lanes,
+// the shape that lifted the u8 resize (resize_cols_kernel, k_resize_direct.hip).
+// A wave owns 64 output columns x kYuvRows output rows of one image; lane l
+// keeps column x0 + l for all of them, so its horizontal tap (index, weights)
+// and chroma byte selector are computed once, not per pixel (yuv_resize_kernel
+// numbered pixels row-major and recomputed tap_of, chroma_sel and the row
+// select for every one); the rows' vertical taps and source-row offsets are
+// computed by lanes 0..kYuvRows-1 in parallel and broadcast as scalars
+// (readlane).  Per pixel and weighted row what is left: two dword gathers
+// (one contiguous run of a source row per instruction), the packed decode
+// and the blend.  Results leave through the wave's LDS buffer, kYuvHalf rows
+// at a time, as 16-byte non-temporal stores (plane-major for NCHW).
+constexpr int kYuvRows = 8;   // output rows per wave task
+constexpr int kYuvHalf = 4;   // rows per LDS exchange round
+template <int OUT, int MODE, bool CHW, bool ONE_ROW>
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(yuv_waves(OUT, ONE_ROW))))
+yuv_cols_kernel(YuvResizeLaunch L, int col_blocks, int row_groups) {
+    using TOut = typename std::conditional<(OUT == kOutSame), uint8_t, float>::type;
+    constexpr int kES = (int)sizeof(TOut);
+    constexpr int NR = ONE_ROW ? 1 : 2;
+    constexpr int kRowB = 64 * kES * (CHW ? 1 : 3);          // bytes of one block row (per plane)
+    constexpr int kPlaneB = kYuvHalf * kRowB;                 // one round's bytes per plane
+    __shared__ __attribute__((aligned(16))) unsigned char xch[4][3 * kYuvHalf * 64 * kES];
+    const int lane = (int)threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
+    const int task = (int)blockIdx.x * 4 + wave;              // (row group, column block), column block fastest
+    if (task >= col_blocks * row_groups) return;              // whole wave
+    const int img = blockIdx.y;
+    const int rg = task / col_blocks, cb = task - rg * col_blocks;
+    const int W = L.wo, H = L.ho;
+    const int x0 = cb * 64, y0 = rg * kYuvRows;
+    const int ncol = min(64, W - x0), nrow = min(kYuvRows, H - y0);  // uniform
+    const int x = lane < ncol ? x0 + lane : W - 1;
+
+    const unsigned char* sp = L.src + (int64_t)img * L.src_img;
+    const Rsrc rs = make_rsrc(sp, L.src_bytes);
+    const uint32_t rp = (uint32_t)L.src_row;
+    const uint32_t uvbase = (uint32_t)L.h * rp;
+
+    // the column's tap and chroma selector (once)
+    const FixedTap tx = tap_of<MODE>(x, L.w, W, L.scale_xf, L.scale_xd);
+    const us2 wx = __builtin_bit_cast(us2, (uint32_t)tx.w0 | ((uint32_t)tx.w1 << 16));
+    const uint32_t cs = chroma_sel(L.w, tx.i);
+    const uint32_t ycol = (uint32_t)tx.i;
+    const uint32_t ccol = (uint32_t)min(tx.i & ~1, L.w - 4);
+    // lane r < kYuvRows: row r's tap -- source Y / chroma row offsets (rows i
+    // and i + 1) and weights wA | wB << 16
+    uint32_t my_y0 = 0, my_c0 = 0, my_y1 = 0, my_c1 = 0, my_w = 0;
+    if (lane < kYuvRows) {
+        FixedTap ty = tap_of<MODE>(min(y0 + lane, H - 1), L.h, H, L.scale_yf, L.scale_yd);
+        if (ONE_ROW && ty.w0 == 0) { ty.i += 1; ty.w0 = ty.w1; ty.w1 = 0; }  // the weighted row as row A
+        const RowOffs ro = row_offs(ty.i, rp, uvbase, rs.delta);
+        my_y0 = ro.y0; my_c0 = ro.c0; my_y1 = ro.y1; my_c1 = ro.c1;
+        my_w = (uint32_t)ty.w0 | ((uint32_t)ty.w1 << 16);
+    }
+    // every gather of the task, issued before any decode
+    RowTaps t[kYuvRows][NR];
+#pragma unroll
+    for (int r = 0; r < kYuvRows; ++r) {
+        const uint32_t ya = (uint32_t)__builtin_amdgcn_readlane((int)my_y0, r);
+        const uint32_t ca = (uint32_t)__builtin_amdgcn_readlane((int)my_c0, r);
+        t[r][0].y = __builtin_amdgcn_raw_buffer_load_b32(rs.r, (int)(ya + ycol), 0, kYuvAux);
+        t[r][0].c = __builtin_amdgcn_raw_buffer_load_b32(rs.r, (int)(ca + ccol), 0, kYuvAux);
+        if constexpr (!ONE_ROW) {
+            const uint32_t yb = (uint32_t)__builtin_amdgcn_readlane((int)my_y1, r);
+            const uint32_t cb2 = (uint32_t)__builtin_amdgcn_readlane((int)my_c1, r);
+            t[r][1].y = __builtin_amdgcn_raw_buffer_load_b32(rs.r, (int)(yb + ycol), 0, kYuvAux);
+            t[r][1].c = __builtin_amdgcn_raw_buffer_load_b32(rs.r, (int)(cb2 + ccol), 0, kYuvAux);
+        }
+    }
+    ChanNorm cn[3] = {};
+    if (OUT == kOutNorm) {
+#pragma unroll
+        for (int k = 0; k < 3; ++k) cn[k] = chan_norm(L.norm, img, k);
+    }
+    unsigned char* dimg = L.dst + (int64_t)img * L.dst_img;
+    const Rsrc rd = make_rsrc(dimg, CHW ? L.dst_plane * 3 : L.dst_img);
+    // 16-byte chunks wherever the block row's bytes are whole chunks (the
+    // host checked the alignment): every block but a partial last one whose
+    // width is not (e.g. 224 = 3.5 blocks: 32 fp32 columns are 8 chunks)
+    const int rbytes = ncol * kES * (CHW ? 1 : 3);
+    const bool chunks = (rbytes & 15) == 0;  // uniform
+    const int cpr = rbytes >> 4;
+    TOut* xo = reinterpret_cast<TOut*>(xch[wave]);
+    const unsigned char* xs = xch[wave];
+#pragma unroll
+    for (int g = 0; g < kYuvRows / kYuvHalf; ++g) {
+#pragma unroll
+        for (int j = 0; j < kYuvHalf; ++j) {
+            const int r = g * kYuvHalf + j;
+            const uint32_t wr = (uint32_t)__builtin_amdgcn_readlane((int)my_w, r);
+            uint32_t pa[3], pb[3] = {0u, 0u, 0u};  // rows A/B: B, G, R as u16 pairs {left, right}
+            decode_row(t[r][0], cs, L.v_first, pa[0], pa[1], pa[2]);
+            if (!ONE_ROW) decode_row(t[r][NR - 1], cs, L.v_first, pb[0], pb[1], pb[2]);
+            if (L.rgb) {  // output order R, G, B
+                const uint32_t q0 = pa[0], q1 = pb[0];
+                pa[0] = pa[2]; pa[2] = q0;
+                pb[0] = pb[2]; pb[2] = q1;
+            }
+            const uint32_t wA = wr & 0xFFFFu, wB = ONE_ROW ? 0u : wr >> 16;
+#pragma unroll
+            for (int k = 0; k < 3; ++k) {
+                const int v = blend_fixed<MODE>(pa[k], pb[k], wx, wA, wB);
+                TOut ov;
+                if (OUT == kOutSame) ov = (TOut)v;
+                else if (OUT == kOutF32) ov = (TOut)(float)v;
+                else ov = (TOut)normalize_u8v(cn[k], v);
+                xo[CHW ? k * (kYuvHalf * 64) + j * 64 + lane : (j * 64 + lane) * 3 + k] = ov;
+            }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        const int rows = min(kYuvHalf, nrow - g * kYuvHalf);  // uniform
+        if (rows > 0) {
+            const uint32_t base = (uint32_t)(y0 + g * kYuvHalf) * (uint32_t)L.dst_row +
+                                  (uint32_t)(x0 * kES * (CHW ? 1 : 3)) + rd.delta;
+#pragma unroll
+            for (int k = 0; k < (CHW ? 3 : 1); ++k) {
+                const uint32_t pbase = base + (uint32_t)(k * L.dst_plane);
+                const unsigned char* xk = xs + k * kPlaneB;
+                if (chunks) {
+                    for (int c = lane; c < rows * cpr; c += 64) {
+                        const int rr = c / cpr, cc = c - rr * cpr;
+                        __builtin_amdgcn_raw_buffer_store_b128(*reinterpret_cast<const u32x4*>(xk + rr * kRowB + 16 * cc),
+                                                               rd.r,
+                                                               (int)(pbase + (uint32_t)rr * (uint32_t)L.dst_row + 16u * cc),
+                                                               0, VACV_STORE_AUX);
+                    }
+                } else {  // a partial last column block of odd bytes: bytes
+                    const int rb = rbytes;
+                    for (int e = lane; e < rows * rb; e += 64) {
+                        const int rr = e / rb, cc = e - rr * rb;
+                        __builtin_amdgcn_raw_buffer_store_b8(xk[rr * kRowB + cc], rd.r,
+                                                             (int)(pbase + (uint32_t)rr * (uint32_t)L.dst_row + cc), 0,
+                                                             VACV_STORE_AUX);
+                    }
+                }
+            }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+}
+
+template <int OUT, int MODE, bool CHW>
+hipError_t launch_cols_t(const YuvResizeLaunch& L, bool one_row, hipStream_t s) {
+    const int col_blocks = (L.wo + 63) / 64, row_groups = (L.ho + kYuvRows - 1) / kYuvRows;
+    const dim3 grid((unsigned)((col_blocks * row_groups + 3) / 4), (unsigned)L.n);
+    if (one_row) hipLaunchKernelGGL((yuv_cols_kernel<OUT, MODE, CHW, true>), grid, dim3(kBlock), 0, s, L, col_blocks, row_groups);
+    else hipLaunchKernelGGL((yuv_cols_kernel<OUT, MODE, CHW, false>), grid, dim3(kBlock), 0, s, L, col_blocks, row_groups);
+    return hipGetLastError();
+}
+
 template <int OUT, int MODE, bool CHW>
 hipError_t launch_rows_t(const YuvResizeLaunch& L, bool one_row, dim3 grid, hipStream_t s) {
     if (one_row) hipLaunchKernelGGL((yuv_resize_kernel<OUT, MODE, CHW, true>), grid, dim3(64, 4), 0, s, L);
@@ -307,6 +463,17 @@ hipError_t launch_rows_t(const YuvResizeLaunch& L, bool one_row, dim3 grid, hipS
 
 template <int OUT, int MODE>
 hipError_t launch_layout_t(const YuvResizeLaunch& L, bool one_row, dim3 grid, hipStream_t s) {
+    // the column kernel needs 16-byte aligned block rows (and plane and image
+    // pitches) in the destination; VACV_TUNE_RESIZE_DIRECT = 2 forces the
+    // row-major kernel (A/B)
+    constexpr int kES = OUT == kOutSame ? 1 : 4;
+    const int64_t rowb = 64 * kES * (L.chw ? 1 : 3);
+    const uintptr_t bits = reinterpret_cast<uintptr_t>(L.dst) | (uintptr_t)L.dst_row | (uintptr_t)L.dst_img |
+                           (uintptr_t)(L.chw ? L.dst_plane : 0);
+    const int64_t span = L.chw ? L.dst_plane * 3 : L.dst_img;
+    if (!(bits & 15) && rowb % 16 == 0 && tune(VACV_TUNE_RESIZE_DIRECT) != 2 && span < kMaxPlaneBytes &&
+        (int64_t)L.wo * L.ho < 0x7FFFFFF0LL / 4)
+        return L.chw ? launch_cols_t<OUT, MODE, true>(L, one_row, s) : launch_cols_t<OUT, MODE, false>(L, one_row, s);
     return L.chw ? launch_rows_t<OUT, MODE, true>(L, one_row, grid, s)
                  : launch_rows_t<OUT, MODE, false>(L, one_row, grid, s);
 }

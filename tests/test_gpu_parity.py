@@ -1463,6 +1463,19 @@ def test_cvt_color_resize_batch_and_pitch(ops, dev, oracle):
     ops.cvt_color_resize_normalize(yuv[:2], 224, 224, MEAN, STD, out=view)
     assert torch.equal(view, out[:2])
     assert bool((big[:, :, :3] == -7.0).all()) and bool((big[:, :, :, :5] == -7.0).all())
+    # the column-stationary kernel (yuv_cols_kernel, default where the
+    # destination's block rows are 16-byte aligned) and the row-major one
+    # (VACV_TUNE_RESIZE_DIRECT = 2) agree bit for bit: the bench workload
+    # (640x360 NCHW fp32), NHWC fp32 / u8, NCHW u8, a two-tap geometry
+    for wo, ho, layout, kw in ((640, 360, V.NCHW, {}), (640, 360, V.NHWC, {}), (1280, 720, V.NCHW, {}),
+                               (300, 200, V.NHWC, {})):
+        for fn in (lambda: ops.cvt_color_resize_normalize(yuv[:8], wo, ho, MEAN, STD, layout=layout),
+                   lambda: ops.cvt_color_resize(yuv[:8], wo, ho, layout=layout)):
+            a = fn()
+            with ops.tuning(RESIZE_DIRECT=2):
+                b = fn()
+            torch.cuda.synchronize(dev)
+            assert torch.equal(a, b), f"{wo}x{ho} layout {layout}: {(a != b).sum().item()} values differ"
     # the fused op equals the unfused GPU chain (cvt_color, resize_normalize, layout)
     bgr = ops.cvt_color(yuv[:4])
     chain = ops.change_layout(ops.resize_normalize(bgr, 224, 224, MEAN, STD), V.NCHW)
