@@ -24,6 +24,7 @@
 // non-temporal stores: one store instruction writes 1 KiB of contiguous output.
 #pragma clang fp contract(off)
 
+#include <cmath>
 #include <cstdlib>
 
 #include "vacv_device.hpp"
@@ -241,15 +242,22 @@ resize_direct_kernel(ResizeLaunch L, int blocks_per_plane, int total, int xcd) {
 #ifndef VACV_COLS_ROWS
 #define VACV_COLS_ROWS 8
 #endif
-constexpr int kColsRows = VACV_COLS_ROWS;  // output rows per wave task (a multiple of 8)
-template <int CC, int OUT, int MODE, bool ONE_ROW>
+constexpr int kColsRows = VACV_COLS_ROWS;  // output rows per wave task at 64 columns (a multiple of 8)
+// Column blocks of CW x 64 output columns (lane l keeps columns x0 + l,
+// x0 + 64 + l, ...) and kColsRows / CW rows, so a task's pixels stay 512.
+// CW = 2 at an exact 3x downscale of 3-channel u8: a block's source span is
+// 128 x 9 = 1,152 bytes = 9 whole 128-byte lines, so no line is split
+// between two blocks (64-column blocks split every other one: PMC read
+// 1.067 x the weighted rows) -- the host picks CW (cols_cw).
+template <int CC, int OUT, int MODE, bool ONE_ROW, int CW>
 __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8)))
 resize_cols_kernel(ResizeLaunch L, int col_blocks, int row_groups, int tasks, int xcd_groups) {
     constexpr int NR = ONE_ROW ? 1 : 2;           // gathered source rows per output row
+    constexpr int ROWS = kColsRows / CW;          // output rows per task
     using TOut = typename std::conditional<(OUT == kOutSame), uint8_t, float>::type;
     constexpr int kOutPx = CC * (int)sizeof(TOut);
-    constexpr int kHalf = 4;                       // rows per LDS exchange round
-    constexpr int kRowB = 64 * kOutPx;             // output bytes of one block row
+    constexpr int kHalf = 4 / CW;                  // rows per LDS exchange round
+    constexpr int kRowB = 64 * CW * kOutPx;        // output bytes of one block row
     constexpr int kLoadAux = OUT == kOutSame ? VACV_LOAD_AUX : VACV_DIRECT_LAUX;
     constexpr int kStoreAux = OUT == kOutSame ? VACV_STORE_AUX : VACV_DIRECT_SAUX;
     __shared__ __attribute__((aligned(16))) unsigned char xch[4][kHalf * kRowB];
@@ -269,52 +277,69 @@ resize_cols_kernel(ResizeLaunch L, int col_blocks, int row_groups, int tasks, in
     const int rg = rem / col_blocks, cb = rem - rg * col_blocks;
     const int img = pidx / L.src.planes, plane = pidx - img * L.src.planes;
     const int W = L.dst.w, H = L.dst.h;
-    const int x0 = cb * 64, y0 = rg * kColsRows;
-    const int ncol = min(64, W - x0);              // uniform
-    const int nrow = min(kColsRows, H - y0);       // uniform
-    const bool col_ok = lane < ncol;
-    const int x = col_ok ? x0 + lane : W - 1;
+    const int x0 = cb * 64 * CW, y0 = rg * ROWS;
+    const int ncol = min(64 * CW, W - x0);         // uniform
+    const int nrow = min(ROWS, H - y0);            // uniform
 
     const unsigned char* sp = L.src.base + (int64_t)img * L.src.img_pitch + (int64_t)plane * L.src.plane_pitch;
     const Rsrc srs = make_rsrc(sp, L.src.plane_bytes);
     const uint32_t slimit = (uint32_t)L.src.plane_bytes + srs.delta;
     const uint32_t rp = (uint32_t)L.src.row_pitch;
 
-    // the column's tap (once), the rows' taps (lanes 0..7, then broadcast)
-    const FixedTap tx = tap_of<MODE>(x, L.src.w, W, L.scale_xf, L.scale_xd);
-    const us2 wx = __builtin_bit_cast(us2, (uint32_t)tx.w0 | ((uint32_t)tx.w1 << 16));
-    const uint32_t xoff = (uint32_t)(tx.i * CC) + srs.delta;
-    uint32_t my_row = 0, my_w = 0;  // lane r < kColsRows: row r's first source row offset, weights (w0 | w1 << 16)
-    if (lane < kColsRows) {
+    // the columns' taps (once), the rows' taps (lanes 0..ROWS-1, then broadcast)
+    us2 wx[CW];
+    uint32_t xoff[CW];
+    // CW = 2: the block's last column loads its 8 bytes from 2 bytes earlier
+    // (its 6 tap bytes end where the block's source span does), so no gather
+    // reaches into the next block's first line
+    constexpr bool kTail = CW == 2 && CC == 3;
+    const uint32_t tsh = kTail && lane == 63 ? 2u : 0u;
+#pragma unroll
+    for (int c = 0; c < CW; ++c) {
+        const int xc = 64 * c + lane < ncol ? x0 + 64 * c + lane : W - 1;
+        const FixedTap tx = tap_of<MODE>(xc, L.src.w, W, L.scale_xf, L.scale_xd);
+        wx[c] = __builtin_bit_cast(us2, (uint32_t)tx.w0 | ((uint32_t)tx.w1 << 16));
+        xoff[c] = (uint32_t)(tx.i * CC) + srs.delta - (c == CW - 1 ? tsh : 0u);
+    }
+    uint32_t my_row = 0, my_w = 0;  // lane r < ROWS: row r's first source row offset, weights (w0 | w1 << 16)
+    if (lane < ROWS) {
         FixedTap ty = tap_of<MODE>(min(y0 + lane, H - 1), L.src.h, H, L.scale_yf, L.scale_yd);
         if (ONE_ROW && ty.w0 == 0) { ty.i += 1; ty.w0 = ty.w1; ty.w1 = 0; }  // the weighted row
         my_row = (uint32_t)ty.i * rp;
         my_w = (uint32_t)ty.w0 | ((uint32_t)ty.w1 << 16);
     }
-    uint32_t tap[kColsRows][NR][2];
+    uint32_t tap[ROWS][CW][NR][2];
     // uniform: can any gather of the task reach past the plane's last byte
     // (only tasks holding the plane's last source row)?  If not, the gathers
     // are issued without a per-lane range check (no exec-mask branch per load)
     const uint32_t last_ro = (uint32_t)__builtin_amdgcn_readlane((int)my_row, nrow - 1) + (uint32_t)(NR - 1) * rp;
-    const bool safe = __builtin_amdgcn_ballot_w64(last_ro + xoff + 8u > slimit) == 0;
+    const bool safe = __builtin_amdgcn_ballot_w64(last_ro + xoff[CW - 1] + 8u > slimit) == 0;
     auto gather = [&](auto safe_c) {
         constexpr bool SAFE = decltype(safe_c)::value;
 #pragma unroll
-        for (int r = 0; r < kColsRows; ++r) {
+        for (int r = 0; r < ROWS; ++r) {
             const uint32_t ro = (uint32_t)__builtin_amdgcn_readlane((int)my_row, r);
             const uint32_t wr = (uint32_t)__builtin_amdgcn_readlane((int)my_w, r);
 #pragma unroll
-            for (int n = 0; n < NR; ++n) {
-                const uint32_t o = ro + (uint32_t)n * rp + xoff;
-                tap[r][n][0] = tap[r][n][1] = 0u;
-                // a row of zero weight is not read (its product is 0 either way)
-                if (r < nrow && (n == 0 ? (ONE_ROW || (wr & 0xFFFFu)) : (wr >> 16))) {
-                    if (SAFE || o + 8u <= slimit) {
-                        load_taps<CC, false, kLoadAux>(srs, o, tap[r][n][0], tap[r][n][1]);
-                    } else {  // the plane's last pixels: bytewise (an overhanging load reads zeros)
-                        const unsigned char* b = sp + (int64_t)(o - srs.delta);
+            for (int c = 0; c < CW; ++c) {
 #pragma unroll
-                        for (int e = 0; e < 2 * CC; ++e) tap[r][n][e >> 2] |= (uint32_t)b[e] << (8 * (e & 3));
+                for (int n = 0; n < NR; ++n) {
+                    const uint32_t o = ro + (uint32_t)n * rp + xoff[c];
+                    tap[r][c][n][0] = tap[r][c][n][1] = 0u;
+                    // a row of zero weight is not read (its product is 0 either way)
+                    if (r < nrow && (n == 0 ? (ONE_ROW || (wr & 0xFFFFu)) : (wr >> 16))) {
+                        const uint32_t sh = c == CW - 1 ? tsh : 0u;
+                        if (SAFE || o + 8u <= slimit) {
+                            // (the shifted load's 2 leading bytes are skipped by the blend's selectors)
+                            load_taps<CC, false, kLoadAux>(srs, o, tap[r][c][n][0], tap[r][c][n][1]);
+                        } else {  // the plane's last pixels: bytewise (an overhanging load reads zeros)
+                            const unsigned char* b = sp + (int64_t)(o - srs.delta);
+                            // (positions sh .. sh + 2 CC - 1, as the shifted load has them)
+#pragma unroll
+                            for (int e = 0; e < 2 * CC + (kTail ? 2 : 0); ++e)
+                                if (e >= (int)sh && e < (int)sh + 2 * CC)
+                                    tap[r][c][n][e >> 2] |= (uint32_t)b[e] << (8 * (e & 3));
+                        }
                     }
                 }
             }
@@ -330,27 +355,33 @@ resize_cols_kernel(ResizeLaunch L, int col_blocks, int row_groups, int tasks, in
     unsigned char* dp = const_cast<unsigned char*>(L.dst.base) + (int64_t)img * L.dst.img_pitch +
                         (int64_t)plane * L.dst.plane_pitch;
     const Rsrc rd = make_rsrc(dp, L.dst.plane_bytes);
-    const bool full = ncol == 64;  // 16-byte chunks (the host checked the alignment)
+    const bool full = ncol == 64 * CW;  // 16-byte chunks (the host checked the alignment)
     TOut* xo = reinterpret_cast<TOut*>(xch[wave]);
     const unsigned char* xs = xch[wave];
 #pragma unroll
-    for (int g = 0; g < kColsRows / kHalf; ++g) {
+    for (int g = 0; g < ROWS / kHalf; ++g) {
 #pragma unroll
         for (int j = 0; j < kHalf; ++j) {
             const int r = g * kHalf + j;
             const uint32_t wr = (uint32_t)__builtin_amdgcn_readlane((int)my_w, r);
             const uint32_t wA = wr & 0xFFFFu, wB = ONE_ROW ? 0u : wr >> 16;
 #pragma unroll
-            for (int k = 0; k < CC; ++k) {
-                const uint32_t sel = (uint32_t)k | (0x0Cu << 8) | ((uint32_t)(CC + k) << 16) | (0x0Cu << 24);
-                const uint32_t top = __builtin_amdgcn_perm(tap[r][0][1], tap[r][0][0], sel);
-                const uint32_t bot = ONE_ROW ? 0u : __builtin_amdgcn_perm(tap[r][NR - 1][1], tap[r][NR - 1][0], sel);
-                const int v = blend_fixed<MODE>(top, bot, wx, wA, wB);
-                TOut ov;
-                if (OUT == kOutSame) ov = (TOut)v;
-                else if (OUT == kOutF32) ov = (TOut)(float)v;
-                else ov = (TOut)normalize_u8v(cn[k], v);
-                xo[(j * 64 + lane) * CC + k] = ov;
+            for (int c = 0; c < CW; ++c) {
+#pragma unroll
+                for (int k = 0; k < CC; ++k) {
+                    // the block's last column (kTail, lane 63) finds its bytes 2 later
+                    const uint32_t sel = ((uint32_t)k | (0x0Cu << 8) | ((uint32_t)(CC + k) << 16) | (0x0Cu << 24)) +
+                                         (kTail && c == CW - 1 ? tsh * 0x00010001u : 0u);
+                    const uint32_t top = __builtin_amdgcn_perm(tap[r][c][0][1], tap[r][c][0][0], sel);
+                    const uint32_t bot =
+                        ONE_ROW ? 0u : __builtin_amdgcn_perm(tap[r][c][NR - 1][1], tap[r][c][NR - 1][0], sel);
+                    const int v = blend_fixed<MODE>(top, bot, wx[c], wA, wB);
+                    TOut ov;
+                    if (OUT == kOutSame) ov = (TOut)v;
+                    else if (OUT == kOutF32) ov = (TOut)(float)v;
+                    else ov = (TOut)normalize_u8v(cn[k], v);
+                    xo[(j * 64 * CW + 64 * c + lane) * CC + k] = ov;
+                }
             }
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -384,15 +415,32 @@ resize_cols_kernel(ResizeLaunch L, int col_blocks, int row_groups, int tasks, in
     }
 }
 
+// CW for a geometry: 2 where a 128-column block's source span is whole
+// 128-byte lines and 64-column blocks' spans are not (the column step times
+// 64 x CC is an odd number of 64-byte halves: e.g. 3x of 3 channels, 576 B),
+// the output has whole 128-column blocks and the source rows are line-aligned
+// (VACV_TUNE_RESIZE_TILE_W = 64 / 128 forces 1 / 2).
+int cols_cw(const ResizeLaunch& L) {
+    const int knob = tune(VACV_TUNE_RESIZE_TILE_W);
+    if (knob == 64) return 1;
+    if (knob == 128) return 2;
+    const double step = (double)L.src.w / L.dst.w;  // source columns per output column
+    if (step != std::floor(step) || L.dst.w % 128) return 1;
+    const int64_t span64 = (int64_t)step * 64 * L.src.cc * L.src.esize;
+    const bool lines = L.src.row_pitch % 128 == 0 && (reinterpret_cast<uintptr_t>(L.src.base) & 127) == 0 &&
+                       L.src.img_pitch % 128 == 0 && L.src.plane_pitch % 128 == 0;
+    return lines && span64 % 128 != 0 && (2 * span64) % 128 == 0 ? 2 : 1;
+}
+
 // The column kernel's grid, or false where it does not apply (it needs
 // 16-byte aligned block rows in the destination).
-bool cols_plan(const ResizeLaunch& L, int out_px, int& col_blocks, int& row_groups, int64_t& tasks) {
+bool cols_plan(const ResizeLaunch& L, int out_px, int cw, int& col_blocks, int& row_groups, int64_t& tasks) {
     if (!VACV_DIRECT_COLS) return false;
     const uintptr_t dbits = reinterpret_cast<uintptr_t>(L.dst.base) | (uintptr_t)L.dst.row_pitch |
                             (uintptr_t)L.dst.img_pitch | (uintptr_t)L.dst.plane_pitch;
     if ((dbits & 15) || (64 * out_px) % 16) return false;
-    col_blocks = (L.dst.w + 63) / 64;
-    row_groups = (L.dst.h + kColsRows - 1) / kColsRows;
+    col_blocks = (L.dst.w + 64 * cw - 1) / (64 * cw);
+    row_groups = (L.dst.h + kColsRows / cw - 1) / (kColsRows / cw);
     tasks = (int64_t)col_blocks * row_groups * L.n * L.src.planes;
     return tasks < 0x7FFFFFF0LL;
 }
@@ -403,12 +451,17 @@ hipError_t launch_one(const ResizeLaunch& L, hipStream_t s) {
         constexpr int kOutPx = CC * (OUT == kOutSame ? 1 : 4);
         int col_blocks = 0, row_groups = 0;
         int64_t tasks = 0;
-        if (cols_plan(L, kOutPx, col_blocks, row_groups, tasks)) {
+        const int cw = cols_cw(L);
+        if (cols_plan(L, kOutPx, cw, col_blocks, row_groups, tasks)) {
             const int64_t groups = (tasks + 3) / 4;
             const int xcd = tune_or(VACV_TUNE_DIRECT_XCD, 0) ? (int)((groups + 7) / 8) : 0;
             const int64_t grid = xcd ? (int64_t)xcd * 8 : groups;
-            hipLaunchKernelGGL((resize_cols_kernel<CC, OUT, MODE, ONE_ROW>), dim3((unsigned)grid), dim3(kBlock), 0, s, L,
-                               col_blocks, row_groups, (int)tasks, xcd);
+            if (cw == 2)
+                hipLaunchKernelGGL((resize_cols_kernel<CC, OUT, MODE, ONE_ROW, 2>), dim3((unsigned)grid), dim3(kBlock), 0,
+                                   s, L, col_blocks, row_groups, (int)tasks, xcd);
+            else
+                hipLaunchKernelGGL((resize_cols_kernel<CC, OUT, MODE, ONE_ROW, 1>), dim3((unsigned)grid), dim3(kBlock), 0,
+                                   s, L, col_blocks, row_groups, (int)tasks, xcd);
             return hipGetLastError();
         }
     }

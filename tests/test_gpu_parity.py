@@ -778,6 +778,13 @@ def test_resize_normalize_bench_batch(ops, dev, oracle):
     for k in (3, 200):
         single = ops.resize_normalize(src[k:k + 1], 640, 360, MEAN, STD)
         assert torch.equal(single[0], out[k]), f"batch invariance {k}"
+    # 64-column wave blocks (VACV_TUNE_RESIZE_TILE_W = 64) against the default
+    # 128-column blocks of this geometry: the whole batch, bit for bit
+    with ops.tuning(RESIZE_TILE_W=64):
+        out64 = ops.resize_normalize(src, 640, 360, MEAN, STD)
+    torch.cuda.synchronize(dev)
+    assert torch.equal(out64.view(torch.int32), out.view(torch.int32)), "64- vs 128-column blocks"
+    del out64
     # u8 resize of the same batch: per-image checksums of a stripe vs the oracle
     r8 = ops.resize(src, 640, 360)
     for k in range(16, 24):
