@@ -100,13 +100,13 @@ __device__ __forceinline__ s16x2 clamp_u8x2(s16x2 v) {
 // lane is exact.  Out: B, G, R as u16 pairs {left, right} -- the layout the
 // blend's v_dot2_u32_u16 takes.
 __device__ __forceinline__ void decode_row(const RowTaps& t, uint32_t cs, int v_first, uint32_t& bp, uint32_t& gp,
-                                           uint32_t& rp) {
+                                           uint32_t& rp, uint32_t ysel = 0x0C010C00u) {
     // v_perm selectors: byte (a + vi) -> lane 0, byte (b + vi) -> lane 1, 0x0C = 0
     const uint32_t base = (cs & 3u) | ((cs >> 2) << 16) | 0x0C000C00u;
     const uint32_t vo = v_first ? 0u : 0x00010001u;  // NV21: V first in a pair
     const s16x2 V = __builtin_bit_cast(s16x2, __builtin_amdgcn_perm(0u, t.c, base + vo));
     const s16x2 U = __builtin_bit_cast(s16x2, __builtin_amdgcn_perm(0u, t.c, base + (0x00010001u - vo)));
-    const s16x2 Y = __builtin_bit_cast(s16x2, __builtin_amdgcn_perm(0u, t.y, 0x0C010C00u));
+    const s16x2 Y = __builtin_bit_cast(s16x2, __builtin_amdgcn_perm(0u, t.y, ysel));  // Y bytes -> u16 lanes
     const s16x2 vm = V - (short)128, um = U - (short)128;
     const s16x2 ra = (vm * (short)179) >> (short)7;
     const s16x2 ga = (um * (short)44 + vm * (short)91) >> (short)7;
@@ -338,12 +338,22 @@ yuv_cols_kernel(YuvResizeLaunch L, int col_blocks, int row_groups) {
     const uint32_t rp = (uint32_t)L.src_row;
     const uint32_t uvbase = (uint32_t)L.h * rp;
 
-    // the column's tap and chroma selector (once)
+    // the column's tap and chroma selector (once).  The block's last lane
+    // reads its Y dword (and, at an even tap, its chroma dword) from 2 bytes
+    // earlier, its bytes picked by the selectors: so no gather reaches into
+    // the next block's first 128-byte line, which neighbouring workgroups --
+    // on other XCDs -- would otherwise both fetch from HBM (PMC: reads 413 ->
+    // 372 MB at 256 x NV21 1080p -> 640x360, B_alg 354 MB).
     const FixedTap tx = tap_of<MODE>(x, L.w, W, L.scale_xf, L.scale_xd);
     const us2 wx = __builtin_bit_cast(us2, (uint32_t)tx.w0 | ((uint32_t)tx.w1 << 16));
-    const uint32_t cs = chroma_sel(L.w, tx.i);
-    const uint32_t ycol = (uint32_t)tx.i;
-    const uint32_t ccol = (uint32_t)min(tx.i & ~1, L.w - 4);
+    const bool edge = lane == 63 && tx.i >= 2;
+    const int ca = tx.i & ~1, c0 = min(ca, L.w - 4);
+    const int c1 = edge && (tx.i & 1) == 0 && c0 == ca ? c0 - 2 : c0;
+    const uint32_t ca_rel = (uint32_t)(ca - c1);
+    const uint32_t cs = ca_rel | ((ca_rel + 2u * (uint32_t)(tx.i & 1)) << 2);
+    const uint32_t ycol = (uint32_t)(edge ? tx.i - 2 : tx.i);
+    const uint32_t ysel = edge ? 0x0C030C02u : 0x0C010C00u;
+    const uint32_t ccol = (uint32_t)c1;
     // lane r < kYuvRows: row r's tap -- source Y / chroma row offsets (rows i
     // and i + 1) and weights wA | wB << 16
     uint32_t my_y0 = 0, my_c0 = 0, my_y1 = 0, my_c1 = 0, my_w = 0;
@@ -391,8 +401,8 @@ yuv_cols_kernel(YuvResizeLaunch L, int col_blocks, int row_groups) {
             const int r = g * kYuvHalf + j;
             const uint32_t wr = (uint32_t)__builtin_amdgcn_readlane((int)my_w, r);
             uint32_t pa[3], pb[3] = {0u, 0u, 0u};  // rows A/B: B, G, R as u16 pairs {left, right}
-            decode_row(t[r][0], cs, L.v_first, pa[0], pa[1], pa[2]);
-            if (!ONE_ROW) decode_row(t[r][NR - 1], cs, L.v_first, pb[0], pb[1], pb[2]);
+            decode_row(t[r][0], cs, L.v_first, pa[0], pa[1], pa[2], ysel);
+            if (!ONE_ROW) decode_row(t[r][NR - 1], cs, L.v_first, pb[0], pb[1], pb[2], ysel);
             if (L.rgb) {  // output order R, G, B
                 const uint32_t q0 = pa[0], q1 = pb[0];
                 pa[0] = pa[2]; pa[2] = q0;

@@ -272,7 +272,7 @@ def make_workload(name: str, batch: int, dev, rank: int, world: int, ops) -> dic
         src = u8(B, 720, 1280, 3)
         dst = torch.empty_like(src)
         m = ops.rotation_matrix(0.9, 15.0, (640, 360, 640, 360))
-        return {"batch": B, "px": 1280 * 720, "b_alg": B * 2 * 1280 * 720 * 3, "kernel": "warp_ring_kernel",
+        return {"batch": B, "px": 1280 * 720, "b_alg": B * 2 * 1280 * 720 * 3, "kernel": "warp_exp_kernel",
                 "frame": "1280x720x3", "output": "1280x720x3 u8",
                 "desc": "warp_affine INTER_LINEAR BORDER_CONSTANT 1280x720x3 u8, scale 0.9 rot 15 aux (640,360,640,360)",
                 "main": lambda stream=None: ops.warp_affine(src, m, 1280, 720, out=dst, stream=stream)}
@@ -289,7 +289,7 @@ def make_workload(name: str, batch: int, dev, rank: int, world: int, ops) -> dic
         yuv = u8(B, 1620, 1920)
         dst = torch.empty((B, 3, 360, 640), dtype=torch.float32, device=dev)
         return {"batch": B, "px": 1920 * 1080, "b_alg": B * yuv_resize_bytes(1920, 1080, 640, 360),
-                "kernel": "yuv_resize_kernel", "frame": "NV21 1920x1620", "output": "3x360x640 fp32 (NCHW)",
+                "kernel": "yuv_cols_kernel", "frame": "NV21 1920x1620", "output": "3x360x640 fp32 (NCHW)",
                 "desc": "cvt_color NV21 -> resize INTER_LINEAR 640x360 -> normalize -> NCHW, one kernel",
                 "main": lambda stream=None: ops.cvt_color_resize_normalize(yuv, 640, 360, MEAN, STD, out=dst,
                                                                            stream=stream)}
