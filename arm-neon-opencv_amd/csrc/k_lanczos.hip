@@ -57,6 +57,8 @@ struct LanczosTabsDev {
     const short* yai;    // [dst.h][8]
     const int* yrot;     // [dst.h][4] u8: the 8 coefficients per ring SLOT (row mod 8) as short pairs
     const float* yaf;    // [dst.h][8]
+    const int* yrec;     // [dst.h][16] u8, lanczos_u8_kernel: [0, 8) the coefficients by slot (row - rs) & 7, rs
+                         // the first source row of the row's band; [8] its last tap row
     int xmin, xmax;      // output columns [xmin, xmax) take the unrolled horizontal sum
 };
 
@@ -137,8 +139,13 @@ constexpr int kLzWaves = VACV_LZ_WAVES;  // waves (strip tasks) per workgroup; e
 #ifndef VACV_LZ_SLOTS
 #define VACV_LZ_SLOTS 1
 #endif
+// diagnosis builds (0 in the product): 1 no horizontal arithmetic, 2 no
+// window loads, 4 the dropped stores from one lane, 8 no output stores
+#ifndef VACV_LZ_DBG
+#define VACV_LZ_DBG 0
+#endif
 template <typename TIn, int OUT, int CC>
-__global__ void __launch_bounds__(64 * kLzWaves) lanczos_kernel(LanczosLaunch L, int strips, int bands, int band_rows) {
+__global__ void __launch_bounds__(64 * kLzWaves) lanczos_kernel(LanczosLaunch L, int strips, int bands, int band_rows, int blocks, int xcd_per) {
     constexpr bool U8 = std::is_same<TIn, uint8_t>::value;
     using TW = typename std::conditional<U8, int, float>::type;
     using TOut = typename std::conditional<(OUT == kOutSame), TIn, float>::type;
@@ -156,7 +163,13 @@ __global__ void __launch_bounds__(64 * kLzWaves) lanczos_kernel(LanczosLaunch L,
     // wave-uniform, and said so: the plane's buffer resource stays in SGPRs
     // (derived from a per-lane value it would be waterfalled at every load)
     const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)), lane = (int)(threadIdx.x & 63);
-    const int task = (int)blockIdx.x * kLzWaves + wave;  // (plane, band, strip), strip fastest
+    // xcd_per > 0: XCD-contiguous order -- workgroup b runs on XCD b % 8, and
+    // each XCD takes a run of xcd_per consecutive workgroups, so the strips
+    // that share the 128-byte lines at their windows' edges (a window reaches
+    // 7 pixels past the strip) are fetched into one L2, not two
+    const int blk = xcd_per > 0 ? (int)(blockIdx.x % 8) * xcd_per + (int)(blockIdx.x / 8) : (int)blockIdx.x;
+    if (blk >= blocks) return;  // whole workgroup: the grid's round-up to 8
+    const int task = blk * kLzWaves + wave;  // (plane, band, strip), strip fastest
     const int strip = task % strips;
     const int rest = task / strips;
     const int band = rest % bands;
@@ -202,6 +215,11 @@ __global__ void __launch_bounds__(64 * kLzWaves) lanczos_kernel(LanczosLaunch L,
     auto load = [&](auto safe_c, uint32_t (&d)[ND], int r) {
         constexpr bool SAFE = decltype(safe_c)::value;
         const uint32_t a = (uint32_t)r * rp + (wbyte & ~3u);
+        if constexpr ((VACV_LZ_DBG & 2) != 0) {
+#pragma unroll
+            for (int q = 0; q < ND; ++q) d[q] = a + 977u * q;
+            return;
+        }
         if (!SAFE || a + 4u * ND <= slimit) {
             int q = 0;
 #pragma unroll
@@ -237,7 +255,10 @@ __global__ void __launch_bounds__(64 * kLzWaves) lanczos_kernel(LanczosLaunch L,
             uint32_t wv[ND - 1];
 #pragma unroll
             for (int q = 0; q < ND - 1; ++q) wv[q] = __builtin_amdgcn_alignbyte(d[q + 1], d[q], wsh);
-            if (interior) lz_h_u8<CC, 0, ND - 1>(wv, cp, hv);
+            if constexpr ((VACV_LZ_DBG & 1) != 0) {
+#pragma unroll
+                for (int k = 0; k < CC; ++k) hv[k] = (int)(wv[k % (ND - 1)] ^ wv[(k + 1) % (ND - 1)]);
+            } else if (interior) lz_h_u8<CC, 0, ND - 1>(wv, cp, hv);
             else switch (shift) {  // divergent: the strips at the image's edges
                 case -4: lz_h_u8<CC, -4, ND - 1>(wv, cp, hv); break;
                 case -3: lz_h_u8<CC, -3, ND - 1>(wv, cp, hv); break;
@@ -368,7 +389,8 @@ __global__ void __launch_bounds__(64 * kLzWaves) lanczos_kernel(LanczosLaunch L,
                 o[q] = (TOut)v;
             }
         }
-        const uint32_t orow = (uint32_t)y * (uint32_t)L.dst.row_pitch + drs.delta;
+        uint32_t orow = (uint32_t)y * (uint32_t)L.dst.row_pitch + drs.delta;
+        if constexpr ((VACV_LZ_DBG & 8) != 0) orow = kOobStore;
         if constexpr (sizeof(TOut) == 1) {
             // u8: the quad's 4 CC bytes as CC dword stores (quad_pack) where the
             // quad is whole and the destination dword-aligned, else bytes
@@ -459,7 +481,7 @@ __global__ void __launch_bounds__(64 * kLzWaves) lanczos_kernel(LanczosLaunch L,
                         ++y;
                         if (y < y1) need = min(lz_const(L.t.yofs, y) + 4, h - 1);
                     } while (y < y1 && need == rr);
-                } else {
+                } else if ((VACV_LZ_DBG & 4) == 0 || lane == 0) {
                     __builtin_amdgcn_raw_buffer_store_b32(0u, drs.r, (int)kOobStore, 0, 0);
                 }
                 load(safe_c, buf[u], min(rr + D, re));
@@ -467,6 +489,233 @@ __global__ void __launch_bounds__(64 * kLzWaves) lanczos_kernel(LanczosLaunch L,
         }
     };
     // uniform: can any lane's window of the band's last row overhang the plane?
+    const bool over = (uint32_t)re * rp + (wbyte & ~3u) + 4u * ND > slimit;
+    if (__builtin_amdgcn_ballot_w64(over) != 0) walk(std::integral_constant<bool, true>());
+    else walk(std::integral_constant<bool, false>());
+}
+
+// u8 sources: lanczos_u8_kernel.  The same strip walk as lanczos_kernel, but
+// the 8 most recent horizontal rows live in REGISTERS, not an LDS ring: the
+// walk is unrolled by 8 source rows, so row rr's values land in register row
+// (rr - rs) & 7 -- a compile-time index (rs = the band's first source row).
+// The host regroups each output row's 8 vertical coefficients by that
+// relative slot (yrec), so an output row is 8 multiply-adds per channel on
+// registers: no ring stores and reads, no LDS waits.  Diagnosis builds of the
+// LDS-ring kernel (VACV_LZ_DBG) ran 0.41 ms without any window load against
+// 0.49 with them: the per-row instruction stream around the loads, not the
+// loads, bounded it.  Also: the border clamp is folded into each lane's
+// coefficients once (window pixel p weighs the sum of the taps that clamp to
+// it -- exact, the u8 sums are int arithmetic), so every lane runs the same
+// unrolled horizontal sum and the per-row 9-way shift switch is gone.
+#ifndef VACV_LZR_D
+#define VACV_LZR_D 4  // windows in flight per wave (a divisor of 8, the unroll)
+#endif
+template <int OUT, int CC>
+__global__ void __launch_bounds__(64 * kLzWaves) lanczos_u8_kernel(LanczosLaunch L, int strips, int bands, int band_rows,
+                                                                     int blocks, int xcd_per) {
+    using TOut = typename std::conditional<(OUT == kOutSame), uint8_t, float>::type;
+    constexpr int ND = (8 * CC + 6) / 4;
+    constexpr int D = VACV_LZR_D;
+    static_assert(8 % D == 0, "the window buffers rotate with the 8-row unroll");
+
+    const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)), lane = (int)(threadIdx.x & 63);
+    const int blk = xcd_per > 0 ? (int)(blockIdx.x % 8) * xcd_per + (int)(blockIdx.x / 8) : (int)blockIdx.x;
+    if (blk >= blocks) return;
+    const int task = blk * kLzWaves + wave;  // (plane, band, strip), strip fastest
+    const int strip = task % strips;
+    const int rest = task / strips;
+    const int band = rest % bands;
+    const int pidx = rest / bands;
+    if (pidx >= L.n * L.src.planes) return;  // whole wave
+    const int y0 = band * band_rows, y1 = min(y0 + band_rows, L.dst.h);
+    const int x = strip * 64 + lane;
+    const bool live = x < L.dst.w;
+    const int xc = live ? x : L.dst.w - 1;
+    const int img = pidx / L.src.planes;
+    const int plane = pidx - img * L.src.planes;
+    const int w = L.src.w, h = L.src.h;
+    const unsigned char* sp = L.src.base + (int64_t)img * L.src.img_pitch + (int64_t)plane * L.src.plane_pitch;
+    const Rsrc srs = make_rsrc(sp, L.src.plane_bytes);
+    const uint32_t slimit = (uint32_t)L.src.plane_bytes + srs.delta;
+    const uint32_t rp = (uint32_t)L.src.row_pitch;
+
+    const int sx = L.t.xofs[xc];
+    const int wstart = min(max(sx - 3, 0), w - 8);
+    const int shift = (sx - 3) - wstart;  // [-4, 4]
+    int cw[8];
+#pragma unroll
+    for (int p = 0; p < 8; ++p) cw[p] = 0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const int c = (int)L.t.xai[8 * xc + j];
+#pragma unroll
+        for (int p = 0; p < 8; ++p) cw[p] += min(max(j + shift, 0), 7) == p ? c : 0;
+    }
+    uint32_t cp[4];  // (cw[2m], cw[2m + 1]) short pairs; a folded sum stays within +-2^15
+#pragma unroll
+    for (int m = 0; m < 4; ++m) cp[m] = ((uint32_t)cw[2 * m] & 0xFFFFu) | ((uint32_t)cw[2 * m + 1] << 16);
+    const uint32_t wbyte = (uint32_t)(wstart * CC) + srs.delta;
+    const uint32_t wsh = wbyte & 3u;
+
+    auto load = [&](auto safe_c, uint32_t (&d)[ND], int r) {
+        constexpr bool SAFE = decltype(safe_c)::value;
+        const uint32_t a = (uint32_t)r * rp + (wbyte & ~3u);
+        if (!SAFE || a + 4u * ND <= slimit) {
+            int q = 0;
+#pragma unroll
+            for (; q + 4 <= ND; q += 4) {
+                const auto v = __builtin_amdgcn_raw_buffer_load_b128(srs.r, (int)(a + 4 * q), 0, 0);
+                d[q] = v[0]; d[q + 1] = v[1]; d[q + 2] = v[2]; d[q + 3] = v[3];
+            }
+            if constexpr (ND % 4 == 3) {
+                const auto v = __builtin_amdgcn_raw_buffer_load_b96(srs.r, (int)(a + 4 * q), 0, 0);
+                d[q] = v[0]; d[q + 1] = v[1]; d[q + 2] = v[2];
+            } else if constexpr (ND % 4 == 2) {
+                const auto v = __builtin_amdgcn_raw_buffer_load_b64(srs.r, (int)(a + 4 * q), 0, 0);
+                d[q] = v[0]; d[q + 1] = v[1];
+            } else if constexpr (ND % 4 == 1) {
+                d[q] = __builtin_amdgcn_raw_buffer_load_b32(srs.r, (int)(a + 4 * q), 0, 0);
+            }
+        } else {  // the window overhangs the plane's end: bytewise
+#pragma unroll
+            for (int q = 0; q < ND; ++q) {
+                uint32_t v = 0;
+#pragma unroll
+                for (int e = 0; e < 4; ++e)
+                    if (a + 4u * q + e < slimit)
+                        v |= (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(srs.r, (int)(a + 4u * q + e), 0, 0) << (8 * e);
+                d[q] = v;
+            }
+        }
+    };
+    auto hrow = [&](const uint32_t (&d)[ND], int (&hv)[CC]) {
+        uint32_t wv[ND - 1];
+#pragma unroll
+        for (int q = 0; q < ND - 1; ++q) wv[q] = __builtin_amdgcn_alignbyte(d[q + 1], d[q], wsh);
+        lz_h_u8<CC, 0, ND - 1>(wv, cp, hv);
+    };
+
+    unsigned char* dp = const_cast<unsigned char*>(L.dst.base) + (int64_t)img * L.dst.img_pitch +
+                        (int64_t)plane * L.dst.plane_pitch;
+    const Rsrc drs = make_rsrc(dp, L.dst.plane_bytes);
+    const bool dst_al = ((reinterpret_cast<uintptr_t>(dp) | (uintptr_t)L.dst.row_pitch) & 3) == 0;
+    const bool full = strip * 64 + 64 <= L.dst.w;
+    ChanNorm cn[CC] = {};
+    if (OUT == kOutNorm) {
+#pragma unroll
+        for (int k = 0; k < CC; ++k) cn[k] = chan_norm(L.norm, img, CC == 1 ? plane % L.norm.c_total : k);
+    }
+    constexpr uint32_t kOobStore = 0x80000000u;  // a store offset past every plane: dropped
+
+    // VResizeLanczos4 of output row y from the register rows; bb = its
+    // coefficients by relative slot (wave-uniform)
+    auto emit = [&](int y, const int (&hs)[8][CC], const int (&bb)[8]) {
+        TOut o[CC];
+#pragma unroll
+        for (int q = 0; q < CC; ++q) {
+            // 24-bit multiplies: |h| < 2^23, |b| < 2^12 (as lanczos_kernel)
+            const int s0 = __mul24(hs[0][q], bb[0]) + __mul24(hs[1][q], bb[1]) + __mul24(hs[2][q], bb[2]) +
+                           __mul24(hs[3][q], bb[3]);
+            const int s1 = __mul24(hs[4][q], bb[4]) + __mul24(hs[5][q], bb[5]) + __mul24(hs[6][q], bb[6]) +
+                           __mul24(hs[7][q], bb[7]);
+            const int vi = min(max((s0 + s1 + (1 << 21)) >> 22, 0), 255);  // FixedPtCast<int, uchar, 22>
+            if (OUT == kOutSame) o[q] = (TOut)vi;
+            else if (OUT == kOutF32) o[q] = (TOut)(float)vi;
+            else o[q] = (TOut)normalize_u8v(cn[q], vi);
+        }
+        const uint32_t orow = (uint32_t)y * (uint32_t)L.dst.row_pitch + drs.delta;
+        if constexpr (sizeof(TOut) == 1) {
+            uint32_t own = 0;
+#pragma unroll
+            for (int q = 0; q < CC; ++q) own |= (uint32_t)(uint8_t)o[q] << (8 * q);
+            const int xq = x & ~3;
+            const bool quad = dst_al && (full || xq + 4 <= L.dst.w);
+            const uint32_t word = quad_pack<CC>(own, lane & 3);
+            if (quad) {
+                if ((lane & 3) < CC)
+                    __builtin_amdgcn_raw_buffer_store_b32(word, drs.r, (int)(orow + (uint32_t)(xq * CC + 4 * (lane & 3))),
+                                                          0, 0);
+            } else if (live) {
+#pragma unroll
+                for (int q = 0; q < CC; ++q)
+                    __builtin_amdgcn_raw_buffer_store_b8((unsigned char)(own >> (8 * q)), drs.r,
+                                                         (int)(orow + (uint32_t)(x * CC + q)), 0, 0);
+            }
+        } else if (live) {
+            const uint32_t off = orow + (uint32_t)(x * CC) * 4u;
+            uint32_t ov[CC];
+#pragma unroll
+            for (int q = 0; q < CC; ++q) ov[q] = __float_as_uint(o[q]);
+            if (dst_al) {
+                if constexpr (CC == 1) {
+                    __builtin_amdgcn_raw_buffer_store_b32(ov[0], drs.r, (int)off, 0, 0);
+                } else if constexpr (CC == 2) {
+                    typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+                    __builtin_amdgcn_raw_buffer_store_b64(u32x2{ov[0], ov[1]}, drs.r, (int)off, 0, 0);
+                } else if constexpr (CC == 3) {
+                    typedef unsigned int u32x3 __attribute__((ext_vector_type(3)));
+                    __builtin_amdgcn_raw_buffer_store_b96(u32x3{ov[0], ov[1], ov[2]}, drs.r, (int)off, 0, 0);
+                } else {
+                    __builtin_amdgcn_raw_buffer_store_b128(u32x4{ov[0], ov[1], ov[2], ov[3]}, drs.r, (int)off, 0, 0);
+                }
+            } else {
+                TOut* dq = reinterpret_cast<TOut*>(dp + (off - drs.delta));
+#pragma unroll
+                for (int q = 0; q < CC; ++q) dq[q] = o[q];
+            }
+        }
+    };
+
+    // The walk: every step resizes one source row into its register row,
+    // emits the output rows whose last tap row it is, and issues the window
+    // load D rows ahead; a step that emits nothing issues a dropped store, so
+    // every step holds at least one store and the compiler's wait for a
+    // window leaves the later stores in flight (lanczos_kernel's walk).  The
+    // next output row's record (coefficients, last tap row) is fetched when
+    // the previous one is emitted, a step or more before it is read.
+    const int rs = max(lz_const(L.t.yofs, y0) - 3, 0);
+    const int re = min(lz_const(L.t.yofs, y1 - 1) + 4, h - 1);
+    auto walk = [&](auto safe_c) {
+        int hs[8][CC];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+#pragma unroll
+            for (int q = 0; q < CC; ++q) hs[j][q] = 0;
+        }
+        int y = __builtin_amdgcn_readfirstlane(y0);
+        int bb[8], need;
+        auto fetch = [&](int yy) {
+#pragma unroll
+            for (int k = 0; k < 8; ++k) bb[k] = lz_const(L.t.yrec, 16 * yy + k);
+            need = lz_const(L.t.yrec, 16 * yy + 8);
+        };
+        fetch(y);
+        uint32_t buf[D][ND];
+#pragma unroll
+        for (int u = 0; u < D; ++u) load(safe_c, buf[u], min(rs + u, re));
+#pragma unroll
+        for (int u = 0; u + 1 < D; ++u) __builtin_amdgcn_raw_buffer_store_b32(0u, drs.r, (int)kOobStore, 0, 0);
+        for (int r = rs;; r += 8) {
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const int rr = r + u;
+                hrow(buf[u % D], hs[u]);
+                if (need == rr) {  // uniform; y < y1 while the walk runs
+                    do {
+                        y = __builtin_amdgcn_readfirstlane(y);
+                        emit(y, hs, bb);
+                        ++y;
+                        if (y >= y1) break;
+                        fetch(y);
+                    } while (need == rr);
+                } else {
+                    __builtin_amdgcn_raw_buffer_store_b32(0u, drs.r, (int)kOobStore, 0, 0);
+                }
+                if (y >= y1) return;  // the band's last output row is out
+                load(safe_c, buf[u % D], min(rr + D, re));
+            }
+        }
+    };
     const bool over = (uint32_t)re * rp + (wbyte & ~3u) + 4u * ND > slimit;
     if (__builtin_amdgcn_ballot_w64(over) != 0) walk(std::integral_constant<bool, true>());
     else walk(std::integral_constant<bool, false>());
@@ -593,13 +842,13 @@ struct CachedLanczos {
     LanczosTabsDev t{};
 };
 std::mutex g_lz_mu;
-std::map<std::tuple<int, int, int, int, int, double, double>, CachedLanczos> g_lz_tabs;
+std::map<std::tuple<int, int, int, int, int, double, double, int>, CachedLanczos> g_lz_tabs;
 bool free_lz(CachedLanczos& c) { return hipFree(c.dev) == hipSuccess; }
 
-int lanczos_tables(const ResizeLaunch& R, double inv_x, double inv_y, hipStream_t s, LanczosTabsDev& out) {
+int lanczos_tables(const ResizeLaunch& R, double inv_x, double inv_y, int band_rows, hipStream_t s, LanczosTabsDev& out) {
     int device = 0;
     if (hipGetDevice(&device) != hipSuccess) return VACV_ERR_HIP;
-    const auto key = std::make_tuple(device, R.src.w, R.src.h, R.dst.w, R.dst.h, inv_x, inv_y);
+    const auto key = std::make_tuple(device, R.src.w, R.src.h, R.dst.w, R.dst.h, inv_x, inv_y, band_rows);
     std::lock_guard<std::mutex> lk(g_lz_mu);
     auto it = g_lz_tabs.find(key);
     if (it == g_lz_tabs.end()) {
@@ -626,10 +875,22 @@ int lanczos_tables(const ResizeLaunch& R, double inv_x, double inv_y, hipStream_
             for (int m = 0; m < 4; ++m)
                 yr[4 * (size_t)y + m] = (int)(((uint32_t)b[2 * m] & 0xFFFFu) | ((uint32_t)b[2 * m + 1] << 16));
         }
+        // lanczos_u8_kernel: the same regrouping by slot relative to the band's
+        // first source row (the kernel's rs), and the row's last tap row
+        std::vector<int> yc(16 * (size_t)R.dst.h, 0);
+        for (int y = 0; y < R.dst.h; ++y) {
+            const int y0 = band_rows > 0 ? y / band_rows * band_rows : 0;
+            const int rs = std::max(yo[y0] - 3, 0);
+            for (int k = 0; k < 8; ++k) {
+                const int row = std::min(std::max(yo[y] - 3 + k, 0), R.src.h - 1);
+                yc[16 * (size_t)y + ((row - rs) & 7)] += yi[8 * (size_t)y + k];
+            }
+            yc[16 * (size_t)y + 8] = std::min(yo[y] + 4, R.src.h - 1);
+        }
         const size_t o0 = put(xo.data(), xo.size() * 4), o1 = put(xi.data(), xi.size() * 2),
                      o2 = put(xf.data(), xf.size() * 4), o3 = put(yo.data(), yo.size() * 4),
                      o4 = put(yi.data(), yi.size() * 2), o5 = put(yf.data(), yf.size() * 4),
-                     o6 = put(yr.data(), yr.size() * 4);
+                     o6 = put(yr.data(), yr.size() * 4), o7 = put(yc.data(), yc.size() * 4);
         if (g_lz_tabs.size() > 64)  // bounded cache
             (void)evict_device_cache(g_lz_tabs, free_lz);
         CachedLanczos c;
@@ -649,6 +910,7 @@ int lanczos_tables(const ResizeLaunch& R, double inv_x, double inv_y, hipStream_
         c.t.yai = reinterpret_cast<const short*>(b + o4);
         c.t.yaf = reinterpret_cast<const float*>(b + o5);
         c.t.yrot = reinterpret_cast<const int*>(b + o6);
+        c.t.yrec = reinterpret_cast<const int*>(b + o7);
         c.t.xmin = xmin;
         c.t.xmax = xmax;
         it = g_lz_tabs.emplace(key, c).first;
@@ -658,17 +920,30 @@ int lanczos_tables(const ResizeLaunch& R, double inv_x, double inv_y, hipStream_
 }
 
 struct LzGrid {
-    int blocks, strips, bands, band_rows;
+    int blocks, strips, bands, band_rows, xcd_per;
 };
 
 template <typename TIn, int OUT>
 hipError_t launch_out(const LanczosLaunch& A, const LzGrid& g, hipStream_t s) {
-    const dim3 grid((unsigned)g.blocks), block(64 * kLzWaves);
+    const dim3 grid((unsigned)(g.xcd_per > 0 ? 8 * g.xcd_per : g.blocks)), block(64 * kLzWaves);
     switch (A.src.cc) {
-        case 1: hipLaunchKernelGGL((lanczos_kernel<TIn, OUT, 1>), grid, block, 0, s, A, g.strips, g.bands, g.band_rows); break;
-        case 2: hipLaunchKernelGGL((lanczos_kernel<TIn, OUT, 2>), grid, block, 0, s, A, g.strips, g.bands, g.band_rows); break;
-        case 3: hipLaunchKernelGGL((lanczos_kernel<TIn, OUT, 3>), grid, block, 0, s, A, g.strips, g.bands, g.band_rows); break;
-        case 4: hipLaunchKernelGGL((lanczos_kernel<TIn, OUT, 4>), grid, block, 0, s, A, g.strips, g.bands, g.band_rows); break;
+        case 1: hipLaunchKernelGGL((lanczos_kernel<TIn, OUT, 1>), grid, block, 0, s, A, g.strips, g.bands, g.band_rows, g.blocks, g.xcd_per); break;
+        case 2: hipLaunchKernelGGL((lanczos_kernel<TIn, OUT, 2>), grid, block, 0, s, A, g.strips, g.bands, g.band_rows, g.blocks, g.xcd_per); break;
+        case 3: hipLaunchKernelGGL((lanczos_kernel<TIn, OUT, 3>), grid, block, 0, s, A, g.strips, g.bands, g.band_rows, g.blocks, g.xcd_per); break;
+        case 4: hipLaunchKernelGGL((lanczos_kernel<TIn, OUT, 4>), grid, block, 0, s, A, g.strips, g.bands, g.band_rows, g.blocks, g.xcd_per); break;
+        default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+template <int OUT>
+hipError_t launch_u8(const LanczosLaunch& A, const LzGrid& g, hipStream_t s) {
+    const dim3 grid((unsigned)(g.xcd_per > 0 ? 8 * g.xcd_per : g.blocks)), block(64 * kLzWaves);
+    switch (A.src.cc) {
+        case 1: hipLaunchKernelGGL((lanczos_u8_kernel<OUT, 1>), grid, block, 0, s, A, g.strips, g.bands, g.band_rows, g.blocks, g.xcd_per); break;
+        case 2: hipLaunchKernelGGL((lanczos_u8_kernel<OUT, 2>), grid, block, 0, s, A, g.strips, g.bands, g.band_rows, g.blocks, g.xcd_per); break;
+        case 3: hipLaunchKernelGGL((lanczos_u8_kernel<OUT, 3>), grid, block, 0, s, A, g.strips, g.bands, g.band_rows, g.blocks, g.xcd_per); break;
+        case 4: hipLaunchKernelGGL((lanczos_u8_kernel<OUT, 4>), grid, block, 0, s, A, g.strips, g.bands, g.band_rows, g.blocks, g.xcd_per); break;
         default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
@@ -691,9 +966,22 @@ int launch_resize_lanczos(const ResizeLaunch& R, double inv_x, double inv_y, hip
     A.n = R.n;
     A.out = R.out;
     A.norm = R.norm;
-    const int st = lanczos_tables(R, inv_x, inv_y, s, A.t);
+    // wave tasks: 64-column strips x bands of output rows x planes; bands
+    // shrink until there are ~16K tasks (a band's first row resizes all 8 of
+    // its source rows, later rows only the new ones)
+    LzGrid g{};
+    const int64_t planes = (int64_t)R.n * R.src.planes;
+    const bool narrow = R.src.w < 8;
+    if (!narrow) {
+        g.strips = (R.dst.w + 63) / 64;
+        const int64_t want = (16384 + g.strips * planes - 1) / (g.strips * planes);
+        g.bands = (int)std::max<int64_t>(1, std::min<int64_t>(want, (R.dst.h + 15) / 16));
+        g.band_rows = (R.dst.h + g.bands - 1) / g.bands;
+        g.bands = (R.dst.h + g.band_rows - 1) / g.band_rows;
+    }
+    const int st = lanczos_tables(R, inv_x, inv_y, g.band_rows, s, A.t);
     if (st) return st;
-    if (R.src.w < 8) {
+    if (narrow) {
         // narrower than lanczos_kernel's 8-pixel row window: per-pixel kernel
         const int64_t total = (int64_t)R.dst.w * R.dst.h * R.n * R.src.planes;
         const int64_t blocks = (total + 255) / 256;
@@ -710,20 +998,18 @@ int launch_resize_lanczos(const ResizeLaunch& R, double inv_x, double inv_y, hip
         }
         return hipGetLastError() == hipSuccess ? VACV_OK : VACV_ERR_HIP;
     }
-    // wave tasks: 64-column strips x bands of output rows x planes; bands
-    // shrink until there are ~16K tasks (a band's first row resizes all 8 of
-    // its source rows, later rows only the new ones)
-    LzGrid g;
-    const int64_t planes = (int64_t)R.n * R.src.planes;
-    g.strips = (R.dst.w + 63) / 64;
-    const int64_t want = (16384 + g.strips * planes - 1) / (g.strips * planes);
-    g.bands = (int)std::max<int64_t>(1, std::min<int64_t>(want, (R.dst.h + 15) / 16));
-    g.band_rows = (R.dst.h + g.bands - 1) / g.bands;
-    g.bands = (R.dst.h + g.band_rows - 1) / g.band_rows;
     const int64_t tasks = (int64_t)g.strips * g.bands * planes;
     if ((tasks + kLzWaves - 1) / kLzWaves > 0x7FFFFFF0LL) return VACV_ERR_UNSUPPORTED;
     g.blocks = (int)((tasks + kLzWaves - 1) / kLzWaves);
-    const hipError_t e = R.src.esize == 1 ? launch_t<uint8_t>(A, g, s) : launch_t<float>(A, g, s);
+    g.xcd_per = tune_or(VACV_TUNE_DIRECT_XCD, 1) ? (g.blocks + 7) / 8 : 0;
+    hipError_t e;
+    if (R.src.esize == 1 && tune_or(VACV_TUNE_LANCZOS_KERNEL, 0) == 0) {
+        if (A.out == kOutSame) e = launch_u8<kOutSame>(A, g, s);
+        else if (A.out == kOutF32) e = launch_u8<kOutF32>(A, g, s);
+        else e = launch_u8<kOutNorm>(A, g, s);
+    } else {
+        e = R.src.esize == 1 ? launch_t<uint8_t>(A, g, s) : launch_t<float>(A, g, s);
+    }
     return e == hipSuccess ? VACV_OK : VACV_ERR_HIP;
 }
 

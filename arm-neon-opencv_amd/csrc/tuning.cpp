@@ -34,6 +34,7 @@ const char* const kNames[VACV_TUNE_COUNT] = {
     "VACV_WARP_FRAMES",        // VACV_TUNE_WARP_FRAMES
     "VACV_WARP_TILE_H",        // VACV_TUNE_WARP_TILE_H
     "VACV_WARP_SLOTS",         // VACV_TUNE_WARP_SLOTS
+    "VACV_LANCZOS_KERNEL",     // VACV_TUNE_LANCZOS_KERNEL
 };
 
 struct Table {

@@ -103,7 +103,8 @@ SIGNATURES = {
 TUNE = {"RESIZE_DIRECT": 0, "CUBIC_DIRECT": 1, "RESIZE_INTERLEAVE": 2, "DIRECT_XCD": 3, "WARP_PX": 4,
         "NEAREST_KERNEL": 5, "AREA_KERNEL": 6, "AREA_ROWS": 7, "RESIZE_WGS": 8, "RESIZE_TILE_H": 9,
         "RESIZE_TILE_W": 10, "RESIZE_WORK": 11, "WARP_KERNEL": 12, "RESIZE_STRIP": 13, "MATCH_KERNEL": 14,
-        "WARP_FRAMES": 15, "WARP_TILE_H": 16, "WARP_SLOTS": 17}
+        "WARP_FRAMES": 15, "WARP_TILE_H": 16, "WARP_SLOTS": 17,
+        "LANCZOS_KERNEL": 18}
 
 # include/vacv_hip.h VACV_ABI_VERSION: the tuning enum above and every
 # signature here are laid out for it (tests/test_abi.py checks the header)
