@@ -58,7 +58,8 @@ struct LanczosTabsDev {
     const int* yrot;     // [dst.h][4] u8: the 8 coefficients per ring SLOT (row mod 8) as short pairs
     const float* yaf;    // [dst.h][8]
     const int* yrec;     // [dst.h][16] u8, lanczos_u8_kernel: [0, 8) the coefficients by slot (row - rs) & 7, rs
-                         // the first source row of the row's band; [8] its last tap row
+                         // the first source row of the row's band; [8] its last tap row; [9] 1 if row y + 1's
+                         // last tap row is the same
     int xmin, xmax;      // output columns [xmin, xmax) take the unrolled horizontal sum
 };
 
@@ -507,6 +508,9 @@ __global__ void __launch_bounds__(64 * kLzWaves) lanczos_kernel(LanczosLaunch L,
 // coefficients once (window pixel p weighs the sum of the taps that clamp to
 // it -- exact, the u8 sums are int arithmetic), so every lane runs the same
 // unrolled horizontal sum and the per-row 9-way shift switch is gone.
+#ifndef VACV_LZ_TASKS
+#define VACV_LZ_TASKS 65536  // wave tasks a launch aims for (bands shrink until there are about this many)
+#endif
 #ifndef VACV_LZR_D
 #define VACV_LZR_D 4  // windows in flight per wave (a divisor of 8, the unroll)
 #endif
@@ -683,11 +687,12 @@ __global__ void __launch_bounds__(64 * kLzWaves) lanczos_u8_kernel(LanczosLaunch
             for (int q = 0; q < CC; ++q) hs[j][q] = 0;
         }
         int y = __builtin_amdgcn_readfirstlane(y0);
-        int bb[8], need;
+        int bb[8], need, same;
         auto fetch = [&](int yy) {
 #pragma unroll
             for (int k = 0; k < 8; ++k) bb[k] = lz_const(L.t.yrec, 16 * yy + k);
             need = lz_const(L.t.yrec, 16 * yy + 8);
+            same = lz_const(L.t.yrec, 16 * yy + 9);
         };
         fetch(y);
         uint32_t buf[D][ND];
@@ -701,13 +706,25 @@ __global__ void __launch_bounds__(64 * kLzWaves) lanczos_u8_kernel(LanczosLaunch
                 const int rr = r + u;
                 hrow(buf[u % D], hs[u]);
                 if (need == rr) {  // uniform; y < y1 while the walk runs
-                    do {
+                    // the first output row of the step outside any loop: the
+                    // multiplies then take the register rows as they are (in
+                    // a loop LLVM hoists a sign extension of all 8 CC rows
+                    // out of it, 8 CC extra VALU per output row); `same`
+                    // (the record's flag: the next row ends on this source
+                    // row too) decides the loop without waiting for the
+                    // next record, which is read a step later
+                    y = __builtin_amdgcn_readfirstlane(y);
+                    emit(y, hs, bb);
+                    bool more = same != 0;
+                    ++y;
+                    if (y < y1) fetch(y);
+                    while (more && y < y1) {  // upscales: more output rows per source row
                         y = __builtin_amdgcn_readfirstlane(y);
                         emit(y, hs, bb);
+                        more = same != 0;
                         ++y;
-                        if (y >= y1) break;
-                        fetch(y);
-                    } while (need == rr);
+                        if (y < y1) fetch(y);
+                    }
                 } else {
                     __builtin_amdgcn_raw_buffer_store_b32(0u, drs.r, (int)kOobStore, 0, 0);
                 }
@@ -887,6 +904,7 @@ int lanczos_tables(const ResizeLaunch& R, double inv_x, double inv_y, int band_r
             }
             yc[16 * (size_t)y + 8] = std::min(yo[y] + 4, R.src.h - 1);
         }
+        for (int y = 0; y + 1 < R.dst.h; ++y) yc[16 * (size_t)y + 9] = yc[16 * (size_t)y + 8] == yc[16 * (size_t)y + 24];
         const size_t o0 = put(xo.data(), xo.size() * 4), o1 = put(xi.data(), xi.size() * 2),
                      o2 = put(xf.data(), xf.size() * 4), o3 = put(yo.data(), yo.size() * 4),
                      o4 = put(yi.data(), yi.size() * 2), o5 = put(yf.data(), yf.size() * 4),
@@ -974,7 +992,7 @@ int launch_resize_lanczos(const ResizeLaunch& R, double inv_x, double inv_y, hip
     const bool narrow = R.src.w < 8;
     if (!narrow) {
         g.strips = (R.dst.w + 63) / 64;
-        const int64_t want = (16384 + g.strips * planes - 1) / (g.strips * planes);
+        const int64_t want = (VACV_LZ_TASKS + g.strips * planes - 1) / (g.strips * planes);
         g.bands = (int)std::max<int64_t>(1, std::min<int64_t>(want, (R.dst.h + 15) / 16));
         g.band_rows = (R.dst.h + g.bands - 1) / g.bands;
         g.bands = (R.dst.h + g.band_rows - 1) / g.band_rows;
