@@ -511,11 +511,21 @@ __global__ void __launch_bounds__(64 * kLzWaves) lanczos_kernel(LanczosLaunch L,
 #ifndef VACV_LZ_TASKS
 #define VACV_LZ_TASKS 65536  // wave tasks a launch aims for (bands shrink until there are about this many)
 #endif
+#ifndef VACV_LZ_MINROWS
+#define VACV_LZ_MINROWS 16  // output rows per band at least
+#endif
+#ifndef VACV_LZ_WPE
+#define VACV_LZ_WPE 0  // lanczos_u8_kernel: waves per SIMD the register allocation aims for (0: the compiler's choice)
+#endif
 #ifndef VACV_LZR_D
 #define VACV_LZR_D 4  // windows in flight per wave (a divisor of 8, the unroll)
 #endif
 template <int OUT, int CC>
-__global__ void __launch_bounds__(64 * kLzWaves) lanczos_u8_kernel(LanczosLaunch L, int strips, int bands, int band_rows,
+__global__ void __launch_bounds__(64 * kLzWaves)
+#if VACV_LZ_WPE
+__attribute__((amdgpu_waves_per_eu(VACV_LZ_WPE)))
+#endif
+lanczos_u8_kernel(LanczosLaunch L, int strips, int bands, int band_rows,
                                                                      int blocks, int xcd_per) {
     using TOut = typename std::conditional<(OUT == kOutSame), uint8_t, float>::type;
     constexpr int ND = (8 * CC + 6) / 4;
@@ -993,7 +1003,7 @@ int launch_resize_lanczos(const ResizeLaunch& R, double inv_x, double inv_y, hip
     if (!narrow) {
         g.strips = (R.dst.w + 63) / 64;
         const int64_t want = (VACV_LZ_TASKS + g.strips * planes - 1) / (g.strips * planes);
-        g.bands = (int)std::max<int64_t>(1, std::min<int64_t>(want, (R.dst.h + 15) / 16));
+        g.bands = (int)std::max<int64_t>(1, std::min<int64_t>(want, (R.dst.h + VACV_LZ_MINROWS - 1) / VACV_LZ_MINROWS));
         g.band_rows = (R.dst.h + g.bands - 1) / g.bands;
         g.bands = (R.dst.h + g.band_rows - 1) / g.band_rows;
     }

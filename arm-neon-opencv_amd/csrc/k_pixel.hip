@@ -15,6 +15,9 @@ namespace {
 __device__ __forceinline__ int64_t gtid() { return (int64_t)blockIdx.x * blockDim.x + threadIdx.x; }
 __device__ __forceinline__ int64_t gstride() { return (int64_t)gridDim.x * blockDim.x; }
 
+#ifndef VACV_COLOR_NT
+#define VACV_COLOR_NT 1  // fp32 colour / dtype output stores: 1 non-temporal, 0 the default policy (A/B)
+#endif
 constexpr int kColorPairs = 1;  // row pairs per wave in color_kernel (4 measured 15 % slower)
 
 int grid_for(int64_t work_items, int cap = 256 * 16) {
@@ -145,7 +148,8 @@ __global__ void __launch_bounds__(kBlock) u8_to_f32_flat_kernel(DtypeLaunch L) {
         const uint32_t w = __builtin_nontemporal_load(reinterpret_cast<const uint32_t*>(L.src) + i);
         const u32x4 f = {__float_as_uint((float)(w & 0xFF)), __float_as_uint((float)((w >> 8) & 0xFF)),
                          __float_as_uint((float)((w >> 16) & 0xFF)), __float_as_uint((float)(w >> 24))};
-        __builtin_nontemporal_store(f, reinterpret_cast<u32x4*>(L.dst) + i);
+        if (VACV_COLOR_NT) __builtin_nontemporal_store(f, reinterpret_cast<u32x4*>(L.dst) + i);
+        else reinterpret_cast<u32x4*>(L.dst)[i] = f;
     } else if (i - n4 < (L.count & 3)) {
         const int64_t e = (n4 << 2) + (i - n4);
         reinterpret_cast<float*>(L.dst)[e] = (float)L.src[e];
@@ -281,8 +285,10 @@ __global__ void __launch_bounds__(kBlock) color_kernel(ColorLaunch L) {
                 __builtin_amdgcn_wave_barrier();
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 #pragma unroll
-                for (int b = 0; b < 3; ++b)
-                    __builtin_nontemporal_store(w[b * 64 + lane], reinterpret_cast<u32x4*>(wbase) + b * 64 + lane);
+                for (int b = 0; b < 3; ++b) {
+                    if (VACV_COLOR_NT) __builtin_nontemporal_store(w[b * 64 + lane], reinterpret_cast<u32x4*>(wbase) + b * 64 + lane);
+                    else reinterpret_cast<u32x4*>(wbase)[b * 64 + lane] = w[b * 64 + lane];
+                }
                 __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
                 __builtin_amdgcn_wave_barrier();  // the next row reuses the exchange buffer
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
