@@ -1202,6 +1202,199 @@ hipError_t launch_area_u8_colsum(const ResizeLaunch& L, hipStream_t s, int vb) {
                     : launch_area_u8_colsum_t<4>(L, s, tw, rows, grid);
 }
 
+// u8 INTER_AREA at integer scales, lane-stationary (round 5), for the shapes
+// whose unit (lcm(16, AX*CC) bytes) is too wide for area_u8_unit_kernel's
+// registers -- 3x3 over BGR / BGRA, 1080p -> 640x360 among them.  A lane
+// owns PXL = 4 / gcd(4, AX*CC) consecutive output pixels of one row, i.e. NW
+// = PXL*AX*CC/4 whole, dword-aligned source dwords of each of its AY source
+// rows (no byte shifts, no LDS): all AY rows' loads are issued together,
+// summed down the rows as packed u16 pairs (even / odd bytes, 255 * AY <
+// 2^16), then across each pixel's AX columns at compile-time byte positions.
+// A wave is 64 * PXL output pixels of a row; its loads of a source row cover
+// one contiguous run of 256 * NW bytes (3x3 BGR: 2,304 B = 18 whole lines
+// where the row starts on a line), its output one contiguous run too.
+// Integer sums, then OpenCV's rounding: bit-identical to the other kernels.
+template <int AX, int CC>
+struct AreaLane {
+    static constexpr int gcd(int a, int b) { return b == 0 ? a : gcd(b, a % b); }
+    static constexpr int PXL = 4 / gcd(4, AX * CC);  // output pixels per lane
+    static constexpr int NW = PXL * AX * CC / 4;      // source dwords per lane and row
+    static constexpr int OB = PXL * CC;               // output elements per lane
+};
+
+template <int OUT, int AX, int CC>
+__global__ void __launch_bounds__(kBlock) area_lane_kernel(ResizeLaunch L, int blocks_per_row, int tasks, int dst_al) {
+    using A = AreaLane<AX, CC>;
+    constexpr int PXL = A::PXL, NW = A::NW, OB = A::OB;
+    static_assert(OB % 4 == 0 || OUT != kOutSame, "u8 output as whole dwords");
+    const int lane = threadIdx.x & 63;
+    const int task = (int)blockIdx.x * (kBlock / 64) + __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
+    if (task >= tasks) return;  // whole wave
+    const int blk = task % blocks_per_row;
+    const int rest = task / blocks_per_row;
+    const int y = rest % L.dst.h;
+    const int pidx = rest / L.dst.h;
+    const int img = pidx / L.src.planes, plane = pidx - img * L.src.planes;
+    const int x0 = (blk * 64 + lane) * PXL;  // the lane's first output pixel
+    const int vx = min(PXL, L.dst.w - x0);    // its valid pixels (<= 0: none)
+    const bool full = (blk + 1) * 64 * PXL <= L.dst.w;  // uniform: every lane has PXL pixels
+    const Rsrc srs = make_rsrc(L.src.base + (int64_t)img * L.src.img_pitch + (int64_t)plane * L.src.plane_pitch,
+                               L.src.plane_bytes);
+    const uint32_t rp = (uint32_t)L.src.row_pitch;
+    const uint32_t lo = (uint32_t)(y * L.area_y) * rp + (uint32_t)(x0 * AX * CC) + srs.delta;
+
+    // one source row's NW dwords: 16-byte loads where the wave is whole; else
+    // dword loads, and bytewise the one dword that straddles the plane's
+    // last byte (a straddling load reads as zeros)
+    const uint32_t slim = (uint32_t)L.src.plane_bytes + srs.delta;
+    auto load_row = [&](uint32_t off, uint32_t (&d)[NW]) {
+        if (full) {
+            int q = 0;
+#pragma unroll
+            for (; q + 4 <= NW; q += 4) {
+                const auto v = __builtin_amdgcn_raw_buffer_load_b128(srs.r, (int)(off + 4 * q), 0, 0);
+                d[q] = v[0]; d[q + 1] = v[1]; d[q + 2] = v[2]; d[q + 3] = v[3];
+            }
+            if constexpr (NW % 4 == 3) {
+                const auto v = __builtin_amdgcn_raw_buffer_load_b96(srs.r, (int)(off + 4 * q), 0, 0);
+                d[q] = v[0]; d[q + 1] = v[1]; d[q + 2] = v[2];
+            } else if constexpr (NW % 4 == 2) {
+                const auto v = __builtin_amdgcn_raw_buffer_load_b64(srs.r, (int)(off + 4 * q), 0, 0);
+                d[q] = v[0]; d[q + 1] = v[1];
+            } else if constexpr (NW % 4 == 1) {
+                d[q] = __builtin_amdgcn_raw_buffer_load_b32(srs.r, (int)(off + 4 * q), 0, 0);
+            }
+        } else {
+#pragma unroll
+            for (int q = 0; q < NW; ++q) {
+                const uint32_t o = off + 4u * (uint32_t)q;
+                if (o + 4u <= slim) {
+                    d[q] = __builtin_amdgcn_raw_buffer_load_b32(srs.r, (int)o, 0, 0);
+                } else {
+                    uint32_t v = 0;
+#pragma unroll
+                    for (uint32_t e = 0; e < 4u; ++e)
+                        if (o + e < slim) v |= (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(srs.r, (int)(o + e), 0, 0) << (8 * e);
+                    d[q] = v;
+                }
+            }
+        }
+    };
+    uint32_t ev[NW], od[NW];
+#pragma unroll
+    for (int q = 0; q < NW; ++q) ev[q] = od[q] = 0u;
+    auto add = [&](const uint32_t (&d)[NW]) {
+#pragma unroll
+        for (int q = 0; q < NW; ++q) {
+            ev[q] += __builtin_amdgcn_perm(0u, d[q], 0x0C020C00u);  // bytes 0, 2 as u16 pairs
+            od[q] += __builtin_amdgcn_perm(0u, d[q], 0x0C030C01u);  // bytes 1, 3
+        }
+    };
+    int r = 0;
+    for (; r + 3 <= L.area_y; r += 3) {  // three rows in flight (the 3x3 case: all of them)
+        uint32_t d0[NW], d1[NW], d2[NW];
+        load_row(lo + (uint32_t)r * rp, d0);
+        load_row(lo + (uint32_t)(r + 1) * rp, d1);
+        load_row(lo + (uint32_t)(r + 2) * rp, d2);
+        add(d0);
+        add(d1);
+        add(d2);
+    }
+    for (; r < L.area_y; ++r) {
+        uint32_t d0[NW];
+        load_row(lo + (uint32_t)r * rp, d0);
+        add(d0);
+    }
+    if (vx <= 0) return;
+    // output element e: pixel p = e / CC, channel k; its source bytes
+    // j = (p * AX + a) * CC + k, a < AX -- all positions compile-time
+    auto colsum = [&](int j) -> int {
+        const uint32_t w = (j & 1) ? od[j >> 2] : ev[j >> 2];
+        return (int)((w >> (16 * ((j >> 1) & 1))) & 0xFFFFu);
+    };
+    unsigned char* dp = const_cast<unsigned char*>(L.dst.base) + (int64_t)img * L.dst.img_pitch +
+                        (int64_t)plane * L.dst.plane_pitch;
+    const Rsrc drs = make_rsrc(dp, L.dst.plane_bytes);
+    constexpr int ES = OUT == kOutSame ? 1 : 4;
+    const uint32_t ro = (uint32_t)y * (uint32_t)L.dst.row_pitch + (uint32_t)(x0 * CC * ES) + drs.delta;
+    uint32_t outw[OUT == kOutSame ? (OB + 3) / 4 : OB];
+#pragma unroll
+    for (int e = 0; e < OB; ++e) {
+        const int p = e / CC, k = e - p * CC;
+        int sum = 0;
+#pragma unroll
+        for (int a = 0; a < AX; ++a) sum += colsum((p * AX + a) * CC + k);
+        const int v = L.area_half_up ? (sum + 2) >> 2 : (int)rintf(__fmul_rn((float)sum, L.area_scale));
+        if constexpr (OUT == kOutSame) {
+            if (e % 4 == 0) outw[e / 4] = 0u;
+            outw[e / 4] |= (uint32_t)(v & 0xFF) << (8 * (e % 4));
+        } else if constexpr (OUT == kOutF32) {
+            outw[e] = __builtin_bit_cast(uint32_t, (float)v);
+        } else {
+            const ChanNorm cn = chan_norm(L.norm, img, CC == 1 ? plane % L.norm.c_total : k);
+            outw[e] = __builtin_bit_cast(uint32_t, normalize_u8v(cn, v));
+        }
+    }
+    constexpr int NO = OUT == kOutSame ? OB / 4 : OB;  // output dwords per lane
+    if (vx == PXL && dst_al) {
+        int i = 0;
+#pragma unroll
+        for (; i + 4 <= NO; i += 4)
+            __builtin_amdgcn_raw_buffer_store_b128(u32x4{outw[i], outw[i + 1], outw[i + 2], outw[i + 3]}, drs.r,
+                                                   (int)(ro + 4u * (uint32_t)i), 0, 0);
+        if constexpr (NO % 4 == 3) {
+            typedef unsigned int u32x3 __attribute__((ext_vector_type(3)));
+            __builtin_amdgcn_raw_buffer_store_b96(u32x3{outw[i], outw[i + 1], outw[i + 2]}, drs.r, (int)(ro + 4u * (uint32_t)i), 0, 0);
+        } else if constexpr (NO % 4 == 2) {
+            typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+            __builtin_amdgcn_raw_buffer_store_b64(u32x2{outw[i], outw[i + 1]}, drs.r, (int)(ro + 4u * (uint32_t)i), 0, 0);
+        } else if constexpr (NO % 4 == 1) {
+            __builtin_amdgcn_raw_buffer_store_b32(outw[i], drs.r, (int)(ro + 4u * (uint32_t)i), 0, 0);
+        }
+    } else {  // the row's partial last lane or an unaligned destination: element by element
+#pragma unroll
+        for (int e = 0; e < OB; ++e) {
+            if (e >= vx * CC) break;
+            if constexpr (OUT == kOutSame)
+                __builtin_amdgcn_raw_buffer_store_b8((unsigned char)(outw[e / 4] >> (8 * (e % 4))), drs.r, (int)(ro + (uint32_t)e), 0, 0);
+            else
+                __builtin_amdgcn_raw_buffer_store_b32(outw[e], drs.r, (int)(ro + 4u * (uint32_t)e), 0, 0);
+        }
+    }
+}
+
+template <int AX, int CC>
+hipError_t launch_area_lane_c(const ResizeLaunch& L, hipStream_t s) {
+    using A = AreaLane<AX, CC>;
+    const int bpr = (L.dst.w + 64 * A::PXL - 1) / (64 * A::PXL);
+    const int64_t tasks = (int64_t)bpr * L.dst.h * L.n * L.src.planes;
+    if (tasks >= 0x7FFFFF00LL) return hipErrorInvalidValue;
+    const int es = L.out == kOutSame ? 1 : 4;
+    const uintptr_t dbits = reinterpret_cast<uintptr_t>(L.dst.base) | (uintptr_t)L.dst.img_pitch |
+                            (uintptr_t)L.dst.plane_pitch | (uintptr_t)L.dst.row_pitch;
+    // a lane's output starts at x0 * CC * es bytes: aligned to the widest store it issues
+    const int ob = A::OB * es;
+    const int wst = ob % 16 == 0 ? 16 : ob % 8 == 0 ? 8 : 4;
+    const int dst_al = (dbits % (uintptr_t)wst) == 0;
+    const dim3 grid((unsigned)((tasks + kBlock / 64 - 1) / (kBlock / 64)));
+    if (L.out == kOutSame) hipLaunchKernelGGL((area_lane_kernel<kOutSame, AX, CC>), grid, dim3(kBlock), 0, s, L, bpr, (int)tasks, dst_al);
+    else if (L.out == kOutF32) hipLaunchKernelGGL((area_lane_kernel<kOutF32, AX, CC>), grid, dim3(kBlock), 0, s, L, bpr, (int)tasks, dst_al);
+    else hipLaunchKernelGGL((area_lane_kernel<kOutNorm, AX, CC>), grid, dim3(kBlock), 0, s, L, bpr, (int)tasks, dst_al);
+    return hipGetLastError();
+}
+
+// the lane kernel's (AX, CC) instances; plane bytes < 2^31
+bool area_lane_applies(const ResizeLaunch& L) {
+    const int ax = L.area_x, cc = L.src.cc;
+    return ((ax == 3 && (cc == 3 || cc == 4))) && L.area_y >= 1 && L.area_y <= 257 &&
+           L.src.plane_bytes < (1LL << 31) - 64 && L.dst.plane_bytes < (1LL << 31) - 64;
+}
+
+hipError_t launch_area_lane(const ResizeLaunch& L, hipStream_t s) {
+    if (L.src.cc == 3) return launch_area_lane_c<3, 3>(L, s);
+    return launch_area_lane_c<3, 4>(L, s);
+}
+
 template <typename TIn>
 hipError_t launch_area_t(const ResizeLaunch& L, hipStream_t s) {
     const dim3 grid((L.dst.w + kBlock - 1) / kBlock, L.dst.h, L.n * L.src.planes);
@@ -1238,9 +1431,11 @@ hipError_t launch_resize_area(const ResizeLaunch& L, hipStream_t s) {
     if (L.src.esize == 1) {
         const uintptr_t bits = reinterpret_cast<uintptr_t>(L.src.base) | (uintptr_t)L.src.img_pitch |
                                (uintptr_t)L.src.plane_pitch | (uintptr_t)L.src.row_pitch;
-        // A/B: 1 per-pixel, 2 dword column sums, 3 16-byte column sums (LDS)
+        // A/B: 1 per-pixel, 2 dword column sums, 3 16-byte column sums (LDS);
+        // default: the unit kernel, else the lane kernel, where they apply
         const int knob = tune(VACV_TUNE_AREA_KERNEL);
         if ((bits & 15) == 0 && knob <= 0 && area_unit_applies(L)) return launch_area_u8_unit(L, s);
+        if ((bits & 3) == 0 && knob <= 0 && area_lane_applies(L)) return launch_area_lane(L, s);
         const int vb = (bits & 15) == 0 && L.area_x * L.src.cc <= 256 ? 16 : (bits & 3) == 0 ? 4 : 0;
         if (vb && L.area_x * L.src.cc <= 1024 && L.area_y <= 257 && knob != 1)  // u16 column sums: 255 * ay < 2^16
             return launch_area_u8_colsum(L, s, knob == 2 ? 4 : vb);

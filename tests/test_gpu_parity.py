@@ -421,8 +421,9 @@ def test_resize_area(ops, dev, oracle):
 
 
 def test_area_unit_kernel(ops, dev, oracle):
-    """The streaming u8 INTER_AREA kernel (area_u8_unit_kernel, k_pixel.hip:
-    16-byte aligned rows, AX in {2, 4} with 1-4 channels, AX = 3 with one):
+    """The streaming u8 INTER_AREA kernels (area_u8_unit_kernel, k_pixel.hip:
+    16-byte aligned rows, AX in {2, 4} with 1-4 channels, AX = 3 with one;
+    area_lane_kernel: AX = 3 with 3 or 4 channels):
     bit-exact against the oracle and against the LDS column-sum kernel
     (VACV_TUNE_AREA_KERNEL = 3) for every instance, with row pitches padded
     so that a row's last unit is partial (and, on the last row, its chunks
@@ -430,10 +431,12 @@ def test_area_unit_kernel(ops, dev, oracle):
     and a destination that forbids the vector stores."""
     import torch
     from vacv_amd import INTER_AREA, NCHW
+    # (3, *, 3) and (3, *, 4): area_lane_kernel (whole source dwords per lane;
+    # 300-pixel rows take its 16-byte loads, the others its dword loads)
     cases = [(2, 2, 1), (2, 2, 2), (2, 2, 3), (2, 2, 4), (3, 3, 1), (3, 1, 1), (4, 4, 1), (4, 2, 2), (4, 4, 3),
-             (4, 3, 4), (2, 3, 3), (2, 5, 1)]
+             (4, 3, 4), (2, 3, 3), (2, 5, 1), (3, 3, 3), (3, 3, 4), (3, 2, 3), (3, 4, 4)]
     for i, (ax, ay, c) in enumerate(cases):
-        for wo, ho in [(37, 11), (64, 9)]:
+        for wo, ho in [(37, 11), (64, 9)] + ([(300, 5), (1027, 3)] if ax == 3 and c >= 3 else []):
             w, h = wo * ax, ho * ay
             pitch = -(-(w * c + 1) // 16) * 16  # 16-byte rows, padded
             imgs = [synthetic_image(790 + 10 * i + k, h, w, c).reshape(h, w, c) for k in range(2)]
