@@ -1222,6 +1222,9 @@ struct AreaLane {
     static constexpr int OB = PXL * CC;               // output elements per lane
 };
 
+#ifndef VACV_AREA_XCH
+#define VACV_AREA_XCH 1  // area_lane_kernel: 1 lane-contiguous 16-byte loads + an LDS exchange for whole waves (0.3325 vs 0.3708 ms)
+#endif
 #ifndef VACV_AREA_RG
 #define VACV_AREA_RG 1  // area_lane_kernel: output rows per wave, the next row's loads in flight while one is summed (1 / 2 / 4 / 8: 0.369 / 0.382 / 0.385 / 0.418 ms)
 #endif
@@ -1355,6 +1358,69 @@ __global__ void __launch_bounds__(kBlock) area_lane_kernel(ResizeLaunch L, int b
             }
         }
     };
+#if VACV_AREA_XCH
+    if (full && L.area_y <= 257) {
+        // uniform (whole waves): the wave's run of 16 NW chunks of a source
+        // row moves as lane-contiguous 16-byte loads (chunk 64 i + lane), is
+        // summed down the rows per chunk, and goes to the lanes' windows
+        // through the wave's own LDS slice -- the loads then cover whole lines
+        // per instruction instead of 64 windows NW dwords apart
+        constexpr int NCK = 16 * NW;           // 16-byte chunks of the run (64 lanes x NW dwords)
+        constexpr int NI = (NCK + 63) / 64;    // load instructions per source row
+        __shared__ __attribute__((aligned(16))) uint32_t xs[kBlock / 64][2][4 * NCK];
+        const int wv = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
+        const uint32_t run = (uint32_t)(blk * 64 * PXL * AX * CC) + srs.delta;  // the run's first byte
+        for (int k = 0; k < RG; ++k) {
+            const int y = y0 + k;
+            if (y >= L.dst.h) break;  // uniform
+            uint32_t cev[NI][4], cod[NI][4];
+#pragma unroll
+            for (int i = 0; i < NI; ++i) {
+#pragma unroll
+                for (int d = 0; d < 4; ++d) cev[i][d] = cod[i][d] = 0u;
+            }
+            const uint32_t ry = run + (uint32_t)(y * L.area_y) * rp;
+            for (int r = 0; r < L.area_y; ++r) {
+                u32x4 t[NI];
+#pragma unroll
+                for (int i = 0; i < NI; ++i) {
+                    const int q = 64 * i + lane;
+                    t[i] = q < NCK ? __builtin_amdgcn_raw_buffer_load_b128(srs.r, (int)(ry + (uint32_t)r * rp + 16u * (uint32_t)q), 0, 0)
+                                   : u32x4{0u, 0u, 0u, 0u};
+                }
+#pragma unroll
+                for (int i = 0; i < NI; ++i) {
+#pragma unroll
+                    for (int d = 0; d < 4; ++d) {
+                        cev[i][d] += __builtin_amdgcn_perm(0u, t[i][d], 0x0C020C00u);
+                        cod[i][d] += __builtin_amdgcn_perm(0u, t[i][d], 0x0C030C01u);
+                    }
+                }
+            }
+#pragma unroll
+            for (int i = 0; i < NI; ++i) {
+                const int q = 64 * i + lane;
+                if (q < NCK) {
+                    *reinterpret_cast<u32x4*>(&xs[wv][0][4 * q]) = u32x4{cev[i][0], cev[i][1], cev[i][2], cev[i][3]};
+                    *reinterpret_cast<u32x4*>(&xs[wv][1][4 * q]) = u32x4{cod[i][0], cod[i][1], cod[i][2], cod[i][3]};
+                }
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+            for (int q = 0; q < NW; ++q) {
+                ev[q] = xs[wv][0][NW * lane + q];
+                od[q] = xs[wv][1][NW * lane + q];
+            }
+            emit(y);
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();  // the next row reuses the slice
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        }
+        return;
+    }
+#endif
     if (L.area_y == 3) {
         // uniform: the 3 source rows of output row y + 1 are in flight while
         // row y is summed and stored
