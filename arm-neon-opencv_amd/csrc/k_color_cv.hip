@@ -162,6 +162,102 @@ __global__ void __launch_bounds__(256) yuv420_cv8_kernel(CvColorLaunch L, int up
     }
 }
 
+// The same decode with each WAVE on 64 consecutive 8 x 2 units of ONE row
+// pair (round 5): its output row segment (64 x 8 pixels x DCN bytes) is
+// contiguous, so the lanes' pixels go through the wave's own LDS slice and
+// leave as 16-byte stores, each instruction 1 KiB of one row.  The kernel
+// above wrote each lane's 32 (BGRA) / 24 (BGR) bytes from the lane itself,
+// its store instructions' lanes 32 / 24 bytes apart.  Needs 16-byte aligned
+// destination rows (host-checked).
+#ifndef VACV_CV8X_NT
+#define VACV_CV8X_NT 1  // the exchanged stores: 1 non-temporal, 0 the default policy
+#endif
+template <int DCN>
+__global__ void __launch_bounds__(256) yuv420_cv8x_kernel(CvColorLaunch L, int upr, int wrow) {
+    __shared__ __attribute__((aligned(16))) uint32_t xch[4][64 * 2 * DCN];
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
+    const int img = blockIdx.y;
+    const int bh = L.h >> 1;
+    const int task = (int)blockIdx.x * 4 + wave;
+    if (task >= wrow * bh) return;  // whole wave
+    const int by = task / wrow, blk = task - by * wrow;
+    const int nl = min(64, upr - blk * 64);  // live lanes (uniform)
+    const int u = blk * 64 + min(lane, nl - 1);  // idle lanes decode the last live unit again
+    const int x0 = 8 * u;
+    const unsigned char* s = L.src + (int64_t)img * L.src_img;
+    uint32_t cu, cv;
+    if (L.layout <= 1) {
+        typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+        const u32x2 c = *reinterpret_cast<const u32x2*>(s + (int64_t)(L.h + by) * L.src_row + x0);
+        const uint32_t ev = __builtin_amdgcn_perm(c[1], c[0], 0x06040200u);
+        const uint32_t od = __builtin_amdgcn_perm(c[1], c[0], 0x07050301u);
+        cu = L.layout == 0 ? ev : od;
+        cv = L.layout == 0 ? od : ev;
+    } else {
+        const unsigned char* c0 = s + (int64_t)L.h * L.src_row;
+        const int64_t q = (int64_t)(L.w >> 1) * bh, k = (int64_t)by * (L.w >> 1) + (x0 >> 1);
+        const uint32_t p0 = *reinterpret_cast<const uint32_t*>(c0 + k);
+        const uint32_t p1 = *reinterpret_cast<const uint32_t*>(c0 + q + k);
+        cu = L.layout == 2 ? p1 : p0;
+        cv = L.layout == 2 ? p0 : p1;
+    }
+    int ruv[4], guv[4], buv[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int uu = (int)((cu >> (8 * i)) & 0xFFu) - 128, vv = (int)((cv >> (8 * i)) & 0xFFu) - 128;
+        ruv[i] = (1 << 19) + 1673527 * vv;
+        guv[i] = (1 << 19) - 852492 * vv - 409993 * uu;
+        buv[i] = (1 << 19) + 2116026 * uu;
+    }
+    uint32_t* xw = xch[wave];
+    const int nck = nl * 8 * DCN / 16;  // whole 16-byte chunks of the segment
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+        typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+        const u32x2 yv = *reinterpret_cast<const u32x2*>(s + (int64_t)(2 * by + r) * L.src_row + x0);
+        uint32_t px[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const int Y = (int)((yv[j >> 2] >> (8 * (j & 3))) & 0xFFu);
+            px[j] = bt601(Y, ruv[j >> 1], guv[j >> 1], buv[j >> 1], L.bidx);
+        }
+        if constexpr (DCN == 4) {
+            *reinterpret_cast<u32x4*>(xw + 8 * lane) = u32x4{px[0], px[1], px[2], px[3]};
+            *reinterpret_cast<u32x4*>(xw + 8 * lane + 4) = u32x4{px[4], px[5], px[6], px[7]};
+        } else {
+            uint32_t w[6];
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                const uint32_t a = px[4 * i], b = px[4 * i + 1], c = px[4 * i + 2], d = px[4 * i + 3];
+                w[3 * i] = __builtin_amdgcn_perm(b, a, 0x04020100u);
+                w[3 * i + 1] = __builtin_amdgcn_perm(c, b, 0x05040201u);
+                w[3 * i + 2] = __builtin_amdgcn_perm(d, c, 0x06050402u);
+            }
+#pragma unroll
+            for (int k = 0; k < 3; ++k) *reinterpret_cast<u32x2*>(xw + 6 * lane + 2 * k) = u32x2{w[2 * k], w[2 * k + 1]};
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        unsigned char* o = L.dst + (int64_t)img * L.dst_img + (int64_t)(2 * by + r) * L.dst_row + (int64_t)blk * 64 * 8 * DCN;
+#pragma unroll
+        for (int j = 0; j < (2 * DCN + 3) / 4; ++j) {  // 16-byte chunks per lane, rounded up: BGRA 2, BGR 2
+            const int q = 64 * j + lane;
+            if (q < nck) {
+                const u32x4 v = *reinterpret_cast<const u32x4*>(xw + 4 * q);
+                if (VACV_CV8X_NT) __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(o) + q);
+                else reinterpret_cast<u32x4*>(o)[q] = v;
+            }
+        }
+        if (DCN == 3 && (nl & 1) && lane == 0)  // an odd lane count leaves 8 bytes
+            *reinterpret_cast<u32x2*>(o + 16 * nck) = *reinterpret_cast<const u32x2*>(xw + 4 * nck);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();  // the next row reuses the slice
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+}
+
 template <typename T>
 constexpr int gray_px() { return sizeof(T) == 1 ? 16 : 4; }
 template <int DCN, typename T>
@@ -250,6 +346,16 @@ hipError_t launch_color_cv(const CvColorLaunch& L, hipStream_t s) {
                ((reinterpret_cast<uintptr_t>(L.dst) | (uintptr_t)L.dst_img | (uintptr_t)L.dst_row) & (L.dcn == 4 ? 15 : 7)) == 0) {
         // 8 x 2 pixels per thread (the planar chroma rows are w / 2 bytes: 4-byte aligned as w % 8 == 0)
         const int upr8 = L.w >> 3;
+        const bool dst16 = ((reinterpret_cast<uintptr_t>(L.dst) | (uintptr_t)L.dst_img | (uintptr_t)L.dst_row) & 15) == 0;
+        if (dst16 && tune(VACV_TUNE_RESIZE_DIRECT) != 2) {
+            // a wave per 64 units of a row pair (VACV_TUNE_RESIZE_DIRECT = 2: the kernel below, A/B)
+            const int wrow = (upr8 + 63) / 64;
+            const int64_t gx = ((int64_t)wrow * (L.h >> 1) + 3) / 4;
+            const dim3 gg((unsigned)gx, (unsigned)L.n);
+            if (L.dcn == 4) hipLaunchKernelGGL(yuv420_cv8x_kernel<4>, gg, dim3(256), 0, s, L, upr8, wrow);
+            else hipLaunchKernelGGL(yuv420_cv8x_kernel<3>, gg, dim3(256), 0, s, L, upr8, wrow);
+            return hipGetLastError();
+        }
         const int64_t g8 = ((int64_t)upr8 * (L.h >> 1) + 255) / 256;
         const dim3 gg((unsigned)g8, (unsigned)L.n);
         if (L.dcn == 4) hipLaunchKernelGGL(yuv420_cv8_kernel<4>, gg, dim3(256), 0, s, L, upr8);

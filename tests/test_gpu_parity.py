@@ -1633,15 +1633,22 @@ def test_cvt_color_opencv_codes(ops, dev, oracle):
     from vacv_amd import (COLOR_GRAY2BGR, COLOR_YUV2BGR_YV12, COLOR_YUV2BGRA_NV12, COLOR_YUV2BGRA_NV21,
                           COLOR_YUV2RGBA_NV12, COLOR_YUV2RGBA_NV21)
     rng = np.random.default_rng(91)
-    for h, w in ((6, 10), (72, 130), (1080, 1920)):
+    # widths 616 / 1032: the wave-per-row-pair kernel's partial last wave (13
+    # and 1 live lanes: the odd-lane BGR tail); it is also checked against
+    # the lane-strided 8 x 2 kernel (RESIZE_DIRECT = 2)
+    for h, w in ((6, 10), (72, 130), (10, 616), (8, 1032), (1080, 1920)):
         yuv = rng.integers(0, 256, (3, h * 3 // 2, w), dtype=np.uint8)
         yuv[0, :h // 2] = 255
         yuv[0, h:] = 0
         for code in (COLOR_YUV2RGBA_NV12, COLOR_YUV2BGRA_NV12, COLOR_YUV2RGBA_NV21, COLOR_YUV2BGRA_NV21,
                      COLOR_YUV2BGR_YV12):
-            got = host(ops.cvt_color(to_dev(yuv, dev), code))
+            a = ops.cvt_color(to_dev(yuv, dev), code)
+            got = host(a)
             for k in range(3):
                 assert_same(got[k], oracle.yuv420_cv(yuv[k], code), f"cvt code {code} {w}x{h} image {k}")
+            with ops.tuning(RESIZE_DIRECT=2):
+                b = ops.cvt_color(to_dev(yuv, dev), code)
+            assert torch.equal(a, b), f"cvt code {code} {w}x{h}: the two 8 x 2 kernels differ"
     # a pitched RGBA destination (rows not 8-byte aligned: the byte-store path)
     yuv = rng.integers(0, 256, (2, 30, 26), dtype=np.uint8)
     big = torch.zeros((2, 20, 31, 4), dtype=torch.uint8, device=dev)
