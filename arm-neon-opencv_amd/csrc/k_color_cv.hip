@@ -320,6 +320,66 @@ __global__ void __launch_bounds__(256) gray_kernel(CvColorLaunch L, int upr) {
     }
 }
 
+// GRAY2BGR(A) with each WAVE on 64 units of ONE row (round 5), for aligned
+// images whose width is a whole number of units: the lanes' expanded pixels
+// go through the wave's LDS slice and leave as 16-byte non-temporal stores,
+// each instruction 1 KiB of the row (gray_kernel's lanes wrote their own
+// 48 / 64 bytes, its store instructions' lanes that far apart).
+template <int DCN, typename T>
+__global__ void __launch_bounds__(256) gray_x_kernel(CvColorLaunch L, int upr, int wrow) {
+    constexpr int PX = gray_px<T>();
+    constexpr int OW = PX * DCN * (int)sizeof(T) / 4;  // output dwords per lane: 12 (BGR) or 16 (BGRA)
+    __shared__ __attribute__((aligned(16))) uint32_t xch[4][64 * OW];
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
+    const int img = blockIdx.y;
+    const int task = (int)blockIdx.x * 4 + wave;
+    if (task >= wrow * L.h) return;  // whole wave
+    const int y = task / wrow, blk = task - y * wrow;
+    const int nl = min(64, upr - blk * 64);  // live lanes (uniform)
+    const int x0 = PX * (blk * 64 + min(lane, nl - 1));
+    const unsigned char* srow = L.src + (int64_t)img * L.src_img + (int64_t)y * L.src_row;
+    unsigned char* o = L.dst + (int64_t)img * L.dst_img + (int64_t)y * L.dst_row + (int64_t)blk * 64 * PX * DCN * sizeof(T);
+    const u32x4 v = *reinterpret_cast<const u32x4*>(srow + (int64_t)x0 * sizeof(T));
+    uint32_t w[OW];
+    if constexpr (sizeof(T) == 1) {
+        if constexpr (DCN == 3) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                w[3 * i] = __builtin_amdgcn_perm(v[i], v[i], 0x01000000u);
+                w[3 * i + 1] = __builtin_amdgcn_perm(v[i], v[i], 0x02020101u);
+                w[3 * i + 2] = __builtin_amdgcn_perm(v[i], v[i], 0x03030302u);
+            }
+        } else {
+#pragma unroll
+            for (int i = 0; i < 16; ++i) w[i] = ((v[i >> 2] >> (8 * (i & 3))) & 0xFFu) * 0x010101u | 0xFF000000u;
+        }
+    } else {
+        if constexpr (DCN == 3) {
+            const uint32_t e[12] = {v[0], v[0], v[0], v[1], v[1], v[1], v[2], v[2], v[2], v[3], v[3], v[3]};
+#pragma unroll
+            for (int i = 0; i < 12; ++i) w[i] = e[i];
+        } else {
+            const uint32_t one = __float_as_uint(1.f);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) { w[4 * i] = w[4 * i + 1] = w[4 * i + 2] = v[i]; w[4 * i + 3] = one; }
+        }
+    }
+    uint32_t* xw = xch[wave];
+#pragma unroll
+    for (int k = 0; k < OW / 4; ++k)
+        *reinterpret_cast<u32x4*>(xw + OW * lane + 4 * k) = u32x4{w[4 * k], w[4 * k + 1], w[4 * k + 2], w[4 * k + 3]};
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const int nck = nl * OW / 4;  // 16-byte chunks of the wave's output run
+#pragma unroll
+    for (int j = 0; j < OW / 4; ++j) {
+        const int q = 64 * j + lane;
+        if (q < nck) __builtin_nontemporal_store(*reinterpret_cast<const u32x4*>(xw + 4 * q), reinterpret_cast<u32x4*>(o) + q);
+    }
+}
+
 }  // namespace
 
 hipError_t launch_color_cv(const CvColorLaunch& L, hipStream_t s) {
@@ -334,6 +394,20 @@ hipError_t launch_color_cv(const CvColorLaunch& L, hipStream_t s) {
         const uintptr_t bits = reinterpret_cast<uintptr_t>(L.src) | reinterpret_cast<uintptr_t>(L.dst) |
                                (uintptr_t)L.src_img | (uintptr_t)L.src_row | (uintptr_t)L.dst_img | (uintptr_t)L.dst_row;
         G.aligned = (bits & 15) == 0;
+        const int px = L.esize == 4 ? 4 : 16;
+        if (G.aligned && L.w % px == 0 && tune(VACV_TUNE_RESIZE_DIRECT) != 2) {
+            // a wave per 64 units of a row (VACV_TUNE_RESIZE_DIRECT = 2: gray_kernel, A/B)
+            const int wrow = (upr + 63) / 64;
+            const dim3 gg((unsigned)(((int64_t)wrow * L.h + 3) / 4), (unsigned)L.n);
+            if (L.esize == 4) {
+                if (L.dcn == 4) hipLaunchKernelGGL((gray_x_kernel<4, float>), gg, dim3(256), 0, s, G, upr, wrow);
+                else hipLaunchKernelGGL((gray_x_kernel<3, float>), gg, dim3(256), 0, s, G, upr, wrow);
+            } else {
+                if (L.dcn == 4) hipLaunchKernelGGL((gray_x_kernel<4, unsigned char>), gg, dim3(256), 0, s, G, upr, wrow);
+                else hipLaunchKernelGGL((gray_x_kernel<3, unsigned char>), gg, dim3(256), 0, s, G, upr, wrow);
+            }
+            return hipGetLastError();
+        }
         if (L.esize == 4) {
             if (L.dcn == 4) hipLaunchKernelGGL((gray_kernel<4, float>), g, dim3(256), 0, s, G, upr);
             else hipLaunchKernelGGL((gray_kernel<3, float>), g, dim3(256), 0, s, G, upr);

@@ -1664,15 +1664,21 @@ def test_cvt_color_opencv_codes(ops, dev, oracle):
         assert_same(g[k, :, 1:27], oracle.yuv420_cv(yuv[k], COLOR_YUV2BGRA_NV21), "pitched rgba")
     g[:, :, 1:27] = 0
     assert not g.any(), "cvt_color wrote outside the window"
-    # 53 wide: elementwise (unaligned rows); 64 / 1920 wide: 4-pixel units
-    # with vector loads and stores; a pitched source (a 61-wide slice of 64)
+    # 53 wide: elementwise (unaligned rows); 64 / 1920 / 1104 wide: units with
+    # vector loads and stores (gray_x_kernel: a wave per row's 64 units, the
+    # last one partial at 1920 and 1104); a pitched source (a 61-wide slice of 64)
     for dt in (np.uint8, np.float32):
-        for shape, crop in (((2, 37, 53), 53), ((2, 36, 64), 64), ((2, 8, 1920), 1920), ((2, 9, 64), 61)):
+        for shape, crop in (((2, 37, 53), 53), ((2, 36, 64), 64), ((2, 8, 1920), 1920), ((2, 5, 1104), 1104),
+                            ((2, 9, 64), 61)):
             full = (rng.integers(0, 256, shape).astype(dt) * (dt(0.5) if dt == np.float32 else 1)).astype(dt)
             gray = full[:, :, :crop]
-            got = host(ops.cvt_color(to_dev(full, dev)[:, :, :crop], COLOR_GRAY2BGR))
+            a = ops.cvt_color(to_dev(full, dev)[:, :, :crop], COLOR_GRAY2BGR)
+            got = host(a)
             for k in range(2):
                 assert_same(got[k], oracle.gray_to_bgr(np.ascontiguousarray(gray[k])), f"gray2bgr {dt} {shape} {crop}")
+            with ops.tuning(RESIZE_DIRECT=2):  # gray_kernel: lanes write their own pixels
+                b = ops.cvt_color(to_dev(full, dev)[:, :, :crop], COLOR_GRAY2BGR)
+            assert torch.equal(a, b), f"gray2bgr {dt} {shape} {crop}: the unit kernels differ"
 
 
 def test_warp_flags_nearest_and_inverse_map(ops, dev, oracle):
