@@ -61,6 +61,7 @@ struct LanczosTabsDev {
                          // the first source row of the row's band; [8] its last tap row; [9] 1 if row y + 1's
                          // last tap row is the same
     int xmin, xmax;      // output columns [xmin, xmax) take the unrolled horizontal sum
+    int run_ni;          // lanczos_u8_kernel: 16-byte loads per lane of a staged run (0: per-lane windows)
 };
 
 struct LanczosLaunch {
@@ -520,7 +521,12 @@ __global__ void __launch_bounds__(64 * kLzWaves) lanczos_kernel(LanczosLaunch L,
 #ifndef VACV_LZR_D
 #define VACV_LZR_D 4  // windows in flight per wave (a divisor of 8, the unroll)
 #endif
-template <int OUT, int CC>
+// NI > 0 (round 5): the wave's source run of a row (the 64 lanes' windows,
+// <= NI KiB, host-checked) moves as NI lane-contiguous 16-byte loads and
+// reaches the lanes' windows through the wave's own LDS slice: at a 3x
+// downscale one 600-byte instruction instead of two per lane (28 bytes per
+// lane for 9 new ones).  NI = 0: every lane loads its own window.
+template <int OUT, int CC, int NI>
 __global__ void __launch_bounds__(64 * kLzWaves)
 #if VACV_LZ_WPE
 __attribute__((amdgpu_waves_per_eu(VACV_LZ_WPE)))
@@ -570,6 +576,29 @@ lanczos_u8_kernel(LanczosLaunch L, int strips, int bands, int band_rows,
     for (int m = 0; m < 4; ++m) cp[m] = ((uint32_t)cw[2 * m] & 0xFFFFu) | ((uint32_t)cw[2 * m + 1] << 16);
     const uint32_t wbyte = (uint32_t)(wstart * CC) + srs.delta;
     const uint32_t wsh = wbyte & 3u;
+    // NI > 0: the run's first byte (lane 0 has the smallest window start) and
+    // this lane's window within the wave's slice
+    const uint32_t wrun = (uint32_t)__builtin_amdgcn_readfirstlane((int)(wbyte & ~15u));
+    const uint32_t wofs = (wbyte & ~3u) - wrun;
+    __shared__ __attribute__((aligned(16))) uint32_t xs[NI > 0 ? kLzWaves : 1][NI > 0 ? 256 * NI : 1];
+    using RowBuf = typename std::conditional<(NI > 0), u32x4[NI > 0 ? NI : 1], uint32_t[ND]>::type;
+    auto load_run = [&](auto safe_c, u32x4 (&t)[NI > 0 ? NI : 1], int r) {
+        constexpr bool SAFE = decltype(safe_c)::value;
+#pragma unroll
+        for (int i = 0; i < (NI > 0 ? NI : 1); ++i) {
+            const uint32_t a = (uint32_t)r * rp + wrun + 16u * (uint32_t)(64 * i + lane);
+            if (!SAFE || a + 16u <= slimit) {
+                t[i] = __builtin_amdgcn_raw_buffer_load_b128(srs.r, (int)a, 0, 0);
+            } else {  // the chunk overhangs the plane's end: bytewise (past it: zeros)
+                uint32_t v[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+                for (int e = 0; e < 16; ++e)
+                    if (a + (uint32_t)e < slimit)
+                        v[e >> 2] |= (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(srs.r, (int)(a + (uint32_t)e), 0, 0) << (8 * (e & 3));
+                t[i] = u32x4{v[0], v[1], v[2], v[3]};
+            }
+        }
+    };
 
     auto load = [&](auto safe_c, uint32_t (&d)[ND], int r) {
         constexpr bool SAFE = decltype(safe_c)::value;
@@ -607,6 +636,23 @@ lanczos_u8_kernel(LanczosLaunch L, int strips, int bands, int band_rows,
 #pragma unroll
         for (int q = 0; q < ND - 1; ++q) wv[q] = __builtin_amdgcn_alignbyte(d[q + 1], d[q], wsh);
         lz_h_u8<CC, 0, ND - 1>(wv, cp, hv);
+    };
+    // NI > 0: the run through the wave's slice, then this lane's window
+    auto hrow_run = [&](const u32x4 (&t)[NI > 0 ? NI : 1], int (&hv)[CC]) {
+        uint32_t* xw = xs[NI > 0 ? wave : 0];
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();  // the previous row's window reads are done
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+        for (int i = 0; i < (NI > 0 ? NI : 1); ++i) *reinterpret_cast<u32x4*>(xw + 4 * (64 * i + lane)) = t[i];
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        uint32_t d[ND];
+        const uint32_t* wp = xw + (wofs >> 2);
+#pragma unroll
+        for (int q = 0; q < ND; ++q) d[q] = wp[q];
+        hrow(d, hv);
     };
 
     unsigned char* dp = const_cast<unsigned char*>(L.dst.base) + (int64_t)img * L.dst.img_pitch +
@@ -705,16 +751,21 @@ lanczos_u8_kernel(LanczosLaunch L, int strips, int bands, int band_rows,
             same = lz_const(L.t.yrec, 16 * yy + 9);
         };
         fetch(y);
-        uint32_t buf[D][ND];
+        RowBuf buf[D];
+        auto issue = [&](RowBuf& b, int r) {
+            if constexpr (NI > 0) load_run(safe_c, b, r);
+            else load(safe_c, b, r);
+        };
 #pragma unroll
-        for (int u = 0; u < D; ++u) load(safe_c, buf[u], min(rs + u, re));
+        for (int u = 0; u < D; ++u) issue(buf[u], min(rs + u, re));
 #pragma unroll
         for (int u = 0; u + 1 < D; ++u) __builtin_amdgcn_raw_buffer_store_b32(0u, drs.r, (int)kOobStore, 0, 0);
         for (int r = rs;; r += 8) {
 #pragma unroll
             for (int u = 0; u < 8; ++u) {
                 const int rr = r + u;
-                hrow(buf[u % D], hs[u]);
+                if constexpr (NI > 0) hrow_run(buf[u % D], hs[u]);
+                else hrow(buf[u % D], hs[u]);
                 if (need == rr) {  // uniform; y < y1 while the walk runs
                     // the first output row of the step outside any loop: the
                     // multiplies then take the register rows as they are (in
@@ -739,11 +790,12 @@ lanczos_u8_kernel(LanczosLaunch L, int strips, int bands, int band_rows,
                     __builtin_amdgcn_raw_buffer_store_b32(0u, drs.r, (int)kOobStore, 0, 0);
                 }
                 if (y >= y1) return;  // the band's last output row is out
-                load(safe_c, buf[u % D], min(rr + D, re));
+                issue(buf[u % D], min(rr + D, re));
             }
         }
     };
-    const bool over = (uint32_t)re * rp + (wbyte & ~3u) + 4u * ND > slimit;
+    const bool over = NI > 0 ? (uint32_t)re * rp + wrun + 1024u * (uint32_t)NI > slimit
+                             : (uint32_t)re * rp + (wbyte & ~3u) + 4u * ND > slimit;
     if (__builtin_amdgcn_ballot_w64(over) != 0) walk(std::integral_constant<bool, true>());
     else walk(std::integral_constant<bool, false>());
 }
@@ -872,6 +924,22 @@ std::mutex g_lz_mu;
 std::map<std::tuple<int, int, int, int, int, double, double, int>, CachedLanczos> g_lz_tabs;
 bool free_lz(CachedLanczos& c) { return hipFree(c.dev) == hipSuccess; }
 
+// lanczos_u8_kernel's staged runs: the 16-byte loads per lane (1 or 2) that
+// cover every strip's windows (the kernel's run starts at lane 0's window
+// rounded down to 16 bytes; 16 more for a base that is not 16-byte aligned),
+// or 0 where a strip's windows span more than 2 KiB
+int lanczos_run_loads(const ResizeLaunch& R, const std::vector<int>& xofs) {
+    const int cc = R.src.cc, w = R.src.w, nd = (8 * cc + 6) / 4;
+    auto ws = [&](int x) { return std::min(std::max(xofs[x] - 3, 0), w - 8); };
+    int need = 0;
+    for (int s0 = 0; s0 < R.dst.w; s0 += 64) {
+        const int xl = std::min(s0 + 63, R.dst.w - 1);
+        const int start = (ws(s0) * cc) & ~15, end = ((ws(xl) * cc) & ~3) + 4 * nd;
+        need = std::max(need, end - start + 16);
+    }
+    return need <= 1024 ? 1 : need <= 2048 ? 2 : 0;
+}
+
 int lanczos_tables(const ResizeLaunch& R, double inv_x, double inv_y, int band_rows, hipStream_t s, LanczosTabsDev& out) {
     int device = 0;
     if (hipGetDevice(&device) != hipSuccess) return VACV_ERR_HIP;
@@ -941,6 +1009,7 @@ int lanczos_tables(const ResizeLaunch& R, double inv_x, double inv_y, int band_r
         c.t.yrec = reinterpret_cast<const int*>(b + o7);
         c.t.xmin = xmin;
         c.t.xmax = xmax;
+        c.t.run_ni = R.src.w >= 8 ? lanczos_run_loads(R, xo) : 0;
         it = g_lz_tabs.emplace(key, c).first;
     }
     out = it->second.t;
@@ -964,18 +1033,27 @@ hipError_t launch_out(const LanczosLaunch& A, const LzGrid& g, hipStream_t s) {
     return hipGetLastError();
 }
 
-template <int OUT>
-hipError_t launch_u8(const LanczosLaunch& A, const LzGrid& g, hipStream_t s) {
+template <int OUT, int NI>
+hipError_t launch_u8_ni(const LanczosLaunch& A, const LzGrid& g, hipStream_t s) {
     const dim3 grid((unsigned)(g.xcd_per > 0 ? 8 * g.xcd_per : g.blocks)), block(64 * kLzWaves);
     switch (A.src.cc) {
-        case 1: hipLaunchKernelGGL((lanczos_u8_kernel<OUT, 1>), grid, block, 0, s, A, g.strips, g.bands, g.band_rows, g.blocks, g.xcd_per); break;
-        case 2: hipLaunchKernelGGL((lanczos_u8_kernel<OUT, 2>), grid, block, 0, s, A, g.strips, g.bands, g.band_rows, g.blocks, g.xcd_per); break;
-        case 3: hipLaunchKernelGGL((lanczos_u8_kernel<OUT, 3>), grid, block, 0, s, A, g.strips, g.bands, g.band_rows, g.blocks, g.xcd_per); break;
-        case 4: hipLaunchKernelGGL((lanczos_u8_kernel<OUT, 4>), grid, block, 0, s, A, g.strips, g.bands, g.band_rows, g.blocks, g.xcd_per); break;
+        case 1: hipLaunchKernelGGL((lanczos_u8_kernel<OUT, 1, NI>), grid, block, 0, s, A, g.strips, g.bands, g.band_rows, g.blocks, g.xcd_per); break;
+        case 2: hipLaunchKernelGGL((lanczos_u8_kernel<OUT, 2, NI>), grid, block, 0, s, A, g.strips, g.bands, g.band_rows, g.blocks, g.xcd_per); break;
+        case 3: hipLaunchKernelGGL((lanczos_u8_kernel<OUT, 3, NI>), grid, block, 0, s, A, g.strips, g.bands, g.band_rows, g.blocks, g.xcd_per); break;
+        case 4: hipLaunchKernelGGL((lanczos_u8_kernel<OUT, 4, NI>), grid, block, 0, s, A, g.strips, g.bands, g.band_rows, g.blocks, g.xcd_per); break;
         default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
 }
+
+template <int OUT>
+hipError_t launch_u8(const LanczosLaunch& A, const LzGrid& g, int ni, hipStream_t s) {
+    if (ni == 1) return launch_u8_ni<OUT, 1>(A, g, s);
+    if (ni == 2) return launch_u8_ni<OUT, 2>(A, g, s);
+    return launch_u8_ni<OUT, 0>(A, g, s);
+}
+
+
 
 template <typename TIn>
 hipError_t launch_t(const LanczosLaunch& A, const LzGrid& g, hipStream_t s) {
@@ -1031,10 +1109,13 @@ int launch_resize_lanczos(const ResizeLaunch& R, double inv_x, double inv_y, hip
     g.blocks = (int)((tasks + kLzWaves - 1) / kLzWaves);
     g.xcd_per = tune_or(VACV_TUNE_DIRECT_XCD, 1) ? (g.blocks + 7) / 8 : 0;
     hipError_t e;
-    if (R.src.esize == 1 && tune_or(VACV_TUNE_LANCZOS_KERNEL, 0) == 0) {
-        if (A.out == kOutSame) e = launch_u8<kOutSame>(A, g, s);
-        else if (A.out == kOutF32) e = launch_u8<kOutF32>(A, g, s);
-        else e = launch_u8<kOutNorm>(A, g, s);
+    const int knob = tune_or(VACV_TUNE_LANCZOS_KERNEL, 0);
+    if (R.src.esize == 1 && (knob == 0 || knob == 2)) {
+        // the staged runs where they fit (LANCZOS_KERNEL = 2: per-lane windows, A/B)
+        const int ni = knob == 0 ? A.t.run_ni : 0;
+        if (A.out == kOutSame) e = launch_u8<kOutSame>(A, g, ni, s);
+        else if (A.out == kOutF32) e = launch_u8<kOutF32>(A, g, ni, s);
+        else e = launch_u8<kOutNorm>(A, g, ni, s);
     } else {
         e = R.src.esize == 1 ? launch_t<uint8_t>(A, g, s) : launch_t<float>(A, g, s);
     }

@@ -329,7 +329,7 @@ enum {
     VACV_TUNE_WARP_FRAMES = 15,      /* u8 CONSTANT warp, LDS-staged kernel: frames per workgroup */
     VACV_TUNE_WARP_TILE_H = 16,      /* u8 CONSTANT warp, LDS-staged kernel: tile rows (16 or 32) */
     VACV_TUNE_WARP_SLOTS = 17,       /* u8 CONSTANT warp, LDS-staged kernel: source boxes in the LDS ring (2-4) */
-    VACV_TUNE_LANCZOS_KERNEL = 18,   /* u8 INTER_LANCZOS4: 0 register-ring kernel, 1 the LDS-ring kernel (A/B) */
+    VACV_TUNE_LANCZOS_KERNEL = 18,   /* u8 INTER_LANCZOS4: 0 register-ring kernel (staged runs where they fit), 1 the LDS-ring kernel, 2 the register ring with per-lane windows (A/B) */
     VACV_TUNE_COUNT = 19
 };
 /* value < 0 restores the built-in choice.  Returns VACV_OK or INVALID_ARG. */

@@ -518,21 +518,25 @@ def test_resize_lanczos4(ops, dev, oracle):
     big = np.stack([synthetic_image(830 + k, 1080, 1920, 3) for k in range(2)])
     got = host(ops.resize(to_dev(big, dev), 640, 360, interpolation=INTER_LANCZOS4))
     assert_same(got[1], oracle.resize_lanczos4(big[1], 640, 360), "lanczos 1080p -> 640x360")
-    # u8: the register-ring kernel (default) against the LDS-ring kernel
-    # (LANCZOS_KERNEL=1) on batches of 1, 5 and 64 frames -- different band
-    # heights, so different band-relative coefficient tables -- and on all
-    # three output types; the oracle pins one frame of each
+    # u8: the register-ring kernel (default: staged source runs, 1 or 2 KiB
+    # per wave row -- 3x and 10x downscales, an upscale) against the LDS-ring
+    # kernel (LANCZOS_KERNEL=1) and its own per-lane windows (=2) on batches
+    # of 1, 5 and 64 frames -- different band heights, so different
+    # band-relative coefficient tables -- and on all three output types; the
+    # oracle pins one frame of each
     src = to_dev(np.stack([synthetic_image(850 + k, 270, 481, 3) for k in range(64)]), dev)
     for n in (1, 5, 64):
-        for wo, ho in [(160, 90), (333, 401)]:
+        for wo, ho in [(160, 90), (333, 401), (48, 30)]:
             calls = [lambda: ops.resize(src[:n], wo, ho, interpolation=INTER_LANCZOS4),
                      lambda: ops.resize_normalize(src[:n], wo, ho, MEAN, STD, interpolation=INTER_LANCZOS4)]
             for j, fn in enumerate(calls):
                 a = fn()
-                with ops.tuning(LANCZOS_KERNEL=1):
-                    b = fn()
-                torch.cuda.synchronize(dev)
-                assert torch.equal(a.view(torch.uint8), b.view(torch.uint8)), f"lanczos kernels differ n={n} {wo}x{ho} call {j}"
+                for knob in (1, 2):
+                    with ops.tuning(LANCZOS_KERNEL=knob):
+                        b = fn()
+                    torch.cuda.synchronize(dev)
+                    assert torch.equal(a.view(torch.uint8), b.view(torch.uint8)), \
+                        f"lanczos kernels differ n={n} {wo}x{ho} call {j} LANCZOS_KERNEL={knob}"
             k = n - 1
             full = host(ops.resize(src[:n], wo, ho, interpolation=INTER_LANCZOS4))
             assert_same(full[k], oracle.resize_lanczos4(host(src[k]), wo, ho), f"lanczos batch n={n} {wo}x{ho}")
