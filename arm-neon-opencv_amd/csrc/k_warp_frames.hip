@@ -629,11 +629,16 @@ constexpr int kExpTab = 16 + 12 * kExpRows + 64 * 4 * kRingMaxIt + kExpUnits + 1
 #endif
 // NN: INTER_NEAREST (OpenCV 2.4's warpAffine map, see warp_nearest_kernel in
 // k_warp.hip): the same staging, one tap per pixel, no blend.
-template <int OUT, int NP, bool NN>
+// WIDE (round 5): 128 x (2 NP)-pixel tiles instead of 64 x (4 NP), the same
+// pixel count; pixel j of a lane is column lane + 64 (j & 1) of row j >> 1, so
+// a tile's u8 output rows are 384 bytes = 3 whole 128-byte lines (64-pixel
+// rows were 192 bytes, the line between two tiles written by both).
+template <int OUT, int NP, bool NN, bool WIDE = false>
 __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(VACV_EXP_WPE)))
 warp_exp_kernel(WarpLaunch L, int gx, int gy, int kf, int slot_bytes, int exp_units, int dst_al) {
     constexpr int CC = 3;
-    constexpr int TH = 4 * NP;
+    constexpr int TW = WIDE ? 128 : kFrTileW;
+    constexpr int TH = WIDE ? 2 * NP : 4 * NP;
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     // [48 B pad][slot 0][slot 1][64 B pad] (the re-lay reads up to 45 B before
     // and 47 B after a row's chunks: bytes of no tapped pixel)
@@ -674,17 +679,19 @@ warp_exp_kernel(WarpLaunch L, int gx, int gy, int kf, int slot_bytes, int exp_un
     const int f0 = fg * kf, f1 = min(f0 + kf, nfr);
     const float* M = L.inv;
     const float wlim = (float)(L.src.w - 1), hlim = (float)(L.src.h - 1);
-    const int x = bx * kFrTileW + lane;
-    const int yw = by * TH + wave * NP;
+    const int xl = bx * TW + lane;
+    const int yw = by * TH + wave * (WIDE ? NP / 2 : NP);
+    auto px_x = [&](int j) { return WIDE ? xl + 64 * (j & 1) : xl; };  // pixel j's column
+    auto px_y = [&](int j) { return yw + (WIDE ? (j >> 1) : j); };    // and row
     const uint32_t rp = (uint32_t)L.src.row_pitch;
 
     // ---- 1. per-pixel taps, once for every frame (warp_affine_naive.cpp:23-42)
-    const float axm = M[0] * (float)x, aym = M[3] * (float)x;
     uint32_t sxy[NP], vwa[NP], okm = 0;
     int xmin = INT_MAX, xmax = INT_MIN, ymin = INT_MAX, ymax = INT_MIN;
 #pragma unroll
     for (int j = 0; j < NP; ++j) {
-        const int y = yw + j;
+        const int x = px_x(j), y = px_y(j);
+        const float axm = M[0] * (float)x, aym = M[3] * (float)x;
         bool ok;
         int sx, sy;
         if constexpr (NN) {
@@ -953,7 +960,7 @@ warp_exp_kernel(WarpLaunch L, int gx, int gy, int kf, int slot_bytes, int exp_un
     };
 
     const uint32_t dpitch = (uint32_t)L.dst.row_pitch;
-    const bool tile_full = bx * kFrTileW + kFrTileW <= L.dst.w && by * TH + TH <= L.dst.h && dst_al;
+    const bool tile_full = bx * TW + TW <= L.dst.w && by * TH + TH <= L.dst.h && dst_al;
     constexpr uint32_t kOob = 0x80000000u;
     // vector-memory stores per sampled frame (the wait counts; every one is
     // issued): full tiles one 12-byte store per 4 rows (u8) or one 16-byte
@@ -980,7 +987,7 @@ warp_exp_kernel(WarpLaunch L, int gx, int gy, int kf, int slot_bytes, int exp_un
     ChanNorm cn[CC];
     auto emit = [&](auto full_c, int f, int j, const uint32_t (&vv)[CC]) {
         constexpr bool FULL = decltype(full_c)::value;
-        const int y = yw + j;
+        const int x = px_x(j), y = px_y(j);
         const bool inside = FULL || (x < L.dst.w && y < L.dst.h);
         unsigned char* dbase = const_cast<unsigned char*>(L.dst.base) + (int64_t)f * L.dst.img_pitch;
         const Rsrc drs = make_rsrc(dbase, L.dst.plane_bytes);
@@ -994,7 +1001,7 @@ warp_exp_kernel(WarpLaunch L, int gx, int gy, int kf, int slot_bytes, int exp_un
                 const uint32_t off = (VACV_RING_DBG & 8) || (lane & 3) == 3
                                          ? kOob
                                          : (uint32_t)y * dpitch + drs.delta +
-                                               (uint32_t)(bx * kFrTileW * CC + 12 * (lane >> 2) + 4 * (lane & 3));
+                                               (uint32_t)((x - lane) * CC + 12 * (lane >> 2) + 4 * (lane & 3));
                 __builtin_amdgcn_raw_buffer_store_b32(word, drs.r, (int)off, 0, VACV_RING_SAUX);
             } else if constexpr (FULL) {
                 *reinterpret_cast<uint32_t*>(xch + 256 * (j & 3) + 4 * lane) = own;
@@ -1002,13 +1009,16 @@ warp_exp_kernel(WarpLaunch L, int gx, int gy, int kf, int slot_bytes, int exp_un
                     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
                     __builtin_amdgcn_wave_barrier();
                     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-                    const int r = lane >> 4, q = lane & 15;
-                    const u32x4 p = *reinterpret_cast<const u32x4*>(xch + 256 * r + 16 * q);
+                    // 4 rows of 64 pixels (WIDE: 2 rows of 128, entries
+                    // (row, half) = j & 3); a lane stores 4 pixels, 12 bytes
+                    const int r = WIDE ? lane >> 5 : lane >> 4, q = WIDE ? lane & 31 : lane & 15;
+                    const u32x4 p = *reinterpret_cast<const u32x4*>(
+                        xch + (WIDE ? 256 * (2 * r + (q >> 4)) + 16 * (q & 15) : 256 * r + 16 * q));
                     typedef unsigned int u32x3 __attribute__((ext_vector_type(3)));
                     const u32x3 o = {__builtin_amdgcn_perm(p[1], p[0], 0x04020100u),
                                      __builtin_amdgcn_perm(p[2], p[1], 0x05040201u),
                                      __builtin_amdgcn_perm(p[3], p[2], 0x06050402u)};
-                    const uint32_t off = (VACV_RING_DBG & 8) ? kOob : (uint32_t)(y - 3 + r) * dpitch + drs.delta + (uint32_t)(bx * kFrTileW * CC + 12 * q);
+                    const uint32_t off = (VACV_RING_DBG & 8) ? kOob : (uint32_t)(y - (WIDE ? 1 : 3) + r) * dpitch + drs.delta + (uint32_t)(bx * TW * CC + 12 * q);
                     __builtin_amdgcn_raw_buffer_store_b96(o, drs.r, (int)off, 0, VACV_RING_SAUX);
                 }
             } else {
@@ -1034,7 +1044,7 @@ warp_exp_kernel(WarpLaunch L, int gx, int gy, int kf, int slot_bytes, int exp_un
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
                 const u32x4 p = *reinterpret_cast<const u32x4*>(xch + 16 * (lane % (3 * 16)));
                 const uint32_t off = lane < 3 * 16 ? (uint32_t)y * dpitch + drs.delta +
-                                                         (uint32_t)(bx * kFrTileW * CC * 4 + 16 * lane)
+                                                         (uint32_t)((x - lane) * CC * 4 + 16 * lane)
                                                    : kOob;
                 __builtin_amdgcn_raw_buffer_store_b128(p, drs.r, (int)off, 0, VACV_RING_SAUX);
             } else {
@@ -1114,7 +1124,7 @@ warp_exp_kernel(WarpLaunch L, int gx, int gy, int kf, int slot_bytes, int exp_un
                     for (int q = 0; q < CC; ++q) vv[q] = tl << (24 - 8 * q);
                 } else {
                     uint32_t tl, tr, bl, br;
-                    direct_taps<CC>(L, sp, x, yw + j, tl, tr, bl, br);
+                    direct_taps<CC>(L, sp, px_x(j), px_y(j), tl, tr, bl, br);
                     blend3(j, tl, tr, bl, br, vv);
                 }
                 emit(edge_t(), f, j, vv);
@@ -1188,11 +1198,11 @@ int64_t frames_resident(K kernel, size_t lds) {
     return r;
 }
 
-template <int OUT, int NP, bool NN = false>
+template <int OUT, int NP, bool NN = false, bool WIDE = false>
 hipError_t launch_exp(const WarpLaunch& L, const WarpFramesPlan& P, hipStream_t s) {
-    constexpr int TH = 4 * NP;
-    const int gx = (L.dst.w + kFrTileW - 1) / kFrTileW, gy = (L.dst.h + TH - 1) / TH;
-    auto kern = warp_exp_kernel<OUT, NP, NN>;
+    constexpr int TW = WIDE ? 128 : kFrTileW, TH = WIDE ? 2 * NP : 4 * NP;
+    const int gx = (L.dst.w + TW - 1) / TW, gy = (L.dst.h + TH - 1) / TH;
+    auto kern = warp_exp_kernel<OUT, NP, NN, WIDE>;
     int kf = P.kf;
     if (kf <= 0) {
         const int64_t res = std::max<int64_t>(frames_resident(kern, (size_t)P.lds), 256);
@@ -1239,7 +1249,10 @@ hipError_t launch_frames_np(const WarpLaunch& L, const WarpFramesPlan& P, hipStr
 
 template <int OUT>
 hipError_t launch_frames_cc(const WarpLaunch& L, const WarpFramesPlan& P, hipStream_t s) {
-    if (P.se > 0) return P.th == 16 ? launch_exp<OUT, 4>(L, P, s) : launch_exp<OUT, 8>(L, P, s);
+    if (P.se > 0) {
+        if (P.tw == 128) return launch_exp<OUT, 8, false, true>(L, P, s);  // 128 x 16 tiles
+        return P.th == 16 ? launch_exp<OUT, 4>(L, P, s) : launch_exp<OUT, 8>(L, P, s);
+    }
     switch (L.src.cc) {
         case 1: return launch_frames_np<1, OUT>(L, P, s);
         case 2: return launch_frames_np<2, OUT>(L, P, s);
@@ -1350,12 +1363,12 @@ bool ring_layout_th(const WarpLaunch& L, WarpFramesPlan& P, int th) {
 struct ExpNeeds {
     int rows = 0, chunks = 0, units = 0;
 };
-ExpNeeds exp_needs(const WarpLaunch& L, int th, bool nn) {
+ExpNeeds exp_needs(const WarpLaunch& L, int th, bool nn, int tw = kFrTileW) {
     constexpr int CC = 3;
     const float* M = L.inv;
     const double* Md = L.invd;
     const float wlim = (float)(L.src.w - 1), hlim = (float)(L.src.h - 1);
-    const int gx = (L.dst.w + kFrTileW - 1) / kFrTileW, gy = (L.dst.h + th - 1) / th;
+    const int gx = (L.dst.w + tw - 1) / tw, gy = (L.dst.h + th - 1) / th;
     // the kernel's tap of pixel (x, y): (sx, sy) or false outside
     auto tap = [&](int x, int y, int& sx, int& sy) {
         if (x >= L.dst.w || y >= L.dst.h) return false;
@@ -1382,7 +1395,7 @@ ExpNeeds exp_needs(const WarpLaunch& L, int th, bool nn) {
         for (int bx = 0; bx < gx; ++bx) {
             int xmin = INT_MAX, xmax = INT_MIN, ymin = INT_MAX, ymax = INT_MIN, sx, sy;
             for (int y = by * th; y < by * th + th; ++y)
-                for (int x = bx * kFrTileW; x < bx * kFrTileW + kFrTileW; ++x)
+                for (int x = bx * tw; x < bx * tw + tw; ++x)
                     if (tap(x, y, sx, sy)) {
                         xmin = std::min(xmin, sx);
                         xmax = std::max(xmax, sx);
@@ -1394,7 +1407,7 @@ ExpNeeds exp_needs(const WarpLaunch& L, int th, bool nn) {
             rmin.assign(R + 1, INT_MAX);
             rmax.assign(R + 1, -1);
             for (int y = by * th; y < by * th + th; ++y)
-                for (int x = bx * kFrTileW; x < bx * kFrTileW + kFrTileW; ++x)
+                for (int x = bx * tw; x < bx * tw + tw; ++x)
                     if (tap(x, y, sx, sy)) {
                         const int p = sx - bx0, r = sy - ymin;
                         rmin[r] = std::min(rmin[r], p);
@@ -1420,11 +1433,12 @@ ExpNeeds exp_needs(const WarpLaunch& L, int th, bool nn) {
 
 // warp_exp_kernel's LDS: two compact raw slots, the image (at least the setup
 // tables), the output exchange; <= 40 KiB keeps 4 workgroups per CU
-bool exp_layout_th(const WarpLaunch& L, WarpFramesPlan& P, int th, bool nn = false) {
-    const ExpNeeds n = exp_needs(L, th, nn);
+bool exp_layout_th(const WarpLaunch& L, WarpFramesPlan& P, int th, bool nn = false, int tw = kFrTileW) {
+    const ExpNeeds n = exp_needs(L, th, nn, tw);
     const int n_inst = (n.chunks + 63) / 64;
     if (n.rows > kExpRows || n_inst > 4 * kRingMaxIt || n.units > kExpUnits) return false;
     P.th = th;
+    P.tw = tw;
     P.se = 1;
     P.raw_bytes = std::max(n_inst, 1) * 1024;
     P.exp_units = n.units;
@@ -1445,8 +1459,15 @@ bool frames_layout(const WarpLaunch& L, WarpFramesPlan& P) {
     const int th_knob = tune(VACV_TUNE_WARP_TILE_H);
     P.se = 0;
     P.raw_bytes = 0;
+    P.tw = kFrTileW;
     if (L.src.cc == 3 && L.src.planes == 1 && tune(VACV_TUNE_WARP_KERNEL) != 6) {
         WarpFramesPlan Q = P;
+        // 128 x 16 tiles (VACV_TUNE_RESIZE_TILE_W = 128): whole-line u8 output rows
+        if (tune(VACV_TUNE_RESIZE_TILE_W) == 128 && exp_layout_th(L, Q, 16, false, 128)) {
+            P = Q;
+            return true;
+        }
+        Q = P;
         // 32-row tiles (fp32 output too: 0.4155 vs 0.4398 ms normalised at
         // 720p rot15 x128, although its instance spills a few registers)
         const int th0 = 32;
@@ -1485,7 +1506,7 @@ bool warp_frames_plan(const WarpLaunch& L, WarpFramesPlan& P) {
     // layout of byte output carries the store exchange)
     struct Key {
         float inv[6];
-        int sw, sh, dw, dh, th, cc, bytes_out, slots, kernel;
+        int sw, sh, dw, dh, th, cc, bytes_out, slots, kernel, tw;
         bool operator<(const Key& o) const { return std::memcmp(this, &o, sizeof(Key)) < 0; }
     };
     Key k;
@@ -1496,6 +1517,7 @@ bool warp_frames_plan(const WarpLaunch& L, WarpFramesPlan& P) {
     k.bytes_out = L.out == kOutSame ? 1 : 0;
     k.slots = tune(VACV_TUNE_WARP_SLOTS);
     k.kernel = knob;
+    k.tw = tune(VACV_TUNE_RESIZE_TILE_W);
     static std::mutex mu;
     static std::map<Key, std::pair<bool, WarpFramesPlan>> cache;
     bool ok;
