@@ -50,6 +50,13 @@ constexpr int kGroupPx = 256;  // pixels per LDS exchange round (4 per lane)
 #ifndef VACV_DIRECT_LAUX
 #define VACV_DIRECT_LAUX 0
 #endif
+// resize_cols_kernel's fp32-output gathers at CW = 2 on 3 channels: non-temporal (round 5) -- its
+// blocks end on 128-byte lines (CW = 2 / the edge-lane shift), no source line
+// is read by two waves, so nothing is gained by keeping lines in L2
+// (kbench 0.2092 -> 0.2075 ms, bench kernel 0.2127 / 0.2122 -> 0.2107 / 0.2095)
+#ifndef VACV_COLS_LAUX
+#define VACV_COLS_LAUX 2
+#endif
 // column-stationary lanes (resize_cols_kernel) for one-tap-row geometries
 #ifndef VACV_DIRECT_COLS
 #define VACV_DIRECT_COLS 1
@@ -258,7 +265,7 @@ resize_cols_kernel(ResizeLaunch L, int col_blocks, int row_groups, int tasks, in
     constexpr int kOutPx = CC * (int)sizeof(TOut);
     constexpr int kHalf = 4 / CW;                  // rows per LDS exchange round
     constexpr int kRowB = 64 * CW * kOutPx;        // output bytes of one block row
-    constexpr int kLoadAux = OUT == kOutSame ? VACV_LOAD_AUX : VACV_DIRECT_LAUX;
+    constexpr int kLoadAux = OUT == kOutSame ? VACV_LOAD_AUX : (CW == 2 && CC == 3 ? VACV_COLS_LAUX : VACV_DIRECT_LAUX);
     constexpr int kStoreAux = OUT == kOutSame ? VACV_STORE_AUX : VACV_DIRECT_SAUX;
     __shared__ __attribute__((aligned(16))) unsigned char xch[4][kHalf * kRowB];
     const int lane = (int)threadIdx.x & 63;
