@@ -1225,6 +1225,9 @@ struct AreaLane {
 #ifndef VACV_AREA_XCH
 #define VACV_AREA_XCH 1  // area_lane_kernel: 1 lane-contiguous 16-byte loads + an LDS exchange for whole waves (0.3325 vs 0.3708 ms)
 #endif
+#ifndef VACV_AREA_LAUX
+#define VACV_AREA_LAUX 0  // area_lane_kernel's exchange-path loads: cache policy bits (2 non-temporal)
+#endif
 #ifndef VACV_AREA_RG
 #define VACV_AREA_RG 1  // area_lane_kernel: output rows per wave, the next row's loads in flight while one is summed (1 / 2 / 4 / 8: 0.369 / 0.382 / 0.385 / 0.418 ms)
 #endif
@@ -1385,7 +1388,7 @@ __global__ void __launch_bounds__(kBlock) area_lane_kernel(ResizeLaunch L, int b
 #pragma unroll
                 for (int i = 0; i < NI; ++i) {
                     const int q = 64 * i + lane;
-                    t[i] = q < NCK ? __builtin_amdgcn_raw_buffer_load_b128(srs.r, (int)(ry + (uint32_t)r * rp + 16u * (uint32_t)q), 0, 0)
+                    t[i] = q < NCK ? __builtin_amdgcn_raw_buffer_load_b128(srs.r, (int)(ry + (uint32_t)r * rp + 16u * (uint32_t)q), 0, VACV_AREA_LAUX)
                                    : u32x4{0u, 0u, 0u, 0u};
                 }
 #pragma unroll
