@@ -458,6 +458,11 @@ __global__ void match_bfrag_kernel(MatchLaunch M, int KB, uint4* bf, int* tsum) 
     bf[t] = make_uint4(d[0], d[1], d[2], d[3]);
 }
 
+#ifndef VACV_MATCH_PF
+#define VACV_MATCH_PF 4  // match_corr_mfma_kernel: (yy, kb) steps whose operands are in flight
+#endif
+constexpr int kMatchPF = VACV_MATCH_PF;
+
 // workgroup: 64 output rows x 64 output columns of one image; wave w: rows
 // 32 (w & 1) .., columns 32 (w >> 1) ..; the image block (rows r0 .. r0 + 63
 // + th - 1, bytes cn*x0 .. + stride) staged in LDS as i8 (XOR 0x80)
@@ -503,19 +508,59 @@ __global__ void __launch_bounds__(kBlock) match_corr_mfma_kernel(MatchLaunch M, 
     const unsigned char* abase = blk + (mi * 32 + i) * stride + ni * CN * 32 + 16 * h;
     const int per_part = M.th * KB * 64;
     v16i acc_hi = {}, acc_lo = {};
-    for (int yy = 0; yy < M.th; ++yy) {
-        const unsigned char* arow = abase + yy * stride;
-        const uint4* bh = bf + (int64_t)yy * KB * 64 + lane;
-        const uint4* bl = bh + per_part;
-        for (int kb = 0; kb < KB; ++kb) {
-            const v4i a = *reinterpret_cast<const v4i*>(arow + 32 * kb);
-            const uint4 vh = bh[kb * 64], vl = bl[kb * 64];
-            const v4i b_hi = {(int)vh.x, (int)vh.y, (int)vh.z, (int)vh.w};
-            const v4i b_lo = {(int)vl.x, (int)vl.y, (int)vl.z, (int)vl.w};
-            acc_hi = __builtin_amdgcn_mfma_i32_32x32x32_i8(a, b_hi, acc_hi, 0, 0, 0);
-            acc_lo = __builtin_amdgcn_mfma_i32_32x32x32_i8(a, b_lo, acc_lo, 0, 0, 0);
+    // The (yy, kb) steps flattened and software-pipelined (round 5): the B
+    // fragments come from L2 (shared by every workgroup), so each step's
+    // loads are issued kMatchPF steps ahead -- the loop that loaded them just
+    // before its two MFMAs waited out an L2 round trip per step
+    // (s_waitcnt vmcnt(0) between the loads and the MFMAs).
+    constexpr int PF = kMatchPF;
+    const int nit = M.th * KB;
+    v4i pa[2][PF];
+    uint4 ph[2][PF], pl[2][PF];
+    int fy = 0, fk = 0;  // the next step to fetch: (yy, kb), held at the last step once past it
+    auto fetch = [&](v4i& a, uint4& h, uint4& l) {
+        a = *reinterpret_cast<const v4i*>(abase + fy * stride + 32 * fk);
+        const uint4* bh = bf + ((int64_t)fy * KB + fk) * 64 + lane;
+        h = bh[0];
+        l = bh[per_part];
+        if (++fk == KB) {
+            if (fy + 1 < M.th) { fk = 0; ++fy; }
+            else fk = KB - 1;
         }
+    };
+    auto step = [&](const v4i& a, const uint4& h, const uint4& l) {
+        const v4i b_hi = {(int)h.x, (int)h.y, (int)h.z, (int)h.w};
+        const v4i b_lo = {(int)l.x, (int)l.y, (int)l.z, (int)l.w};
+        acc_hi = __builtin_amdgcn_mfma_i32_32x32x32_i8(a, b_hi, acc_hi, 0, 0, 0);
+        acc_lo = __builtin_amdgcn_mfma_i32_32x32x32_i8(a, b_lo, acc_lo, 0, 0, 0);
+    };
+    // two register sets of PF steps: the next set's operands are fetched
+    // before this set's MFMAs, so they are in flight during them (a single
+    // set was refetched only after its own MFMAs).  Past the last step a
+    // fetch reads the last step again, so every group issues all its loads
+    // and the compiler's waits count them exactly.
+#pragma unroll
+    for (int u = 0; u < PF; ++u) fetch(pa[0][u], ph[0][u], pl[0][u]);
+    int it = 0;
+    for (; it + 2 * PF <= nit; it += 2 * PF) {
+#pragma unroll
+        for (int u = 0; u < PF; ++u) fetch(pa[1][u], ph[1][u], pl[1][u]);
+#pragma unroll
+        for (int u = 0; u < PF; ++u) step(pa[0][u], ph[0][u], pl[0][u]);
+#pragma unroll
+        for (int u = 0; u < PF; ++u) fetch(pa[0][u], ph[0][u], pl[0][u]);
+#pragma unroll
+        for (int u = 0; u < PF; ++u) step(pa[1][u], ph[1][u], pl[1][u]);
     }
+    // the remainder (< 2 PF steps, uniform): set 0 holds steps it .. it + PF - 1
+#pragma unroll
+    for (int u = 0; u < PF; ++u) fetch(pa[1][u], ph[1][u], pl[1][u]);
+#pragma unroll
+    for (int u = 0; u < PF; ++u)
+        if (it + u < nit) step(pa[0][u], ph[0][u], pl[0][u]);
+#pragma unroll
+    for (int u = 0; u < PF; ++u)
+        if (it + PF + u < nit) step(pa[1][u], ph[1][u], pl[1][u]);
     const int64_t t128 = 128 * (int64_t)*tsum;  // T <= 255 * K*h: past int32 once multiplied
     const int x = x0 + ni * 32 + i;
     if (x >= M.rw) return;
