@@ -212,12 +212,29 @@ __global__ void __launch_bounds__(kBlock) match_integral_cols_kernel(MatchLaunch
     if (e >= step) return;
     double* sum = M.box + (int64_t)img * 2 * (M.ih + 1) * step;
     double* sq = sum + (int64_t)(M.ih + 1) * step;
+    // the same additions in the same order, kIntU rows at a time: their loads
+    // are issued together before the dependent adds (one row per step waited
+    // out a memory round trip per row of every column)
+    constexpr int kIntU = 16;
     double a = 0, b = 0;
-    for (int y = 1; y <= M.ih; ++y) {
-        a = a + sum[(int64_t)y * step + e];
-        b = b + sq[(int64_t)y * step + e];
-        sum[(int64_t)y * step + e] = a;
-        sq[(int64_t)y * step + e] = b;
+    for (int y = 1; y <= M.ih; y += kIntU) {
+        double va[kIntU], vb[kIntU];
+#pragma unroll
+        for (int u = 0; u < kIntU; ++u) {
+            if (y + u <= M.ih) {
+                va[u] = sum[(int64_t)(y + u) * step + e];
+                vb[u] = sq[(int64_t)(y + u) * step + e];
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < kIntU; ++u) {
+            if (y + u <= M.ih) {
+                a = a + va[u];
+                b = b + vb[u];
+                sum[(int64_t)(y + u) * step + e] = a;
+                sq[(int64_t)(y + u) * step + e] = b;
+            }
+        }
     }
 }
 
