@@ -204,6 +204,72 @@ __global__ void __launch_bounds__(kBlock) match_integral_rows_kernel(MatchLaunch
     }
 }
 
+// pass 1 for u8 (round 5): every running sum is an integer (< 2^31 for rows
+// up to 33,000 pixels: host-checked), exact in int32 and in double, so the
+// order of the additions cannot change a value -- a WAVE per row: 64
+// consecutive row elements per step, an inclusive scan across the lanes of
+// each channel (lanes cn apart), plus the channel's carry from the steps
+// before; its stores are 64 consecutive doubles (the per-thread kernel above
+// wrote one double per lane 30 KiB apart).
+__global__ void __launch_bounds__(kBlock) match_integral_rows_u8_kernel(MatchLaunch M) {
+    const int cn = M.cn;
+    const int lane = threadIdx.x & 63;
+    const int y = (int)blockIdx.x * (kBlock / 64) + __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
+    const int img = blockIdx.y;
+    if (y >= M.ih) return;  // whole wave
+    const int64_t step = (int64_t)(M.iw + 1) * cn;
+    double* sum = M.box + (int64_t)img * 2 * (M.ih + 1) * step;
+    double* sq = sum + (int64_t)(M.ih + 1) * step;
+    const unsigned char* src = M.img + (int64_t)img * M.img_pitch + (int64_t)y * M.img_row;
+    double* os = sum + (int64_t)(y + 1) * step;
+    double* oq = sq + (int64_t)(y + 1) * step;
+    if (lane < cn) {
+        os[lane] = 0;
+        oq[lane] = 0;
+    }
+    if (y == 0) {  // row 0 is zero
+        for (int64_t e = lane; e < step; e += 64) {
+            sum[e] = 0;
+            sq[e] = 0;
+        }
+    }
+    const int n = M.iw * cn;
+    int cs[4] = {0, 0, 0, 0}, cq[4] = {0, 0, 0, 0};  // per-channel carries (uniform)
+    int c0 = 0;                                        // the channel of the step's first element
+    for (int base = 0; base < n; base += 64) {
+        const int e = base + lane;
+        const int v = e < n ? (int)src[e] : 0;
+        const int c = (c0 + lane) % cn;
+        int s = v, q = v * v;
+        for (int d = cn; d < 64; d <<= 1) {
+            const int ts = __shfl_up(s, d, 64), tq = __shfl_up(q, d, 64);
+            if (lane >= d) {
+                s += ts;
+                q += tq;
+            }
+        }
+        s += c == 0 ? cs[0] : c == 1 ? cs[1] : c == 2 ? cs[2] : cs[3];
+        q += c == 0 ? cq[0] : c == 1 ? cq[1] : c == 2 ? cq[2] : cq[3];
+        if (e < n) {
+            os[cn + e] = (double)s;
+            oq[cn + e] = (double)q;
+        }
+        // each channel's carry: its last lane in this step
+        const int m = min(64, n - base);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            if (k < cn) {
+                const int last = m - 1 - (((c0 + m - 1 - k) % cn) + cn) % cn;
+                if (last >= 0) {
+                    cs[k] = __shfl(s, last, 64);
+                    cq[k] = __shfl(q, last, 64);
+                }
+            }
+        }
+        c0 = (c0 + 64) % cn;
+    }
+}
+
 // pass 2: sum[y+1][e] = sum[y][e] + rowsum, down each column, in place
 __global__ void __launch_bounds__(kBlock) match_integral_cols_kernel(MatchLaunch M) {
     const int64_t step = (int64_t)(M.iw + 1) * M.cn;
@@ -654,8 +720,14 @@ hipError_t launch_match_template(const MatchLaunch& M, hipStream_t s) {
     if (M.esize == 1) hipLaunchKernelGGL(match_tstats_kernel<uint8_t>, dim3(1), dim3(kBlock), 0, s, M);
     else hipLaunchKernelGGL(match_tstats_kernel<float>, dim3(1), dim3(kBlock), 0, s, M);
     const dim3 gr((M.ih * M.cn + kBlock - 1) / kBlock, M.n);
-    if (M.esize == 1) hipLaunchKernelGGL(match_integral_rows_kernel<uint8_t>, gr, dim3(kBlock), 0, s, M);
-    else hipLaunchKernelGGL(match_integral_rows_kernel<float>, gr, dim3(kBlock), 0, s, M);
+    if (M.esize == 1 && M.iw <= 33000) {
+        const dim3 gw((M.ih + kBlock / 64 - 1) / (kBlock / 64), M.n);
+        hipLaunchKernelGGL(match_integral_rows_u8_kernel, gw, dim3(kBlock), 0, s, M);
+    } else if (M.esize == 1) {
+        hipLaunchKernelGGL(match_integral_rows_kernel<uint8_t>, gr, dim3(kBlock), 0, s, M);
+    } else {
+        hipLaunchKernelGGL(match_integral_rows_kernel<float>, gr, dim3(kBlock), 0, s, M);
+    }
     const dim3 gc(((M.iw + 1) * M.cn + kBlock - 1) / kBlock, M.n);
     hipLaunchKernelGGL(match_integral_cols_kernel, gc, dim3(kBlock), 0, s, M);
     const dim3 gf((M.rw + kBlock - 1) / kBlock, M.rh, M.n);
