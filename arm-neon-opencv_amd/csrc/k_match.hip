@@ -270,35 +270,32 @@ __global__ void __launch_bounds__(kBlock) match_integral_rows_u8_kernel(MatchLau
     }
 }
 
-// pass 2: sum[y+1][e] = sum[y][e] + rowsum, down each column, in place
+// pass 2: sum[y+1][e] = sum[y][e] + rowsum, down each column, in place; a
+// thread per column of ONE of the two images (sum, sqsum: twice the threads
+// of one per column pair)
 __global__ void __launch_bounds__(kBlock) match_integral_cols_kernel(MatchLaunch M) {
     const int64_t step = (int64_t)(M.iw + 1) * M.cn;
-    const int e = blockIdx.x * kBlock + threadIdx.x;
+    const int64_t g = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     const int img = blockIdx.y;
-    if (e >= step) return;
-    double* sum = M.box + (int64_t)img * 2 * (M.ih + 1) * step;
-    double* sq = sum + (int64_t)(M.ih + 1) * step;
+    if (g >= 2 * step) return;
+    const int arr = g >= step ? 1 : 0;
+    const int64_t e = g - arr * step;
+    double* col = M.box + (int64_t)img * 2 * (M.ih + 1) * step + (int64_t)arr * (M.ih + 1) * step + e;
     // the same additions in the same order, kIntU rows at a time: their loads
     // are issued together before the dependent adds (one row per step waited
     // out a memory round trip per row of every column)
-    constexpr int kIntU = 16;
-    double a = 0, b = 0;
+    constexpr int kIntU = 32;
+    double a = 0;
     for (int y = 1; y <= M.ih; y += kIntU) {
-        double va[kIntU], vb[kIntU];
+        double va[kIntU];
 #pragma unroll
-        for (int u = 0; u < kIntU; ++u) {
-            if (y + u <= M.ih) {
-                va[u] = sum[(int64_t)(y + u) * step + e];
-                vb[u] = sq[(int64_t)(y + u) * step + e];
-            }
-        }
+        for (int u = 0; u < kIntU; ++u)
+            if (y + u <= M.ih) va[u] = col[(int64_t)(y + u) * step];
 #pragma unroll
         for (int u = 0; u < kIntU; ++u) {
             if (y + u <= M.ih) {
                 a = a + va[u];
-                b = b + vb[u];
-                sum[(int64_t)(y + u) * step + e] = a;
-                sq[(int64_t)(y + u) * step + e] = b;
+                col[(int64_t)(y + u) * step] = a;
             }
         }
     }
@@ -728,7 +725,7 @@ hipError_t launch_match_template(const MatchLaunch& M, hipStream_t s) {
     } else {
         hipLaunchKernelGGL(match_integral_rows_kernel<float>, gr, dim3(kBlock), 0, s, M);
     }
-    const dim3 gc(((M.iw + 1) * M.cn + kBlock - 1) / kBlock, M.n);
+    const dim3 gc((2 * (M.iw + 1) * M.cn + kBlock - 1) / kBlock, M.n);
     hipLaunchKernelGGL(match_integral_cols_kernel, gc, dim3(kBlock), 0, s, M);
     const dim3 gf((M.rw + kBlock - 1) / kBlock, M.rh, M.n);
     hipLaunchKernelGGL(match_finish_kernel, gf, dim3(kBlock), 0, s, M);
