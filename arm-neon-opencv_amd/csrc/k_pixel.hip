@@ -953,6 +953,9 @@ __global__ void __launch_bounds__(kBlock) area_u8_colsum_kernel(ResizeLaunch L, 
 // never overlapped (diagnosis builds at 2x2: loads alone 0.263 ms, the rest
 // alone 0.250, both 0.519).  Integer sums: bit-identical to it.
 // cache policy of the unit kernel's stores (A/B builds: EXTRA=-DVACV_AREA_STORE_AUX=n)
+#ifndef VACV_AREA_PACKED
+#define VACV_AREA_PACKED 1  // area_u8_unit_kernel: packed destinations through the wave's LDS slice (0: A/B)
+#endif
 #ifndef VACV_AREA_STORE_AUX
 #define VACV_AREA_STORE_AUX 0
 #endif
@@ -966,7 +969,8 @@ struct AreaUnit {
 };
 
 template <int OUT, int AX, int CC>
-__global__ void __launch_bounds__(kBlock) area_u8_unit_kernel(ResizeLaunch L, int units_per_row, int total, int dst_al) {
+__global__ void __launch_bounds__(kBlock) area_u8_unit_kernel(ResizeLaunch L, int units_per_row, int total, int dst_al,
+                                                               int packed) {
     using A = AreaUnit<AX, CC>;
     constexpr int NCH = A::NCH, ND = 4 * NCH, PX = A::PX, OB = A::OB;
     // the wave's 64 units' column sums, chunk-major: 32 bytes (ev, od) per chunk
@@ -1095,6 +1099,29 @@ __global__ void __launch_bounds__(kBlock) area_u8_unit_kernel(ResizeLaunch L, in
             outw[e] = __builtin_bit_cast(uint32_t, normalize_u8v(cn, v));
         }
     }
+    // a packed destination (rows and images back to back, whole units, 16-byte
+    // aligned; host-checked) and a whole wave: the 64 units' outputs are one
+    // contiguous run -- through the wave's LDS slice as 16-byte non-temporal
+    // stores, 1 KiB per instruction (round 5; the lanes' own stores sit a
+    // unit's bytes apart)
+    if (packed && wu0 + 64 <= total) {  // uniform
+        constexpr int NW = OUT == kOutSame ? OB / 4 : OB;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();  // every lane has read its column sums back
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+        for (int i = 0; i < NW; ++i) xw[NW * lane + i] = outw[i];
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        u32x4* o = reinterpret_cast<u32x4*>(const_cast<unsigned char*>(L.dst.base) + (int64_t)wu0 * OB * ES);
+#pragma unroll
+        for (int j = 0; j < (NW + 3) / 4; ++j) {
+            const int q = 64 * j + lane;
+            if (q < 16 * NW) __builtin_nontemporal_store(*reinterpret_cast<const u32x4*>(xw + 4 * q), o + q);
+        }
+        return;
+    }
     if (vx == PX && dst_al) {  // dword stores (OB * ES is a multiple of 4)
         constexpr int NW = OUT == kOutSame ? OB / 4 : OB;
         if constexpr (NW % 4 == 0) {
@@ -1140,10 +1167,14 @@ hipError_t launch_area_u8_unit_c(const ResizeLaunch& L, hipStream_t s) {
     const int ob = A::OB * es;
     const int wst = ob % 16 == 0 ? 16 : ob % 8 == 0 ? 8 : 4;
     const int dst_al = (dbits % (uintptr_t)wst) == 0;
+    // packed: unit g's output starts at g * ob bytes from the base
+    const int packed = VACV_AREA_PACKED && L.dst.w % A::PX == 0 && L.src.planes == 1 &&
+                       L.dst.row_pitch == (int64_t)upr * ob && L.dst.img_pitch == (int64_t)L.dst.h * L.dst.row_pitch &&
+                       (reinterpret_cast<uintptr_t>(L.dst.base) & 15) == 0;
     const dim3 grid((unsigned)((total + kBlock - 1) / kBlock));
-    if (L.out == kOutSame) hipLaunchKernelGGL((area_u8_unit_kernel<kOutSame, AX, CC>), grid, dim3(kBlock), 0, s, L, upr, (int)total, dst_al);
-    else if (L.out == kOutF32) hipLaunchKernelGGL((area_u8_unit_kernel<kOutF32, AX, CC>), grid, dim3(kBlock), 0, s, L, upr, (int)total, dst_al);
-    else hipLaunchKernelGGL((area_u8_unit_kernel<kOutNorm, AX, CC>), grid, dim3(kBlock), 0, s, L, upr, (int)total, dst_al);
+    if (L.out == kOutSame) hipLaunchKernelGGL((area_u8_unit_kernel<kOutSame, AX, CC>), grid, dim3(kBlock), 0, s, L, upr, (int)total, dst_al, packed);
+    else if (L.out == kOutF32) hipLaunchKernelGGL((area_u8_unit_kernel<kOutF32, AX, CC>), grid, dim3(kBlock), 0, s, L, upr, (int)total, dst_al, packed);
+    else hipLaunchKernelGGL((area_u8_unit_kernel<kOutNorm, AX, CC>), grid, dim3(kBlock), 0, s, L, upr, (int)total, dst_al, packed);
     return hipGetLastError();
 }
 
