@@ -311,6 +311,9 @@ __device__ __forceinline__ void acc_add(int64_t* p, double v, int q) {
 #ifndef VACV_CUBIC_ROWS
 #define VACV_CUBIC_ROWS 4
 #endif
+#ifndef VACV_CUBIC_LAUX
+#define VACV_CUBIC_LAUX VACV_LOAD_AUX  // cubic_cols_kernel's tap loads: cache policy bits (A/B)
+#endif
 #ifndef VACV_CUBIC_SAUX
 #define VACV_CUBIC_SAUX VACV_STORE_AUX
 #endif
@@ -371,7 +374,7 @@ cubic_cols_kernel(ResizeLaunch L, int col_blocks, int plane_tasks, int blocks_pe
                 if (r >= nrow || cq == 0.f) continue;  // uniform
                 const uint32_t a4 = (ro + (uint32_t)q * rp) & ~3u;
                 if (SAFE || a4 + 16u <= slimit) {
-                    const auto v = __builtin_amdgcn_raw_buffer_load_b128(srs.r, (int)a4, 0, VACV_LOAD_AUX);
+                    const auto v = __builtin_amdgcn_raw_buffer_load_b128(srs.r, (int)a4, 0, VACV_CUBIC_LAUX);
                     ch[r][q][0] = v[0];
                     ch[r][q][1] = v[1];
                     ch[r][q][2] = v[2];
