@@ -921,7 +921,8 @@ struct CachedLanczos {
     LanczosTabsDev t{};
 };
 std::mutex g_lz_mu;
-std::map<std::tuple<int, int, int, int, int, double, double, int>, CachedLanczos> g_lz_tabs;
+// run_ni depends on the channel count too, so cc is part of the key
+std::map<std::tuple<int, int, int, int, int, int, double, double, int>, CachedLanczos> g_lz_tabs;
 bool free_lz(CachedLanczos& c) { return hipFree(c.dev) == hipSuccess; }
 
 // lanczos_u8_kernel's staged runs: the 16-byte loads per lane (1 or 2) that
@@ -943,7 +944,7 @@ int lanczos_run_loads(const ResizeLaunch& R, const std::vector<int>& xofs) {
 int lanczos_tables(const ResizeLaunch& R, double inv_x, double inv_y, int band_rows, hipStream_t s, LanczosTabsDev& out) {
     int device = 0;
     if (hipGetDevice(&device) != hipSuccess) return VACV_ERR_HIP;
-    const auto key = std::make_tuple(device, R.src.w, R.src.h, R.dst.w, R.dst.h, inv_x, inv_y, band_rows);
+    const auto key = std::make_tuple(device, R.src.cc, R.src.w, R.src.h, R.dst.w, R.dst.h, inv_x, inv_y, band_rows);
     std::lock_guard<std::mutex> lk(g_lz_mu);
     auto it = g_lz_tabs.find(key);
     if (it == g_lz_tabs.end()) {

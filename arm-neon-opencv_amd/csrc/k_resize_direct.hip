@@ -426,13 +426,15 @@ resize_cols_kernel(ResizeLaunch L, int col_blocks, int row_groups, int tasks, in
 // 128-byte lines and 64-column blocks' spans are not (the column step times
 // 64 x CC is an odd number of 64-byte halves: e.g. 3x of 3 channels, 576 B),
 // the output has whole 128-column blocks and the source rows are line-aligned
-// (VACV_TUNE_RESIZE_TILE_W = 64 / 128 forces 1 / 2).
+// (VACV_TUNE_RESIZE_TILE_W = 64 forces 1; 128 forces 2 where the step is an
+// integer and the output has whole 128-column blocks).
 int cols_cw(const ResizeLaunch& L) {
     const int knob = tune(VACV_TUNE_RESIZE_TILE_W);
     if (knob == 64) return 1;
-    if (knob == 128) return 2;
     const double step = (double)L.src.w / L.dst.w;  // source columns per output column
+    // the 128-column blocks need an integer step and whole blocks, forced or not
     if (step != std::floor(step) || L.dst.w % 128) return 1;
+    if (knob == 128) return 2;
     const int64_t span64 = (int64_t)step * 64 * L.src.cc * L.src.esize;
     const bool lines = L.src.row_pitch % 128 == 0 && (reinterpret_cast<uintptr_t>(L.src.base) & 127) == 0 &&
                        L.src.img_pitch % 128 == 0 && L.src.plane_pitch % 128 == 0;

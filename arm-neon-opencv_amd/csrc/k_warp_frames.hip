@@ -629,16 +629,12 @@ constexpr int kExpTab = 16 + 12 * kExpRows + 64 * 4 * kRingMaxIt + kExpUnits + 1
 #endif
 // NN: INTER_NEAREST (OpenCV 2.4's warpAffine map, see warp_nearest_kernel in
 // k_warp.hip): the same staging, one tap per pixel, no blend.
-// WIDE (round 5): 128 x (2 NP)-pixel tiles instead of 64 x (4 NP), the same
-// pixel count; pixel j of a lane is column lane + 64 (j & 1) of row j >> 1, so
-// a tile's u8 output rows are 384 bytes = 3 whole 128-byte lines (64-pixel
-// rows were 192 bytes, the line between two tiles written by both).
-template <int OUT, int NP, bool NN, bool WIDE = false>
+template <int OUT, int NP, bool NN>
 __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(VACV_EXP_WPE)))
 warp_exp_kernel(WarpLaunch L, int gx, int gy, int kf, int slot_bytes, int exp_units, int dst_al) {
     constexpr int CC = 3;
-    constexpr int TW = WIDE ? 128 : kFrTileW;
-    constexpr int TH = WIDE ? 2 * NP : 4 * NP;
+    constexpr int TW = kFrTileW;
+    constexpr int TH = 4 * NP;
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     // [48 B pad][slot 0][slot 1][64 B pad] (the re-lay reads up to 45 B before
     // and 47 B after a row's chunks: bytes of no tapped pixel)
@@ -680,9 +676,9 @@ warp_exp_kernel(WarpLaunch L, int gx, int gy, int kf, int slot_bytes, int exp_un
     const float* M = L.inv;
     const float wlim = (float)(L.src.w - 1), hlim = (float)(L.src.h - 1);
     const int xl = bx * TW + lane;
-    const int yw = by * TH + wave * (WIDE ? NP / 2 : NP);
-    auto px_x = [&](int j) { return WIDE ? xl + 64 * (j & 1) : xl; };  // pixel j's column
-    auto px_y = [&](int j) { return yw + (WIDE ? (j >> 1) : j); };    // and row
+    const int yw = by * TH + wave * NP;
+    auto px_x = [&](int j) { return xl; };      // pixel j's column
+    auto px_y = [&](int j) { return yw + j; };  // and row
     const uint32_t rp = (uint32_t)L.src.row_pitch;
 
     // ---- 1. per-pixel taps, once for every frame (warp_affine_naive.cpp:23-42)
@@ -1009,16 +1005,14 @@ warp_exp_kernel(WarpLaunch L, int gx, int gy, int kf, int slot_bytes, int exp_un
                     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
                     __builtin_amdgcn_wave_barrier();
                     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-                    // 4 rows of 64 pixels (WIDE: 2 rows of 128, entries
-                    // (row, half) = j & 3); a lane stores 4 pixels, 12 bytes
-                    const int r = WIDE ? lane >> 5 : lane >> 4, q = WIDE ? lane & 31 : lane & 15;
-                    const u32x4 p = *reinterpret_cast<const u32x4*>(
-                        xch + (WIDE ? 256 * (2 * r + (q >> 4)) + 16 * (q & 15) : 256 * r + 16 * q));
+                    // 4 rows of 64 pixels; a lane stores 4 pixels, 12 bytes
+                    const int r = lane >> 4, q = lane & 15;
+                    const u32x4 p = *reinterpret_cast<const u32x4*>(xch + 256 * r + 16 * q);
                     typedef unsigned int u32x3 __attribute__((ext_vector_type(3)));
                     const u32x3 o = {__builtin_amdgcn_perm(p[1], p[0], 0x04020100u),
                                      __builtin_amdgcn_perm(p[2], p[1], 0x05040201u),
                                      __builtin_amdgcn_perm(p[3], p[2], 0x06050402u)};
-                    const uint32_t off = (VACV_RING_DBG & 8) ? kOob : (uint32_t)(y - (WIDE ? 1 : 3) + r) * dpitch + drs.delta + (uint32_t)(bx * TW * CC + 12 * q);
+                    const uint32_t off = (VACV_RING_DBG & 8) ? kOob : (uint32_t)(y - 3 + r) * dpitch + drs.delta + (uint32_t)(bx * TW * CC + 12 * q);
                     __builtin_amdgcn_raw_buffer_store_b96(o, drs.r, (int)off, 0, VACV_RING_SAUX);
                 }
             } else {
@@ -1198,11 +1192,11 @@ int64_t frames_resident(K kernel, size_t lds) {
     return r;
 }
 
-template <int OUT, int NP, bool NN = false, bool WIDE = false>
+template <int OUT, int NP, bool NN = false>
 hipError_t launch_exp(const WarpLaunch& L, const WarpFramesPlan& P, hipStream_t s) {
-    constexpr int TW = WIDE ? 128 : kFrTileW, TH = WIDE ? 2 * NP : 4 * NP;
+    constexpr int TW = kFrTileW, TH = 4 * NP;
     const int gx = (L.dst.w + TW - 1) / TW, gy = (L.dst.h + TH - 1) / TH;
-    auto kern = warp_exp_kernel<OUT, NP, NN, WIDE>;
+    auto kern = warp_exp_kernel<OUT, NP, NN>;
     int kf = P.kf;
     if (kf <= 0) {
         const int64_t res = std::max<int64_t>(frames_resident(kern, (size_t)P.lds), 256);
@@ -1250,7 +1244,6 @@ hipError_t launch_frames_np(const WarpLaunch& L, const WarpFramesPlan& P, hipStr
 template <int OUT>
 hipError_t launch_frames_cc(const WarpLaunch& L, const WarpFramesPlan& P, hipStream_t s) {
     if (P.se > 0) {
-        if (P.tw == 128) return launch_exp<OUT, 8, false, true>(L, P, s);  // 128 x 16 tiles
         return P.th == 16 ? launch_exp<OUT, 4>(L, P, s) : launch_exp<OUT, 8>(L, P, s);
     }
     switch (L.src.cc) {
@@ -1355,79 +1348,94 @@ bool ring_layout_th(const WarpLaunch& L, WarpFramesPlan& P, int th) {
     return P.lds <= 64 * 1024;
 }
 
-// warp_exp_kernel's staging, mirrored on the host with the kernel's
-// arithmetic for EVERY tile of the output (the box and the per-row tapped
-// columns from the pixels' taps): the most span chunks, image units and box
-// rows any tile needs.  The slots and the image are sized for that, so no
-// tile of the planned geometry takes the kernel's unstaged path.
+// warp_exp_kernel's staging needs, bounded analytically per tile: the most
+// span chunks, image units and box rows any tile can need.  A tile's pixels
+// map to a parallelogram in the source; clipped to the valid tap region, its
+// y extent gives the box rows, and its intersection with each row's band
+// (sy in [r - 1, r + 1) bilinear, [r, r + 1) nearest) the row's tapped
+// columns.  Every edge is widened by eps = 1/256 pixel, more than the
+// kernel's float (and INTER_NEAREST's 1/1024 fixed-point) coordinate error,
+// so the bound is never below the kernel's exact per-tile needs; the slots
+// and the image are sized from it, so no tile takes the kernel's unstaged
+// path.  Round 5 evaluated every pixel's tap twice per tile size tried (15-35
+// ms of host time per new matrix at 720p); this is ~1 ms, and against that
+// exact count over 300 random affine maps (1,200 cases) it never fell below
+// and over-counted cfg4's chunks by < 1 % (551 -> 556, the same 9 DMA
+// instructions).
 struct ExpNeeds {
     int rows = 0, chunks = 0, units = 0;
 };
+struct Pt2 {
+    double x, y;
+};
+// a convex polygon clipped to a*x + b*y <= c (Sutherland-Hodgman, one edge)
+int clip_poly(const Pt2* in, int n, double a, double b, double c, Pt2* out) {
+    int m = 0;
+    for (int i = 0; i < n; ++i) {
+        const Pt2 p = in[i], q = in[(i + 1) % n];
+        const double dp = a * p.x + b * p.y - c, dq = a * q.x + b * q.y - c;
+        if (dp <= 0) out[m++] = p;
+        if ((dp < 0 && dq > 0) || (dp > 0 && dq < 0)) {
+            const double t = dp / (dp - dq);
+            out[m++] = {p.x + t * (q.x - p.x), p.y + t * (q.y - p.y)};
+        }
+    }
+    return m;
+}
 ExpNeeds exp_needs(const WarpLaunch& L, int th, bool nn, int tw = kFrTileW) {
     constexpr int CC = 3;
-    const float* M = L.inv;
-    const double* Md = L.invd;
-    const float wlim = (float)(L.src.w - 1), hlim = (float)(L.src.h - 1);
+    double M[6];  // bilinear: the kernel's float map; nearest: OpenCV's fp64 one
+    for (int i = 0; i < 6; ++i) M[i] = nn ? L.invd[i] : (double)L.inv[i];
+    const double eps = 1.0 / 256, sh = nn ? 0.5 : 0.0;  // nearest: sx = floor(fx + 0.5)
+    const double wl = nn ? L.src.w : L.src.w - 1, hl = nn ? L.src.h : L.src.h - 1;
+    const int smax = nn ? L.src.w - 1 : L.src.w - 2, ymaxc = nn ? L.src.h - 1 : L.src.h - 2;
     const int gx = (L.dst.w + tw - 1) / tw, gy = (L.dst.h + th - 1) / th;
-    // the kernel's tap of pixel (x, y): (sx, sy) or false outside
-    auto tap = [&](int x, int y, int& sx, int& sy) {
-        if (x >= L.dst.w || y >= L.dst.h) return false;
-        if (nn) {
-            const int X0 = (int)std::rint((Md[1] * y + Md[2]) * 1024.0) + 512;
-            const int Y0 = (int)std::rint((Md[4] * y + Md[5]) * 1024.0) + 512;
-            int X = (int)((uint32_t)X0 + (uint32_t)(int)std::rint(Md[0] * x * 1024.0)) >> 10;
-            int Y = (int)((uint32_t)Y0 + (uint32_t)(int)std::rint(Md[3] * x * 1024.0)) >> 10;
-            sx = std::min(std::max(X, -32768), 32767);
-            sy = std::min(std::max(Y, -32768), 32767);
-            return (unsigned)sx < (unsigned)L.src.w && (unsigned)sy < (unsigned)L.src.h;
-        }
-        const float axm = M[0] * (float)x, aym = M[3] * (float)x;
-        const float fx = (axm + M[1] * (float)y) + M[2];
-        const float fy = (aym + M[4] * (float)y) + M[5];
-        if (!(fx >= 0.f && fx < wlim && fy >= 0.f && fy < hlim)) return false;
-        sx = (int)fx;
-        sy = (int)fy;
-        return true;
-    };
     ExpNeeds n;
-    std::vector<int> rmin, rmax;
-    for (int by = 0; by < gy; ++by) {
+    for (int by = 0; by < gy; ++by)
         for (int bx = 0; bx < gx; ++bx) {
-            int xmin = INT_MAX, xmax = INT_MIN, ymin = INT_MAX, ymax = INT_MIN, sx, sy;
-            for (int y = by * th; y < by * th + th; ++y)
-                for (int x = bx * tw; x < bx * tw + tw; ++x)
-                    if (tap(x, y, sx, sy)) {
-                        xmin = std::min(xmin, sx);
-                        xmax = std::max(xmax, sx);
-                        ymin = std::min(ymin, sy);
-                        ymax = std::max(ymax, sy);
-                    }
-            if (xmax < 0) continue;
-            const int bx0 = xmin & ~3, R = ymax + 2 - ymin;
-            rmin.assign(R + 1, INT_MAX);
-            rmax.assign(R + 1, -1);
-            for (int y = by * th; y < by * th + th; ++y)
-                for (int x = bx * tw; x < bx * tw + tw; ++x)
-                    if (tap(x, y, sx, sy)) {
-                        const int p = sx - bx0, r = sy - ymin;
-                        rmin[r] = std::min(rmin[r], p);
-                        rmax[r] = std::max(rmax[r], nn ? p : p + 1);
-                        if (!nn) {
-                            rmin[r + 1] = std::min(rmin[r + 1], p);
-                            rmax[r + 1] = std::max(rmax[r + 1], p + 1);
-                        }
-                    }
+            const int x0 = bx * tw, y0 = by * th, x1 = std::min(x0 + tw, L.dst.w) - 1, y1 = std::min(y0 + th, L.dst.h) - 1;
+            auto at = [&](int x, int y) { return Pt2{M[0] * x + M[1] * y + M[2] + sh, M[3] * x + M[4] * y + M[5] + sh}; };
+            Pt2 a[12], b[12];
+            a[0] = at(x0, y0);
+            a[1] = at(x1, y0);
+            a[2] = at(x1, y1);
+            a[3] = at(x0, y1);
+            int k = clip_poly(a, 4, -1, 0, eps, b);  // x >= -eps
+            k = clip_poly(b, k, 1, 0, wl + eps, a);  // x <= wl + eps
+            k = clip_poly(a, k, 0, -1, eps, b);      // y >= -eps
+            k = clip_poly(b, k, 0, 1, hl + eps, a);  // y <= hl + eps
+            if (k == 0) continue;
+            double lx = 1e30, ly = 1e30, hy = -1e30;
+            for (int i = 0; i < k; ++i) {
+                lx = std::min(lx, a[i].x);
+                ly = std::min(ly, a[i].y);
+                hy = std::max(hy, a[i].y);
+            }
+            const int ylo = std::max((int)std::floor(ly - eps), 0), yhi = std::min((int)std::floor(hy + eps), ymaxc);
+            if (yhi < ylo) continue;
+            const int xlo = std::max((int)std::floor(lx - eps), 0), bx0 = xlo & ~3, R = yhi + 2 - ylo;
             int chunks = 0, units = 0;
             for (int t = 0; t < R; ++t) {
-                if (rmin[t] > rmax[t]) continue;
-                chunks += (((rmax[t] + 1) * CC - 1) >> 4) - ((rmin[t] * CC) >> 4) + 1;
-                units += (rmax[t] >> 4) - (rmin[t] >> 4) + 1;
+                const int r = ylo + t;
+                Pt2 c[12], d[12];
+                int m = clip_poly(a, k, 0, -1, -((nn ? r : r - 1) - eps), c);
+                m = clip_poly(c, m, 0, 1, r + 1 + eps, d);
+                if (m == 0) continue;
+                double qx = 1e30, Qx = -1e30;
+                for (int i = 0; i < m; ++i) {
+                    qx = std::min(qx, d[i].x);
+                    Qx = std::max(Qx, d[i].x);
+                }
+                const int s0 = std::max((int)std::floor(qx - eps), xlo), s1 = std::min((int)std::floor(Qx + eps), smax);
+                if (s1 < s0) continue;
+                const int pmin = s0 - bx0, pmax = s1 - bx0 + (nn ? 0 : 1);
+                chunks += (((pmax + 1) * CC - 1) >> 4) - ((pmin * CC) >> 4) + 1;
+                units += (pmax >> 4) - (pmin >> 4) + 1;
             }
             n.rows = std::max(n.rows, R);
             n.chunks = std::max(n.chunks, chunks);
             n.units = std::max(n.units, units);
         }
-    }
     return n;
 }
 
@@ -1462,12 +1470,6 @@ bool frames_layout(const WarpLaunch& L, WarpFramesPlan& P) {
     P.tw = kFrTileW;
     if (L.src.cc == 3 && L.src.planes == 1 && tune(VACV_TUNE_WARP_KERNEL) != 6) {
         WarpFramesPlan Q = P;
-        // 128 x 16 tiles (VACV_TUNE_RESIZE_TILE_W = 128): whole-line u8 output rows
-        if (tune(VACV_TUNE_RESIZE_TILE_W) == 128 && exp_layout_th(L, Q, 16, false, 128)) {
-            P = Q;
-            return true;
-        }
-        Q = P;
         // 32-row tiles (fp32 output too: 0.4155 vs 0.4398 ms normalised at
         // 720p rot15 x128, although its instance spills a few registers)
         const int th0 = 32;
@@ -1506,7 +1508,7 @@ bool warp_frames_plan(const WarpLaunch& L, WarpFramesPlan& P) {
     // layout of byte output carries the store exchange)
     struct Key {
         float inv[6];
-        int sw, sh, dw, dh, th, cc, bytes_out, slots, kernel, tw;
+        int sw, sh, dw, dh, th, cc, bytes_out, slots, kernel;
         bool operator<(const Key& o) const { return std::memcmp(this, &o, sizeof(Key)) < 0; }
     };
     Key k;
@@ -1517,7 +1519,6 @@ bool warp_frames_plan(const WarpLaunch& L, WarpFramesPlan& P) {
     k.bytes_out = L.out == kOutSame ? 1 : 0;
     k.slots = tune(VACV_TUNE_WARP_SLOTS);
     k.kernel = knob;
-    k.tw = tune(VACV_TUNE_RESIZE_TILE_W);
     static std::mutex mu;
     static std::map<Key, std::pair<bool, WarpFramesPlan>> cache;
     bool ok;

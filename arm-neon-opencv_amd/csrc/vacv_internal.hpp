@@ -214,7 +214,7 @@ struct WarpFramesPlan {
     int se;                      // 1: warp_exp_kernel (3 channels, compact spans, a 4-byte-pixel image); 0: warp_ring_kernel
     int raw_bytes;               // warp_exp_kernel: bytes of each of its two raw DMA slots
     int exp_units;               // warp_exp_kernel: 16-pixel units of its image
-    int tw;                      // warp_exp_kernel: tile columns (64; 128 with 16 rows, VACV_TUNE_RESIZE_TILE_W = 128)
+    int tw;                      // warp_exp_kernel: tile columns (64)
 };
 bool warp_frames_plan(const WarpLaunch& L, WarpFramesPlan& P);
 hipError_t launch_warp_frames(const WarpLaunch& L, const WarpFramesPlan& P, hipStream_t s);

@@ -105,10 +105,20 @@ def spawn_ranks(n: int) -> int:
     return rc
 
 
-def ensure_built():
+def ensure_built(rank: int, world: int):
+    """Only rank 0 may build libvacv_hip.so (N ranks running make into one
+    lib/ at once would race); the other ranks wait at a barrier until it is
+    done, then load it or exit non-zero.  The driver's runs find it prebuilt."""
     import vacv_amd
-    if not vacv_amd._lib.HIP_LIB.exists():
+    lib = vacv_amd._lib.HIP_LIB
+    if rank == 0 and not lib.exists():
         vacv_amd._lib.build()
+    if world > 1:
+        import torch.distributed as dist
+        dist.barrier()
+    if not lib.exists():
+        print(f"bench: rank {rank}: {lib} is missing after rank 0's build step", file=sys.stderr)
+        sys.exit(2)
     vacv_amd._lib.load()
 
 
@@ -418,7 +428,7 @@ def main():
     dev = torch.device("cuda", local if world > 1 else 0)
     torch.cuda.set_device(dev)
 
-    ensure_built()
+    ensure_built(rank, world)
     from vacv_amd import ops
     from vacv_amd.roofline import HBM_PEAK_GBS
 

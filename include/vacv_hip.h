@@ -321,7 +321,7 @@ enum {
     VACV_TUNE_AREA_ROWS = 7,         /* u8 INTER_AREA column sums: output rows per workgroup */
     VACV_TUNE_RESIZE_WGS = 8,        /* staged kernel: workgroups launched */
     VACV_TUNE_RESIZE_TILE_H = 9,     /* staged kernel planner: tile height */
-    VACV_TUNE_RESIZE_TILE_W = 10,    /* staged kernel planner: tile width; column kernel (resize_cols_kernel): 64 / 128 output columns per wave; warp_exp_kernel: 128 = 128 x 16 tiles */
+    VACV_TUNE_RESIZE_TILE_W = 10,    /* staged kernel planner: tile width; column kernel (resize_cols_kernel): 64 / 128 output columns per wave */
     VACV_TUNE_RESIZE_WORK = 11,      /* staged kernel planner: work per thread */
     VACV_TUNE_WARP_KERNEL = 12,      /* u8 CONSTANT warp: 0 per-pixel gathers, 2 batched gathers, 4 LDS-staged frames: an LDS-DMA ring of source boxes (k_warp_frames.hip; 3 channels re-laid as 4-byte pixels, warp_exp_kernel), 6 the same without the re-lay (warp_ring_kernel, A/B); 5: INTER_NEAREST u8 on the per-pixel kernel (A/B) */
     VACV_TUNE_RESIZE_STRIP = 13,     /* two-tap u8 bilinear: column strips with an LDS row ring, 1: 64 columns x 16-row batches, 2: 128 x 8; 0 staged kernel */

@@ -94,3 +94,32 @@ def test_bench_main_two_ranks_on_one_gpu(workload):
     assert out["value"] > 0 and out["cpu_baseline"] is None
     if workload == "cubic_stats":
         assert out["global_stats_check"]["ok"], out["global_stats_check"]
+
+
+def test_gpus_8_dry_run_single_line():
+    """The driver's 8-GPU scaling run, rehearsed on the CPU: `--gpus 8` spawns
+    eight ranks (gloo, --dry-run), cfg5's step all-reduces its sums across all
+    eight, and rank 0 alone prints one dp8 line."""
+    rc, lines, err = _run_bench(["--gpus", "8", "--dry-run", "--steps", "2", "--warmup", "1",
+                                 "--workload", "cubic_stats"], timeout=400)
+    assert rc == 0, err[-3000:]
+    assert len(lines) == 1, lines
+    out = lines[0]
+    assert out["n_gpus"] == 8 and out["config"]["parallelism"] == "dp8" and out["dry_run"] is True
+
+
+def test_only_rank0_builds(monkeypatch, tmp_path):
+    """A rank other than 0 never runs the build: with the library missing it
+    exits non-zero instead of racing rank 0's make into the same lib/."""
+    import bench
+    sys.path.insert(0, str(REPO / "arm-neon-opencv_amd"))
+    import vacv_amd
+    calls = []
+    monkeypatch.setattr(vacv_amd._lib, "HIP_LIB", tmp_path / "libvacv_hip.so")
+    monkeypatch.setattr(vacv_amd._lib, "build", lambda: calls.append("build"))
+    with pytest.raises(SystemExit) as e:
+        bench.ensure_built(rank=1, world=1)
+    assert e.value.code == 2 and calls == []
+    with pytest.raises(SystemExit):
+        bench.ensure_built(rank=0, world=1)  # rank 0 builds (stubbed: still missing -> exit)
+    assert calls == ["build"]

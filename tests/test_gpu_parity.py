@@ -540,6 +540,20 @@ def test_resize_lanczos4(ops, dev, oracle):
             k = n - 1
             full = host(ops.resize(src[:n], wo, ho, interpolation=INTER_LANCZOS4))
             assert_same(full[k], oracle.resize_lanczos4(host(src[k]), wo, ho), f"lanczos batch n={n} {wo}x{ho}")
+    # the cached tables' staged-run count depends on the channel count: the
+    # same geometry on 1-channel planes, then 3- and 4-channel pixels (6x and
+    # 10x downscales, where cc = 1 needs fewer loads per lane than cc >= 3)
+    for wo, ho in [(320, 60), (192, 36)]:
+        for c, layout in [(3, NCHW), (3, None), (4, None), (1, None)]:
+            img = synthetic_image(870 + c, 360, 1920, c)
+            img = img if c > 1 else img[..., None]
+            t = to_dev((np.ascontiguousarray(img.transpose(2, 0, 1)) if layout == NCHW else img)[None], dev)
+            kw = dict(interpolation=INTER_LANCZOS4, **({"layout": NCHW} if layout == NCHW else {}))
+            a = ops.resize(t, wo, ho, **kw)
+            with ops.tuning(LANCZOS_KERNEL=1):
+                b = ops.resize(t, wo, ho, **kw)
+            torch.cuda.synchronize(dev)
+            assert torch.equal(a, b), f"lanczos cc={c} layout={layout} {wo}x{ho} after another channel count"
 
 
 def test_resize_area_any_scale(ops, dev, oracle):
