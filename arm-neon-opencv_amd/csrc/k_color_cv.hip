@@ -169,9 +169,6 @@ __global__ void __launch_bounds__(256) yuv420_cv8_kernel(CvColorLaunch L, int up
 // above wrote each lane's 32 (BGRA) / 24 (BGR) bytes from the lane itself,
 // its store instructions' lanes 32 / 24 bytes apart.  Needs 16-byte aligned
 // destination rows (host-checked).
-#ifndef VACV_CV8X_NT
-#define VACV_CV8X_NT 1  // the exchanged stores: 1 non-temporal, 0 the default policy
-#endif
 template <int DCN>
 __global__ void __launch_bounds__(256) yuv420_cv8x_kernel(CvColorLaunch L, int upr, int wrow) {
     __shared__ __attribute__((aligned(16))) uint32_t xch[4][64 * 2 * DCN];
@@ -246,8 +243,7 @@ __global__ void __launch_bounds__(256) yuv420_cv8x_kernel(CvColorLaunch L, int u
             const int q = 64 * j + lane;
             if (q < nck) {
                 const u32x4 v = *reinterpret_cast<const u32x4*>(xw + 4 * q);
-                if (VACV_CV8X_NT) __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(o) + q);
-                else reinterpret_cast<u32x4*>(o)[q] = v;
+                __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(o) + q);
             }
         }
         if (DCN == 3 && (nl & 1) && lane == 0)  // an odd lane count leaves 8 bytes

@@ -19,10 +19,6 @@
 // once per wave.  Results are re-assembled in LDS and leave as 16-byte
 // non-temporal stores.
 #pragma clang fp contract(off)
-// A/B builds: EXTRA=-DVACV_CUBIC_NT_STORES=0 (write-back output stores)
-#ifndef VACV_CUBIC_NT_STORES
-#define VACV_CUBIC_NT_STORES 1
-#endif
 
 #include <cstdlib>
 
@@ -251,12 +247,8 @@ cubic_direct_kernel(ResizeLaunch L, int blocks_per_plane) {
                 off = r * rowp + (b - r * out_row);
             }
             if (c * 16 + 16 <= vbytes) {
-#if VACV_CUBIC_NT_STORES
                 __builtin_nontemporal_store(*reinterpret_cast<const u32x4*>(xs + 16 * c),
                                             reinterpret_cast<u32x4*>(dp + off));
-#else
-                *reinterpret_cast<u32x4*>(dp + off) = *reinterpret_cast<const u32x4*>(xs + 16 * c);
-#endif
             } else {
                 for (uint32_t e = c * 16; e < vbytes; ++e) dp[off + (e - c * 16)] = xs[e];
             }
@@ -305,19 +297,7 @@ __device__ __forceinline__ void acc_add(int64_t* p, double v, int q) {
 // workgroup = 4 full output rows); workgroups never straddle planes, so the
 // SUMS partials stay per workgroup and per image.  SUMS adds each value and
 // its square in fp64 per lane (exact squares), then as the kernel above.
-#ifndef VACV_CUBIC_COLS
-#define VACV_CUBIC_COLS 1
-#endif
-#ifndef VACV_CUBIC_ROWS
-#define VACV_CUBIC_ROWS 4
-#endif
-#ifndef VACV_CUBIC_LAUX
-#define VACV_CUBIC_LAUX VACV_LOAD_AUX  // cubic_cols_kernel's tap loads: cache policy bits (A/B)
-#endif
-#ifndef VACV_CUBIC_SAUX
-#define VACV_CUBIC_SAUX VACV_STORE_AUX
-#endif
-constexpr int kCcRows = VACV_CUBIC_ROWS;  // output rows per wave task
+constexpr int kCcRows = 4;  // output rows per wave task
 constexpr int cubic_cols_waves(int cc) { return cc == 1 ? 8 : 5; }
 template <int CC, int OUT, bool SUMS>
 __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(cubic_cols_waves(CC))))
@@ -374,7 +354,7 @@ cubic_cols_kernel(ResizeLaunch L, int col_blocks, int plane_tasks, int blocks_pe
                 if (r >= nrow || cq == 0.f) continue;  // uniform
                 const uint32_t a4 = (ro + (uint32_t)q * rp) & ~3u;
                 if (SAFE || a4 + 16u <= slimit) {
-                    const auto v = __builtin_amdgcn_raw_buffer_load_b128(srs.r, (int)a4, 0, VACV_CUBIC_LAUX);
+                    const auto v = __builtin_amdgcn_raw_buffer_load_b128(srs.r, (int)a4, 0, VACV_LOAD_AUX);
                     ch[r][q][0] = v[0];
                     ch[r][q][1] = v[1];
                     ch[r][q][2] = v[2];
@@ -456,13 +436,13 @@ cubic_cols_kernel(ResizeLaunch L, int col_blocks, int plane_tasks, int blocks_pe
                 const int rr = c / cpr, cc = c - rr * cpr;
                 __builtin_amdgcn_raw_buffer_store_b128(*reinterpret_cast<const u32x4*>(xs + rr * kRowB + 16 * cc), rd.r,
                                                        (int)(base + (uint32_t)rr * rowp + 16u * (uint32_t)cc), 0,
-                                                       VACV_CUBIC_SAUX);
+                                                       VACV_STORE_AUX);
             }
         } else {
             for (int e = lane; e < nrow * rb; e += 64) {
                 const int rr = e / rb, cc = e - rr * rb;
                 __builtin_amdgcn_raw_buffer_store_b8(xs[rr * kRowB + cc], rd.r, (int)(base + (uint32_t)rr * rowp + cc), 0,
-                                                     VACV_CUBIC_SAUX);
+                                                     VACV_STORE_AUX);
             }
         }
     }
@@ -496,7 +476,7 @@ cubic_cols_kernel(ResizeLaunch L, int col_blocks, int plane_tasks, int blocks_pe
 // The column kernel's grid, or false where it does not apply (16-byte aligned
 // destination rows, the tuning knob).
 bool cubic_cols_plan(const ResizeLaunch& L, int& col_blocks, int& plane_tasks, int& blocks_per_plane) {
-    if (!VACV_CUBIC_COLS || tune(VACV_TUNE_CUBIC_DIRECT) == 2) return false;  // 2: the gather kernel (A/B)
+    if (tune(VACV_TUNE_CUBIC_DIRECT) == 2) return false;  // 2: the gather kernel (A/B)
     const uintptr_t dbits = reinterpret_cast<uintptr_t>(L.dst.base) | (uintptr_t)L.dst.row_pitch |
                             (uintptr_t)L.dst.img_pitch | (uintptr_t)L.dst.plane_pitch;
     if (dbits & 15) return false;

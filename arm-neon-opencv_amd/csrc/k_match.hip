@@ -538,10 +538,7 @@ __global__ void match_bfrag_kernel(MatchLaunch M, int KB, uint4* bf, int* tsum) 
     bf[t] = make_uint4(d[0], d[1], d[2], d[3]);
 }
 
-#ifndef VACV_MATCH_PF
-#define VACV_MATCH_PF 4  // match_corr_mfma_kernel: (yy, kb) steps whose operands are in flight
-#endif
-constexpr int kMatchPF = VACV_MATCH_PF;
+constexpr int kMatchPF = 4;  // match_corr_mfma_kernel: (yy, kb) steps whose operands are in flight
 
 // workgroup: 64 output rows x 64 output columns of one image; wave w: rows
 // 32 (w & 1) .., columns 32 (w >> 1) ..; the image block (rows r0 .. r0 + 63

@@ -15,9 +15,6 @@ namespace {
 __device__ __forceinline__ int64_t gtid() { return (int64_t)blockIdx.x * blockDim.x + threadIdx.x; }
 __device__ __forceinline__ int64_t gstride() { return (int64_t)gridDim.x * blockDim.x; }
 
-#ifndef VACV_COLOR_NT
-#define VACV_COLOR_NT 1  // fp32 colour / dtype output stores: 1 non-temporal, 0 the default policy (A/B)
-#endif
 constexpr int kColorPairs = 1;  // row pairs per wave in color_kernel (4 measured 15 % slower)
 
 int grid_for(int64_t work_items, int cap = 256 * 16) {
@@ -148,8 +145,7 @@ __global__ void __launch_bounds__(kBlock) u8_to_f32_flat_kernel(DtypeLaunch L) {
         const uint32_t w = __builtin_nontemporal_load(reinterpret_cast<const uint32_t*>(L.src) + i);
         const u32x4 f = {__float_as_uint((float)(w & 0xFF)), __float_as_uint((float)((w >> 8) & 0xFF)),
                          __float_as_uint((float)((w >> 16) & 0xFF)), __float_as_uint((float)(w >> 24))};
-        if (VACV_COLOR_NT) __builtin_nontemporal_store(f, reinterpret_cast<u32x4*>(L.dst) + i);
-        else reinterpret_cast<u32x4*>(L.dst)[i] = f;
+        __builtin_nontemporal_store(f, reinterpret_cast<u32x4*>(L.dst) + i);
     } else if (i - n4 < (L.count & 3)) {
         const int64_t e = (n4 << 2) + (i - n4);
         reinterpret_cast<float*>(L.dst)[e] = (float)L.src[e];
@@ -286,8 +282,7 @@ __global__ void __launch_bounds__(kBlock) color_kernel(ColorLaunch L) {
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 #pragma unroll
                 for (int b = 0; b < 3; ++b) {
-                    if (VACV_COLOR_NT) __builtin_nontemporal_store(w[b * 64 + lane], reinterpret_cast<u32x4*>(wbase) + b * 64 + lane);
-                    else reinterpret_cast<u32x4*>(wbase)[b * 64 + lane] = w[b * 64 + lane];
+                    __builtin_nontemporal_store(w[b * 64 + lane], reinterpret_cast<u32x4*>(wbase) + b * 64 + lane);
                 }
                 __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
                 __builtin_amdgcn_wave_barrier();  // the next row reuses the exchange buffer
@@ -952,13 +947,7 @@ __global__ void __launch_bounds__(kBlock) area_u8_colsum_kernel(ResizeLaunch L, 
 // above alternated a load phase and an LDS/output phase per workgroup that
 // never overlapped (diagnosis builds at 2x2: loads alone 0.263 ms, the rest
 // alone 0.250, both 0.519).  Integer sums: bit-identical to it.
-// cache policy of the unit kernel's stores (A/B builds: EXTRA=-DVACV_AREA_STORE_AUX=n)
-#ifndef VACV_AREA_PACKED
-#define VACV_AREA_PACKED 1  // area_u8_unit_kernel: packed destinations through the wave's LDS slice (0: A/B)
-#endif
-#ifndef VACV_AREA_STORE_AUX
-#define VACV_AREA_STORE_AUX 0
-#endif
+// cache policy of the unit kernel's stores (A/B builds: EXTRA=-D0=n)
 template <int AX, int CC>
 struct AreaUnit {
     static constexpr int gcd(int a, int b) { return b == 0 ? a : gcd(b, a % b); }
@@ -1128,17 +1117,17 @@ __global__ void __launch_bounds__(kBlock) area_u8_unit_kernel(ResizeLaunch L, in
 #pragma unroll
             for (int i = 0; i < NW; i += 4)
                 __builtin_amdgcn_raw_buffer_store_b128(u32x4{outw[i], outw[i + 1], outw[i + 2], outw[i + 3]}, drs.r,
-                                                       (int)(ro + 4u * (uint32_t)i), 0, VACV_AREA_STORE_AUX);
+                                                       (int)(ro + 4u * (uint32_t)i), 0, 0);
         } else if constexpr (NW % 2 == 0) {
             typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
 #pragma unroll
             for (int i = 0; i < NW; i += 2)
                 __builtin_amdgcn_raw_buffer_store_b64(u32x2{outw[i], outw[i + 1]}, drs.r, (int)(ro + 4u * (uint32_t)i), 0,
-                                                      VACV_AREA_STORE_AUX);
+                                                      0);
         } else {
 #pragma unroll
             for (int i = 0; i < NW; ++i)
-                __builtin_amdgcn_raw_buffer_store_b32(outw[i], drs.r, (int)(ro + 4u * (uint32_t)i), 0, VACV_AREA_STORE_AUX);
+                __builtin_amdgcn_raw_buffer_store_b32(outw[i], drs.r, (int)(ro + 4u * (uint32_t)i), 0, 0);
         }
     } else {  // the row's partial last unit or an unaligned destination: element by element
 #pragma unroll
@@ -1146,9 +1135,9 @@ __global__ void __launch_bounds__(kBlock) area_u8_unit_kernel(ResizeLaunch L, in
             if (e >= vx * CC) break;
             if constexpr (OUT == kOutSame)
                 __builtin_amdgcn_raw_buffer_store_b8((unsigned char)(outw[e / 4] >> (8 * (e % 4))), drs.r, (int)(ro + (uint32_t)e), 0,
-                                                     VACV_AREA_STORE_AUX);
+                                                     0);
             else
-                __builtin_amdgcn_raw_buffer_store_b32(outw[e], drs.r, (int)(ro + 4u * (uint32_t)e), 0, VACV_AREA_STORE_AUX);
+                __builtin_amdgcn_raw_buffer_store_b32(outw[e], drs.r, (int)(ro + 4u * (uint32_t)e), 0, 0);
         }
     }
 }
@@ -1168,7 +1157,7 @@ hipError_t launch_area_u8_unit_c(const ResizeLaunch& L, hipStream_t s) {
     const int wst = ob % 16 == 0 ? 16 : ob % 8 == 0 ? 8 : 4;
     const int dst_al = (dbits % (uintptr_t)wst) == 0;
     // packed: unit g's output starts at g * ob bytes from the base
-    const int packed = VACV_AREA_PACKED && L.dst.w % A::PX == 0 && L.src.planes == 1 &&
+    const int packed = L.dst.w % A::PX == 0 && L.src.planes == 1 &&
                        L.dst.row_pitch == (int64_t)upr * ob && L.dst.img_pitch == (int64_t)L.dst.h * L.dst.row_pitch &&
                        (reinterpret_cast<uintptr_t>(L.dst.base) & 15) == 0;
     const dim3 grid((unsigned)((total + kBlock - 1) / kBlock));
@@ -1253,20 +1242,14 @@ struct AreaLane {
     static constexpr int OB = PXL * CC;               // output elements per lane
 };
 
-#ifndef VACV_AREA_XCH
-#define VACV_AREA_XCH 1  // area_lane_kernel: 1 lane-contiguous 16-byte loads + an LDS exchange for whole waves (0.3325 vs 0.3708 ms)
-#endif
-#ifndef VACV_AREA_LAUX
-#define VACV_AREA_LAUX 0  // area_lane_kernel's exchange-path loads: cache policy bits (2 non-temporal)
-#endif
-#ifndef VACV_AREA_RG
-#define VACV_AREA_RG 1  // area_lane_kernel: output rows per wave, the next row's loads in flight while one is summed (1 / 2 / 4 / 8: 0.369 / 0.382 / 0.385 / 0.418 ms)
-#endif
+// area_lane_kernel: output rows per wave, the next row's loads in flight while
+// one is summed (1 / 2 / 4 / 8: 0.369 / 0.382 / 0.385 / 0.418 ms)
+constexpr int kAreaRG = 1;
 template <int OUT, int AX, int CC>
 __global__ void __launch_bounds__(kBlock) area_lane_kernel(ResizeLaunch L, int blocks_per_row, int tasks, int dst_al) {
     using A = AreaLane<AX, CC>;
     constexpr int PXL = A::PXL, NW = A::NW, OB = A::OB;
-    constexpr int RG = VACV_AREA_RG;
+    constexpr int RG = kAreaRG;
     static_assert(OB % 4 == 0 || OUT != kOutSame, "u8 output as whole dwords");
     const int lane = threadIdx.x & 63;
     const int task = (int)blockIdx.x * (kBlock / 64) + __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
@@ -1392,7 +1375,6 @@ __global__ void __launch_bounds__(kBlock) area_lane_kernel(ResizeLaunch L, int b
             }
         }
     };
-#if VACV_AREA_XCH
     if (full && L.area_y <= 257) {
         // uniform (whole waves): the wave's run of 16 NW chunks of a source
         // row moves as lane-contiguous 16-byte loads (chunk 64 i + lane), is
@@ -1419,7 +1401,7 @@ __global__ void __launch_bounds__(kBlock) area_lane_kernel(ResizeLaunch L, int b
 #pragma unroll
                 for (int i = 0; i < NI; ++i) {
                     const int q = 64 * i + lane;
-                    t[i] = q < NCK ? __builtin_amdgcn_raw_buffer_load_b128(srs.r, (int)(ry + (uint32_t)r * rp + 16u * (uint32_t)q), 0, VACV_AREA_LAUX)
+                    t[i] = q < NCK ? __builtin_amdgcn_raw_buffer_load_b128(srs.r, (int)(ry + (uint32_t)r * rp + 16u * (uint32_t)q), 0, 0)
                                    : u32x4{0u, 0u, 0u, 0u};
                 }
 #pragma unroll
@@ -1454,7 +1436,6 @@ __global__ void __launch_bounds__(kBlock) area_lane_kernel(ResizeLaunch L, int b
         }
         return;
     }
-#endif
     if (L.area_y == 3) {
         // uniform: the 3 source rows of output row y + 1 are in flight while
         // row y is summed and stored
@@ -1502,7 +1483,7 @@ template <int AX, int CC>
 hipError_t launch_area_lane_c(const ResizeLaunch& L, hipStream_t s) {
     using A = AreaLane<AX, CC>;
     const int bpr = (L.dst.w + 64 * A::PXL - 1) / (64 * A::PXL);
-    const int64_t tasks = (int64_t)bpr * ((L.dst.h + VACV_AREA_RG - 1) / VACV_AREA_RG) * L.n * L.src.planes;
+    const int64_t tasks = (int64_t)bpr * ((L.dst.h + kAreaRG - 1) / kAreaRG) * L.n * L.src.planes;
     if (tasks >= 0x7FFFFF00LL) return hipErrorInvalidValue;
     const int es = L.out == kOutSame ? 1 : 4;
     const uintptr_t dbits = reinterpret_cast<uintptr_t>(L.dst.base) | (uintptr_t)L.dst.img_pitch |

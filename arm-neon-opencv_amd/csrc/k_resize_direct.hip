@@ -35,32 +35,15 @@ namespace {
 
 constexpr int kGroupPx = 256;  // pixels per LDS exchange round (4 per lane)
 
-// Diagnosis builds (make EXTRA=-DVACV_DIRECT_DBG=n LIB=... OBJ=...;
-// tools/kbench_lib.py), results wrong: bit 0 no normalisation (the u8 value
-// converted), bit 1 no blend either (the tap bytes stored as they are),
-// bit 2 no output stores.
-#ifndef VACV_DIRECT_DBG
-#define VACV_DIRECT_DBG 0
-#endif
 // cache policy of the fp32-output stores and tap gathers (aux bits:
 // 1 sc0, 2 nt, 16 sc1)
-#ifndef VACV_DIRECT_SAUX
-#define VACV_DIRECT_SAUX VACV_STORE_AUX
-#endif
-#ifndef VACV_DIRECT_LAUX
-#define VACV_DIRECT_LAUX 0
-#endif
+constexpr int kDirectSaux = VACV_STORE_AUX;
+constexpr int kDirectLaux = 0;
 // resize_cols_kernel's fp32-output gathers at CW = 2 on 3 channels: non-temporal (round 5) -- its
 // blocks end on 128-byte lines (CW = 2 / the edge-lane shift), no source line
 // is read by two waves, so nothing is gained by keeping lines in L2
 // (kbench 0.2092 -> 0.2075 ms, bench kernel 0.2127 / 0.2122 -> 0.2107 / 0.2095)
-#ifndef VACV_COLS_LAUX
-#define VACV_COLS_LAUX 2
-#endif
-// column-stationary lanes (resize_cols_kernel) for one-tap-row geometries
-#ifndef VACV_DIRECT_COLS
-#define VACV_DIRECT_COLS 1
-#endif
+constexpr int kColsLaux = 2;
 
 // Pixels per lane: 8 when one tap row is gathered and the kernel still fits
 // 64 VGPRs (8 waves per SIMD) at 8, else 4 (measured: spills otherwise).
@@ -81,8 +64,8 @@ resize_direct_kernel(ResizeLaunch L, int blocks_per_plane, int total, int xcd) {
     // source line split between two waves is re-read from L2, not HBM
     // (headline 0.2206 -> 0.2180 ms; sc0 0.2185); non-temporal under byte
     // output, where the default policy measured slower (0.1232 -> 0.1267 ms)
-    constexpr int kLoadAux = OUT == kOutSame ? VACV_LOAD_AUX : VACV_DIRECT_LAUX;
-    constexpr int kStoreAux = OUT == kOutSame ? VACV_STORE_AUX : VACV_DIRECT_SAUX;
+    constexpr int kLoadAux = OUT == kOutSame ? VACV_LOAD_AUX : kDirectLaux;
+    constexpr int kStoreAux = OUT == kOutSame ? VACV_STORE_AUX : kDirectSaux;
     __shared__ __attribute__((aligned(16))) unsigned char xch[4][kGroupPx * kOutPx];
 
     // xcd: workgroup b runs on XCD b % 8; give each XCD one contiguous eighth
@@ -190,9 +173,9 @@ resize_direct_kernel(ResizeLaunch L, int blocks_per_plane, int total, int xcd) {
                 const uint32_t sel = (uint32_t)k | (0x0Cu << 8) | ((uint32_t)(CC + k) << 16) | (0x0Cu << 24);
                 const uint32_t top = __builtin_amdgcn_perm(tap[q][0][1], tap[q][0][0], sel);
                 const uint32_t bot = ONE_ROW ? 0u : __builtin_amdgcn_perm(tap[q][NR - 1][1], tap[q][NR - 1][0], sel);
-                const int v = (VACV_DIRECT_DBG & 2) ? (int)top : blend_fixed<MODE>(top, bot, wx, wA, wB);
+                const int v = blend_fixed<MODE>(top, bot, wx, wA, wB);
                 if (OUT == kOutSame) o[k] = (TOut)v;
-                else if (OUT == kOutF32 || (VACV_DIRECT_DBG & 3)) o[k] = (TOut)(float)v;
+                else if (OUT == kOutF32) o[k] = (TOut)(float)v;
                 else o[k] = (TOut)normalize_u8v(cn[k], v);
             }
         }
@@ -203,7 +186,7 @@ resize_direct_kernel(ResizeLaunch L, int blocks_per_plane, int total, int xcd) {
         // ---- LDS -> HBM: dense byte b of the plane's output lives at row
         // b / out_row, column byte b % out_row ---------------------------------
         const int gp = npx - g * kGroupPx;  // valid pixels of this round (uniform)
-        if (gp > 0 && !(VACV_DIRECT_DBG & 4)) {
+        if (gp > 0) {
             // 32-bit offsets: the plane is < 2^31 bytes (kMaxPlaneBytes)
             const uint32_t vbytes = (uint32_t)(min(gp, kGroupPx) * kOutPx);
             const uint32_t b0 = (uint32_t)(p0 + g * kGroupPx) * kOutPx;  // 16-byte aligned (256 | p0)
@@ -246,10 +229,7 @@ resize_direct_kernel(ResizeLaunch L, int blocks_per_plane, int total, int xcd) {
 // instruction still reads one contiguous run of a source row (64 columns),
 // and the 8 x 64 results leave through the wave's LDS buffer as 16-byte
 // non-temporal stores, 4 rows at a time.  Same arithmetic as above.
-#ifndef VACV_COLS_ROWS
-#define VACV_COLS_ROWS 8
-#endif
-constexpr int kColsRows = VACV_COLS_ROWS;  // output rows per wave task at 64 columns (a multiple of 8)
+constexpr int kColsRows = 8;  // output rows per wave task at 64 columns (a multiple of 8)
 // Column blocks of CW x 64 output columns (lane l keeps columns x0 + l,
 // x0 + 64 + l, ...) and kColsRows / CW rows, so a task's pixels stay 512.
 // CW = 2 at an exact 3x downscale of 3-channel u8: a block's source span is
@@ -265,8 +245,8 @@ resize_cols_kernel(ResizeLaunch L, int col_blocks, int row_groups, int tasks, in
     constexpr int kOutPx = CC * (int)sizeof(TOut);
     constexpr int kHalf = 4 / CW;                  // rows per LDS exchange round
     constexpr int kRowB = 64 * CW * kOutPx;        // output bytes of one block row
-    constexpr int kLoadAux = OUT == kOutSame ? VACV_LOAD_AUX : (CW == 2 && CC == 3 ? VACV_COLS_LAUX : VACV_DIRECT_LAUX);
-    constexpr int kStoreAux = OUT == kOutSame ? VACV_STORE_AUX : VACV_DIRECT_SAUX;
+    constexpr int kLoadAux = OUT == kOutSame ? VACV_LOAD_AUX : (CW == 2 && CC == 3 ? kColsLaux : kDirectLaux);
+    constexpr int kStoreAux = OUT == kOutSame ? VACV_STORE_AUX : kDirectSaux;
     __shared__ __attribute__((aligned(16))) unsigned char xch[4][kHalf * kRowB];
     const int lane = (int)threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
@@ -444,7 +424,6 @@ int cols_cw(const ResizeLaunch& L) {
 // The column kernel's grid, or false where it does not apply (it needs
 // 16-byte aligned block rows in the destination).
 bool cols_plan(const ResizeLaunch& L, int out_px, int cw, int& col_blocks, int& row_groups, int64_t& tasks) {
-    if (!VACV_DIRECT_COLS) return false;
     const uintptr_t dbits = reinterpret_cast<uintptr_t>(L.dst.base) | (uintptr_t)L.dst.row_pitch |
                             (uintptr_t)L.dst.img_pitch | (uintptr_t)L.dst.plane_pitch;
     if ((dbits & 15) || (64 * out_px) % 16) return false;

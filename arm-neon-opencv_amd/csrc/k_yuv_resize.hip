@@ -67,10 +67,7 @@ __device__ __forceinline__ uint32_t chroma_sel(int w, int tx) {
 // shares its 128-byte lines with the neighbouring wave's, and the chroma row
 // serves two Y rows; in L2 they are fetched once (256 x NV21 1080p ->
 // 640x360: u8 0.1447 -> 0.1361 ms, CHW fp32 0.1986 -> 0.1950 ms).
-#ifndef VACV_YUV_LAUX
-#define VACV_YUV_LAUX 0
-#endif
-constexpr int kYuvAux = VACV_YUV_LAUX;
+constexpr int kYuvAux = 0;
 __device__ __forceinline__ void gather_row(const Rsrc& rs, uint32_t yo, uint32_t co, int w, int tx, RowTaps& t) {
     t.y = __builtin_amdgcn_raw_buffer_load_b32(rs.r, (int)(yo + (uint32_t)tx), 0, kYuvAux);
     const int ca = tx & ~1;

@@ -23,9 +23,6 @@ typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 #ifndef VACV_STORE_AUX
 #define VACV_STORE_AUX 2
 #endif
-#ifndef VACV_NO_F32_NORM
-#define VACV_NO_F32_NORM 0
-#endif
 
 // A raw buffer resource over [base16, base16 + bytes): loads past the end
 // return zeros instead of faulting, so a 16-byte staging load may overhang
@@ -130,9 +127,7 @@ __device__ __forceinline__ ChanNorm chan_norm(const NormSpec& ns, int img, int c
 // (float)((double)d / ((double)std + 1e-6)) for all 256 values (norm_spec)
 __device__ __forceinline__ float normalize_u8v(const ChanNorm& c, int v) {
     const float d = (float)v - c.mean;
-#if !VACV_NO_F32_NORM
     if (c.f32) return __builtin_fmaf(d, c.hi, d * c.lo);
-#endif
     if (c.mul) return (float)((double)d * c.inv);
     return (float)((double)d / ((double)c.stdv + 1e-6));
 }
