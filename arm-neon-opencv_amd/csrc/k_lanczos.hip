@@ -580,15 +580,22 @@ lanczos_u8_kernel(LanczosLaunch L, int strips, int bands, int band_rows,
     // this lane's window within the wave's slice
     const uint32_t wrun = (uint32_t)__builtin_amdgcn_readfirstlane((int)(wbyte & ~15u));
     const uint32_t wofs = (wbyte & ~3u) - wrun;
+    // the run's bytes: up to the last lane's window end (windows are monotone
+    // in the lane); chunks past it are not loaded (they belong to the next
+    // strip's run: loading them here fetched 1.11 x the source rows)
+    const uint32_t run_end = (uint32_t)__builtin_amdgcn_readlane((int)(wofs + 4u * ND), 63);
     __shared__ __attribute__((aligned(16))) uint32_t xs[NI > 0 ? kLzWaves : 1][NI > 0 ? 256 * NI : 1];
     using RowBuf = typename std::conditional<(NI > 0), u32x4[NI > 0 ? NI : 1], uint32_t[ND]>::type;
     auto load_run = [&](auto safe_c, u32x4 (&t)[NI > 0 ? NI : 1], int r) {
         constexpr bool SAFE = decltype(safe_c)::value;
 #pragma unroll
         for (int i = 0; i < (NI > 0 ? NI : 1); ++i) {
-            const uint32_t a = (uint32_t)r * rp + wrun + 16u * (uint32_t)(64 * i + lane);
-            if (!SAFE || a + 16u <= slimit) {
-                t[i] = __builtin_amdgcn_raw_buffer_load_b128(srs.r, (int)a, 0, 0);
+            const uint32_t c16 = 16u * (uint32_t)(64 * i + lane);
+            const uint32_t a = (uint32_t)r * rp + wrun + c16;
+            // past the run: an out-of-range offset, no memory access (its LDS
+            // words are never read)
+            if (!SAFE || (c16 >= run_end || a + 16u <= slimit)) {
+                t[i] = __builtin_amdgcn_raw_buffer_load_b128(srs.r, (int)(c16 < run_end ? a : 0x80000000u), 0, 0);
             } else {  // the chunk overhangs the plane's end: bytewise (past it: zeros)
                 uint32_t v[4] = {0u, 0u, 0u, 0u};
 #pragma unroll

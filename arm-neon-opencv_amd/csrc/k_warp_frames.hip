@@ -629,10 +629,9 @@ constexpr int kExpTab = 16 + 12 * kExpRows + 64 * 4 * kRingMaxIt + kExpUnits + 1
 #endif
 // NN: INTER_NEAREST (OpenCV 2.4's warpAffine map, see warp_nearest_kernel in
 // k_warp.hip): the same staging, one tap per pixel, no blend.
-// One tile's frames f0 .. f1 - 1 (the whole per-tile pipeline below).
 template <int OUT, int NP, bool NN>
-__device__ __forceinline__ void exp_tile(const WarpLaunch& L, int gx, int tile, int f0, int f1, int slot_bytes,
-                                         int exp_units, int dst_al) {
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(VACV_EXP_WPE)))
+warp_exp_kernel(WarpLaunch L, int gx, int gy, int kf, int slot_bytes, int exp_units, int dst_al) {
     constexpr int CC = 3;
     constexpr int TW = kFrTileW;
     constexpr int TH = 4 * NP;
@@ -649,12 +648,7 @@ __device__ __forceinline__ void exp_tile(const WarpLaunch& L, int gx, int tile, 
 #else
     constexpr int kAux = OUT == kOutSame ? 1 : VACV_LOAD_AUX;
 #endif
-    // the thread index through an opaque move: per-lane values of one call
-    // are not CSE'd into the other (the kernel's two tile segments), which
-    // would keep them live across the whole first segment
-    int tid_;
-    asm volatile("v_mov_b32 %0, %1" : "=v"(tid_) : "v"((int)threadIdx.x));
-    const int tid = tid_, lane = tid & 63;
+    const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     int* red = reinterpret_cast<int*>(lds + xbase);  // 4 waves x 4 ints, setup only
     unsigned char* xch = lds + xbase + wave * kXB;
@@ -670,7 +664,15 @@ __device__ __forceinline__ void exp_tile(const WarpLaunch& L, int gx, int tile, 
     int* t_min = reinterpret_cast<int*>(t_crow);  // per-row tapped columns (until the chunk map is built)
     int* t_max = t_min + kExpRows;
 
+    const int tiles = gx * gy;
+    const int nfr = L.n;
+    const int total = tiles * ((nfr + kf - 1) / kf);
+    const int per_xcd = (total + 7) / 8;
+    const int id = (int)(blockIdx.x % 8) * per_xcd + (int)(blockIdx.x / 8);
+    if (id >= total) return;  // uniform
+    const int fg = id / tiles, tile = id - fg * tiles;
     const int by = tile / gx, bx = tile - by * gx;
+    const int f0 = fg * kf, f1 = min(f0 + kf, nfr);
     const float* M = L.inv;
     const float wlim = (float)(L.src.w - 1), hlim = (float)(L.src.h - 1);
     const int xl = bx * TW + lane;
@@ -1172,47 +1174,6 @@ __device__ __forceinline__ void exp_tile(const WarpLaunch& L, int gx, int tile, 
 #undef EXP_STAMP
 }
 
-// The batch's (tile, frame) units, tile-major, split evenly over a grid the
-// size of the chip's resident workgroups (the host sizes it): workgroup rank r
-// takes units [r T / G, (r + 1) T / G) -- about 57 consecutive frames of one
-// or two tiles at cfg4 -- so every workgroup finishes together (the round-5
-// grid of 16-frame workgroups ran 3.6 residency rounds, its last one part
-// full) and a tile's setup is amortised over all of its frames in the
-// workgroup.  Ranks are XCD-contiguous (workgroup b runs on XCD b % 8): an
-// XCD's workgroups hold neighbouring tiles, whose shared source lines then
-// come from one L2.
-template <int OUT, int NP, bool NN>
-__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(VACV_EXP_WPE)))
-warp_exp_kernel(WarpLaunch L, int gx, int gy, int kf, int slot_bytes, int exp_units, int dst_al) {
-    const int64_t nfr = L.n;
-    if constexpr (OUT == kOutSame) {
-        const int64_t T = (int64_t)gx * gy * nfr;
-        const int G = (int)gridDim.x;  // a multiple of 8, and T / G <= nfr (host): at most two tiles
-        const int rank = (int)(blockIdx.x % 8) * (G / 8) + (int)(blockIdx.x / 8);
-        const int64_t u = T * rank / G, u1 = T * (rank + 1) / G;
-        if (u >= u1) return;  // uniform
-        const int tile = (int)(u / nfr);
-        const int f0 = (int)(u - (int64_t)tile * nfr);
-        const int64_t seg = min(u1, (int64_t)(tile + 1) * nfr);
-        exp_tile<OUT, NP, NN>(L, gx, tile, f0, f0 + (int)(seg - u), slot_bytes, exp_units, dst_al);
-        if (seg < u1) {  // uniform: the next tile's first frames
-            __syncthreads();  // the previous tile's last image reads are done
-            exp_tile<OUT, NP, NN>(L, gx, tile + 1, 0, (int)(u1 - seg), slot_bytes, exp_units, dst_al);
-        }
-    } else {
-        // fp32 output: one tile's kf frames per workgroup (the two-segment
-        // form spills ~26 registers in the 32-row normalised instance)
-        const int tiles = gx * gy;
-        const int total = tiles * (int)((nfr + kf - 1) / kf);
-        const int per_xcd = (total + 7) / 8;
-        const int id = (int)(blockIdx.x % 8) * per_xcd + (int)(blockIdx.x / 8);
-        if (id >= total) return;  // uniform
-        const int fg = id / tiles, tile = id - fg * tiles;
-        const int f0 = fg * kf;
-        exp_tile<OUT, NP, NN>(L, gx, tile, f0, min(f0 + kf, (int)nfr), slot_bytes, exp_units, dst_al);
-    }
-}
-
 template <typename K>
 int64_t frames_resident(K kernel, size_t lds) {
     static std::mutex mu;
@@ -1236,23 +1197,15 @@ hipError_t launch_exp(const WarpLaunch& L, const WarpFramesPlan& P, hipStream_t 
     constexpr int TW = kFrTileW, TH = 4 * NP;
     const int gx = (L.dst.w + TW - 1) / TW, gy = (L.dst.h + TH - 1) / TH;
     auto kern = warp_exp_kernel<OUT, NP, NN>;
-    const int64_t tiles = (int64_t)gx * gy, units = tiles * L.n;
-    if (units >= ((int64_t)1 << 40)) return hipErrorInvalidValue;
-    const int64_t res = std::max<int64_t>(frames_resident(kern, (size_t)P.lds), 256);
-    int64_t blocks;
     int kf = P.kf;
-    if (OUT == kOutSame) {
-        // one workgroup per resident slot (VACV_TUNE_WARP_FRAMES > 0: about
-        // that many frames per workgroup instead), never more than the units,
-        // at most L.n units per workgroup
-        int64_t g = P.kf > 0 ? (units + P.kf - 1) / P.kf : res;
-        g = std::max<int64_t>(std::min(g, units), tiles);
-        blocks = (g + 7) / 8 * 8;
-    } else {
-        if (kf <= 0) kf = (int)std::max<int64_t>(1, std::min<int64_t>(16, units / (3 * res)));
-        blocks = (tiles * ((L.n + kf - 1) / kf) + 7) / 8 * 8;
+    if (kf <= 0) {
+        const int64_t res = std::max<int64_t>(frames_resident(kern, (size_t)P.lds), 256);
+        const int64_t tiles = (int64_t)gx * gy;
+        kf = (int)std::max<int64_t>(1, std::min<int64_t>(16, tiles * L.n / (3 * res)));
     }
-    if (blocks >= 0x7FFFFFF0LL) return hipErrorInvalidValue;
+    const int64_t total = (int64_t)gx * gy * ((L.n + kf - 1) / kf);
+    if (total >= 0x7FFFFFF0LL) return hipErrorInvalidValue;
+    const int64_t blocks = (total + 7) / 8 * 8;
     hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(kBlock), (size_t)P.lds, s, L, gx, gy, kf, P.raw_bytes,
                        P.exp_units, P.dst_al);
     return hipGetLastError();
