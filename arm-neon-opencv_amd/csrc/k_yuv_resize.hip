@@ -311,16 +311,25 @@ yuv_resize_kernel(YuvResizeLaunch L) {
 // (one contiguous run of a source row per instruction), the packed decode
 // and the blend.  Results leave through the wave's LDS buffer, kYuvHalf rows
 // at a time, as 16-byte non-temporal stores (plane-major for NCHW).
-constexpr int kYuvRows = 8;   // output rows per wave task
-constexpr int kYuvHalf = 4;   // rows per LDS exchange round
-template <int OUT, int MODE, bool CHW, bool ONE_ROW>
+//
+// CW = 2 (round 6): blocks of 128 output columns x kYuvRows / 2 rows (lane l
+// keeps columns x0 + l and x0 + 64 + l), chosen where a 128-column block's
+// Y and chroma spans are whole 128-byte lines and a 64-column block's are not
+// (an odd integer step, e.g. 1080p -> 640x360: 384 bytes = 3 lines per row):
+// no line is then split between two blocks, which neighbouring workgroups on
+// other XCDs would both fetch from HBM (the headline kernel's CW = 2, k_resize_direct.hip).
+constexpr int kYuvRows = 8;   // output rows per wave task (at CW = 1)
+constexpr int kYuvHalf = 4;   // rows per LDS exchange round (at CW = 1)
+template <int OUT, int MODE, bool CHW, bool ONE_ROW, int CW>
 __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(yuv_waves(OUT, ONE_ROW))))
 yuv_cols_kernel(YuvResizeLaunch L, int col_blocks, int row_groups) {
     using TOut = typename std::conditional<(OUT == kOutSame), uint8_t, float>::type;
     constexpr int kES = (int)sizeof(TOut);
     constexpr int NR = ONE_ROW ? 1 : 2;
-    constexpr int kRowB = 64 * kES * (CHW ? 1 : 3);          // bytes of one block row (per plane)
-    constexpr int kPlaneB = kYuvHalf * kRowB;                 // one round's bytes per plane
+    constexpr int ROWS = kYuvRows / CW;                       // output rows per task
+    constexpr int HALF = kYuvHalf / CW;                       // rows per exchange round
+    constexpr int kRowB = 64 * CW * kES * (CHW ? 1 : 3);      // bytes of one block row (per plane)
+    constexpr int kPlaneB = HALF * kRowB;                     // one round's bytes per plane
     __shared__ __attribute__((aligned(16))) unsigned char xch[4][3 * kYuvHalf * 64 * kES];
     const int lane = (int)threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
@@ -329,35 +338,40 @@ yuv_cols_kernel(YuvResizeLaunch L, int col_blocks, int row_groups) {
     const int img = blockIdx.y;
     const int rg = task / col_blocks, cb = task - rg * col_blocks;
     const int W = L.wo, H = L.ho;
-    const int x0 = cb * 64, y0 = rg * kYuvRows;
-    const int ncol = min(64, W - x0), nrow = min(kYuvRows, H - y0);  // uniform
-    const int x = lane < ncol ? x0 + lane : W - 1;
+    const int x0 = cb * 64 * CW, y0 = rg * ROWS;
+    const int ncol = min(64 * CW, W - x0), nrow = min(ROWS, H - y0);  // uniform
 
     const unsigned char* sp = L.src + (int64_t)img * L.src_img;
     const Rsrc rs = make_rsrc(sp, L.src_bytes);
     const uint32_t rp = (uint32_t)L.src_row;
     const uint32_t uvbase = (uint32_t)L.h * rp;
 
-    // the column's tap and chroma selector (once).  The block's last lane
-    // reads its Y dword (and, at an even tap, its chroma dword) from 2 bytes
-    // earlier, its bytes picked by the selectors: so no gather reaches into
-    // the next block's first 128-byte line, which neighbouring workgroups --
-    // on other XCDs -- would otherwise both fetch from HBM (PMC: reads 413 ->
-    // 372 MB at 256 x NV21 1080p -> 640x360, B_alg 354 MB).
-    const FixedTap tx = tap_of<MODE>(x, L.w, W, L.scale_xf, L.scale_xd);
-    const us2 wx = __builtin_bit_cast(us2, (uint32_t)tx.w0 | ((uint32_t)tx.w1 << 16));
-    const bool edge = lane == 63 && tx.i >= 2;
-    const int ca = tx.i & ~1, c0 = min(ca, L.w - 4);
-    const int c1 = edge && (tx.i & 1) == 0 && c0 == ca ? c0 - 2 : c0;
-    const uint32_t ca_rel = (uint32_t)(ca - c1);
-    const uint32_t cs = ca_rel | ((ca_rel + 2u * (uint32_t)(tx.i & 1)) << 2);
-    const uint32_t ycol = (uint32_t)(edge ? tx.i - 2 : tx.i);
-    const uint32_t ysel = edge ? 0x0C030C02u : 0x0C010C00u;
-    const uint32_t ccol = (uint32_t)c1;
-    // lane r < kYuvRows: row r's tap -- source Y / chroma row offsets (rows i
+    // the columns' taps and chroma selectors (once).  The block's last column
+    // (lane 63 of its last 64) reads its Y dword (and, at an even tap, its
+    // chroma dword) from 2 bytes earlier, its bytes picked by the selectors:
+    // so no gather reaches into the next block's first 128-byte line, which
+    // neighbouring workgroups -- on other XCDs -- would otherwise both fetch
+    // from HBM (PMC: reads 413 -> 372 MB at 256 x NV21 1080p -> 640x360, B_alg 354 MB).
+    us2 wx[CW];
+    uint32_t cs[CW], ycol[CW], ysel[CW], ccol[CW];
+#pragma unroll
+    for (int c = 0; c < CW; ++c) {
+        const int x = 64 * c + lane < ncol ? x0 + 64 * c + lane : W - 1;
+        const FixedTap tx = tap_of<MODE>(x, L.w, W, L.scale_xf, L.scale_xd);
+        wx[c] = __builtin_bit_cast(us2, (uint32_t)tx.w0 | ((uint32_t)tx.w1 << 16));
+        const bool edge = c == CW - 1 && lane == 63 && tx.i >= 2;
+        const int ca = tx.i & ~1, c0 = min(ca, L.w - 4);
+        const int c1 = edge && (tx.i & 1) == 0 && c0 == ca ? c0 - 2 : c0;
+        const uint32_t ca_rel = (uint32_t)(ca - c1);
+        cs[c] = ca_rel | ((ca_rel + 2u * (uint32_t)(tx.i & 1)) << 2);
+        ycol[c] = (uint32_t)(edge ? tx.i - 2 : tx.i);
+        ysel[c] = edge ? 0x0C030C02u : 0x0C010C00u;
+        ccol[c] = (uint32_t)c1;
+    }
+    // lane r < ROWS: row r's tap -- source Y / chroma row offsets (rows i
     // and i + 1) and weights wA | wB << 16
     uint32_t my_y0 = 0, my_c0 = 0, my_y1 = 0, my_c1 = 0, my_w = 0;
-    if (lane < kYuvRows) {
+    if (lane < ROWS) {
         FixedTap ty = tap_of<MODE>(min(y0 + lane, H - 1), L.h, H, L.scale_yf, L.scale_yd);
         if (ONE_ROW && ty.w0 == 0) { ty.i += 1; ty.w0 = ty.w1; ty.w1 = 0; }  // the weighted row as row A
         const RowOffs ro = row_offs(ty.i, rp, uvbase, rs.delta);
@@ -365,18 +379,21 @@ yuv_cols_kernel(YuvResizeLaunch L, int col_blocks, int row_groups) {
         my_w = (uint32_t)ty.w0 | ((uint32_t)ty.w1 << 16);
     }
     // every gather of the task, issued before any decode
-    RowTaps t[kYuvRows][NR];
+    RowTaps t[ROWS][CW][NR];
 #pragma unroll
-    for (int r = 0; r < kYuvRows; ++r) {
+    for (int r = 0; r < ROWS; ++r) {
         const uint32_t ya = (uint32_t)__builtin_amdgcn_readlane((int)my_y0, r);
         const uint32_t ca = (uint32_t)__builtin_amdgcn_readlane((int)my_c0, r);
-        t[r][0].y = __builtin_amdgcn_raw_buffer_load_b32(rs.r, (int)(ya + ycol), 0, kYuvAux);
-        t[r][0].c = __builtin_amdgcn_raw_buffer_load_b32(rs.r, (int)(ca + ccol), 0, kYuvAux);
-        if constexpr (!ONE_ROW) {
-            const uint32_t yb = (uint32_t)__builtin_amdgcn_readlane((int)my_y1, r);
-            const uint32_t cb2 = (uint32_t)__builtin_amdgcn_readlane((int)my_c1, r);
-            t[r][1].y = __builtin_amdgcn_raw_buffer_load_b32(rs.r, (int)(yb + ycol), 0, kYuvAux);
-            t[r][1].c = __builtin_amdgcn_raw_buffer_load_b32(rs.r, (int)(cb2 + ccol), 0, kYuvAux);
+        const uint32_t yb = ONE_ROW ? 0u : (uint32_t)__builtin_amdgcn_readlane((int)my_y1, r);
+        const uint32_t cb2 = ONE_ROW ? 0u : (uint32_t)__builtin_amdgcn_readlane((int)my_c1, r);
+#pragma unroll
+        for (int c = 0; c < CW; ++c) {
+            t[r][c][0].y = __builtin_amdgcn_raw_buffer_load_b32(rs.r, (int)(ya + ycol[c]), 0, kYuvAux);
+            t[r][c][0].c = __builtin_amdgcn_raw_buffer_load_b32(rs.r, (int)(ca + ccol[c]), 0, kYuvAux);
+            if constexpr (!ONE_ROW) {
+                t[r][c][1].y = __builtin_amdgcn_raw_buffer_load_b32(rs.r, (int)(yb + ycol[c]), 0, kYuvAux);
+                t[r][c][1].c = __builtin_amdgcn_raw_buffer_load_b32(rs.r, (int)(cb2 + ccol[c]), 0, kYuvAux);
+            }
         }
     }
     ChanNorm cn[3] = {};
@@ -395,36 +412,40 @@ yuv_cols_kernel(YuvResizeLaunch L, int col_blocks, int row_groups) {
     TOut* xo = reinterpret_cast<TOut*>(xch[wave]);
     const unsigned char* xs = xch[wave];
 #pragma unroll
-    for (int g = 0; g < kYuvRows / kYuvHalf; ++g) {
+    for (int g = 0; g < ROWS / HALF; ++g) {
 #pragma unroll
-        for (int j = 0; j < kYuvHalf; ++j) {
-            const int r = g * kYuvHalf + j;
+        for (int j = 0; j < HALF; ++j) {
+            const int r = g * HALF + j;
             const uint32_t wr = (uint32_t)__builtin_amdgcn_readlane((int)my_w, r);
-            uint32_t pa[3], pb[3] = {0u, 0u, 0u};  // rows A/B: B, G, R as u16 pairs {left, right}
-            decode_row(t[r][0], cs, L.v_first, pa[0], pa[1], pa[2], ysel);
-            if (!ONE_ROW) decode_row(t[r][NR - 1], cs, L.v_first, pb[0], pb[1], pb[2], ysel);
-            if (L.rgb) {  // output order R, G, B
-                const uint32_t q0 = pa[0], q1 = pb[0];
-                pa[0] = pa[2]; pa[2] = q0;
-                pb[0] = pb[2]; pb[2] = q1;
-            }
             const uint32_t wA = wr & 0xFFFFu, wB = ONE_ROW ? 0u : wr >> 16;
 #pragma unroll
-            for (int k = 0; k < 3; ++k) {
-                const int v = blend_fixed<MODE>(pa[k], pb[k], wx, wA, wB);
-                TOut ov;
-                if (OUT == kOutSame) ov = (TOut)v;
-                else if (OUT == kOutF32) ov = (TOut)(float)v;
-                else ov = (TOut)normalize_u8v(cn[k], v);
-                xo[CHW ? k * (kYuvHalf * 64) + j * 64 + lane : (j * 64 + lane) * 3 + k] = ov;
+            for (int c = 0; c < CW; ++c) {
+                uint32_t pa[3], pb[3] = {0u, 0u, 0u};  // rows A/B: B, G, R as u16 pairs {left, right}
+                decode_row(t[r][c][0], cs[c], L.v_first, pa[0], pa[1], pa[2], ysel[c]);
+                if (!ONE_ROW) decode_row(t[r][c][NR - 1], cs[c], L.v_first, pb[0], pb[1], pb[2], ysel[c]);
+                if (L.rgb) {  // output order R, G, B
+                    const uint32_t q0 = pa[0], q1 = pb[0];
+                    pa[0] = pa[2]; pa[2] = q0;
+                    pb[0] = pb[2]; pb[2] = q1;
+                }
+#pragma unroll
+                for (int k = 0; k < 3; ++k) {
+                    const int v = blend_fixed<MODE>(pa[k], pb[k], wx[c], wA, wB);
+                    TOut ov;
+                    if (OUT == kOutSame) ov = (TOut)v;
+                    else if (OUT == kOutF32) ov = (TOut)(float)v;
+                    else ov = (TOut)normalize_u8v(cn[k], v);
+                    const int px = j * 64 * CW + 64 * c + lane;  // pixel in the round
+                    xo[CHW ? k * (HALF * 64 * CW) + px : px * 3 + k] = ov;
+                }
             }
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        const int rows = min(kYuvHalf, nrow - g * kYuvHalf);  // uniform
+        const int rows = min(HALF, nrow - g * HALF);  // uniform
         if (rows > 0) {
-            const uint32_t base = (uint32_t)(y0 + g * kYuvHalf) * (uint32_t)L.dst_row +
+            const uint32_t base = (uint32_t)(y0 + g * HALF) * (uint32_t)L.dst_row +
                                   (uint32_t)(x0 * kES * (CHW ? 1 : 3)) + rd.delta;
 #pragma unroll
             for (int k = 0; k < (CHW ? 3 : 1); ++k) {
@@ -455,13 +476,30 @@ yuv_cols_kernel(YuvResizeLaunch L, int col_blocks, int row_groups) {
     }
 }
 
+// CW for a geometry (see yuv_cols_kernel): 2 where the column step is an odd
+// integer, the output has whole 128-column blocks and the source rows are
+// line-aligned (VACV_TUNE_RESIZE_TILE_W = 64 forces 1)
+int yuv_cols_cw(const YuvResizeLaunch& L) {
+    if (tune(VACV_TUNE_RESIZE_TILE_W) == 64) return 1;
+    if (L.w % L.wo || L.wo % 128) return 1;
+    const int step = L.w / L.wo;
+    const bool lines = L.src_row % 128 == 0 && (reinterpret_cast<uintptr_t>(L.src) & 127) == 0 && L.src_img % 128 == 0;
+    return lines && (step & 1) ? 2 : 1;
+}
+
+template <int OUT, int MODE, bool CHW, bool ONE_ROW, int CW>
+hipError_t launch_cols_cw(const YuvResizeLaunch& L, hipStream_t s) {
+    const int col_blocks = (L.wo + 64 * CW - 1) / (64 * CW), row_groups = (L.ho + kYuvRows / CW - 1) / (kYuvRows / CW);
+    const dim3 grid((unsigned)((col_blocks * row_groups + 3) / 4), (unsigned)L.n);
+    hipLaunchKernelGGL((yuv_cols_kernel<OUT, MODE, CHW, ONE_ROW, CW>), grid, dim3(kBlock), 0, s, L, col_blocks, row_groups);
+    return hipGetLastError();
+}
+
 template <int OUT, int MODE, bool CHW>
 hipError_t launch_cols_t(const YuvResizeLaunch& L, bool one_row, hipStream_t s) {
-    const int col_blocks = (L.wo + 63) / 64, row_groups = (L.ho + kYuvRows - 1) / kYuvRows;
-    const dim3 grid((unsigned)((col_blocks * row_groups + 3) / 4), (unsigned)L.n);
-    if (one_row) hipLaunchKernelGGL((yuv_cols_kernel<OUT, MODE, CHW, true>), grid, dim3(kBlock), 0, s, L, col_blocks, row_groups);
-    else hipLaunchKernelGGL((yuv_cols_kernel<OUT, MODE, CHW, false>), grid, dim3(kBlock), 0, s, L, col_blocks, row_groups);
-    return hipGetLastError();
+    if (yuv_cols_cw(L) == 2)
+        return one_row ? launch_cols_cw<OUT, MODE, CHW, true, 2>(L, s) : launch_cols_cw<OUT, MODE, CHW, false, 2>(L, s);
+    return one_row ? launch_cols_cw<OUT, MODE, CHW, true, 1>(L, s) : launch_cols_cw<OUT, MODE, CHW, false, 1>(L, s);
 }
 
 template <int OUT, int MODE, bool CHW>

@@ -9,6 +9,9 @@ One step = one vacv_resize_normalize call over the whole per-GPU batch (one
 kernel launch: resize_cols_kernel, k_resize_direct.hip).  Metric = input-frame Mpixels/s over all GPUs ("at 1080p").
 
 Other BASELINE configs (--workload; the default is the headline above):
+  resize_normalize_720p  the headline op at 1080p -> 1280x720 fp32: every output
+                row weights two source rows (SURVEY 8(d)'s "honest roofline
+                case"; resize_strip_kernel), 256 per GPU
   warp          cfg4: warp_affine INTER_LINEAR 1280x720x3 u8, scale 0.9, rot 15,
                 aux (640,360,640,360), 128 frames per GPU (1024 over 8 GPUs)
   cvt_normalize cfg3: NV21 1920x1620 -> BGR 1920x1080x3 fp32 normalised, 256 per GPU
@@ -62,7 +65,8 @@ def parse():
     # warmups vs 0.2285 after 10 (the GPU's clocks settle under the load)
     ap.add_argument("--warmup", type=int, default=50)
     ap.add_argument("--workload", default="resize_normalize",
-                    choices=["resize_normalize", "warp", "cvt_normalize", "cubic_stats", "yuv_resize"])
+                    choices=["resize_normalize", "resize_normalize_720p", "warp", "cvt_normalize", "cubic_stats",
+                             "yuv_resize"])
     ap.add_argument("--batch", type=int, default=0, help="images per GPU (0: the workload's default)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget of the CPU baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -167,14 +171,15 @@ def cpu_case(workload: str):
             return stats(cubic(img.astype(np.float32), 224, 224))
         return one, imgs, 2560 * 1440, kind, "u8->fp32 2560x1440 + cubic 224x224 + mean_stddev"
     imgs = [synthetic_image(1000 + k, H_IN, W_IN, C) for k in range(4)]
+    wo, ho = (1280, 720) if workload == "resize_normalize_720p" else (W_OUT, H_OUT)
     if R:
         def one(img):
-            r = R.resize_linear(img, W_OUT, H_OUT)           # resize_naive.cpp:10-68
+            r = R.resize_linear(img, wo, ho)           # resize_naive.cpp:10-68
             return R.normalize(r.astype(np.float32), mean, std)  # tensor.cpp:477-481 + normalize_naive.cpp:74-90
     else:
         def one(img):
-            return O.normalize(O.u8_to_f32(O.resize_linear(img, W_OUT, H_OUT)), mean, std)
-    return one, imgs, W_IN * H_IN, kind, "1920x1080x3 u8 frames, resize_naive 640x360 + u8->fp32 + normalize"
+            return O.normalize(O.u8_to_f32(O.resize_linear(img, wo, ho)), mean, std)
+    return one, imgs, W_IN * H_IN, kind, f"1920x1080x3 u8 frames, resize_naive {wo}x{ho} + u8->fp32 + normalize"
 
 
 def host_cpus():
@@ -335,6 +340,15 @@ def make_workload(name: str, batch: int, dev, rank: int, world: int, ops) -> dic
                 "kernel": "cubic_cols_kernel", "frame": "2560x1440x3", "output": "224x224x3 fp32 + global mean/std",
                 "desc": "resize INTER_CUBIC 2560x1440x3 u8 -> 224x224x3 fp32 + global mean_stddev (RCCL all-reduce)",
                 "main": main, "extra": extra, "stats": stats, "inputs": src}
+    if name == "resize_normalize_720p":
+        B = batch or 256
+        src = u8(B, H_IN, W_IN, C)
+        dst = torch.empty((B, 720, 1280, C), dtype=torch.float32, device=dev)
+        return {"batch": B, "px": W_IN * H_IN, "b_alg": resize_bytes(W_IN, H_IN, C, 1280, 720, 1, 4) * B,
+                "kernel": "resize_strip_kernel", "frame": "1920x1080x3", "output": "1280x720x3 fp32",
+                "desc": "resize_normalize INTER_LINEAR 1920x1080x3 u8 NHWC -> 1280x720x3 fp32 "
+                        "(reference arithmetic, two weighted source rows per output row) + per-channel normalize",
+                "main": lambda stream=None: ops.resize_normalize(src, 1280, 720, MEAN, STD, out=dst, stream=stream)}
     B = batch or 256
     src = u8(B, H_IN, W_IN, C)
     dst = torch.empty((B, H_OUT, W_OUT, C), dtype=torch.float32, device=dev)

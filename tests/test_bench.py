@@ -12,7 +12,7 @@ REPO = Path(__file__).resolve().parent.parent
 if str(REPO) not in sys.path:
     sys.path.insert(0, str(REPO))
 
-WORKLOADS = {"resize_normalize": 1920 * 1080, "warp": 1280 * 720, "cvt_normalize": 1920 * 1080,
+WORKLOADS = {"resize_normalize": 1920 * 1080, "resize_normalize_720p": 1920 * 1080, "warp": 1280 * 720, "cvt_normalize": 1920 * 1080,
              "cubic_stats": 2560 * 1440, "yuv_resize": 1920 * 1080}
 
 

@@ -1012,6 +1012,19 @@ def test_match_template(ops, dev, oracle):
     assert (got == np.float32(255.0 * 255.0 * 226 * 141)).all()
     with ops.tuning(MATCH_KERNEL=0):
         assert_same(host(ops.match_template(to_dev(sat, dev), to_dev(stpl, dev), 2)), got, "match dot4 int32 limit")
+    # u8 window statistics as uint32 box sums (match_vsum_u8_kernel /
+    # match_finish_u8_kernel): the saturated image puts 255^2 * 31,866 =
+    # 2.07e9 in every window's square sum (uint32, exact) -- every method;
+    # and a row too wide for the workgroup's LDS prefix rows (2,800 x 3
+    # channels) takes the double integral images, against the oracle too
+    for m in (0, 1, 3, 4, 5):
+        assert_same(host(ops.match_template(to_dev(sat, dev), to_dev(stpl, dev), m)),
+                    oracle.match_template(sat, stpl, m), f"match box sums saturated method {m}")
+    wide = synthetic_image(980, 20, 2800, 3).reshape(20, 2800, 3)
+    wtpl = np.ascontiguousarray(wide[4:11, 100:109])
+    for m in (1, 5):
+        assert_same(host(ops.match_template(to_dev(wide[None], dev), to_dev(wtpl, dev), m))[0],
+                    oracle.match_template(wide, wtpl, m), f"match integral images wide row method {m}")
     # minMaxIdx on a match result finds the template's position
     got = ops.match_template(to_dev(img, dev), to_dev(small, dev), 0)
     mn, mx, imn, imx = ops.min_max_idx(got)
@@ -1520,8 +1533,13 @@ def test_cvt_color_resize_batch_and_pitch(ops, dev, oracle):
             a = fn()
             with ops.tuning(RESIZE_DIRECT=2):
                 b = fn()
+            # 64-column blocks instead of the 128-column ones (CW = 2) of the
+            # odd-step geometries (1080p -> 640x360)
+            with ops.tuning(RESIZE_TILE_W=64):
+                c = fn()
             torch.cuda.synchronize(dev)
             assert torch.equal(a, b), f"{wo}x{ho} layout {layout}: {(a != b).sum().item()} values differ"
+            assert torch.equal(a, c), f"{wo}x{ho} layout {layout} 64-column blocks: {(a != c).sum().item()} differ"
     # the fused op equals the unfused GPU chain (cvt_color, resize_normalize, layout)
     bgr = ops.cvt_color(yuv[:4])
     chain = ops.change_layout(ops.resize_normalize(bgr, 224, 224, MEAN, STD), V.NCHW)
