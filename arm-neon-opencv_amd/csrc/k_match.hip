@@ -355,6 +355,187 @@ __global__ void __launch_bounds__(kBlock) match_finish_kernel(MatchLaunch M) {
     *out = (float)num;
 }
 
+// ---- u8 window statistics: exact integer box sums (round 6) -----------------
+// For u8 every window sum is an integer: per channel S_c <= 255 tw th and Q_c
+// <= 255^2 tw th, both < 2^32 for tw th <= 66,000 (host-checked), so they are
+// kept in uint32 -- with wrap-around: the difference of two wrapped prefix
+// sums is the exact window sum whenever that sum is < 2^32 -- and they equal
+// the 4-term differences of the double integrals above exactly (every double
+// there is an integer < 2^53).  Two passes of 4-byte sums instead of three
+// over 8-byte integral images:
+//  * match_vsum_u8_kernel: the vertical window sums V[r][e] = the sum of rows
+//    r .. r + th - 1 of row element e (= x cn + c), and the same of squares;
+//    a thread per element and chunk of kVsRows result rows, sliding down;
+//  * match_finish_u8_kernel: a workgroup per result row stages V's row (both
+//    arrays) in LDS, turns each channel into exclusive prefix sums, and each
+//    result element takes S_c and Q_c as 2-term differences, then applies
+//    match_finish_kernel's normalisation in the same operation order.
+// Layout per image: [2][rh][iw * cn] uint32 (sums, then squares).
+constexpr int kVsRows = 64;  // result rows per thread of the vertical pass
+constexpr int kVsU = 8;      // rows whose loads are issued together
+
+__global__ void __launch_bounds__(kBlock) match_vsum_u8_kernel(MatchLaunch M) {
+    const int E = M.iw * M.cn;
+    const int e = (int)blockIdx.x * kBlock + (int)threadIdx.x;
+    const int img = blockIdx.z;
+    if (e >= E) return;
+    const int r0 = (int)blockIdx.y * kVsRows, r1 = min(r0 + kVsRows, M.rh);
+    const unsigned char* col = M.img + (int64_t)img * M.img_pitch + e;
+    const int64_t row = M.img_row;
+    uint32_t s = 0, q = 0;
+    for (int y = 0; y < M.th; y += kVsU) {  // the first window: rows r0 .. r0 + th - 1
+        uint32_t v[kVsU];
+#pragma unroll
+        for (int u = 0; u < kVsU; ++u) v[u] = y + u < M.th ? (uint32_t)col[(int64_t)(r0 + y + u) * row] : 0u;
+#pragma unroll
+        for (int u = 0; u < kVsU; ++u) {
+            s += v[u];
+            q += v[u] * v[u];
+        }
+    }
+    uint32_t* vs = reinterpret_cast<uint32_t*>(M.box) + (int64_t)img * 2 * M.rh * E + e;
+    uint32_t* vq = vs + (int64_t)M.rh * E;
+    for (int r = r0; r < r1; r += kVsU) {  // then slide: + row r + th, - row r
+        uint32_t a[kVsU], b[kVsU];
+#pragma unroll
+        for (int u = 0; u < kVsU; ++u) {
+            const bool in = r + u + 1 < r1;
+            a[u] = in ? (uint32_t)col[(int64_t)(r + u + M.th) * row] : 0u;
+            b[u] = in ? (uint32_t)col[(int64_t)(r + u) * row] : 0u;
+        }
+#pragma unroll
+        for (int u = 0; u < kVsU; ++u) {
+            if (r + u < r1) {
+                vs[(int64_t)(r + u) * E] = s;
+                vq[(int64_t)(r + u) * E] = q;
+            }
+            s += a[u] - b[u];  // wraps when negative: the sum stays exact modulo 2^32
+            q += a[u] * a[u] - b[u] * b[u];
+        }
+    }
+}
+
+// grid (rh, n); dynamic LDS 2 (iw + 1) cn uint32
+__global__ void __launch_bounds__(kBlock) match_finish_u8_kernel(MatchLaunch M) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t pre[];
+    const int cn = M.cn, E = M.iw * cn, PE = E + cn;  // prefix row: cn leading zeros
+    const int r = blockIdx.x, img = blockIdx.y;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const uint32_t* vs = reinterpret_cast<const uint32_t*>(M.box) + (int64_t)img * 2 * M.rh * E + (int64_t)r * E;
+    const uint32_t* vq = vs + (int64_t)M.rh * E;
+    uint32_t* ps = pre;
+    uint32_t* pq = pre + PE;
+    for (int i = tid; i < E; i += kBlock) {
+        ps[cn + i] = vs[i];
+        pq[cn + i] = vq[i];
+    }
+    if (tid < cn) ps[tid] = pq[tid] = 0u;
+    __syncthreads();
+    // thread t: pixels [t L, min((t + 1) L, iw)) -- a running sum per channel
+    // (its elements are 15 dwords apart for L = 5, cn = 3: no bank conflicts)
+    const int L = (M.iw + kBlock - 1) / kBlock;
+    const int p0 = min(tid * L, M.iw), p1 = min(p0 + L, M.iw);
+    uint32_t ts[4] = {0u, 0u, 0u, 0u}, tq[4] = {0u, 0u, 0u, 0u};
+    for (int x = p0; x < p1; ++x) {
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            if (c < cn) {
+                const int i = cn + x * cn + c;
+                ts[c] += ps[i];
+                tq[c] += pq[i];
+                ps[i] = ts[c];
+                pq[i] = tq[c];
+            }
+        }
+    }
+    // exclusive scan of the thread totals over the workgroup, per channel
+    __shared__ uint32_t wtot[2][4][kBlock / 64];
+    uint32_t xs[4], xq[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        uint32_t a = ts[c], b = tq[c];
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t ua = (uint32_t)__shfl_up((int)a, o, 64), ub = (uint32_t)__shfl_up((int)b, o, 64);
+            if (lane >= o) {
+                a += ua;
+                b += ub;
+            }
+        }
+        xs[c] = a - ts[c];
+        xq[c] = b - tq[c];
+        if (lane == 63) {
+            wtot[0][c][wave] = a;
+            wtot[1][c][wave] = b;
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        for (int w = 0; w < wave; ++w) {
+            xs[c] += wtot[0][c][w];
+            xq[c] += wtot[1][c][w];
+        }
+    }
+    for (int x = p0; x < p1; ++x) {
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            if (c < cn) {
+                const int i = cn + x * cn + c;
+                ps[i] += xs[c];
+                pq[i] += xq[c];
+            }
+        }
+    }
+    __syncthreads();
+    // the result row: match_finish_kernel's formula with the window sums
+    const double* tsd = M.tstats;  // tmean[4], templNorm, templSum2, all-ones flag
+    const int method = M.method;
+    const int numType = (method == VACV_TM_CCORR || method == VACV_TM_CCORR_NORMED)     ? 0
+                        : (method == VACV_TM_CCOEFF || method == VACV_TM_CCOEFF_NORMED) ? 1
+                                                                                        : 2;
+    const bool isNormed = method == VACV_TM_CCORR_NORMED || method == VACV_TM_SQDIFF_NORMED ||
+                          method == VACV_TM_CCOEFF_NORMED;
+    const double invArea = M.inv_area;
+    const int dw = M.tw * cn;
+    float* orow = reinterpret_cast<float*>(M.res + (int64_t)img * M.res_pitch + (int64_t)r * M.res_row);
+    for (int x = tid; x < M.rw; x += kBlock) {
+        float* out = orow + x;
+        if (tsd[6] != 0.0) {  // CCOEFF_NORMED of a flat template
+            *out = 1.f;
+            continue;
+        }
+        const int i0 = x * cn;
+        double num = (double)*out, t;
+        double wndMean2 = 0, wndSum2 = 0;
+        if (numType == 1) {
+            for (int c = 0; c < cn; ++c) {
+                t = (double)(ps[i0 + dw + c] - ps[i0 + c]);
+                wndMean2 += t * t;
+                num -= t * tsd[c];
+            }
+            wndMean2 *= invArea;
+        }
+        if (isNormed || numType == 2) {
+            for (int c = 0; c < cn; ++c) {
+                t = (double)(pq[i0 + dw + c] - pq[i0 + c]);
+                wndSum2 += t;
+            }
+            if (numType == 2) {
+                num = wndSum2 - 2 * num + tsd[5];
+                num = num > 0. ? num : 0.;
+            }
+        }
+        if (isNormed) {
+            t = sqrt(wndSum2 - wndMean2 > 0. ? wndSum2 - wndMean2 : 0.) * tsd[4];
+            if (fabs(num) < t) num /= t;
+            else if (fabs(num) < t * 1.125) num = num > 0 ? 1 : -1;
+            else num = method != VACV_TM_SQDIFF_NORMED ? 0 : 1;
+        }
+        *out = (float)num;
+    }
+}
+
 // the template's mean / population stddev per channel (one workgroup per
 // image's template -- templates are shared: blockIdx.x = 0 only), then the
 // method's constants as templmatch.cpp derives them
@@ -713,6 +894,14 @@ hipError_t launch_match_template(const MatchLaunch& M, hipStream_t s) {
     if (e != hipSuccess || M.method == VACV_TM_CCORR) return e;
     if (M.esize == 1) hipLaunchKernelGGL(match_tstats_kernel<uint8_t>, dim3(1), dim3(kBlock), 0, s, M);
     else hipLaunchKernelGGL(match_tstats_kernel<float>, dim3(1), dim3(kBlock), 0, s, M);
+    if (M.esize == 1 && (int64_t)M.tw * M.th <= 66000 && 2 * (int64_t)(M.iw + 1) * M.cn * 4 <= 64 * 1024) {
+        // u8: exact integer box sums (the same values as the integrals)
+        const int E = M.iw * M.cn;
+        const dim3 gv((E + kBlock - 1) / kBlock, (M.rh + kVsRows - 1) / kVsRows, M.n);
+        hipLaunchKernelGGL(match_vsum_u8_kernel, gv, dim3(kBlock), 0, s, M);
+        hipLaunchKernelGGL(match_finish_u8_kernel, dim3(M.rh, M.n), dim3(kBlock), (size_t)(2 * (E + M.cn) * 4), s, M);
+        return hipGetLastError();
+    }
     const dim3 gr((M.ih * M.cn + kBlock - 1) / kBlock, M.n);
     if (M.esize == 1 && M.iw <= 33000) {
         const dim3 gw((M.ih + kBlock / 64 - 1) / (kBlock / 64), M.n);
