@@ -107,8 +107,10 @@ TUNE = {"RESIZE_DIRECT": 0, "CUBIC_DIRECT": 1, "RESIZE_INTERLEAVE": 2, "DIRECT_X
         "LANCZOS_KERNEL": 18}
 
 # include/vacv_hip.h VACV_ABI_VERSION: the tuning enum above and every
-# signature here are laid out for it (tests/test_abi.py checks the header)
-ABI_VERSION = 2
+# signature here are laid out for it (tests/test_abi.py checks the header).
+# Bumped with every change to a signature or to the tuning enum (3: round 6,
+# after round 5 added LANCZOS_KERNEL under version 2)
+ABI_VERSION = 3
 
 _lib = None
 
@@ -141,6 +143,13 @@ def load() -> ctypes.CDLL:
         # e.g. a stale variant build under VACV_LIB_DIR: its tuning knobs and
         # entry points would not mean what this binding passes
         raise ImportError(f"{path} implements C ABI version {got}, this binding expects {ABI_VERSION}: rebuild it")
+    # and the tuning enum has exactly this binding's keys (VACV_TUNE_COUNT):
+    # the last key is accepted (set to the value it holds: an environment
+    # override survives), the one after it is not.  vacv_get_tuning alone
+    # cannot tell: its "built-in choice" -1 is INVALID_ARG's code
+    n = len(TUNE)
+    if lib.vacv_set_tuning(n - 1, lib.vacv_get_tuning(n - 1)) != OK or lib.vacv_set_tuning(n, -1) != ERR_INVALID_ARG:
+        raise ImportError(f"{path}: its tuning enum does not have the {n} keys this binding knows: rebuild it")
     _lib = lib
     return lib
 

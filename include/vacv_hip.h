@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define VACV_ABI_VERSION 2
+#define VACV_ABI_VERSION 3
 #define VACV_MAX_CHANNELS 16
 
 typedef enum vacv_status {

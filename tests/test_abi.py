@@ -44,6 +44,12 @@ def test_version_and_status(lib):
     declared = int(re.search(r"#define VACV_ABI_VERSION (\d+)", hdr).group(1))
     assert vacv_amd._lib.ABI_VERSION == declared, "binding and header disagree on the ABI version"
     assert lib.vacv_abi_version() == declared
+    # the binding's tuning keys are the header's enum, and the library's
+    count = int(re.search(r"VACV_TUNE_COUNT = (\d+)", hdr).group(1))
+    assert len(vacv_amd._lib.TUNE) == count and sorted(vacv_amd._lib.TUNE.values()) == list(range(count))
+    for name, key in vacv_amd._lib.TUNE.items():
+        assert re.search(rf"VACV_TUNE_{name} = {key},", hdr), name
+    assert lib.vacv_set_tuning(count - 1, -1) == 0 and lib.vacv_set_tuning(count, -1) == -1
     assert lib.vacv_status_string(0) == b"ok"
     assert lib.vacv_status_string(-2) == b"unsupported"
 
