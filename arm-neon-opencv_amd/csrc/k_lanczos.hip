@@ -131,21 +131,8 @@ __device__ __forceinline__ T lz_const(const T* p, int i) {
     return ((const __attribute__((address_space(4))) T*)(uintptr_t)p)[i];
 }
 
-#ifndef VACV_LZ_WAVES
-#define VACV_LZ_WAVES 4
-#endif
-constexpr int kLzWaves = VACV_LZ_WAVES;  // waves (strip tasks) per workgroup; each owns its own ring
-#ifndef VACV_LZ_D
-#define VACV_LZ_D 3  // u8 source rows in flight per wave (1 / 2 / 3 / 4 / 6 / 8: 0.580 / 0.522 / 0.495 / 0.525 / 0.534 / 0.565 ms)
-#endif
-#ifndef VACV_LZ_SLOTS
-#define VACV_LZ_SLOTS 1
-#endif
-// diagnosis builds (0 in the product): 1 no horizontal arithmetic, 2 no
-// window loads, 4 the dropped stores from one lane, 8 no output stores
-#ifndef VACV_LZ_DBG
-#define VACV_LZ_DBG 0
-#endif
+constexpr int kLzWaves = 4;  // waves (strip tasks) per workgroup; each owns its own ring
+constexpr int kLzD = 3;      // u8 source rows in flight per wave (1 / 2 / 3 / 4 / 6 / 8: 0.580 / 0.522 / 0.495 / 0.525 / 0.534 / 0.565 ms)
 template <typename TIn, int OUT, int CC>
 __global__ void __launch_bounds__(64 * kLzWaves) lanczos_kernel(LanczosLaunch L, int strips, int bands, int band_rows, int blocks, int xcd_per) {
     constexpr bool U8 = std::is_same<TIn, uint8_t>::value;
@@ -155,7 +142,7 @@ __global__ void __launch_bounds__(64 * kLzWaves) lanczos_kernel(LanczosLaunch L,
     constexpr int ND = U8 ? (8 * CC + 6) / 4 : 8 * CC;
     // source rows in flight per wave (the loads of rows r + 1 .. r + D - 1
     // run while row r is resized)
-    constexpr int D = U8 ? VACV_LZ_D : 2;
+    constexpr int D = U8 ? kLzD : 2;
     // per wave: 8 source rows x 64 columns x RS (padding c = 3 to 4, for one
     // 16-byte LDS access per lane and row, cost a workgroup per CU of LDS:
     // 0.589 vs 0.530 ms)
@@ -217,11 +204,6 @@ __global__ void __launch_bounds__(64 * kLzWaves) lanczos_kernel(LanczosLaunch L,
     auto load = [&](auto safe_c, uint32_t (&d)[ND], int r) {
         constexpr bool SAFE = decltype(safe_c)::value;
         const uint32_t a = (uint32_t)r * rp + (wbyte & ~3u);
-        if constexpr ((VACV_LZ_DBG & 2) != 0) {
-#pragma unroll
-            for (int q = 0; q < ND; ++q) d[q] = a + 977u * q;
-            return;
-        }
         if (!SAFE || a + 4u * ND <= slimit) {
             int q = 0;
 #pragma unroll
@@ -257,10 +239,7 @@ __global__ void __launch_bounds__(64 * kLzWaves) lanczos_kernel(LanczosLaunch L,
             uint32_t wv[ND - 1];
 #pragma unroll
             for (int q = 0; q < ND - 1; ++q) wv[q] = __builtin_amdgcn_alignbyte(d[q + 1], d[q], wsh);
-            if constexpr ((VACV_LZ_DBG & 1) != 0) {
-#pragma unroll
-                for (int k = 0; k < CC; ++k) hv[k] = (int)(wv[k % (ND - 1)] ^ wv[(k + 1) % (ND - 1)]);
-            } else if (interior) lz_h_u8<CC, 0, ND - 1>(wv, cp, hv);
+            if (interior) lz_h_u8<CC, 0, ND - 1>(wv, cp, hv);
             else switch (shift) {  // divergent: the strips at the image's edges
                 case -4: lz_h_u8<CC, -4, ND - 1>(wv, cp, hv); break;
                 case -3: lz_h_u8<CC, -3, ND - 1>(wv, cp, hv); break;
@@ -321,7 +300,7 @@ __global__ void __launch_bounds__(64 * kLzWaves) lanczos_kernel(LanczosLaunch L,
             // reads gets 0).  No per-row slot arithmetic on the scalar unit.
             int hs[8][CC];
             int bb[8];
-            if constexpr (VACV_LZ_SLOTS && OUT != kOutNorm) {  // (normalising: 0.647 vs 0.599 ms, registers)
+            if constexpr (OUT != kOutNorm) {  // (normalising: 0.647 vs 0.599 ms, registers)
 #pragma unroll
                 for (int j = 0; j < 8; ++j) {
 #pragma unroll
@@ -392,7 +371,6 @@ __global__ void __launch_bounds__(64 * kLzWaves) lanczos_kernel(LanczosLaunch L,
             }
         }
         uint32_t orow = (uint32_t)y * (uint32_t)L.dst.row_pitch + drs.delta;
-        if constexpr ((VACV_LZ_DBG & 8) != 0) orow = kOobStore;
         if constexpr (sizeof(TOut) == 1) {
             // u8: the quad's 4 CC bytes as CC dword stores (quad_pack) where the
             // quad is whole and the destination dword-aligned, else bytes
@@ -483,7 +461,7 @@ __global__ void __launch_bounds__(64 * kLzWaves) lanczos_kernel(LanczosLaunch L,
                         ++y;
                         if (y < y1) need = min(lz_const(L.t.yofs, y) + 4, h - 1);
                     } while (y < y1 && need == rr);
-                } else if ((VACV_LZ_DBG & 4) == 0 || lane == 0) {
+                } else {
                     __builtin_amdgcn_raw_buffer_store_b32(0u, drs.r, (int)kOobStore, 0, 0);
                 }
                 load(safe_c, buf[u], min(rr + D, re));
@@ -503,24 +481,15 @@ __global__ void __launch_bounds__(64 * kLzWaves) lanczos_kernel(LanczosLaunch L,
 // The host regroups each output row's 8 vertical coefficients by that
 // relative slot (yrec), so an output row is 8 multiply-adds per channel on
 // registers: no ring stores and reads, no LDS waits.  Diagnosis builds of the
-// LDS-ring kernel (VACV_LZ_DBG) ran 0.41 ms without any window load against
+// LDS-ring kernel (round 4) ran 0.41 ms without any window load against
 // 0.49 with them: the per-row instruction stream around the loads, not the
 // loads, bounded it.  Also: the border clamp is folded into each lane's
 // coefficients once (window pixel p weighs the sum of the taps that clamp to
 // it -- exact, the u8 sums are int arithmetic), so every lane runs the same
 // unrolled horizontal sum and the per-row 9-way shift switch is gone.
-#ifndef VACV_LZ_TASKS
-#define VACV_LZ_TASKS 65536  // wave tasks a launch aims for (bands shrink until there are about this many)
-#endif
-#ifndef VACV_LZ_MINROWS
-#define VACV_LZ_MINROWS 16  // output rows per band at least
-#endif
-#ifndef VACV_LZ_WPE
-#define VACV_LZ_WPE 0  // lanczos_u8_kernel: waves per SIMD the register allocation aims for (0: the compiler's choice)
-#endif
-#ifndef VACV_LZR_D
-#define VACV_LZR_D 4  // windows in flight per wave (a divisor of 8, the unroll)
-#endif
+constexpr int kLzTasks = 65536;  // wave tasks a launch aims for (bands shrink until there are about this many)
+constexpr int kLzMinRows = 16;  // output rows per band at least
+constexpr int kLzrD = 4;  // windows in flight per wave (a divisor of 8, the unroll)
 // NI > 0 (round 5): the wave's source run of a row (the 64 lanes' windows,
 // <= NI KiB, host-checked) moves as NI lane-contiguous 16-byte loads and
 // reaches the lanes' windows through the wave's own LDS slice: at a 3x
@@ -528,14 +497,11 @@ __global__ void __launch_bounds__(64 * kLzWaves) lanczos_kernel(LanczosLaunch L,
 // lane for 9 new ones).  NI = 0: every lane loads its own window.
 template <int OUT, int CC, int NI>
 __global__ void __launch_bounds__(64 * kLzWaves)
-#if VACV_LZ_WPE
-__attribute__((amdgpu_waves_per_eu(VACV_LZ_WPE)))
-#endif
 lanczos_u8_kernel(LanczosLaunch L, int strips, int bands, int band_rows,
                                                                      int blocks, int xcd_per) {
     using TOut = typename std::conditional<(OUT == kOutSame), uint8_t, float>::type;
     constexpr int ND = (8 * CC + 6) / 4;
-    constexpr int D = VACV_LZR_D;
+    constexpr int D = kLzrD;
     static_assert(8 % D == 0, "the window buffers rotate with the 8-row unroll");
 
     const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)), lane = (int)(threadIdx.x & 63);
@@ -1088,8 +1054,8 @@ int launch_resize_lanczos(const ResizeLaunch& R, double inv_x, double inv_y, hip
     const bool narrow = R.src.w < 8;
     if (!narrow) {
         g.strips = (R.dst.w + 63) / 64;
-        const int64_t want = (VACV_LZ_TASKS + g.strips * planes - 1) / (g.strips * planes);
-        g.bands = (int)std::max<int64_t>(1, std::min<int64_t>(want, (R.dst.h + VACV_LZ_MINROWS - 1) / VACV_LZ_MINROWS));
+        const int64_t want = (kLzTasks + g.strips * planes - 1) / (g.strips * planes);
+        g.bands = (int)std::max<int64_t>(1, std::min<int64_t>(want, (R.dst.h + kLzMinRows - 1) / kLzMinRows));
         g.band_rows = (R.dst.h + g.bands - 1) / g.bands;
         g.bands = (R.dst.h + g.band_rows - 1) / g.band_rows;
     }

@@ -94,36 +94,19 @@ __device__ __forceinline__ void direct_taps(const WarpLaunch& L, const unsigned 
 // wave's part, and frame f + ns - 1's DMA reuses the slot that frame f - 1
 // was sampled from -- every wave has consumed those reads before the barrier.
 constexpr int kRingMaxIt = 6;  // DMA instructions per wave and frame, at most (a box of 24 KiB)
-// Diagnosis builds (make EXTRA=-DVACV_RING_DBG=n LIB=... OBJ=...; tools/kbench_lib.py):
-// bit 0 no sampling and stores, bit 1 no DMA, bit 2 every lane reads its taps at
-// one LDS address (no bank conflicts), bit 3 (warp_exp_kernel, u8) every output
-// store dropped (offset past the plane).  Results are wrong in those builds.
-#ifndef VACV_RING_DBG
-#define VACV_RING_DBG 0
-#endif
-
 
 // L: launch block; gx, gy: tiles per frame; kf: frames per workgroup; S: LDS
 // bytes per staged row (a multiple of 16); rows_max: staged rows per slot;
 // ns, slot: LDS slots and their bytes; dst_al: the destination allows dword
 // (u8 out) stores; ginv = ceil(2^20 / (S / 16)) (row of chunk c = c ginv >> 20,
 // exact for c < 4096 and S / 16 <= 256).
-// cache policy of the ring kernel's output stores (A/B builds: EXTRA=-DVACV_RING_SAUX=n)
-#ifndef VACV_RING_SAUX
-#define VACV_RING_SAUX VACV_STORE_AUX
-#endif
-#ifndef VACV_RING_WPE
-#define VACV_RING_WPE 1
-#endif
-#ifndef VACV_RING_GRP
 // u8 output: pixels whose taps are read before their blends.  4: 103 VGPRs, 4
 // waves per SIMD; 2: 95, 5 waves (round 4, one box, 720p rot15: 0.1761 /
 // 0.1776 vs 0.1807 / 0.1812 ms; round 2's register-staged kernel preferred 2).
 // Other outputs keep 2.
-#define VACV_RING_GRP 4
-#endif
+constexpr int kRingGrp = 4;
 template <int CC, int OUT, int NP, bool PLANAR>
-__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(VACV_RING_WPE)))
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1)))
 warp_ring_kernel(WarpLaunch L, int gx, int gy, int kf, int S, int rows_max, int ns, int slot, int dst_al,
                  uint32_t ginv) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
@@ -131,11 +114,7 @@ warp_ring_kernel(WarpLaunch L, int gx, int gy, int kf, int S, int rows_max, int 
     // staging loads: sc0 for byte output (neighbouring tiles' boxes share
     // rows through L2), non-temporal for fp32 output, whose 4x larger stores
     // want the L2
-#ifdef VACV_RING_AUX
-    constexpr int kAux = VACV_RING_AUX;
-#else
     constexpr int kAux = OUT == kOutSame ? 1 : VACV_LOAD_AUX;
-#endif
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     int* red = reinterpret_cast<int*>(lds + ns * slot);  // 4 waves x 4 ints
@@ -315,7 +294,6 @@ warp_ring_kernel(WarpLaunch L, int gx, int gy, int kf, int S, int rows_max, int 
     // frame f's box -> slot s: n_w instructions, idle lanes out of range
     // (an out-of-range lane writes zeros to its own 16 bytes of the slot)
     auto dma = [&](int f, int s, bool live) {
-        if (VACV_RING_DBG & 2) return;
         const Rsrc rs = make_rsrc(L.src.base + frame_off(min(f, nfr - 1), L.src), L.src.plane_bytes);
         unsigned char* base = lds + s * slot + 16 + 1024 * wave;
 #pragma unroll
@@ -357,7 +335,7 @@ warp_ring_kernel(WarpLaunch L, int gx, int gy, int kf, int S, int rows_max, int 
     // at per-row addresses, which the compiler cannot merge, so the count is
     // exact; edge tiles count 0, i.e. their wait also drains the previous
     // frame's byte stores (conservative: ~9 % of cfg4's tiles).
-    const int n_st = (VACV_RING_DBG & 1) || !tile_full ? 0 : OUT != kOutSame ? NP : NP / 2;
+    const int n_st = !tile_full ? 0 : OUT != kOutSame ? NP : NP / 2;
 
     auto emit = [&](auto full_c, int fv, int j, uint32_t tlo, uint32_t thi, uint32_t blo, uint32_t bhi) {
         constexpr bool FULL = decltype(full_c)::value;
@@ -408,14 +386,14 @@ warp_ring_kernel(WarpLaunch L, int gx, int gy, int kf, int S, int rows_max, int 
                     const uint32_t off = lane < 2 * kChunks
                                              ? rowoff + (uint32_t)(bx * kFrTileW * CC + 16 * (m % kChunks))
                                              : kOob;
-                    __builtin_amdgcn_raw_buffer_store_b128(v, drs.r, (int)off, 0, VACV_RING_SAUX);
+                    __builtin_amdgcn_raw_buffer_store_b128(v, drs.r, (int)off, 0, VACV_STORE_AUX);
                 }
             } else {  // the edges, or a byte-aligned destination: CC byte stores, all issued
                 const uint32_t off = inside ? drow + (uint32_t)(x * CC) : kOob;
 #pragma unroll
                 for (int k = 0; k < CC; ++k)
                     __builtin_amdgcn_raw_buffer_store_b8((unsigned char)(own >> (8 * k)), drs.r,
-                                                         (int)(inside ? off + k : kOob), 0, VACV_RING_SAUX);
+                                                         (int)(inside ? off + k : kOob), 0, VACV_STORE_AUX);
             }
         } else {
             u32x4 o;
@@ -434,16 +412,16 @@ warp_ring_kernel(WarpLaunch L, int gx, int gy, int kf, int S, int rows_max, int 
             }
             const int off = (int)(inside ? drow + (uint32_t)(x * CC * 4) : kOob);
             if constexpr (CC == 1) {
-                __builtin_amdgcn_raw_buffer_store_b32(o[0], drs.r, off, 0, VACV_RING_SAUX);
+                __builtin_amdgcn_raw_buffer_store_b32(o[0], drs.r, off, 0, VACV_STORE_AUX);
             } else if constexpr (CC == 2) {
                 typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
-                __builtin_amdgcn_raw_buffer_store_b64(u32x2{o[0], o[1]}, drs.r, off, 0, VACV_RING_SAUX);
+                __builtin_amdgcn_raw_buffer_store_b64(u32x2{o[0], o[1]}, drs.r, off, 0, VACV_STORE_AUX);
             } else if constexpr (CC == 3) {
                 typedef unsigned int u32x3 __attribute__((ext_vector_type(3)));
                 const u32x3 o3 = {o[0], o[1], o[2]};
-                __builtin_amdgcn_raw_buffer_store_b96(o3, drs.r, off, 0, VACV_RING_SAUX);
+                __builtin_amdgcn_raw_buffer_store_b96(o3, drs.r, off, 0, VACV_STORE_AUX);
             } else {
-                __builtin_amdgcn_raw_buffer_store_b128(o, drs.r, off, 0, VACV_RING_SAUX);
+                __builtin_amdgcn_raw_buffer_store_b128(o, drs.r, off, 0, VACV_STORE_AUX);
             }
         }
     };
@@ -477,7 +455,7 @@ warp_ring_kernel(WarpLaunch L, int gx, int gy, int kf, int S, int rows_max, int 
                         const uint32_t off = lane < 2 * kChunks
                                                  ? rowoff + (uint32_t)(bx * kFrTileW * CC + 16 * (m % kChunks))
                                                  : kOob;
-                        __builtin_amdgcn_raw_buffer_store_b128(v, drs.r, (int)off, 0, VACV_RING_SAUX);
+                        __builtin_amdgcn_raw_buffer_store_b128(v, drs.r, (int)off, 0, VACV_STORE_AUX);
                     }
                 }
                 return;
@@ -540,13 +518,13 @@ warp_ring_kernel(WarpLaunch L, int gx, int gy, int kf, int S, int rows_max, int 
         }
     };
     auto sample = [&](auto full_c, int f, uint32_t sbase) {
-        constexpr int kGrp = OUT == kOutSame ? VACV_RING_GRP : 2;
+        constexpr int kGrp = OUT == kOutSame ? kRingGrp : 2;
 #pragma unroll
         for (int j0 = 0; j0 < NP; j0 += kGrp) {
             uint32_t tp[kGrp][4];
 #pragma unroll
             for (int j = 0; j < kGrp; ++j) {
-                const uint32_t ra = (VACV_RING_DBG & 4) ? 16u : rw[j0 + j] & 0xFFFFu;
+                const uint32_t ra = rw[j0 + j] & 0xFFFFu;
                 const unsigned char* a = lds + sbase + (ra & ~3u);
                 taps_at(a, ra & 3u, tp[j][0], tp[j][1]);
                 taps_at(a + S, ra & 3u, tp[j][2], tp[j][3]);
@@ -570,10 +548,8 @@ warp_ring_kernel(WarpLaunch L, int gx, int gy, int kf, int S, int rows_max, int 
         __builtin_amdgcn_s_barrier();  // every wave's part of frame f is in; frame f - 1's reads are done
         const int sn = s == 0 ? ns - 1 : s - 1;  // (f + ns - 1) mod ns: the slot frame f - 1 used
         dma(f + ns - 1, sn, f + ns - 1 < f1);
-        if (!(VACV_RING_DBG & 1)) {
-            if (tile_full) sample(full_t(), f, (uint32_t)(s * slot));
-            else sample(edge_t(), f, (uint32_t)(s * slot));
-        }
+        if (tile_full) sample(full_t(), f, (uint32_t)(s * slot));
+        else sample(edge_t(), f, (uint32_t)(s * slot));
         s = s + 1 == ns ? 0 : s + 1;
     }
     wait_vm(0);  // no LDS-DMA may outlive the workgroup's LDS
@@ -615,22 +591,15 @@ constexpr int kExpQ = 4;         // re-lay quarter units (4 pixels of one box ro
 constexpr int kExpUnits = kExpQ * kBlock / 4;  // image units (16 pixels) per tile, at most
 constexpr int kExpRows = 128;    // staged rows per tile, at most (the setup tables)
 constexpr int kExpTab = 16 + 12 * kExpRows + 64 * 4 * kRingMaxIt + kExpUnits + 16;  // setup tables, bytes
-#ifndef VACV_EXP_GRP
-#define VACV_EXP_GRP 2  // pixels whose taps are read before their blends (4: spills at <= 128 VGPRs)
-#endif
-#ifndef VACV_EXP_XCH
-#define VACV_EXP_XCH 1  // u8 output: 1 a 4-row LDS exchange + 12-byte stores; 0 DPP quad packing + dword stores per row
-#endif
-#ifndef VACV_EXP_F32XCH
-#define VACV_EXP_F32XCH 1  // fp32 output: 1 through the LDS exchange as 16-byte stores; 0 one 12-byte store per pixel (lanes contiguous)
-#endif
-#ifndef VACV_EXP_WPE
-#define VACV_EXP_WPE 4  // 4 waves per SIMD: <= 128 VGPRs (4 workgroups per CU, as the LDS plan)
-#endif
+constexpr int kExpGrp = 2;  // pixels whose taps are read before their blends (4: spills at <= 128 VGPRs)
+// Output through a per-wave LDS exchange: u8 4 rows -> 12-byte stores (DPP quad
+// packing with one dword store per row measured 0.186 vs 0.176 ms), fp32 one
+// row -> 16-byte stores (one 12-byte store per pixel: 0.422 vs 0.416 ms).
+constexpr int kExpXB(int out) { return out == kOutSame ? 4 * 64 * 4 : 64 * 3 * 4; }  // exchange bytes per wave
 // NN: INTER_NEAREST (OpenCV 2.4's warpAffine map, see warp_nearest_kernel in
 // k_warp.hip): the same staging, one tap per pixel, no blend.
 template <int OUT, int NP, bool NN>
-__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(VACV_EXP_WPE)))
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4)))  // <= 128 VGPRs: 4 workgroups per CU, as the LDS plan
 warp_exp_kernel(WarpLaunch L, int gx, int gy, int kf, int slot_bytes, int exp_units, int dst_al) {
     constexpr int CC = 3;
     constexpr int TW = kFrTileW;
@@ -640,14 +609,10 @@ warp_exp_kernel(WarpLaunch L, int gx, int gy, int kf, int slot_bytes, int exp_un
     // and 47 B after a row's chunks: bytes of no tapped pixel)
     // [image: 16 B border pixel head, then exp_units x 16 pixels; the setup
     //  tables live here until the first re-lay] [exchange: 4 waves x kXB]
-    constexpr int kXB = OUT == kOutSame ? (VACV_EXP_XCH ? 4 * 64 * 4 : 16) : (VACV_EXP_F32XCH ? 64 * CC * 4 : 16);
+    constexpr int kXB = kExpXB(OUT);
     const uint32_t ebase = 48u + 2u * (uint32_t)slot_bytes + 64u;
     const uint32_t xbase = ebase + 16u + 64u * (uint32_t)max(exp_units, (kExpTab + 63) / 64);
-#ifdef VACV_RING_AUX
-    constexpr int kAux = VACV_RING_AUX;
-#else
     constexpr int kAux = OUT == kOutSame ? 1 : VACV_LOAD_AUX;
-#endif
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     int* red = reinterpret_cast<int*>(lds + xbase);  // 4 waves x 4 ints, setup only
@@ -898,7 +863,6 @@ warp_exp_kernel(WarpLaunch L, int gx, int gy, int kf, int slot_bytes, int exp_un
         }
     }
     auto dma = [&](int f, int s) {
-        if (VACV_RING_DBG & 2) return;
         const Rsrc rs = make_rsrc(L.src.base + (int64_t)f * L.src.img_pitch, L.src.plane_bytes);
         unsigned char* base = lds + 48 + s * slot_bytes + 1024 * wave;
 #pragma unroll
@@ -962,8 +926,7 @@ warp_exp_kernel(WarpLaunch L, int gx, int gy, int kf, int slot_bytes, int exp_un
     // issued): full tiles one 12-byte store per 4 rows (u8) or one 16-byte
     // store per row (fp32); edge tiles count 0, so their waits also drain
     // the stores of the frames before (conservative)
-    const int n_st = (VACV_RING_DBG & 1) || !tile_full ? 0 : (OUT != kOutSame || !VACV_EXP_XCH) ? NP : NP / 4;
-    const uint32_t qsel = (lane & 3) == 0 ? 0x04020100u : (lane & 3) == 1 ? 0x05040201u : 0x06050402u;
+    const int n_st = !tile_full ? 0 : OUT != kOutSame ? NP : NP / 4;
 
     // one pixel's channels from its 4 taps ([b g r x] each): the sum << 2, the
     // result in bits 24..31 (warp_affine_naive.cpp:50-54)
@@ -989,17 +952,7 @@ warp_exp_kernel(WarpLaunch L, int gx, int gy, int kf, int slot_bytes, int exp_un
         const Rsrc drs = make_rsrc(dbase, L.dst.plane_bytes);
         if constexpr (OUT == kOutSame) {
             const uint32_t own = __builtin_amdgcn_perm(vv[2], __builtin_amdgcn_perm(vv[1], vv[0], 0x0C0C0703u), 0x0C070100u);
-            if constexpr (FULL && !VACV_EXP_XCH) {
-                // the quad's 4 pixels as 3 dwords in its lanes 0..2 (DPP), one
-                // dword store per row: 48 lanes, 192 contiguous bytes
-                const uint32_t nxt = (uint32_t)__builtin_amdgcn_mov_dpp((int)own, 0xF9, 0xF, 0xF, false);  // [1,2,3,3]
-                const uint32_t word = __builtin_amdgcn_perm(nxt, own, qsel);
-                const uint32_t off = (VACV_RING_DBG & 8) || (lane & 3) == 3
-                                         ? kOob
-                                         : (uint32_t)y * dpitch + drs.delta +
-                                               (uint32_t)((x - lane) * CC + 12 * (lane >> 2) + 4 * (lane & 3));
-                __builtin_amdgcn_raw_buffer_store_b32(word, drs.r, (int)off, 0, VACV_RING_SAUX);
-            } else if constexpr (FULL) {
+            if constexpr (FULL) {
                 *reinterpret_cast<uint32_t*>(xch + 256 * (j & 3) + 4 * lane) = own;
                 if ((j & 3) == 3) {
                     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -1012,15 +965,15 @@ warp_exp_kernel(WarpLaunch L, int gx, int gy, int kf, int slot_bytes, int exp_un
                     const u32x3 o = {__builtin_amdgcn_perm(p[1], p[0], 0x04020100u),
                                      __builtin_amdgcn_perm(p[2], p[1], 0x05040201u),
                                      __builtin_amdgcn_perm(p[3], p[2], 0x06050402u)};
-                    const uint32_t off = (VACV_RING_DBG & 8) ? kOob : (uint32_t)(y - 3 + r) * dpitch + drs.delta + (uint32_t)(bx * TW * CC + 12 * q);
-                    __builtin_amdgcn_raw_buffer_store_b96(o, drs.r, (int)off, 0, VACV_RING_SAUX);
+                    const uint32_t off = (uint32_t)(y - 3 + r) * dpitch + drs.delta + (uint32_t)(bx * TW * CC + 12 * q);
+                    __builtin_amdgcn_raw_buffer_store_b96(o, drs.r, (int)off, 0, VACV_STORE_AUX);
                 }
             } else {
                 const uint32_t off = (uint32_t)y * dpitch + drs.delta + (uint32_t)(x * CC);
 #pragma unroll
                 for (int k = 0; k < CC; ++k)
                     __builtin_amdgcn_raw_buffer_store_b8((unsigned char)(own >> (8 * k)), drs.r,
-                                                         (int)(inside ? off + k : kOob), 0, VACV_RING_SAUX);
+                                                         (int)(inside ? off + k : kOob), 0, VACV_STORE_AUX);
             }
         } else {
             uint32_t o[CC];
@@ -1030,7 +983,7 @@ warp_exp_kernel(WarpLaunch L, int gx, int gy, int kf, int slot_bytes, int exp_un
                 const float fv = OUT == kOutF32 ? (float)v : normalize_u8v(cn[k], v);
                 o[k] = __builtin_bit_cast(uint32_t, fv);
             }
-            if constexpr (FULL && VACV_EXP_F32XCH) {
+            if constexpr (FULL) {
 #pragma unroll
                 for (int k = 0; k < CC; ++k) *reinterpret_cast<uint32_t*>(xch + 12 * lane + 4 * k) = o[k];
                 __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -1040,11 +993,11 @@ warp_exp_kernel(WarpLaunch L, int gx, int gy, int kf, int slot_bytes, int exp_un
                 const uint32_t off = lane < 3 * 16 ? (uint32_t)y * dpitch + drs.delta +
                                                          (uint32_t)((x - lane) * CC * 4 + 16 * lane)
                                                    : kOob;
-                __builtin_amdgcn_raw_buffer_store_b128(p, drs.r, (int)off, 0, VACV_RING_SAUX);
+                __builtin_amdgcn_raw_buffer_store_b128(p, drs.r, (int)off, 0, VACV_STORE_AUX);
             } else {
                 typedef unsigned int u32x3 __attribute__((ext_vector_type(3)));
                 const uint32_t off = inside ? (uint32_t)y * dpitch + drs.delta + (uint32_t)(x * CC * 4) : kOob;
-                __builtin_amdgcn_raw_buffer_store_b96(u32x3{o[0], o[1], o[2]}, drs.r, (int)off, 0, VACV_RING_SAUX);
+                __builtin_amdgcn_raw_buffer_store_b96(u32x3{o[0], o[1], o[2]}, drs.r, (int)off, 0, VACV_STORE_AUX);
             }
         }
     };
@@ -1055,15 +1008,15 @@ warp_exp_kernel(WarpLaunch L, int gx, int gy, int kf, int slot_bytes, int exp_un
 #pragma unroll
             for (int k = 0; k < CC; ++k) cn[k] = chan_norm(L.norm, f, k);
         }
-        constexpr int kGrp = VACV_EXP_GRP;
+        constexpr int kGrp = kExpGrp;
 #pragma unroll
         for (int j0 = 0; j0 < NP; j0 += kGrp) {
             uint32_t tp[kGrp][4];
 #pragma unroll
             for (int j = 0; j < kGrp; ++j) {
                 const uint32_t e = eaTB[j0 + j];
-                const uint32_t* pt = reinterpret_cast<const uint32_t*>(lds + ((VACV_RING_DBG & 4) ? ebase : e & 0xFFFFu));
-                const uint32_t* pb = reinterpret_cast<const uint32_t*>(lds + ((VACV_RING_DBG & 4) ? ebase : e >> 16));
+                const uint32_t* pt = reinterpret_cast<const uint32_t*>(lds + (e & 0xFFFFu));
+                const uint32_t* pb = reinterpret_cast<const uint32_t*>(lds + (e >> 16));
                 tp[j][0] = pt[0];
                 if constexpr (!NN) {
                     tp[j][1] = pt[1];
@@ -1129,49 +1082,25 @@ warp_exp_kernel(WarpLaunch L, int gx, int gy, int kf, int slot_bytes, int exp_un
     // prologue: frames f0 and f0 + 1 in flight
     dma(f0, 0);
     if (f0 + 1 < f1) dma(f0 + 1, 1);
-#if VACV_RING_DBG & 16
-    // diagnosis build: per-phase shader-clock totals of a few waves (printf)
-    uint64_t tph[6] = {0, 0, 0, 0, 0, 0};
-    uint64_t t_ = __builtin_amdgcn_s_memtime();
-#define EXP_STAMP(i) do { const uint64_t n_ = __builtin_amdgcn_s_memtime(); tph[i] += n_ - t_; t_ = n_; } while (0)
-#else
-#define EXP_STAMP(i) do {} while (0)
-#endif
     for (int f = f0; f < f1; ++f) {
         const int s = (f - f0) & 1;
         // this wave's DMA of frame f has landed; issued after it and possibly
         // still in flight: frame f + 1's DMA and the stores of the (up to 2)
         // frames sampled since
         wait_vm((f + 1 < f1 ? n_w : 0) + min(f - f0, 2) * n_st);
-        EXP_STAMP(0);
         if (tailm) {
             fix_tail(f, s);
             wait_lgkm();  // its LDS stores land before the barrier (s_barrier does not wait for them)
         }
         __builtin_amdgcn_s_barrier();  // every wave's part of frame f is in; frame f - 1's image reads are done
-        EXP_STAMP(1);
-        if (!(VACV_RING_DBG & 1)) relay(s);
+        relay(s);
         wait_lgkm();
-        EXP_STAMP(2);
         __builtin_amdgcn_s_barrier();  // the image holds frame f; slot s is free
-        EXP_STAMP(3);
         if (f + 2 < f1) dma(f + 2, s);
-        EXP_STAMP(4);
-        if (!(VACV_RING_DBG & 1)) {
-            if (tile_full) sample(full_t(), f);
-            else sample(edge_t(), f);
-        }
-        EXP_STAMP(5);
+        if (tile_full) sample(full_t(), f);
+        else sample(edge_t(), f);
     }
     wait_vm(0);  // no LDS-DMA may outlive the workgroup's LDS
-#if VACV_RING_DBG & 16
-    if (lane == 0 && (blockIdx.x % 911) == 7)
-        printf("expprof blk %u wave %d frames %d full %d: dmawait %llu b1 %llu relay %llu b2 %llu dmaissue %llu sample %llu\n",
-               blockIdx.x, wave, f1 - f0, (int)tile_full, (unsigned long long)tph[0], (unsigned long long)tph[1],
-               (unsigned long long)tph[2], (unsigned long long)tph[3], (unsigned long long)tph[4],
-               (unsigned long long)tph[5]);
-#endif
-#undef EXP_STAMP
 }
 
 template <typename K>
@@ -1454,7 +1383,7 @@ bool exp_layout_th(const WarpLaunch& L, WarpFramesPlan& P, int th, bool nn = fal
     P.S = 0;
     P.ns = 2;
     P.slot = P.raw_bytes;
-    const int xb = 4 * (L.out == kOutSame ? (VACV_EXP_XCH ? 4 * 64 * 4 : 16) : (VACV_EXP_F32XCH ? 64 * 3 * 4 : 16));
+    const int xb = 4 * kExpXB(L.out == kOutSame ? kOutSame : kOutF32);
     P.lds = 48 + 2 * P.raw_bytes + 64 + 16 + 64 * std::max(n.units, (kExpTab + 63) / 64) + xb;
     return P.lds <= 64 * 1024;
 }

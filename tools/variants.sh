@@ -3,7 +3,7 @@
 # each reuses the main build's objects and recompiles only the named sources
 # with extra flags.
 #   tools/variants.sh <name> "<sources without .hip>" "<EXTRA flags>"
-# e.g. tools/variants.sh d1 "k_resize_direct" "-DVACV_DIRECT_DBG=1"
+# e.g. tools/variants.sh s0 "k_resize_strip" "-DVACV_STRIP_AUX=2"
 #   -> arm-neon-opencv_amd/lib_d1/libvacv_hip.so
 set -e
 N=$1; SRCS=$2; X=$3
