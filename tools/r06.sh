@@ -12,6 +12,7 @@
 #   pmc:WL:KEY       PMC passes (tools/pmc_bench.txt) over bench.py WL, kernel KEY
 #   kpmc:OP:ONLY:KEY PMC passes over kbench
 #   lib:DIR          run the following steps on lib variant DIR (VACV_LIB_DIR)
+#   clocks:OP:ONLY   kbench twice with rocm-smi sclk / power sampled beside it
 # Output: gpurun_out/${TAG}_*.  Only gpurun_out/ travels back.
 set -o pipefail
 T=$1; shift
@@ -56,6 +57,7 @@ for S in "$@"; do
           -- python3 "$R/bench.py" --workload "$a" --steps 5 --warmup 2 --no-cpu-baseline > "gpurun_out/${T}_pmc_$a.log" 2>&1 || exit $?
       python3 tools/pmc_summary.py "gpurun_out/${T}_pmc_$a" "$b" --out "gpurun_out/${T}_pmc_$a.json" \
           > "gpurun_out/${T}_pmc_${a}_summary.txt" || exit 1
+      cp "gpurun_out/${T}_pmc_$a.json" "profiles/pmc_$a.json"  # later bench steps of this call read it
       cat "gpurun_out/${T}_pmc_${a}_summary.txt" | cut -c1-200 ;;
     kpmc)
       timeout -s KILL 300 rocprofv3 -i "$R/tools/pmc_bench.txt" -d "$R/gpurun_out/${T}_kpmc_$c" -o pmc --output-format csv \
@@ -65,6 +67,18 @@ for S in "$@"; do
       cat "gpurun_out/${T}_kpmc_${c}_summary.txt" | cut -c1-200 ;;
     lib)
       export VACV_LIB_DIR="$R/arm-neon-opencv_amd/$a" ;;
+    clocks)
+      # kbench OP:ONLY twice with rocm-smi's sclk / power sampled beside it
+      ( while true; do date +%T.%N; rocm-smi --showclocks --showpower 2>/dev/null | grep -E "sclk|mclk|Power"; sleep 0.2; done ) \
+          > "gpurun_out/${T}_clocks_$b.txt" 2>&1 &
+      SMI=$!
+      for i in 1 2; do
+        timeout -k 10 300 python3 tools/kbench.py --op "$a" --only "$b" --iters 30 >> "gpurun_out/${T}_clocks_$b.jsonl" 2>> "gpurun_out/${T}_kbench.err" \
+            || { kill $SMI; exit 1; }
+        sleep 1
+      done
+      kill $SMI; wait $SMI 2>/dev/null
+      cat "gpurun_out/${T}_clocks_$b.jsonl" | cut -c1-200 ;;
     *) echo "unknown step $S"; exit 2 ;;
   esac
 done
