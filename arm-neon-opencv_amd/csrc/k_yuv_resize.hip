@@ -93,12 +93,23 @@ __device__ __forceinline__ s16x2 clamp_u8x2(s16x2 v) {
     return __builtin_elementwise_max(__builtin_elementwise_min(v, (s16x2)(short)255), (s16x2)(short)0);
 }
 
-// Decode the row's two tap pixels, cvt_color.cpp:66-88, on packed 16-bit
-// pairs {left, right}: every intermediate of the reference's int arithmetic
-// fits in int16 (|179(v-128)|, |44(u-128) + 91(v-128)|, |227(u-128)| < 2^15,
-// Y + term in [-227, 481]), >> is arithmetic as in the reference, so each
-// lane is exact.  Out: B, G, R as u16 pairs {left, right} -- the layout the
-// blend's v_dot2_u32_u16 takes.
+// Decode two pixels, cvt_color.cpp:66-88, on packed 16-bit pairs (Y, V, U
+// as u16 lanes): every intermediate of the reference's int arithmetic fits in
+// int16 (|179(v-128)|, |44(u-128) + 91(v-128)|, |227(u-128)| < 2^15, Y + term
+// in [-227, 481]), >> is arithmetic as in the reference, so each lane is
+// exact.  Out: B, G, R as u16 pairs.
+__device__ __forceinline__ void decode_yuv(s16x2 Y, s16x2 V, s16x2 U, uint32_t& bp, uint32_t& gp, uint32_t& rp) {
+    const s16x2 vm = V - (short)128, um = U - (short)128;
+    const s16x2 ra = (vm * (short)179) >> (short)7;
+    const s16x2 ga = (um * (short)44 + vm * (short)91) >> (short)7;
+    const s16x2 ba = (um * (short)227) >> (short)7;
+    bp = __builtin_bit_cast(uint32_t, clamp_u8x2(Y + ba));
+    gp = __builtin_bit_cast(uint32_t, clamp_u8x2(Y - ga));
+    rp = __builtin_bit_cast(uint32_t, clamp_u8x2(Y + ra));
+}
+
+// A row's two tap pixels {left, right} decoded -- the layout the blend's
+// v_dot2_u32_u16 takes.
 __device__ __forceinline__ void decode_row(const RowTaps& t, uint32_t cs, int v_first, uint32_t& bp, uint32_t& gp,
                                            uint32_t& rp, uint32_t ysel = 0x0C010C00u) {
     // v_perm selectors: byte (a + vi) -> lane 0, byte (b + vi) -> lane 1, 0x0C = 0
@@ -107,13 +118,7 @@ __device__ __forceinline__ void decode_row(const RowTaps& t, uint32_t cs, int v_
     const s16x2 V = __builtin_bit_cast(s16x2, __builtin_amdgcn_perm(0u, t.c, base + vo));
     const s16x2 U = __builtin_bit_cast(s16x2, __builtin_amdgcn_perm(0u, t.c, base + (0x00010001u - vo)));
     const s16x2 Y = __builtin_bit_cast(s16x2, __builtin_amdgcn_perm(0u, t.y, ysel));  // Y bytes -> u16 lanes
-    const s16x2 vm = V - (short)128, um = U - (short)128;
-    const s16x2 ra = (vm * (short)179) >> (short)7;
-    const s16x2 ga = (um * (short)44 + vm * (short)91) >> (short)7;
-    const s16x2 ba = (um * (short)227) >> (short)7;
-    bp = __builtin_bit_cast(uint32_t, clamp_u8x2(Y + ba));
-    gp = __builtin_bit_cast(uint32_t, clamp_u8x2(Y - ga));
-    rp = __builtin_bit_cast(uint32_t, clamp_u8x2(Y + ra));
+    decode_yuv(Y, V, U, bp, gp, rp);
 }
 
 // Output pixels per wave and per LDS exchange round (4 per lane).
@@ -318,11 +323,20 @@ yuv_resize_kernel(YuvResizeLaunch L) {
 // (an odd integer step, e.g. 1080p -> 640x360: 384 bytes = 3 lines per row):
 // no line is then split between two blocks, which neighbouring workgroups on
 // other XCDs would both fetch from HBM (the headline kernel's CW = 2, k_resize_direct.hip).
+//
+// POINT (round 6): every output row and column weights one source row and
+// column, with 2048 (an odd integer downscale: 1080p -> 640x360 taps rows and
+// columns 3d + 1).  The blend then returns the tapped pixel in every mode
+// (reference (p*2048*2048) >> 22 = p; NEON / OpenCV ((4p) + 2) >> 2 = p), so
+// the output pixel IS the decoded source pixel: one Y byte and one VU pair
+// are gathered per output pixel, a lane's pixels are decoded two at a time
+// (the packed decode's lanes = two output pixels, not two taps), no blend.
 constexpr int kYuvRows = 8;   // output rows per wave task (at CW = 1)
 constexpr int kYuvHalf = 4;   // rows per LDS exchange round (at CW = 1)
-template <int OUT, int MODE, bool CHW, bool ONE_ROW, int CW>
+template <int OUT, int MODE, bool CHW, bool ONE_ROW, int CW, bool POINT = false>
 __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(yuv_waves(OUT, ONE_ROW))))
 yuv_cols_kernel(YuvResizeLaunch L, int col_blocks, int row_groups) {
+    static_assert(!POINT || ONE_ROW, "POINT gathers one row");
     using TOut = typename std::conditional<(OUT == kOutSame), uint8_t, float>::type;
     constexpr int kES = (int)sizeof(TOut);
     constexpr int NR = ONE_ROW ? 1 : 2;
@@ -359,6 +373,13 @@ yuv_cols_kernel(YuvResizeLaunch L, int col_blocks, int row_groups) {
         const int x = 64 * c + lane < ncol ? x0 + 64 * c + lane : W - 1;
         const FixedTap tx = tap_of<MODE>(x, L.w, W, L.scale_xf, L.scale_xd);
         wx[c] = __builtin_bit_cast(us2, (uint32_t)tx.w0 | ((uint32_t)tx.w1 << 16));
+        if constexpr (POINT) {
+            // the weighted column and its VU pair (no neighbour is read)
+            const int xi = tx.w0 == 0 ? tx.i + 1 : tx.i;
+            ycol[c] = (uint32_t)xi;
+            ccol[c] = (uint32_t)(xi & ~1);
+            continue;
+        }
         const bool edge = c == CW - 1 && lane == 63 && tx.i >= 2;
         const int ca = tx.i & ~1, c0 = min(ca, L.w - 4);
         const int c1 = edge && (tx.i & 1) == 0 && c0 == ca ? c0 - 2 : c0;
@@ -388,6 +409,11 @@ yuv_cols_kernel(YuvResizeLaunch L, int col_blocks, int row_groups) {
         const uint32_t cb2 = ONE_ROW ? 0u : (uint32_t)__builtin_amdgcn_readlane((int)my_c1, r);
 #pragma unroll
         for (int c = 0; c < CW; ++c) {
+            if constexpr (POINT) {
+                t[r][c][0].y = __builtin_amdgcn_raw_buffer_load_b8(rs.r, (int)(ya + ycol[c]), 0, kYuvAux);
+                t[r][c][0].c = __builtin_amdgcn_raw_buffer_load_b16(rs.r, (int)(ca + ccol[c]), 0, kYuvAux);
+                continue;
+            }
             t[r][c][0].y = __builtin_amdgcn_raw_buffer_load_b32(rs.r, (int)(ya + ycol[c]), 0, kYuvAux);
             t[r][c][0].c = __builtin_amdgcn_raw_buffer_load_b32(rs.r, (int)(ca + ccol[c]), 0, kYuvAux);
             if constexpr (!ONE_ROW) {
@@ -416,6 +442,39 @@ yuv_cols_kernel(YuvResizeLaunch L, int col_blocks, int row_groups) {
 #pragma unroll
         for (int j = 0; j < HALF; ++j) {
             const int r = g * HALF + j;
+            if constexpr (POINT) {
+                // pixels A, B of the pair: the lane's two columns of row r
+                // (CW = 2) or its column in rows r and r + 1
+                if (CW == 1 && (j & 1)) continue;
+                const RowTaps& ta = t[r][0][0];
+                const RowTaps& tb = CW == 2 ? t[r][CW - 1][0] : t[min(r + 1, ROWS - 1)][0][0];
+                const uint32_t vsel = L.v_first ? 0x0C040C00u : 0x0C050C01u;
+                const s16x2 Y = __builtin_bit_cast(s16x2, __builtin_amdgcn_perm(tb.y, ta.y, 0x0C040C00u));
+                const s16x2 V = __builtin_bit_cast(s16x2, __builtin_amdgcn_perm(tb.c, ta.c, vsel));
+                const s16x2 U = __builtin_bit_cast(s16x2, __builtin_amdgcn_perm(tb.c, ta.c, vsel ^ 0x00010001u));
+                uint32_t q[3];
+                decode_yuv(Y, V, U, q[0], q[1], q[2]);
+                if (L.rgb) {  // output order R, G, B
+                    const uint32_t q0 = q[0];
+                    q[0] = q[2];
+                    q[2] = q0;
+                }
+#pragma unroll
+                for (int e = 0; e < 2; ++e) {
+                    const int jj = CW == 2 ? j : j + e, cc = CW == 2 ? e : 0;
+#pragma unroll
+                    for (int k = 0; k < 3; ++k) {
+                        const int v = (int)((q[k] >> (16 * e)) & 0xFFu);
+                        TOut ov;
+                        if (OUT == kOutSame) ov = (TOut)v;
+                        else if (OUT == kOutF32) ov = (TOut)(float)v;
+                        else ov = (TOut)normalize_u8v(cn[k], v);
+                        const int px = jj * 64 * CW + 64 * cc + lane;
+                        xo[CHW ? k * (HALF * 64 * CW) + px : px * 3 + k] = ov;
+                    }
+                }
+                continue;
+            }
             const uint32_t wr = (uint32_t)__builtin_amdgcn_readlane((int)my_w, r);
             const uint32_t wA = wr & 0xFFFFu, wB = ONE_ROW ? 0u : wr >> 16;
 #pragma unroll
@@ -487,19 +546,24 @@ int yuv_cols_cw(const YuvResizeLaunch& L) {
     return lines && (step & 1) ? 2 : 1;
 }
 
-template <int OUT, int MODE, bool CHW, bool ONE_ROW, int CW>
+template <int OUT, int MODE, bool CHW, bool ONE_ROW, int CW, bool POINT = false>
 hipError_t launch_cols_cw(const YuvResizeLaunch& L, hipStream_t s) {
     const int col_blocks = (L.wo + 64 * CW - 1) / (64 * CW), row_groups = (L.ho + kYuvRows / CW - 1) / (kYuvRows / CW);
     const dim3 grid((unsigned)((col_blocks * row_groups + 3) / 4), (unsigned)L.n);
-    hipLaunchKernelGGL((yuv_cols_kernel<OUT, MODE, CHW, ONE_ROW, CW>), grid, dim3(kBlock), 0, s, L, col_blocks, row_groups);
+    hipLaunchKernelGGL((yuv_cols_kernel<OUT, MODE, CHW, ONE_ROW, CW, POINT>), grid, dim3(kBlock), 0, s, L, col_blocks,
+                       row_groups);
     return hipGetLastError();
 }
 
+// taps: 0 two rows, 1 one row (ONE_ROW), 2 one row and one column (POINT)
 template <int OUT, int MODE, bool CHW>
-hipError_t launch_cols_t(const YuvResizeLaunch& L, bool one_row, hipStream_t s) {
-    if (yuv_cols_cw(L) == 2)
-        return one_row ? launch_cols_cw<OUT, MODE, CHW, true, 2>(L, s) : launch_cols_cw<OUT, MODE, CHW, false, 2>(L, s);
-    return one_row ? launch_cols_cw<OUT, MODE, CHW, true, 1>(L, s) : launch_cols_cw<OUT, MODE, CHW, false, 1>(L, s);
+hipError_t launch_cols_t(const YuvResizeLaunch& L, int taps, hipStream_t s) {
+    if (yuv_cols_cw(L) == 2) {
+        if (taps == 2) return launch_cols_cw<OUT, MODE, CHW, true, 2, true>(L, s);
+        return taps ? launch_cols_cw<OUT, MODE, CHW, true, 2>(L, s) : launch_cols_cw<OUT, MODE, CHW, false, 2>(L, s);
+    }
+    if (taps == 2) return launch_cols_cw<OUT, MODE, CHW, true, 1, true>(L, s);
+    return taps ? launch_cols_cw<OUT, MODE, CHW, true, 1>(L, s) : launch_cols_cw<OUT, MODE, CHW, false, 1>(L, s);
 }
 
 template <int OUT, int MODE, bool CHW>
@@ -510,7 +574,8 @@ hipError_t launch_rows_t(const YuvResizeLaunch& L, bool one_row, dim3 grid, hipS
 }
 
 template <int OUT, int MODE>
-hipError_t launch_layout_t(const YuvResizeLaunch& L, bool one_row, dim3 grid, hipStream_t s) {
+hipError_t launch_layout_t(const YuvResizeLaunch& L, int taps, dim3 grid, hipStream_t s) {
+    const bool one_row = taps > 0;
     // the column kernel needs 16-byte aligned block rows (and plane and image
     // pitches) in the destination; VACV_TUNE_RESIZE_DIRECT = 2 forces the
     // row-major kernel (A/B)
@@ -521,18 +586,28 @@ hipError_t launch_layout_t(const YuvResizeLaunch& L, bool one_row, dim3 grid, hi
     const int64_t span = L.chw ? L.dst_plane * 3 : L.dst_img;
     if (!(bits & 15) && rowb % 16 == 0 && tune(VACV_TUNE_RESIZE_DIRECT) != 2 && span < kMaxPlaneBytes &&
         (int64_t)L.wo * L.ho < 0x7FFFFFF0LL / 4)
-        return L.chw ? launch_cols_t<OUT, MODE, true>(L, one_row, s) : launch_cols_t<OUT, MODE, false>(L, one_row, s);
+        return L.chw ? launch_cols_t<OUT, MODE, true>(L, taps, s) : launch_cols_t<OUT, MODE, false>(L, taps, s);
     return L.chw ? launch_rows_t<OUT, MODE, true>(L, one_row, grid, s)
                  : launch_rows_t<OUT, MODE, false>(L, one_row, grid, s);
 }
 
 template <int OUT>
-hipError_t launch_mode_t(const YuvResizeLaunch& L, bool one_row, dim3 grid, hipStream_t s) {
+hipError_t launch_mode_t(const YuvResizeLaunch& L, int taps, dim3 grid, hipStream_t s) {
     switch (L.mode) {
-        case VACV_LINEAR_REFERENCE: return launch_layout_t<OUT, VACV_LINEAR_REFERENCE>(L, one_row, grid, s);
-        case VACV_LINEAR_NEON: return launch_layout_t<OUT, VACV_LINEAR_NEON>(L, one_row, grid, s);
-        default: return launch_layout_t<OUT, VACV_LINEAR_OPENCV>(L, one_row, grid, s);
+        case VACV_LINEAR_REFERENCE: return launch_layout_t<OUT, VACV_LINEAR_REFERENCE>(L, taps, grid, s);
+        case VACV_LINEAR_NEON: return launch_layout_t<OUT, VACV_LINEAR_NEON>(L, taps, grid, s);
+        default: return launch_layout_t<OUT, VACV_LINEAR_OPENCV>(L, taps, grid, s);
     }
+}
+
+// every tap of the axis weights one source index, with 2048 (then the blend
+// returns that pixel, see yuv_cols_kernel's POINT)
+bool point_axis(int n_in, int n_out, float scale_f, double scale_d, int mode) {
+    for (int d = 0; d < n_out; ++d) {
+        const FixedTap t = fixed_tap(d, n_in, n_out, scale_f, scale_d, mode);
+        if (!((t.w0 == 2048 && t.w1 == 0) || (t.w0 == 0 && t.w1 == 2048))) return false;
+    }
+    return true;
 }
 
 }  // namespace
@@ -550,9 +625,15 @@ hipError_t launch_yuv_resize(const YuvResizeLaunch& L, hipStream_t s) {
     }
     const int64_t block_px = 4 * 64 * yuv_pxl(one_row);
     const dim3 grid((unsigned)((P + block_px - 1) / block_px), (unsigned)L.n);
-    if (L.out == kOutSame) return launch_mode_t<kOutSame>(L, one_row, grid, s);
-    if (L.out == kOutF32) return launch_mode_t<kOutF32>(L, one_row, grid, s);
-    return launch_mode_t<kOutNorm>(L, one_row, grid, s);
+    const int taps = !one_row                                                       ? 0
+                     : tune(VACV_TUNE_RESIZE_DIRECT) != 3 &&
+                               point_axis(L.h, L.ho, L.scale_yf, L.scale_yd, L.mode) &&
+                               point_axis(L.w, L.wo, L.scale_xf, L.scale_xd, L.mode)
+                         ? 2
+                         : 1;
+    if (L.out == kOutSame) return launch_mode_t<kOutSame>(L, taps, grid, s);
+    if (L.out == kOutF32) return launch_mode_t<kOutF32>(L, taps, grid, s);
+    return launch_mode_t<kOutNorm>(L, taps, grid, s);
 }
 
 }  // namespace vacv

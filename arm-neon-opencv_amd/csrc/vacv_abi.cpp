@@ -348,12 +348,13 @@ int resize_impl(const vacv_image* src_d, const vacv_image* dst_d, int interpolat
     // an integer factor >= 2, e.g. the 1080p -> 640x360 headline): the
     // per-pixel gather kernel (k_resize_direct.hip).  Elsewhere the staged
     // kernel measured faster (1280x720: 0.63 vs 0.69 ms).  VACV_TUNE_RESIZE_DIRECT
-    // = 0 never / 2 always uses the gather kernel, for A/B tests.
+    // = 0 never / 2 always uses the gather kernel, for A/B tests (3: as 1; the
+    // NV21 resize then also leaves out its point-sampling instance, A/B).
     // Otherwise resize_kernel with interleaved (address-ordered) tasks;
     // VACV_TUNE_RESIZE_INTERLEAVE = 0 selects its strip order.
     const int direct = tune_or(VACV_TUNE_RESIZE_DIRECT, 1);
     if (L.kind == kLinearFixed && L.src.cc <= 4 && dst.w < (1 << 23) && dst.h < (1 << 23) &&
-        (direct == 2 || (direct == 1 && resize_one_tap_rows(L))))
+        (direct == 2 || ((direct == 1 || direct == 3) && resize_one_tap_rows(L))))
         return hip_status(launch_resize_direct(L, s));
     // the other u8 bilinear geometries (two weighted rows per output row):
     // column strips with an LDS ring of source rows (k_resize_strip.hip;

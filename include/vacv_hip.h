@@ -311,7 +311,7 @@ int vacv_min_max_idx(const vacv_image* src, const vacv_image* mask, double* vals
  * Each starts from the environment variable of the same name (read once,
  * when the library loads), else -1 = the built-in choice. */
 enum {
-    VACV_TUNE_RESIZE_DIRECT = 0,     /* u8 bilinear: 0 staged, 1 gather kernel for one-tap rows, 2 gather always */
+    VACV_TUNE_RESIZE_DIRECT = 0,     /* u8 bilinear: 0 staged, 1 gather kernel for one-tap rows, 2 gather always, 3 as 1 without the NV21 resize's point-sampling instance (A/B) */
     VACV_TUNE_CUBIC_DIRECT = 1,      /* u8 cubic: 0 staged kernel, else the gather kernel */
     VACV_TUNE_RESIZE_INTERLEAVE = 2, /* staged kernel: 0 strip order, else address-ordered tasks */
     VACV_TUNE_DIRECT_XCD = 3,        /* gather kernel block order: 0 plain, 1 XCD-contiguous */

@@ -1475,7 +1475,10 @@ def test_cvt_color_resize(ops, dev, oracle, v_first, rgb):
     code = {(True, False): V.COLOR_YUV2BGR_NV21, (False, True): V.COLOR_YUV2RGB_NV12}[(v_first, rgb)]
     rng = np.random.default_rng(29)
     cases = [((36, 50), (17, 11)), ((144, 176), (64, 48)), ((120, 160), (224, 224)), ((1080, 1920), (640, 360)),
-             ((1080, 1920), (224, 224)), ((4, 4), (3, 5)), ((360, 640), (640, 360))]
+             ((1080, 1920), (224, 224)), ((4, 4), (3, 5)), ((360, 640), (640, 360)),
+             # point-sampling geometries (odd integer steps: every tap weight 2048)
+             # on 64-column blocks: 3x to 320x120, 5x to 100x50
+             ((360, 960), (320, 120)), ((250, 500), (100, 50))]
     for (h, w), (wo, ho) in cases:
         yuv = np.stack([rng.integers(0, 256, (h * 3 // 2, w), dtype=np.uint8) for _ in range(2)])
         ydev = to_dev(yuv, dev)
@@ -1537,9 +1540,14 @@ def test_cvt_color_resize_batch_and_pitch(ops, dev, oracle):
             # odd-step geometries (1080p -> 640x360)
             with ops.tuning(RESIZE_TILE_W=64):
                 c = fn()
+            # the point-sampling instance (odd integer steps) against the
+            # blending one (RESIZE_DIRECT = 3)
+            with ops.tuning(RESIZE_DIRECT=3):
+                e = fn()
             torch.cuda.synchronize(dev)
             assert torch.equal(a, b), f"{wo}x{ho} layout {layout}: {(a != b).sum().item()} values differ"
             assert torch.equal(a, c), f"{wo}x{ho} layout {layout} 64-column blocks: {(a != c).sum().item()} differ"
+            assert torch.equal(a, e), f"{wo}x{ho} layout {layout} without POINT: {(a != e).sum().item()} differ"
     # the fused op equals the unfused GPU chain (cvt_color, resize_normalize, layout)
     bgr = ops.cvt_color(yuv[:4])
     chain = ops.change_layout(ops.resize_normalize(bgr, 224, 224, MEAN, STD), V.NCHW)

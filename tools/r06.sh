@@ -12,7 +12,7 @@
 #   pmc:WL:KEY       PMC passes (tools/pmc_bench.txt) over bench.py WL, kernel KEY
 #   kpmc:OP:ONLY:KEY PMC passes over kbench
 #   lib:DIR          run the following steps on lib variant DIR (VACV_LIB_DIR)
-#   clocks:OP:ONLY   kbench twice with rocm-smi sclk / power sampled beside it
+#   clocks:OP:ONLY[:ITERS]  kbench twice with rocm-smi sclk / power sampled beside it
 # Output: gpurun_out/${TAG}_*.  Only gpurun_out/ travels back.
 set -o pipefail
 T=$1; shift
@@ -73,7 +73,7 @@ for S in "$@"; do
           > "gpurun_out/${T}_clocks_$b.txt" 2>&1 &
       SMI=$!
       for i in 1 2; do
-        timeout -k 10 300 python3 tools/kbench.py --op "$a" --only "$b" --iters 30 >> "gpurun_out/${T}_clocks_$b.jsonl" 2>> "gpurun_out/${T}_kbench.err" \
+        timeout -k 10 300 python3 tools/kbench.py --op "$a" --only "$b" --iters "${c:-30}" >> "gpurun_out/${T}_clocks_$b.jsonl" 2>> "gpurun_out/${T}_kbench.err" \
             || { kill $SMI; exit 1; }
         sleep 1
       done
