@@ -57,42 +57,82 @@ constexpr int kMaxLds = 64 * 1024;
 // is a counted vmcnt that leaves them in flight.  u8: the lane quad's dword
 // store always; the CC byte stores of partial quads only in strips that have
 // them (a uniform branch: every path still holds the dword stores).
-constexpr uint32_t kOobStore = 0x80000000u;
+constexpr uint32_t kOobStore = 0x80000000u;  // a lane offset (voffset) past the plane: the store is dropped
+
+// blend_fixed with the value in bits 24..31 of the result (the bits below are
+// not zero).  In the reference mode the row weights come times 4 (kRowW4: the
+// row table holds them so), so the sum (tl*a0 + tr*a1)*4wA + (bl*a0 + br*a1)*4wB
+// is the reference's int32 sum << 2 (<= 255*2049^2*4 < 2^32; every 24-bit
+// multiply exact) and its top byte is sum >> 22: a pixel's channels pack with
+// two v_perm, fp32 converts from the top byte (no shift, no mask)
+template <int MODE>
+constexpr uint32_t kRowW4 = MODE == VACV_LINEAR_REFERENCE ? 4u : 1u;
+template <int MODE>
+__device__ __forceinline__ uint32_t blend_fixed_hi(uint32_t top, uint32_t bot, us2 wx, uint32_t wA, uint32_t wB) {
+    if constexpr (MODE == VACV_LINEAR_REFERENCE) {
+        const uint32_t ht = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, top), wx, 0u, false);
+        const uint32_t hb = __builtin_amdgcn_udot2(__builtin_bit_cast(us2, bot), wx, 0u, false);
+        return __umul24(ht, wA) + __umul24(hb, wB);
+    } else {
+        return (uint32_t)blend_fixed<MODE>(top, bot, wx, wA, wB) << 24;
+    }
+}
+
+// the channels' values (bits 24..31 of vh[k]) as the pixel's CC bytes
+template <int CC>
+__device__ __forceinline__ uint32_t pack_hi(const uint32_t (&vh)[CC]) {
+    if constexpr (CC == 1) return vh[0] >> 24;
+    else if constexpr (CC == 2) return __builtin_amdgcn_perm(vh[1], vh[0], 0x0C0C0703u);
+    else if constexpr (CC == 3)
+        return __builtin_amdgcn_perm(vh[2], __builtin_amdgcn_perm(vh[1], vh[0], 0x0C0C0703u), 0x0C070100u);
+    else
+        return __builtin_amdgcn_perm(__builtin_amdgcn_perm(vh[3], vh[2], 0x0C0C0703u),
+                                     __builtin_amdgcn_perm(vh[1], vh[0], 0x0C0C0703u), 0x05040100u);
+}
+
 template <int CC, int OUT>
-__device__ __forceinline__ void store_pixel(const int (&v)[CC], const ChanNorm (&cn)[CC], const Rsrc& drs, uint32_t row_off,
-                                            int ox, int qx, int W, bool quad_full, bool strip_full, int lane) {
+__device__ __forceinline__ void store_pixel(const uint32_t (&vh)[CC], const ChanNorm (&cn)[CC], const Rsrc& drs,
+                                            uint32_t row_off, int ox, int qx, int W, bool quad_full, bool strip_full,
+                                            int lane) {
     if constexpr (OUT == kOutSame) {
-        uint32_t own = 0;
-#pragma unroll
-        for (int k = 0; k < CC; ++k) own |= (uint32_t)v[k] << (8 * k);
+        const uint32_t own = pack_hi<CC>(vh);
         const uint32_t word = quad_pack<CC>(own, lane & 3);
         const bool wq = quad_full && (lane & 3) < CC;
-        __builtin_amdgcn_raw_buffer_store_b32(word, drs.r, (int)(wq ? row_off + (uint32_t)(qx * CC + 4 * (lane & 3)) : kOobStore),
-                                              0, VACV_STRIP_SAUX);
+        // the row's offset (uniform) as soffset, the lane's (fixed per strip) as
+        // voffset (never out of range as a soffset: it is not range-checked)
+        __builtin_amdgcn_raw_buffer_store_b32(word, drs.r, (int)(wq ? (uint32_t)(qx * CC + 4 * (lane & 3)) : kOobStore),
+                                              (int)row_off, VACV_STRIP_SAUX);
         if (!strip_full) {  // uniform: the partial quads' bytes
             const bool wb = !quad_full && ox < W;
 #pragma unroll
             for (int k = 0; k < CC; ++k)
-                __builtin_amdgcn_raw_buffer_store_b8((unsigned char)v[k], drs.r,
-                                                     (int)(wb ? row_off + (uint32_t)(ox * CC + k) : kOobStore), 0,
+                __builtin_amdgcn_raw_buffer_store_b8((unsigned char)(own >> (8 * k)), drs.r,
+                                                     (int)(wb ? (uint32_t)(ox * CC + k) : kOobStore), (int)row_off,
                                                      VACV_STRIP_SAUX);
         }
     } else {
         uint32_t f[CC];
 #pragma unroll
-        for (int k = 0; k < CC; ++k)
-            f[k] = __builtin_bit_cast(uint32_t, OUT == kOutF32 ? (float)v[k] : normalize_u8v(cn[k], v[k]));
+        for (int k = 0; k < CC; ++k) {
+            const int v = (int)(vh[k] >> 24);
+            f[k] = __builtin_bit_cast(uint32_t, OUT == kOutF32 ? (float)v : normalize_u8v(cn[k], v));
+        }
+        // the row in voffset here, soffset 0: with a register soffset the
+        // compiler leaves out the wait between a store of more than 8 bytes
+        // and a VALU write of its data registers, and on gfx950 the next
+        // instruction then overwrote the third dword before it was stored
         const int off = (int)(ox < W ? row_off + (uint32_t)(ox * CC * 4) : kOobStore);
+        const int soff = 0;
         if constexpr (CC == 1) {
-            __builtin_amdgcn_raw_buffer_store_b32(f[0], drs.r, off, 0, VACV_STRIP_SAUX);
+            __builtin_amdgcn_raw_buffer_store_b32(f[0], drs.r, off, soff, VACV_STRIP_SAUX);
         } else if constexpr (CC == 2) {
             typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
-            __builtin_amdgcn_raw_buffer_store_b64(u32x2{f[0], f[1]}, drs.r, off, 0, VACV_STRIP_SAUX);
+            __builtin_amdgcn_raw_buffer_store_b64(u32x2{f[0], f[1]}, drs.r, off, soff, VACV_STRIP_SAUX);
         } else if constexpr (CC == 3) {
             typedef unsigned int u32x3 __attribute__((ext_vector_type(3)));
-            __builtin_amdgcn_raw_buffer_store_b96(u32x3{f[0], f[1], f[2]}, drs.r, off, 0, VACV_STRIP_SAUX);
+            __builtin_amdgcn_raw_buffer_store_b96(u32x3{f[0], f[1], f[2]}, drs.r, off, soff, VACV_STRIP_SAUX);
         } else {
-            __builtin_amdgcn_raw_buffer_store_b128(u32x4{f[0], f[1], f[2], f[3]}, drs.r, off, 0, VACV_STRIP_SAUX);
+            __builtin_amdgcn_raw_buffer_store_b128(u32x4{f[0], f[1], f[2], f[3]}, drs.r, off, soff, VACV_STRIP_SAUX);
         }
     }
 }
@@ -237,11 +277,11 @@ resize_strip_kernel(ResizeLaunch L, int strips_x, int groups, int rows_per_group
     unsigned char* rtab = lds + ring * stride + 16;
     auto put_rows = [&](int b) {
         if (tid < BR) {
-            const int oy = min(oy_begin + b * BR + tid, H - 1);
+            const int oy = min(oy_begin + b * BR + tid, oy_end - 1);  // rows past the group: its last
             const FixedTap ty = tap_of<MODE>(oy, L.src.h, H, L.scale_yf, L.scale_yd);
             *reinterpret_cast<uint4*>(rtab + ((b & 1) * BR + tid) * 16) =
                 make_uint4(slot((uint32_t)ty.i) * (uint32_t)stride, slot((uint32_t)ty.i + 1u) * (uint32_t)stride,
-                           (uint32_t)ty.w0 | ((uint32_t)ty.w1 << 16), 0u);
+                           kRowW4<MODE> * ((uint32_t)ty.w0 | ((uint32_t)ty.w1 << 16)), 0u);
         }
     };
 
@@ -305,14 +345,17 @@ resize_strip_kernel(ResizeLaunch L, int strips_x, int groups, int rows_per_group
                         c1 = __builtin_amdgcn_alignbyte(t1[j][2], t1[j][1], sh[q]);
                     }
                     const uint32_t wA = wyv[j] & 0xFFFFu, wB = wyv[j] >> 16;
-                    int v[CC];
+                    uint32_t v[CC];
 #pragma unroll
                     for (int k = 0; k < CC; ++k) {
                         const uint32_t sel = (uint32_t)k | (0x0Cu << 8) | ((uint32_t)(CC + k) << 16) | (0x0Cu << 24);
-                        v[k] = blend_fixed<MODE>(__builtin_amdgcn_perm(a1, a0, sel), __builtin_amdgcn_perm(c1, c0, sel), wx, wA, wB);
+                        v[k] = blend_fixed_hi<MODE>(__builtin_amdgcn_perm(a1, a0, sel), __builtin_amdgcn_perm(c1, c0, sel),
+                                                    wx, wA, wB);
                     }
-                    // rows past the group: stores dropped (issued all the same)
-                    const uint32_t row_off = oy < oy_end ? (uint32_t)oy * (uint32_t)L.dst.row_pitch + drs.delta : kOobStore;
+                    // rows past the group (its last batch) repeat the group's last
+                    // row (put_rows), value for value: the soffset of a buffer
+                    // store is not range-checked, so it always names a real row
+                    const uint32_t row_off = (uint32_t)min(oy, oy_end - 1) * (uint32_t)L.dst.row_pitch + drs.delta;
                     store_pixel<CC, OUT>(v, cn, drs, row_off, ox, qx, W, quad_full, strip_full, lane);
                 }
             }
@@ -349,10 +392,13 @@ bool strip_plan(const ResizeLaunch& L, StripPlan& p) {
     p.lds = ring * p.stride + 16 + 2 * p.br * 16;  // + the last tap dword's overhang, the row-tap tables
     if (p.lds > kMaxLds) return false;
     p.strips_x = (L.dst.w + p.sw - 1) / p.sw;
-    // enough workgroups for the chip: split the rows when the strips are few
+    // enough workgroups for the chip: split the rows until there are >= 8192
+    // (~4 rounds of the 2,048 resident at 64-column strips), so the last round's
+    // partial occupancy is a small part of the run (256 x 1080p -> 1280x720:
+    // 5,120 whole-height strips are 2.5 rounds, the last half-empty)
     const int64_t strips = (int64_t)p.strips_x * L.n * L.src.planes;
     p.groups = 1;
-    while (strips * p.groups < 2048 && L.dst.h / (p.groups * 2) >= 4 * p.br) p.groups *= 2;
+    while (strips * p.groups < 8192 && L.dst.h / (p.groups * 2) >= 4 * p.br) p.groups *= 2;
     p.rows_per_group = (L.dst.h + p.groups - 1) / p.groups;
     return strips * p.groups < 0x7FFFFFF0LL;
 }
