@@ -1049,7 +1049,7 @@ int launch_resize_lanczos(const ResizeLaunch& R, double inv_x, double inv_y, hip
     A.out = R.out;
     A.norm = R.norm;
     // wave tasks: 64-column strips x bands of output rows x planes; bands
-    // shrink until there are ~16K tasks (a band's first row resizes all 8 of
+    // shrink until there are ~kLzTasks tasks (a band's first row resizes all 8 of
     // its source rows, later rows only the new ones)
     LzGrid g{};
     const int64_t planes = (int64_t)R.n * R.src.planes;
