@@ -324,7 +324,7 @@ enum {
     VACV_TUNE_RESIZE_TILE_W = 10,    /* staged kernel planner: tile width; column kernel (resize_cols_kernel): 64 / 128 output columns per wave */
     VACV_TUNE_RESIZE_WORK = 11,      /* staged kernel planner: work per thread */
     VACV_TUNE_WARP_KERNEL = 12,      /* u8 CONSTANT warp: 0 per-pixel gathers, 2 batched gathers, 4 LDS-staged frames: an LDS-DMA ring of source boxes (k_warp_frames.hip; 3 channels re-laid as 4-byte pixels, warp_exp_kernel), 6 the same without the re-lay (warp_ring_kernel, A/B); 5: INTER_NEAREST u8 on the per-pixel kernel (A/B) */
-    VACV_TUNE_RESIZE_STRIP = 13,     /* two-tap u8 bilinear: column strips with an LDS row ring, 1: 64 columns x 16-row batches, 2: 128 x 8; 0 staged kernel */
+    VACV_TUNE_RESIZE_STRIP = 13,     /* two-tap u8 bilinear: column strips with an LDS row ring, 1: 64 columns x 16-row batches, 2 (default): 128 x 8; 0 staged kernel */
     VACV_TUNE_MATCH_KERNEL = 14,     /* u8 match_template correlation: 0 v_dot4 kernel, else i8 MFMA where it fits */
     VACV_TUNE_WARP_FRAMES = 15,      /* u8 CONSTANT warp, LDS-staged kernel: frames per workgroup */
     VACV_TUNE_WARP_TILE_H = 16,      /* u8 CONSTANT warp, LDS-staged kernel: tile rows (16 or 32) */
